@@ -1,0 +1,34 @@
+# Build of libcbft_hipcrypto (gfx950) and of the CPU oracle used by the tests.
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+CSRC    := concord-bft_amd/csrc
+LIB     := concord-bft_amd/libcbft_hipcrypto.so
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall -Wno-unused-function
+ORACLE_LIB := oracle/libcbft_oracle.so
+
+.PHONY: all lib oracle clean
+all: lib oracle cpu
+
+lib: $(LIB)
+
+$(CSRC)/ed25519_verify.o: $(CSRC)/ed25519_verify.hip $(CSRC)/*.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/cbft_hipcrypto.o: $(CSRC)/cbft_hipcrypto.cpp include/cbft_hipcrypto.h $(CSRC)/ed25519_verify.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(CSRC)/ed25519_verify.o $(CSRC)/cbft_hipcrypto.o
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
+
+oracle: $(ORACLE_LIB)
+
+$(ORACLE_LIB): oracle/ed25519_oracle.c oracle/sha512_oracle.h
+	gcc -O2 -std=c11 -fPIC -shared -Wall -o $@ oracle/ed25519_oracle.c
+
+clean:
+	rm -f $(CSRC)/*.o $(LIB) $(ORACLE_LIB)
+
+CPU_LIB := tools/cpu_baseline/libcbft_cpu_openssl.so
+cpu: $(CPU_LIB)
+$(CPU_LIB): tools/cpu_baseline/openssl_ed25519.c
+	gcc -O2 -std=gnu11 -fPIC -shared -Wall -o $@ $< -lcrypto -lpthread

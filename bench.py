@@ -1,0 +1,231 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Ed25519 batch verification on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+
+A step = one batch of `--batch` (default 65,536) synthetic signed 256-byte messages per GPU,
+4,096 keys (BASELINE config #2), verified by libcbft_hipcrypto with every
+input already resident in HBM, followed — when N > 1 — by the RCCL all-gather of the
+per-signature verdict bitmaps (the only cross-GPU traffic north_star prescribes).  Weak scaling:
+each rank verifies its own static shard.  value = signatures verified by all ranks / max-over-
+ranks wall time.  Verdicts are checked bit-exact against the host OpenSSL before any number is
+printed.  Also reported: the dominant kernel's roofline (INT32 VALU), the host-CPU OpenSSL
+baseline (rank 0, N = 1) and the p50 end-to-end latency at batch 1K.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (os.path.join(ROOT, "concord-bft_amd"), os.path.join(ROOT, "tools")):
+    sys.path.insert(0, p)
+
+import cbft_hipcrypto as cb  # noqa: E402
+import workload  # noqa: E402
+
+METRIC = "Ed25519 verifies/sec at batch 64K on 1–8 MI355X; p50 latency @ batch 1K"
+# INT32 VALU peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (CDNA4 SIMDs are 32-wide;
+# MI355X_MICROARCH.md; v_add_u32 measured at 0.88 of it, tools/microbench/intrate.hip)
+INT32_PEAK = 256 * 4 * 32 * 2.4e9
+# Algorithmic INT32 ops per verify, SURVEY.md §8(d) model (8x32-bit limbs: M = 72, S = 44):
+OPS_DSM = 1020 * 44 + 1460 * 72            # double-scalar multiplication [S]B - [h]A
+OPS_DECODE = 256 * 44 + 20 * 72            # A decode
+OPS_ENCODE = 254 * 44 + 13 * 72            # R' inversion + encode
+SHA_OPS_PER_BLOCK = 5000
+
+
+def ops_per_verify(m: int) -> int:
+    return OPS_DSM + OPS_DECODE + OPS_ENCODE + SHA_OPS_PER_BLOCK * ((64 + m + 17 + 127) // 128)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=65536)
+    ap.add_argument("--msg-len", type=int, default=256)
+    ap.add_argument("--nkeys", type=int, default=4096)
+    ap.add_argument("--key-mode", choices=["keytable", "perkey"], default="keytable")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--latency-runs", type=int, default=200)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")  # RCCL on ROCm
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+
+    # ---- workload: this rank's static shard (weak scaling), signed by host OpenSSL
+    n = args.batch
+    ss = workload.make_sigset(n, nkeys=args.nkeys, msg_len=args.msg_len, seed=0xC0FFEE + rank,
+                              threads=args.cpu_threads)
+    ctx = cb.Context(device=dev.index, max_batch=n)
+
+    def to_dev(a: np.ndarray, dtype):
+        return torch.from_numpy(np.ascontiguousarray(a).view(dtype)).to(dev)
+
+    d_sig = to_dev(ss.sig.reshape(-1), np.uint8)
+    d_blob = to_dev(ss.blob, np.uint8)
+    d_off = to_dev(ss.off.view(np.int64), np.int64)
+    d_len = to_dev(ss.len.view(np.int32), np.int32)
+    if args.key_mode == "keytable":
+        tid = ctx.load_keys(ss.pk)  # key table resident, like SigManager's per-key verifiers
+        d_kidx = to_dev(ss.key_idx.view(np.int32), np.int32)
+        d_pk = None
+    else:
+        tid = cb.CBFT_NO_KEY_TABLE
+        d_pk = to_dev(ss.per_sig_pk().reshape(-1), np.uint8)
+        d_kidx = None
+    nwords = (n + 63) // 64
+    d_verdict = torch.zeros(nwords, dtype=torch.int64, device=dev)
+    gathered = torch.zeros(world * nwords, dtype=torch.int64, device=dev) if world > 1 else None
+    stream = torch.cuda.current_stream().cuda_stream
+
+    def step():
+        ctx.verify_device(tid, d_pk.data_ptr() if d_pk is not None else 0,
+                          d_kidx.data_ptr() if d_kidx is not None else 0, d_sig.data_ptr(), d_blob.data_ptr(),
+                          d_off.data_ptr(), d_len.data_ptr(), n, d_verdict.data_ptr(), stream)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, d_verdict)
+
+    # ---- parity gate: bit-exact vs host OpenSSL before any number is reported
+    step()
+    torch.cuda.synchronize()
+    got = cb.bitmap_to_bools(d_verdict.cpu().numpy().view(np.uint8).tobytes(), n)
+    if not np.array_equal(got, ss.expected):
+        raise SystemExit(f"rank {rank}: GPU verdicts differ from OpenSSL on {(got != ss.expected).sum()} sigs")
+    if world > 1:
+        torch.cuda.synchronize()
+        mine = gathered.view(world, nwords)[rank]
+        assert torch.equal(mine, d_verdict), "all-gather lost this rank's bitmap"
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = world * n * args.steps / elapsed
+
+    # ---- dominant kernel (ladder) timed with HIP events on its own stream
+    ctx.set_profiling(True)
+    stage = {"hash": [], "ladder": [], "finish": []}
+    for _ in range(5):
+        step()
+        for k, v in ctx.stage_times_ms().items():
+            stage[k].append(v)
+    ctx.set_profiling(False)
+    ladder_ms = statistics.median(stage["ladder"])
+    pipe_ms = sum(statistics.median(v) for v in stage.values())
+    achieved = OPS_DSM * n / (ladder_ms * 1e-3)
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "pmc_ladder.json")
+    if os.path.exists(pmc):
+        try:
+            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "valu_int32", "achieved": achieved / 1e12, "peak": INT32_PEAK / 1e12, "unit": "TOP/s",
+                "frac": achieved / INT32_PEAK, "traffic": traffic,
+                "kernel": "ed25519_ladder_kernel", "kernel_ms": ladder_ms,
+                "ops_per_unit": OPS_DSM, "units_per_launch": n,
+                "stage_ms": {k: statistics.median(v) for k, v in stage.items()},
+                "pipeline_frac": (n / (pipe_ms * 1e-3)) * ops_per_verify(args.msg_len) / INT32_PEAK}
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu and world == 1:
+            kc = workload.cpu_lib().cbft_cpu_keys_new(workload._p(ss.pk), ss.pk.shape[0])
+            try:
+                workload.cpu_verify(ss, threads=args.cpu_threads, keycache=kc)  # warm-up batch
+                ts = []
+                for _ in range(5):
+                    c0 = time.perf_counter()
+                    v = workload.cpu_verify(ss, threads=args.cpu_threads, keycache=kc)
+                    ts.append(time.perf_counter() - c0)
+                assert np.array_equal(v.astype(bool), ss.expected)
+            finally:
+                workload.cpu_lib().cbft_cpu_keys_free(kc, ss.pk.shape[0])
+            cpu = {"value": n / statistics.median(ts), "unit": "verifies/s", "cores": args.cpu_threads,
+                   "kind": "reference",
+                   "sample": f"OpenSSL {_openssl_version()} EVP_DigestVerify(ED25519), EVP_PKEY cached per key, "
+                             f"{args.cpu_threads} pthreads, static ranges; median of 5 batches of the same "
+                             f"{n} x {args.msg_len} B set after 1 warm-up batch"}
+        # p50 end-to-end latency at batch 1K (host buffers -> bitmap on host)
+        lat = None
+        if args.latency_runs > 0 and args.key_mode == "keytable":
+            k = min(1024, n)
+            msgs = ss.msgs()[:k]
+            kidx, sig = ss.key_idx[:k], ss.sig[:k]
+            for _ in range(5):
+                ctx.verify(tid, kidx, sig, msgs)
+            lt = []
+            for _ in range(args.latency_runs):
+                c0 = time.perf_counter()
+                bm = ctx.verify(tid, kidx, sig, msgs)
+                lt.append((time.perf_counter() - c0) * 1e3)
+            assert np.array_equal(cb.bitmap_to_bools(bm, k), ss.expected[:k])
+            lat = statistics.median(lt)
+        out = {
+            "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
+            "config": {"workload": "ed25519_verify_64k_256B_4096keys (BASELINE config #2)", "batch_per_gpu": n,
+                       "msg_len": args.msg_len, "nkeys": args.nkeys, "key_mode": args.key_mode,
+                       "parallelism": f"static shard x{world}, RCCL all-gather of verdict bitmaps"},
+            "roofline": roofline, "cpu_baseline": cpu,
+            "p50_latency_ms_batch1k": lat,
+            "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
+            "verdicts": "bit-exact vs host OpenSSL (checked before timing)",
+        }
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _openssl_version():
+    try:
+        import ctypes
+        lib = ctypes.CDLL("libcrypto.so.3")
+        lib.OpenSSL_version.restype = ctypes.c_char_p
+        return lib.OpenSSL_version(0).decode()
+    except Exception:
+        return "libcrypto"
+
+
+if __name__ == "__main__":
+    main()

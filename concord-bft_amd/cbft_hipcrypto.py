@@ -1,0 +1,196 @@
+"""Python binding of libcbft_hipcrypto (ctypes over the C ABI in include/cbft_hipcrypto.h).
+
+This is the binding a maintainer would add next to the reference's own Python tooling (the
+ctypes stub shown in INTEGRATION.md); tests and bench.py drive the GPU through it.  The product
+path has no CPU fallback: if the HIP library is missing or no GPU is visible, every entry point
+raises.
+
+    ctx = Context(device=0)
+    tid = ctx.load_keys(pks)                       # pks: list of 32-byte keys
+    bitmap = ctx.verify(tid, key_idx, sigs, msgs)  # -> bytes, bit i = signature i accepted
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterable, List, Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libcbft_hipcrypto.so")
+
+CBFT_NO_KEY_TABLE = 0xFFFFFFFF
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+# (name, restype, argtypes) for every symbol include/cbft_hipcrypto.h declares
+ABI = [
+    ("cbft_device_count", ctypes.c_int, []),
+    ("cbft_strerror", ctypes.c_char_p, [ctypes.c_int]),
+    ("cbft_last_error", ctypes.c_char_p, []),
+    ("cbft_open", ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_size_t]),
+    ("cbft_close", None, [ctypes.c_void_p]),
+    ("cbft_ed25519_load_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, _u32p]),
+    ("cbft_ed25519_unload_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
+    ("cbft_ed25519_verify_batch", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    ("cbft_ed25519_verify_batch_pk", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_size_t, ctypes.c_void_p]),
+    ("cbft_ed25519_verify_batch_device", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
+    ("cbft_sync", ctypes.c_int, [ctypes.c_void_p]),
+    ("cbft_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    ("cbft_stage_times_ms", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
+]
+
+_lib = None
+
+
+class CbftError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        lib = load_library()
+        detail = lib.cbft_last_error().decode(errors="replace")
+        super().__init__(f"{what}: {lib.cbft_strerror(code).decode()} ({code}) {detail}")
+        self.code = code
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load the HIP library (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: run `make lib` (or __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    for name, res, args in ABI:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise CbftError(rc, what)
+
+
+def pack_messages(msgs: Sequence[bytes]):
+    """Concatenate messages into (blob, offsets u64, lengths u32) as the ABI expects."""
+    lens = np.fromiter((len(m) for m in msgs), dtype=np.uint32, count=len(msgs))
+    offs = np.zeros(len(msgs), dtype=np.uint64)
+    if len(msgs) > 1:
+        np.cumsum(lens[:-1], out=offs[1:])
+    blob = b"".join(msgs)
+    return np.frombuffer(blob, dtype=np.uint8) if blob else np.zeros(1, dtype=np.uint8), offs, lens
+
+
+def bitmap_to_bools(bitmap: bytes, n: int) -> np.ndarray:
+    return np.unpackbits(np.frombuffer(bitmap, dtype=np.uint8), bitorder="little")[:n].astype(bool)
+
+
+def _ptr(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+class Context:
+    """One GPU context (cbft_open / cbft_close)."""
+
+    def __init__(self, device: int = 0, max_batch: int = 0):
+        self.lib = load_library()
+        self.handle = ctypes.c_void_p()
+        _check(self.lib.cbft_open(ctypes.byref(self.handle), device, max_batch), f"cbft_open(device={device})")
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            self.lib.cbft_close(self.handle)
+            self.handle = ctypes.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ keys
+    def load_keys(self, pks: Iterable[bytes] | np.ndarray) -> int:
+        arr = _as_rows(pks, 32)
+        tid = ctypes.c_uint32()
+        _check(self.lib.cbft_ed25519_load_keys(self.handle, _ptr(arr), arr.shape[0], ctypes.byref(tid)),
+               "cbft_ed25519_load_keys")
+        return tid.value
+
+    def unload_keys(self, tid: int):
+        _check(self.lib.cbft_ed25519_unload_keys(self.handle, tid), "cbft_ed25519_unload_keys")
+
+    # ------------------------------------------------------------------ verify
+    def verify(self, tid: int, key_idx, sigs, msgs: Sequence[bytes]) -> bytes:
+        n = len(msgs)
+        kidx = np.ascontiguousarray(np.asarray(key_idx, dtype=np.uint32))
+        s = _as_rows(sigs, 64)
+        assert kidx.shape[0] == n and s.shape[0] == n
+        blob, offs, lens = pack_messages(msgs)
+        out = np.zeros(max(1, (n + 7) // 8), dtype=np.uint8)
+        _check(self.lib.cbft_ed25519_verify_batch(self.handle, tid, _ptr(kidx), _ptr(s), _ptr(blob), _ptr(offs),
+                                                   _ptr(lens), n, _ptr(out)), "cbft_ed25519_verify_batch")
+        return out.tobytes()[: (n + 7) // 8]
+
+    def verify_pk(self, pks, sigs, msgs: Sequence[bytes]) -> bytes:
+        n = len(msgs)
+        p = _as_rows(pks, 32)
+        s = _as_rows(sigs, 64)
+        assert p.shape[0] == n and s.shape[0] == n
+        blob, offs, lens = pack_messages(msgs)
+        out = np.zeros(max(1, (n + 7) // 8), dtype=np.uint8)
+        _check(self.lib.cbft_ed25519_verify_batch_pk(self.handle, _ptr(p), _ptr(s), _ptr(blob), _ptr(offs),
+                                                      _ptr(lens), n, _ptr(out)), "cbft_ed25519_verify_batch_pk")
+        return out.tobytes()[: (n + 7) // 8]
+
+    def verify_device(self, tid: int, d_pk: int, d_key_idx: int, d_sig: int, d_msg: int, d_off: int, d_len: int,
+                      n: int, d_verdict_words: int, stream: int = 0):
+        """All arguments are raw device addresses (e.g. torch tensor .data_ptr())."""
+        _check(self.lib.cbft_ed25519_verify_batch_device(
+            self.handle, tid, ctypes.c_void_p(d_pk), ctypes.c_void_p(d_key_idx), ctypes.c_void_p(d_sig),
+            ctypes.c_void_p(d_msg), ctypes.c_void_p(d_off), ctypes.c_void_p(d_len), n,
+            ctypes.c_void_p(d_verdict_words), ctypes.c_void_p(stream)), "cbft_ed25519_verify_batch_device")
+
+    def sync(self):
+        _check(self.lib.cbft_sync(self.handle), "cbft_sync")
+
+    def set_profiling(self, on: bool = True):
+        _check(self.lib.cbft_set_profiling(self.handle, 1 if on else 0), "cbft_set_profiling")
+
+    def stage_times_ms(self):
+        """{hash, ladder, finish} kernel times (ms) of the last verify (needs set_profiling)."""
+        out = (ctypes.c_float * 3)()
+        _check(self.lib.cbft_stage_times_ms(self.handle, out, 3), "cbft_stage_times_ms")
+        return {"hash": out[0], "ladder": out[1], "finish": out[2]}
+
+
+def _as_rows(x, width: int) -> np.ndarray:
+    if isinstance(x, np.ndarray):
+        a = np.ascontiguousarray(x, dtype=np.uint8).reshape(-1, width)
+    else:
+        rows = list(x)
+        for r in rows:
+            if len(r) != width:
+                raise ValueError(f"expected {width}-byte items, got {len(r)}")
+        a = np.frombuffer(b"".join(rows), dtype=np.uint8).reshape(-1, width) if rows else np.zeros((0, width),
+                                                                                                   np.uint8)
+    return np.ascontiguousarray(a)
+
+
+def device_count() -> int:
+    return load_library().cbft_device_count()

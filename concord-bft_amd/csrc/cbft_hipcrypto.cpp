@@ -1,0 +1,362 @@
+// libcbft_hipcrypto: host side of the C ABI declared in include/cbft_hipcrypto.h.
+//
+// One context = one GPU + one HIP stream + grow-on-demand device work buffers + the loaded key
+// tables.  Calls on a context are serialised by a mutex (the reference calls verifiers
+// concurrently from its RequestThreadPool under a shared_lock, SigManager.cpp:203; a caller
+// that wants concurrency opens one context per thread or per GPU).
+#include "cbft_hipcrypto.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <unordered_map>
+#include <vector>
+
+#include "ed25519_verify.h"
+
+namespace {
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  // (re)allocate to at least `bytes`; contents are not preserved
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) {
+      (void)hipDeviceSynchronize();  // an earlier async launch may still read the old buffer
+      (void)hipFree(p);
+    }
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 4096);
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    cap = want;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+struct KeyTable {
+  uint32_t nkeys = 0;
+  DevBuf pk, tbl, aok;
+};
+
+}  // namespace
+
+struct cbft_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  DevBuf base_table;
+  std::unordered_map<uint32_t, KeyTable> tables;
+  uint32_t next_table_id = 1;
+  // per-batch work buffers
+  DevBuf h, flags, xyz, verdicts;
+  DevBuf sig, msg, off, len, kidx, pk, ps_tbl, ps_aok;
+  std::vector<uint64_t> host_verdicts;
+  // profiling: events around K1 (hash), K3 (ladder), K4 (finish) of the last verify
+  bool profiling = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool ev_valid = false;
+};
+
+// Last failure of this thread, for cbft_last_error() (diagnostics only).
+static thread_local char g_last_error[256];
+
+static int fail(hipError_t e, const char* what, int line) {
+  snprintf(g_last_error, sizeof g_last_error, "%s failed at cbft_hipcrypto.cpp:%d: %s (%d)", what, line,
+           hipGetErrorString(e), (int)e);
+  (void)hipGetLastError();
+  return e == hipErrorOutOfMemory ? CBFT_ENOMEM : CBFT_EIO;
+}
+
+#define CBFT_HIP(expr)                                          \
+  do {                                                          \
+    hipError_t _e = (expr);                                     \
+    if (_e != hipSuccess) return fail(_e, #expr, __LINE__);     \
+  } while (0)
+
+static int reserve_work(cbft_ctx* c, size_t n) {
+  CBFT_HIP(c->h.reserve(n * 8 * sizeof(uint32_t)));
+  CBFT_HIP(c->flags.reserve(n));
+  CBFT_HIP(c->xyz.reserve(n * 27 * sizeof(uint32_t)));
+  CBFT_HIP(c->verdicts.reserve(((n + 63) / 64) * sizeof(uint64_t)));
+  return CBFT_OK;
+}
+
+extern "C" {
+
+const char* cbft_last_error(void) { return g_last_error; }
+
+int cbft_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return CBFT_ENODEV;
+  }
+  return n;
+}
+
+const char* cbft_strerror(int code) {
+  switch (code) {
+    case CBFT_OK:
+      return "ok";
+    case CBFT_EINVAL:
+      return "invalid argument";
+    case CBFT_ENOMEM:
+      return "out of memory";
+    case CBFT_ENODEV:
+      return "no such GPU / HIP runtime unavailable";
+    case CBFT_EIO:
+      return "HIP launch or copy failed";
+    case CBFT_E2BIG:
+      return "batch too large";
+    default:
+      return "unknown error";
+  }
+}
+
+int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
+  if (!out) return CBFT_EINVAL;
+  *out = nullptr;
+  int ndev = cbft_device_count();
+  if (ndev < 0) return ndev;
+  if (device < 0 || device >= ndev) return CBFT_ENODEV;
+  cbft_ctx* c = new (std::nothrow) cbft_ctx();
+  if (!c) return CBFT_ENOMEM;
+  c->device = device;
+  int rc = CBFT_OK;
+  do {
+    if (hipSetDevice(device) != hipSuccess) {
+      rc = CBFT_ENODEV;
+      break;
+    }
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+      rc = CBFT_EIO;
+      break;
+    }
+    if (c->base_table.reserve(cbft_ed25519_base_table_words() * sizeof(uint32_t)) != hipSuccess) {
+      rc = CBFT_ENOMEM;
+      break;
+    }
+    if (cbft_ed25519_build_base_table(c->base_table.as<uint32_t>(), c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess) {
+      rc = CBFT_EIO;
+      break;
+    }
+    if (max_batch) rc = reserve_work(c, max_batch);
+  } while (0);
+  if (rc != CBFT_OK) {
+    (void)hipGetLastError();
+    cbft_close(c);
+    return rc;
+  }
+  *out = c;
+  return CBFT_OK;
+}
+
+void cbft_close(cbft_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (auto& kv : c->tables) {
+    kv.second.pk.release();
+    kv.second.tbl.release();
+    kv.second.aok.release();
+  }
+  for (DevBuf* b : {&c->base_table, &c->h, &c->flags, &c->xyz, &c->verdicts, &c->sig, &c->msg, &c->off, &c->len,
+                    &c->kidx, &c->pk, &c->ps_tbl, &c->ps_aok})
+    b->release();
+  for (hipEvent_t& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+}
+
+int cbft_set_profiling(cbft_ctx* c, int enable) {
+  if (!c) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  CBFT_HIP(hipSetDevice(c->device));
+  if (enable && !c->ev[0])
+    for (hipEvent_t& e : c->ev) CBFT_HIP(hipEventCreate(&e));
+  c->profiling = enable != 0;
+  c->ev_valid = false;
+  return CBFT_OK;
+}
+
+int cbft_stage_times_ms(cbft_ctx* c, float* out, int nout) {
+  if (!c || !out || nout < 3) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (!c->ev_valid) return CBFT_EINVAL;
+  CBFT_HIP(hipSetDevice(c->device));
+  CBFT_HIP(hipEventSynchronize(c->ev[3]));
+  for (int k = 0; k < 3; k++) CBFT_HIP(hipEventElapsedTime(&out[k], c->ev[k], c->ev[k + 1]));
+  return CBFT_OK;
+}
+
+int cbft_sync(cbft_ctx* c) {
+  if (!c) return CBFT_EINVAL;
+  (void)hipSetDevice(c->device);
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  return CBFT_OK;
+}
+
+int cbft_ed25519_load_keys(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, uint32_t* out_id) {
+  if (!c || !out_id || (nkeys && !pk)) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  CBFT_HIP(hipSetDevice(c->device));
+  KeyTable kt;
+  kt.nkeys = nkeys;
+  const size_t n = std::max<uint32_t>(nkeys, 1);
+  CBFT_HIP(kt.pk.reserve(n * 32));
+  CBFT_HIP(kt.tbl.reserve(n * cbft_ed25519_table_words_per_unit() * sizeof(uint32_t)));
+  CBFT_HIP(kt.aok.reserve(n));
+  if (nkeys) {
+    CBFT_HIP(hipMemcpyAsync(kt.pk.p, pk, (size_t)nkeys * 32, hipMemcpyHostToDevice, c->stream));
+    CBFT_HIP(cbft_ed25519_launch_prep(kt.pk.as<uint8_t>(), nkeys, kt.tbl.as<uint32_t>(), kt.aok.as<uint8_t>(),
+                                      c->stream));
+    CBFT_HIP(hipStreamSynchronize(c->stream));
+  }
+  uint32_t id = c->next_table_id++;
+  if (id == CBFT_NO_KEY_TABLE) id = c->next_table_id++;
+  c->tables.emplace(id, std::move(kt));
+  *out_id = id;
+  return CBFT_OK;
+}
+
+int cbft_ed25519_unload_keys(cbft_ctx* c, uint32_t id) {
+  if (!c) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  auto it = c->tables.find(id);
+  if (it == c->tables.end()) return CBFT_EINVAL;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  it->second.pk.release();
+  it->second.tbl.release();
+  it->second.aok.release();
+  c->tables.erase(it);
+  return CBFT_OK;
+}
+
+// Launch the verify pipeline for a batch whose inputs are already on the device.
+static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, const uint32_t* d_kidx,
+                         const uint8_t* d_sig, const uint8_t* d_msg, const uint64_t* d_off, const uint32_t* d_len,
+                         size_t n, uint64_t* d_verdicts, hipStream_t s) {
+  int rc = reserve_work(c, n);
+  if (rc) return rc;
+  Ed25519Batch b{n, d_pk, d_kidx, d_sig, d_msg, d_off, d_len};
+  Ed25519Work w{};
+  w.base_table = c->base_table.as<uint32_t>();
+  w.h_soa = c->h.as<uint32_t>();
+  w.flags = c->flags.as<uint8_t>();
+  w.xyz_soa = c->xyz.as<uint32_t>();
+  w.verdict_words = d_verdicts;
+  if (table_id == CBFT_NO_KEY_TABLE) {
+    // per-signature keys: decode + precompute per signature
+    CBFT_HIP(c->ps_tbl.reserve(n * cbft_ed25519_table_words_per_unit() * sizeof(uint32_t)));
+    CBFT_HIP(c->ps_aok.reserve(n));
+    CBFT_HIP(cbft_ed25519_launch_prep(d_pk, n, c->ps_tbl.as<uint32_t>(), c->ps_aok.as<uint8_t>(), s));
+    b.key_idx = nullptr;
+    w.tbl = c->ps_tbl.as<uint32_t>();
+    w.aok = c->ps_aok.as<uint8_t>();
+  } else {
+    auto it = c->tables.find(table_id);
+    if (it == c->tables.end() || !d_kidx) return CBFT_EINVAL;
+    b.pk = it->second.pk.as<uint8_t>();
+    w.tbl = it->second.tbl.as<uint32_t>();
+    w.aok = it->second.aok.as<uint8_t>();
+  }
+  CBFT_HIP(cbft_ed25519_launch_verify(b, w, s, c->profiling ? c->ev : nullptr));
+  c->ev_valid = c->profiling;
+  return CBFT_OK;
+}
+
+static int verify_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const uint32_t* key_idx,
+                       const uint8_t* sig, const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
+                       size_t n, uint8_t* bitmap) {
+  if (!c || (n && (!sig || !msg_off || !msg_len || !bitmap))) return CBFT_EINVAL;
+  if (n == 0) return CBFT_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  CBFT_HIP(hipSetDevice(c->device));
+  // message blob extent
+  uint64_t blob = 0;
+  for (size_t i = 0; i < n; i++) blob = std::max<uint64_t>(blob, msg_off[i] + msg_len[i]);
+  if (blob && !msg_blob) return CBFT_EINVAL;
+  if (table_id != CBFT_NO_KEY_TABLE) {
+    auto it = c->tables.find(table_id);
+    if (it == c->tables.end() || !key_idx) return CBFT_EINVAL;
+    for (size_t i = 0; i < n; i++)
+      if (key_idx[i] >= it->second.nkeys) return CBFT_EINVAL;
+    CBFT_HIP(c->kidx.reserve(n * 4));
+    CBFT_HIP(hipMemcpyAsync(c->kidx.p, key_idx, n * 4, hipMemcpyHostToDevice, c->stream));
+  } else {
+    if (!pk) return CBFT_EINVAL;
+    CBFT_HIP(c->pk.reserve(n * 32));
+    CBFT_HIP(hipMemcpyAsync(c->pk.p, pk, n * 32, hipMemcpyHostToDevice, c->stream));
+  }
+  // size the work buffers first: the verdict buffer's address is taken below
+  int rc0 = reserve_work(c, n);
+  if (rc0) return rc0;
+  CBFT_HIP(c->sig.reserve(n * 64));
+  CBFT_HIP(c->msg.reserve(blob + 16));
+  CBFT_HIP(c->off.reserve(n * 8));
+  CBFT_HIP(c->len.reserve(n * 4));
+  CBFT_HIP(hipMemcpyAsync(c->sig.p, sig, n * 64, hipMemcpyHostToDevice, c->stream));
+  if (blob) CBFT_HIP(hipMemcpyAsync(c->msg.p, msg_blob, blob, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(hipMemcpyAsync(c->off.p, msg_off, n * 8, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(hipMemcpyAsync(c->len.p, msg_len, n * 4, hipMemcpyHostToDevice, c->stream));
+  int rc = launch_locked(c, table_id, c->pk.as<uint8_t>(), c->kidx.as<uint32_t>(), c->sig.as<uint8_t>(),
+                         c->msg.as<uint8_t>(), c->off.as<uint64_t>(), c->len.as<uint32_t>(), n,
+                         c->verdicts.as<uint64_t>(), c->stream);
+  if (rc) return rc;
+  const size_t nw = (n + 63) / 64;
+  c->host_verdicts.resize(nw);
+  CBFT_HIP(hipMemcpyAsync(c->host_verdicts.data(), c->verdicts.p, nw * 8, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  const size_t nbytes = (n + 7) / 8;
+  std::memcpy(bitmap, c->host_verdicts.data(), nbytes);  // little-endian host: words == bytes
+  if (n % 8) bitmap[nbytes - 1] &= (uint8_t)((1u << (n % 8)) - 1);
+  return CBFT_OK;
+}
+
+int cbft_ed25519_verify_batch(cbft_ctx* c, uint32_t table_id, const uint32_t* key_idx, const uint8_t* sig,
+                              const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
+                              uint8_t* bitmap) {
+  if (table_id == CBFT_NO_KEY_TABLE) return CBFT_EINVAL;
+  return verify_host(c, table_id, nullptr, key_idx, sig, msg_blob, msg_off, msg_len, n, bitmap);
+}
+
+int cbft_ed25519_verify_batch_pk(cbft_ctx* c, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_blob,
+                                 const uint64_t* msg_off, const uint32_t* msg_len, size_t n, uint8_t* bitmap) {
+  return verify_host(c, CBFT_NO_KEY_TABLE, pk, nullptr, sig, msg_blob, msg_off, msg_len, n, bitmap);
+}
+
+int cbft_ed25519_verify_batch_device(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, const uint32_t* d_key_idx,
+                                     const uint8_t* d_sig, const uint8_t* d_msg, const uint64_t* d_off,
+                                     const uint32_t* d_len, size_t n, uint64_t* d_verdicts, void* stream) {
+  if (!c || (n && (!d_sig || !d_off || !d_len || !d_verdicts))) return CBFT_EINVAL;
+  if (table_id == CBFT_NO_KEY_TABLE && n && !d_pk) return CBFT_EINVAL;
+  if (n == 0) return CBFT_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  CBFT_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  return launch_locked(c, table_id, d_pk, d_key_idx, d_sig, d_msg, d_off, d_len, n, d_verdicts, s);
+}
+
+}  // extern "C"

@@ -1,0 +1,296 @@
+// GF(2^255 - 19) arithmetic for gfx950, one field element per lane.
+//
+// Representation ("fe"): 9 unsigned 32-bit limbs in radix 2^29 (261 bits, redundant).
+//   value = sum_i v[i] * 2^(29 i)   (mod p),   2^261 == 64*19 = 1216 (mod p)
+//
+// Why radix 2^29 x 9: the only wide multiplier on the CDNA4 VALU is v_mad_u64_u32
+// (32x32+64 -> 64), measured on MI355X at half the v_add_u32 issue rate
+// (tools/microbench/intrate.hip; 24-bit mads and FP64 FMA are no faster).  With 29-bit
+// limbs a whole product column (<= 9 products of <= 2^60.003) plus carry-in fits in one
+// 64-bit accumulator, so every partial product is exactly ONE v_mad_u64_u32 with no carry
+// chain; 81 mads + 9 fold mads per multiply, 45 + 9 per square.  Two bits of headroom let
+// a lazy sum of two reduced elements feed a multiply directly.
+//
+// Bounds (checked in DESIGN.md §fe):
+//   "reduced"  : every limb < 2^29 + 2^17        (outputs of mul/sq/carry/sub)
+//   "lazy"     : every limb < 2^30 + 2^18        (sum of two reduced)
+//   mul/sq inputs: each operand reduced or lazy.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define FE_LIMBS 9
+#define FE_MASK 0x1fffffffu
+
+struct fe {
+  uint32_t v[FE_LIMBS];
+};
+
+#define FE_INLINE __device__ __forceinline__
+
+FE_INLINE uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
+  return (uint64_t)a * (uint64_t)b + c;  // -> v_mad_u64_u32
+}
+
+FE_INLINE void fe_0(fe& r) {
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; i++) r.v[i] = 0;
+}
+FE_INLINE void fe_1(fe& r) {
+  fe_0(r);
+  r.v[0] = 1;
+}
+FE_INLINE void fe_copy(fe& r, const fe& a) {
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; i++) r.v[i] = a.v[i];
+}
+
+// lazy add: reduced + reduced -> lazy
+FE_INLINE void fe_add(fe& r, const fe& a, const fe& b) {
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; i++) r.v[i] = a.v[i] + b.v[i];
+}
+
+// carry pass on 32-bit limbs (< 2^32 - 8) -> reduced
+FE_INLINE void fe_carry(fe& r) {
+  uint32_t c;
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS - 1; i++) {
+    c = r.v[i] >> 29;
+    r.v[i] &= FE_MASK;
+    r.v[i + 1] += c;
+  }
+  c = r.v[8] >> 29;
+  r.v[8] &= FE_MASK;
+  r.v[0] += c * 1216u;
+}
+
+// r = a - b (mod p), b reduced or lazy, a reduced or lazy -> reduced.
+// Adds 256p = 2^263 - 4864, whose radix-2^29 digits are (2^31-4864, 2^31-4, ..., 2^31-4),
+// every one >= any lazy limb, so no limb underflows.
+FE_INLINE void fe_sub(fe& r, const fe& a, const fe& b) {
+  r.v[0] = a.v[0] + (0x80000000u - 4864u) - b.v[0];
+#pragma unroll
+  for (int i = 1; i < FE_LIMBS; i++) r.v[i] = a.v[i] + (0x80000000u - 4u) - b.v[i];
+  fe_carry(r);
+}
+
+// r = -a
+FE_INLINE void fe_neg(fe& r, const fe& a) {
+  r.v[0] = (0x80000000u - 4864u) - a.v[0];
+#pragma unroll
+  for (int i = 1; i < FE_LIMBS; i++) r.v[i] = (0x80000000u - 4u) - a.v[i];
+  fe_carry(r);
+}
+
+// Column-sum multiply core.  col(k) = sum_{i+j=k} a_i b_j (as mads into a 64-bit acc).
+//   High columns k = 9..16 are computed first and carried into 29-bit digits h0..h7 and an
+//   unbounded top h8 (weight 2^261 * 2^(29(k-9)) == 1216 * 2^(29(k-9))); then the low
+//   columns start their mad chains from (carry + 1216 h_k); the final carry (weight 2^261)
+//   wraps with *1216 into limb 0.  Live state: operands + h[9] + one accumulator.
+#define FE_COLUMN(acc, k, TERM)                                  \
+  _Pragma("unroll") for (int i = 0; i < FE_LIMBS; i++) {         \
+    int j = (k) - i;                                             \
+    if (j >= 0 && j < FE_LIMBS) { TERM }                         \
+  }
+
+FE_INLINE void fe_mul(fe& r, const fe& a, const fe& b) {
+  fe o;  // r may alias a or b
+  uint32_t h[9];
+  uint64_t t = 0;
+#pragma unroll
+  for (int k = 9; k < 17; k++) {
+    uint64_t acc = t;
+    FE_COLUMN(acc, k, acc = mad64(a.v[i], b.v[j], acc);)
+    h[k - 9] = (uint32_t)acc & FE_MASK;
+    t = acc >> 29;
+  }
+  h[8] = (uint32_t)t;  // < 2^32 (c16 <= 2^60.003 + carry)
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    acc = mad64(h[k], 1216u, acc);
+    FE_COLUMN(acc, k, acc = mad64(a.v[i], b.v[j], acc);)
+    o.v[k] = (uint32_t)acc & FE_MASK;
+    acc >>= 29;
+  }
+  // acc < 2^34.2: carry of weight 2^261 == 1216
+  uint64_t w = acc * 1216ull + (uint64_t)o.v[0];
+  o.v[0] = (uint32_t)w & FE_MASK;
+  o.v[1] += (uint32_t)(w >> 29);
+  r = o;
+}
+
+FE_INLINE void fe_sq(fe& r, const fe& a) {
+  fe o;  // r may alias a or b
+  uint32_t a2[FE_LIMBS];
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; i++) a2[i] = a.v[i] << 1;
+  uint32_t h[9];
+  uint64_t t = 0;
+#pragma unroll
+  for (int k = 9; k < 17; k++) {
+    uint64_t acc = t;
+    FE_COLUMN(acc, k, if (j > i) acc = mad64(a2[i], a.v[j], acc);)
+    if ((k & 1) == 0) acc = mad64(a.v[k >> 1], a.v[k >> 1], acc);
+    h[k - 9] = (uint32_t)acc & FE_MASK;
+    t = acc >> 29;
+  }
+  h[8] = (uint32_t)t;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 9; k++) {
+    acc = mad64(h[k], 1216u, acc);
+    FE_COLUMN(acc, k, if (j > i) acc = mad64(a2[i], a.v[j], acc);)
+    if ((k & 1) == 0) acc = mad64(a.v[k >> 1], a.v[k >> 1], acc);
+    o.v[k] = (uint32_t)acc & FE_MASK;
+    acc >>= 29;
+  }
+  uint64_t w = acc * 1216ull + (uint64_t)o.v[0];
+  o.v[0] = (uint32_t)w & FE_MASK;
+  o.v[1] += (uint32_t)(w >> 29);
+  r = o;
+}
+
+// r = a * small (small < 2^16), a reduced/lazy
+FE_INLINE void fe_mul_small(fe& r, const fe& a, uint32_t s) {
+  uint64_t acc = 0;
+  uint32_t t[FE_LIMBS];
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; i++) {
+    acc = mad64(a.v[i], s, acc);
+    t[i] = (uint32_t)acc & FE_MASK;
+    acc >>= 29;
+  }
+  uint64_t w = mad64((uint32_t)acc, 1216u, (uint64_t)t[0]);
+  t[0] = (uint32_t)w & FE_MASK;
+  t[1] += (uint32_t)(w >> 29);
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; i++) r.v[i] = t[i];
+}
+
+// r = a^(2^n) (n >= 1); a runtime (not unrolled) loop keeps code size to one square body
+FE_INLINE void fe_sqn(fe& r, const fe& a, int n) {
+  fe_sq(r, a);
+#pragma nounroll
+  for (int i = 1; i < n; i++) fe_sq(r, r);
+}
+
+// Canonical 8x32-bit little-endian words of a (fully reduced into [0, p)).
+FE_INLINE void fe_to_words(uint32_t* w, const fe& a) {
+  fe t;
+  fe_copy(t, a);
+  fe_carry(t);
+  fe_carry(t);  // every limb < 2^29 now (limb0 < 2^29 + 2^14 after 1st, < 2^29 after 2nd w.h.p.)
+  // fold bits >= 255 (limb 8 bits >= 23) twice
+#pragma unroll
+  for (int rep = 0; rep < 2; rep++) {
+    uint32_t c = t.v[8] >> 23;
+    t.v[8] &= 0x7fffffu;
+    t.v[0] += 19u * c;
+#pragma unroll
+    for (int i = 0; i < FE_LIMBS - 1; i++) {
+      uint32_t cc = t.v[i] >> 29;
+      t.v[i] &= FE_MASK;
+      t.v[i + 1] += cc;
+    }
+  }
+  // now 0 <= t < 2^255 + tiny, t < 2p.  If t + 19 >= 2^255 then t >= p: t = t + 19 - 2^255.
+  uint32_t u[FE_LIMBS];
+  uint32_t c = 19;
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; i++) {
+    uint32_t s = t.v[i] + c;
+    u[i] = s & FE_MASK;
+    c = s >> 29;
+  }
+  bool ge = (u[8] >> 23) & 1u;
+  u[8] &= 0x7fffffu;
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; i++) t.v[i] = ge ? u[i] : t.v[i];
+  // pack radix 2^29 -> 2^32
+  w[0] = t.v[0] | (t.v[1] << 29);
+  w[1] = (t.v[1] >> 3) | (t.v[2] << 26);
+  w[2] = (t.v[2] >> 6) | (t.v[3] << 23);
+  w[3] = (t.v[3] >> 9) | (t.v[4] << 20);
+  w[4] = (t.v[4] >> 12) | (t.v[5] << 17);
+  w[5] = (t.v[5] >> 15) | (t.v[6] << 14);
+  w[6] = (t.v[6] >> 18) | (t.v[7] << 11);
+  w[7] = (t.v[7] >> 21) | (t.v[8] << 8);
+}
+
+// Load 255 low bits of a little-endian 8-word integer (bit 255 ignored, value NOT reduced
+// mod p: a non-canonical y >= p is accepted exactly as OpenSSL's fe_frombytes does).
+FE_INLINE void fe_from_words(fe& r, const uint32_t* w) {
+  r.v[0] = w[0] & FE_MASK;
+  r.v[1] = ((w[0] >> 29) | (w[1] << 3)) & FE_MASK;
+  r.v[2] = ((w[1] >> 26) | (w[2] << 6)) & FE_MASK;
+  r.v[3] = ((w[2] >> 23) | (w[3] << 9)) & FE_MASK;
+  r.v[4] = ((w[3] >> 20) | (w[4] << 12)) & FE_MASK;
+  r.v[5] = ((w[4] >> 17) | (w[5] << 15)) & FE_MASK;
+  r.v[6] = ((w[5] >> 14) | (w[6] << 18)) & FE_MASK;
+  r.v[7] = ((w[6] >> 11) | (w[7] << 21)) & FE_MASK;
+  r.v[8] = (w[7] >> 8) & 0x7fffffu;
+}
+
+FE_INLINE bool fe_iszero(const fe& a) {
+  uint32_t w[8];
+  fe_to_words(w, a);
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) o |= w[i];
+  return o == 0;
+}
+
+FE_INLINE uint32_t fe_isnegative(const fe& a) {
+  uint32_t w[8];
+  fe_to_words(w, a);
+  return w[0] & 1u;
+}
+
+FE_INLINE void fe_cmov(fe& r, const fe& a, bool c) {
+#pragma unroll
+  for (int i = 0; i < FE_LIMBS; i++) r.v[i] = c ? a.v[i] : r.v[i];
+}
+
+// z^(2^250 - 1) and z^11: the shared prefix of inversion (p-2 = 2^255 - 21) and of the
+// square-root power (p-5)/8 = 2^252 - 3.  Chain: 11 multiplies + 254 squarings in total.
+FE_INLINE void fe_pow_2_250_1(fe& z250, fe& z11, const fe& z) {
+  fe z2, z9, t0, t1, t2;
+  fe_sq(z2, z);             // 2
+  fe_sqn(t0, z2, 2);        // 8
+  fe_mul(z9, t0, z);        // 9
+  fe_mul(z11, z9, z2);      // 11
+  fe_sq(t0, z11);           // 22
+  fe_mul(t0, t0, z9);       // 31 = 2^5 - 1
+  fe_sqn(t1, t0, 5);
+  fe_mul(t0, t1, t0);       // 2^10 - 1
+  fe_sqn(t1, t0, 10);
+  fe_mul(t1, t1, t0);       // 2^20 - 1
+  fe_sqn(t2, t1, 20);
+  fe_mul(t1, t2, t1);       // 2^40 - 1
+  fe_sqn(t1, t1, 10);
+  fe_mul(t0, t1, t0);       // 2^50 - 1
+  fe_sqn(t1, t0, 50);
+  fe_mul(t1, t1, t0);       // 2^100 - 1
+  fe_sqn(t2, t1, 100);
+  fe_mul(t1, t2, t1);       // 2^200 - 1
+  fe_sqn(t1, t1, 50);
+  fe_mul(z250, t1, t0);     // 2^250 - 1
+}
+
+// r = z^(p-2) = z^(2^255 - 21)
+FE_INLINE void fe_invert(fe& r, const fe& z) {
+  fe z250, z11;
+  fe_pow_2_250_1(z250, z11, z);
+  fe_sqn(z250, z250, 5);    // 2^255 - 32
+  fe_mul(r, z250, z11);     // 2^255 - 21
+}
+
+// r = z^((p-5)/8) = z^(2^252 - 3)
+FE_INLINE void fe_pow22523(fe& r, const fe& z) {
+  fe z250, z11;
+  fe_pow_2_250_1(z250, z11, z);
+  fe_sqn(z250, z250, 2);    // 2^252 - 4
+  fe_mul(r, z250, z);       // 2^252 - 3
+}

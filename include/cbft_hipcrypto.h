@@ -1,0 +1,113 @@
+/*
+ * libcbft_hipcrypto — C ABI of the MI355X batch signature-verification engine for concord-bft.
+ *
+ * This is the drop-in boundary between the reference's crypto plugin interfaces and the GPU:
+ *
+ *   concord::util::crypto::IVerifier::verify        util/include/crypto_utils.hpp:41-47
+ *   SigManager::verifySig (per-principal verify)     bftengine/src/bftengine/SigManager.cpp:197-238
+ *   serial verify loops it replaces with one batch:  PrePrepareMsg.cpp:116-125,
+ *                                                    PreProcessor.cpp:557-590,
+ *                                                    PreProcessBatchRequestMsg.cpp:62-75,
+ *                                                    PreProcessResultMsg.cpp:57-99
+ *   OpenSSL verify idiom whose verdicts it matches:  util/src/openssl_crypto.cpp:229-253
+ *     (EVP_DigestVerify with EVP_PKEY_ED25519, OpenSSL 3.0.2; accept only on == 1)
+ *
+ * Conventions:
+ *   - every function returns 0 (CBFT_OK) or a negative errno-style code; no C++ exception ever
+ *     crosses this boundary;
+ *   - the caller owns every buffer; host-pointer entry points are blocking;
+ *   - a context is bound to one GPU; calls on one context are serialised internally
+ *     (thread-safe), distinct contexts run concurrently;
+ *   - a verdict never depends on batch composition (each signature is verified independently);
+ *   - a bad signature is a 0 verdict bit, never an error code.
+ * All integers are little-endian; keys are 32 raw bytes (RFC 8032 encoding), signatures are
+ * 64 raw bytes R || S.
+ */
+#ifndef CBFT_HIPCRYPTO_H
+#define CBFT_HIPCRYPTO_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CBFT_OK 0
+#define CBFT_EINVAL (-22) /* bad argument (null pointer with n > 0, unknown table id, ...) */
+#define CBFT_ENOMEM (-12) /* device or host allocation failed */
+#define CBFT_ENODEV (-19) /* no such GPU / HIP runtime unavailable */
+#define CBFT_EIO (-5)     /* a HIP launch or copy failed */
+#define CBFT_E2BIG (-7)   /* batch larger than the context was opened for */
+
+#define CBFT_ED25519_PUBLIC_KEY_BYTES 32
+#define CBFT_ED25519_SIGNATURE_BYTES 64
+
+typedef struct cbft_ctx cbft_ctx;
+
+/* Number of visible GPUs (>= 0), or a negative code. */
+int cbft_device_count(void);
+
+/* Human-readable text for a return code. */
+const char* cbft_strerror(int code);
+
+/* Detail of the calling thread's last CBFT_EIO/CBFT_ENOMEM failure (HIP call + error), or "". */
+const char* cbft_last_error(void);
+
+/* Open a context on GPU `device` for batches of up to `max_batch` signatures (the working
+ * buffers grow on demand above that; max_batch only pre-sizes them). */
+int cbft_open(cbft_ctx** out, int device, size_t max_batch);
+void cbft_close(cbft_ctx* ctx);
+
+/* ---------------------------------------------------------------- Ed25519 ----------------
+ * Verdict semantics are exactly OpenSSL 3.0.2 EVP_DigestVerify(ED25519) == 1:
+ * S < L, A decoded without a canonical-y check, cofactorless [S]B - [h]A, R compared bytewise
+ * after re-encoding (so non-canonical R is rejected, small-order A is not).
+ */
+
+/* Upload and pre-process a key table (decoding and per-key precomputation run once here, like
+ * SigManager's one-verifier-per-key cache, SigManager.cpp:139-150).  A key that does not
+ * decode is accepted into the table; every signature under it verifies false. */
+int cbft_ed25519_load_keys(cbft_ctx* ctx, const uint8_t* pk /* nkeys x 32 */, uint32_t nkeys,
+                           uint32_t* out_key_table_id);
+int cbft_ed25519_unload_keys(cbft_ctx* ctx, uint32_t key_table_id);
+
+/* Verify n signatures against keys of a loaded table.
+ *   key_idx[i]   : index of signature i's key in the table (< nkeys)
+ *   sig          : n x 64 bytes
+ *   msg_blob     : all messages; message i = msg_blob[msg_off[i] .. msg_off[i] + msg_len[i])
+ *   verdict_bitmap: ceil(n/8) bytes, bit (i % 8) of byte i/8 = 1 iff signature i verifies
+ * Bits beyond n in the last byte are written as 0. */
+int cbft_ed25519_verify_batch(cbft_ctx* ctx, uint32_t key_table_id, const uint32_t* key_idx, const uint8_t* sig,
+                              const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
+                              uint8_t* verdict_bitmap);
+
+/* Same, with one raw 32-byte key per signature (pk = n x 32 bytes); the key is decoded per
+ * signature inside the batch. */
+int cbft_ed25519_verify_batch_pk(cbft_ctx* ctx, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_blob,
+                                 const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
+                                 uint8_t* verdict_bitmap);
+
+/* Device-resident variant: every pointer is device memory on the context's GPU, the call is
+ * asynchronous on `stream` (a hipStream_t; NULL = the context's own stream) and writes
+ * ceil(n/64) 64-bit verdict words (bit i % 64 of word i / 64).  key_table_id selects a loaded
+ * table (then key_idx indexes it) or is CBFT_NO_KEY_TABLE (then d_pk holds n raw keys).
+ * Use cbft_sync() (or the stream) before reading the verdicts. */
+#define CBFT_NO_KEY_TABLE 0xffffffffu
+int cbft_ed25519_verify_batch_device(cbft_ctx* ctx, uint32_t key_table_id, const uint8_t* d_pk,
+                                     const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg_blob,
+                                     const uint64_t* d_msg_off, const uint32_t* d_msg_len, size_t n,
+                                     uint64_t* d_verdict_words, void* stream);
+int cbft_sync(cbft_ctx* ctx);
+
+/* Instrumentation: when enabled, each verify records HIP events on its stream around its
+ * three kernels; cbft_stage_times_ms() then returns (waiting for them) the last verify's
+ * {hash, ladder, finish} kernel times in ms into out[0..2] (nout >= 3). */
+int cbft_set_profiling(cbft_ctx* ctx, int enable);
+int cbft_stage_times_ms(cbft_ctx* ctx, float* out, int nout);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* CBFT_HIPCRYPTO_H */

@@ -1,0 +1,143 @@
+"""GPU parity tests: libcbft_hipcrypto (HIP, gfx950) against the golden OpenSSL verdicts, the
+plain-C oracle and the host OpenSSL, through the C ABI.  Bit-exact verdicts are the bar."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import cbft_hipcrypto as cb
+from golden_io import load_ed25519_vectors
+import workload as sigsets
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = cb.Context(device=0, max_batch=1 << 16)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return load_ed25519_vectors()
+
+
+def _bools(bitmap, n):
+    return cb.bitmap_to_bools(bitmap, n)
+
+
+def test_golden_per_signature_keys(ctx, golden):
+    n = len(golden)
+    got = _bools(ctx.verify_pk([v.pk for v in golden], [v.sig for v in golden], [v.msg for v in golden]), n)
+    exp = np.array([bool(v.verdict) for v in golden])
+    bad = np.nonzero(got != exp)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first: {[(int(i), golden[i].cls) for i in bad[:10]]}"
+
+
+def test_golden_key_table(ctx, golden):
+    keys = sorted({v.pk for v in golden})
+    index = {k: i for i, k in enumerate(keys)}
+    tid = ctx.load_keys(keys)
+    try:
+        n = len(golden)
+        got = _bools(ctx.verify(tid, [index[v.pk] for v in golden], [v.sig for v in golden],
+                                [v.msg for v in golden]), n)
+        exp = np.array([bool(v.verdict) for v in golden])
+        assert np.array_equal(got, exp)
+    finally:
+        ctx.unload_keys(tid)
+
+
+@pytest.mark.parametrize("n", [1, 7, 63, 64, 65, 200, 1000])
+def test_ragged_batch_sizes(ctx, golden, n):
+    vs = [golden[i % len(golden)] for i in range(n)]
+    bm = ctx.verify_pk([v.pk for v in vs], [v.sig for v in vs], [v.msg for v in vs])
+    assert len(bm) == (n + 7) // 8
+    got = _bools(bm, n)
+    assert np.array_equal(got, np.array([bool(v.verdict) for v in vs]))
+    if n % 8:
+        assert bm[-1] >> (n % 8) == 0  # bits past n are zero
+
+
+def test_empty_batch(ctx):
+    assert ctx.verify_pk([], [], []) == b""
+
+
+def test_verdict_independent_of_batch_composition(ctx, golden):
+    vs = golden[:300]
+    full = _bools(ctx.verify_pk([v.pk for v in vs], [v.sig for v in vs], [v.msg for v in vs]), len(vs))
+    rev = _bools(ctx.verify_pk([v.pk for v in vs[::-1]], [v.sig for v in vs[::-1]], [v.msg for v in vs[::-1]]),
+                 len(vs))
+    assert np.array_equal(full, rev[::-1])
+
+
+def test_mixed_lengths_with_invalid_vs_openssl_and_oracle(ctx):
+    # config #3 shape (SigManager mixed batch), reduced: 64..4096 B, 10 % adversarially invalid
+    ss = sigsets.make_sigset(3000, nkeys=257, msg_len=(64, 4096), seed=7, invalid_frac=0.10)
+    tid = ctx.load_keys(ss.pk)
+    try:
+        got = _bools(ctx.verify(tid, ss.key_idx, ss.sig, ss.msgs()), ss.n)
+    finally:
+        ctx.unload_keys(tid)
+    assert np.array_equal(got, ss.expected)
+    assert (~ss.expected).sum() > 200
+    # the plain-C oracle agrees on a sample
+    lib = ctypes.CDLL(os.path.join(ROOT, "oracle", "libcbft_oracle.so"))
+    out = np.zeros(200, dtype=np.uint8)
+    p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+    lib.cbft_oracle_ed25519_verify_many(p(ss.pk), p(ss.key_idx), p(ss.sig), p(ss.blob), p(ss.off), p(ss.len),
+                                        ctypes.c_size_t(200), p(out))
+    assert np.array_equal(out.astype(bool), ss.expected[:200])
+
+
+def test_full_size_64k_key_table_and_per_sig(ctx):
+    # config #2 at full size: 64K sigs x 256 B, 4096 keys; every 97th signature corrupted
+    ss = sigsets.make_sigset(65536, nkeys=4096, msg_len=256, seed=11)
+    bad = np.arange(0, ss.n, 97)
+    ss.sig[bad, 40] ^= 0x01
+    ss.expected = sigsets.cpu_verify(ss).astype(bool)
+    assert (~ss.expected).sum() == bad.size
+    tid = ctx.load_keys(ss.pk)
+    try:
+        got = _bools(ctx.verify(tid, ss.key_idx, ss.sig, ss.msgs()), ss.n)
+    finally:
+        ctx.unload_keys(tid)
+    assert np.array_equal(got, ss.expected)
+    got2 = _bools(ctx.verify_pk(ss.per_sig_pk(), ss.sig, ss.msgs()), ss.n)
+    assert np.array_equal(got2, ss.expected)
+
+
+def test_invalid_arguments(ctx):
+    lib = cb.load_library()
+    assert lib.cbft_ed25519_unload_keys(ctx.handle, 123456) == -22
+    out = (ctypes.c_uint8 * 1)()
+    rc = lib.cbft_ed25519_verify_batch(ctx.handle, 999, None, None, None, None, None, 1, out)
+    assert rc == -22
+    tid = ctx.load_keys([bytes(32)])
+    try:
+        idx = np.array([5], dtype=np.uint32)  # out of range key index
+        sig = np.zeros(64, dtype=np.uint8)
+        off = np.zeros(1, dtype=np.uint64)
+        ln = np.zeros(1, dtype=np.uint32)
+        blob = np.zeros(1, dtype=np.uint8)
+        p = lambda a: a.ctypes.data_as(ctypes.c_void_p)  # noqa: E731
+        rc = lib.cbft_ed25519_verify_batch(ctx.handle, tid, p(idx), p(sig), p(blob), p(off), p(ln), 1, out)
+        assert rc == -22
+    finally:
+        ctx.unload_keys(tid)
+
+
+def test_fresh_context_without_presizing(golden):
+    # regression: buffers sized lazily on the first call (max_batch = 0)
+    with cb.Context(device=0) as c:
+        vs = golden[:256]
+        got = _bools(c.verify_pk([v.pk for v in vs], [v.sig for v in vs], [v.msg for v in vs]), len(vs))
+        assert np.array_equal(got, np.array([bool(v.verdict) for v in vs]))
+        vs = golden  # grow
+        got = _bools(c.verify_pk([v.pk for v in vs], [v.sig for v in vs], [v.msg for v in vs]), len(vs))
+        assert np.array_equal(got, np.array([bool(v.verdict) for v in vs]))

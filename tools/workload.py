@@ -1,0 +1,129 @@
+"""Synthetic signed-message sets for tests and bench (BASELINE.json configs), built with the
+host OpenSSL (tools/cpu_baseline/libcbft_cpu_openssl.so).  Key i's seed is
+SHA-512("cbft-key" || le32(i))[:32]; messages come from a seeded numpy PCG64.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # repo root
+CPU_SO = os.path.join(ROOT, "tools", "cpu_baseline", "libcbft_cpu_openssl.so")
+_cpu = None
+
+
+def cpu_lib():
+    global _cpu
+    if _cpu is None:
+        if not os.path.exists(CPU_SO):
+            raise RuntimeError(f"{CPU_SO} missing: run `make cpu`")
+        lib = ctypes.CDLL(CPU_SO)
+        vp = ctypes.c_void_p
+        lib.cbft_cpu_keys_new.restype = vp
+        lib.cbft_cpu_keys_new.argtypes = [vp, ctypes.c_uint32]
+        lib.cbft_cpu_keys_free.argtypes = [vp, ctypes.c_uint32]
+        lib.cbft_cpu_verify.argtypes = [vp, vp, vp, vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_int]
+        lib.cbft_cpu_pubkey.argtypes = [vp, vp]
+        lib.cbft_cpu_sign_many.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_int]
+        _cpu = lib
+    return _cpu
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def key_seeds(nkeys: int) -> np.ndarray:
+    return np.frombuffer(b"".join(hashlib.sha512(b"cbft-key" + i.to_bytes(4, "little")).digest()[:32]
+                                  for i in range(nkeys)), dtype=np.uint8).reshape(nkeys, 32).copy()
+
+
+def pubkeys(sks: np.ndarray) -> np.ndarray:
+    lib = cpu_lib()
+    out = np.zeros_like(sks)
+    for i in range(sks.shape[0]):
+        assert lib.cbft_cpu_pubkey(_p(sks[i]), _p(out[i])) == 0
+    return out
+
+
+@dataclass
+class SigSet:
+    pk: np.ndarray        # nkeys x 32
+    key_idx: np.ndarray   # n u32
+    sig: np.ndarray       # n x 64
+    blob: np.ndarray      # u8
+    off: np.ndarray       # n u64
+    len: np.ndarray       # n u32
+    expected: np.ndarray  # n bool (OpenSSL verdicts)
+
+    @property
+    def n(self):
+        return self.key_idx.shape[0]
+
+    def msgs(self):
+        b = self.blob.tobytes()
+        return [b[o:o + l] for o, l in zip(self.off.tolist(), self.len.tolist())]
+
+    def per_sig_pk(self) -> np.ndarray:
+        return np.ascontiguousarray(self.pk[self.key_idx])
+
+
+def make_sigset(n: int, nkeys: int = 4096, msg_len=256, seed: int = 0xC0FFEE, invalid_frac: float = 0.0,
+                threads: int = 8, compute_expected: bool = True) -> SigSet:
+    """msg_len: int (fixed) or (lo, hi) for log-uniform lengths in [lo, hi]."""
+    rng = np.random.default_rng(seed)
+    sks = key_seeds(nkeys)
+    pk = pubkeys(sks)
+    key_idx = (np.arange(n, dtype=np.uint64) % nkeys).astype(np.uint32)
+    if isinstance(msg_len, tuple):
+        lo, hi = msg_len
+        lens = np.exp(rng.uniform(np.log(lo), np.log(hi + 1), size=n)).astype(np.uint32)
+        lens = np.clip(lens, lo, hi).astype(np.uint32)
+    else:
+        lens = np.full(n, msg_len, dtype=np.uint32)
+    off = np.zeros(n, dtype=np.uint64)
+    if n > 1:
+        np.cumsum(lens[:-1].astype(np.uint64), out=off[1:])
+    total = int(lens.sum())
+    blob = rng.integers(0, 256, size=max(total, 1), dtype=np.uint8)
+    sig = np.zeros((n, 64), dtype=np.uint8)
+    lib = cpu_lib()
+    lib.cbft_cpu_sign_many(_p(sks), nkeys, _p(key_idx), _p(blob), _p(off), _p(lens), n, _p(sig), threads)
+    if invalid_frac > 0:
+        bad = rng.random(n) < invalid_frac
+        kinds = rng.integers(0, 5, size=n)
+        L = 2**252 + 27742317777372353535851937790883648493
+        for i in np.nonzero(bad)[0]:
+            k = kinds[i]
+            if k == 0:      # flip a bit of R
+                sig[i, rng.integers(0, 32)] ^= 1 << int(rng.integers(0, 8))
+            elif k == 1:    # flip a bit of S
+                sig[i, 32 + rng.integers(0, 31)] ^= 1 << int(rng.integers(0, 8))
+            elif k == 2:    # S + L
+                s = int.from_bytes(sig[i, 32:].tobytes(), "little") + L
+                sig[i, 32:] = np.frombuffer(s.to_bytes(32, "little"), dtype=np.uint8)
+            elif k == 3 and lens[i] > 0:  # flip a message byte
+                blob[int(off[i]) + int(rng.integers(0, int(lens[i])))] ^= 0x5A
+            else:           # wrong key
+                key_idx[i] = (key_idx[i] + 1) % nkeys
+    ss = SigSet(pk, key_idx, sig, blob, off, lens, np.zeros(n, dtype=bool))
+    if compute_expected:
+        ss.expected = cpu_verify(ss, threads=threads).astype(bool)
+    return ss
+
+
+def cpu_verify(ss: SigSet, threads: int = 8, keycache=None) -> np.ndarray:
+    lib = cpu_lib()
+    own = keycache is None
+    if own:
+        keycache = lib.cbft_cpu_keys_new(_p(ss.pk), ss.pk.shape[0])
+    out = np.zeros(ss.n, dtype=np.uint8)
+    lib.cbft_cpu_verify(keycache, _p(ss.key_idx), _p(ss.sig), _p(ss.blob), _p(ss.off), _p(ss.len), ss.n, _p(out),
+                        threads)
+    if own:
+        lib.cbft_cpu_keys_free(keycache, ss.pk.shape[0])
+    return out
