@@ -7,7 +7,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wal
 ORACLE_LIB := oracle/libcbft_oracle.so
 
 .PHONY: all lib oracle clean
-all: lib oracle cpu
+all: lib oracle cpu host
 
 lib: $(LIB)
 
@@ -32,3 +32,12 @@ CPU_LIB := tools/cpu_baseline/libcbft_cpu_openssl.so
 cpu: $(CPU_LIB)
 $(CPU_LIB): tools/cpu_baseline/openssl_ed25519.c
 	gcc -O2 -std=gnu11 -fPIC -shared -Wall -o $@ $< -lcrypto -lpthread
+
+HOST_LIB := concord-bft_amd/libcbft_host.so
+HOST_SRC := concord-bft_amd/host/src/crypto_utils.cpp concord-bft_amd/host/src/sig_manager.cpp
+HOST_INC := -Iinclude -Iconcord-bft_amd/host/include
+host: $(HOST_LIB) tests/cpp/test_host
+$(HOST_LIB): $(HOST_SRC) concord-bft_amd/host/include/*.hpp $(LIB)
+	g++ -O2 -std=c++17 -fPIC -shared -Wall $(HOST_INC) -o $@ $(HOST_SRC) -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN'
+tests/cpp/test_host: tests/cpp/test_host.cpp $(HOST_LIB)
+	g++ -O2 -std=c++17 -Wall $(HOST_INC) -o $@ $< -Lconcord-bft_amd -lcbft_host -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN/../../concord-bft_amd'
