@@ -54,7 +54,7 @@ struct DevBuf {
 
 struct KeyTable {
   uint32_t nkeys = 0;
-  DevBuf pk, tbl, aok;
+  DevBuf pk, comb, aok;  // raw keys, per-key comb tables of -A, decode status
 };
 
 }  // namespace
@@ -63,7 +63,7 @@ struct cbft_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
-  DevBuf base_table;
+  DevBuf base_table, base_comb;
   std::unordered_map<uint32_t, KeyTable> tables;
   uint32_t next_table_id = 1;
   // per-batch work buffers
@@ -160,6 +160,29 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
       rc = CBFT_EIO;
       break;
     }
+    {  // comb table of B (the "key" is B's encoding, not negated)
+      static const uint8_t kB[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                                     0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                                     0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
+      DevBuf enc, tmp;
+      if (c->base_comb.reserve(cbft_ed25519_comb_words_per_unit() * 4) != hipSuccess ||
+          enc.reserve(32) != hipSuccess || tmp.reserve(cbft_ed25519_comb_tmp_words_per_unit() * 4) != hipSuccess) {
+        enc.release();
+        tmp.release();
+        rc = CBFT_ENOMEM;
+        break;
+      }
+      bool okb = hipMemcpy(enc.p, kB, 32, hipMemcpyHostToDevice) == hipSuccess &&
+                 cbft_ed25519_launch_comb_tables(enc.as<uint8_t>(), 1, 0, c->base_comb.as<uint32_t>(),
+                                                 tmp.as<uint32_t>(), nullptr, c->stream) == hipSuccess &&
+                 hipStreamSynchronize(c->stream) == hipSuccess;
+      enc.release();
+      tmp.release();
+      if (!okb) {
+        rc = CBFT_EIO;
+        break;
+      }
+    }
     if (max_batch) rc = reserve_work(c, max_batch);
   } while (0);
   if (rc != CBFT_OK) {
@@ -177,10 +200,10 @@ void cbft_close(cbft_ctx* c) {
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   for (auto& kv : c->tables) {
     kv.second.pk.release();
-    kv.second.tbl.release();
+    kv.second.comb.release();
     kv.second.aok.release();
   }
-  for (DevBuf* b : {&c->base_table, &c->h, &c->flags, &c->xyz, &c->verdicts, &c->sig, &c->msg, &c->off, &c->len,
+  for (DevBuf* b : {&c->base_table, &c->base_comb, &c->h, &c->flags, &c->xyz, &c->verdicts, &c->sig, &c->msg, &c->off, &c->len,
                     &c->kidx, &c->pk, &c->ps_tbl, &c->ps_aok})
     b->release();
   for (hipEvent_t& e : c->ev)
@@ -225,13 +248,29 @@ int cbft_ed25519_load_keys(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, uint3
   kt.nkeys = nkeys;
   const size_t n = std::max<uint32_t>(nkeys, 1);
   CBFT_HIP(kt.pk.reserve(n * 32));
-  CBFT_HIP(kt.tbl.reserve(n * cbft_ed25519_table_words_per_unit() * sizeof(uint32_t)));
+  CBFT_HIP(kt.comb.reserve(n * cbft_ed25519_comb_words_per_unit() * sizeof(uint32_t)));
   CBFT_HIP(kt.aok.reserve(n));
   if (nkeys) {
-    CBFT_HIP(hipMemcpyAsync(kt.pk.p, pk, (size_t)nkeys * 32, hipMemcpyHostToDevice, c->stream));
-    CBFT_HIP(cbft_ed25519_launch_prep(kt.pk.as<uint8_t>(), nkeys, kt.tbl.as<uint32_t>(), kt.aok.as<uint8_t>(),
-                                      c->stream));
-    CBFT_HIP(hipStreamSynchronize(c->stream));
+    DevBuf tmp;  // projective staging of the 256 multiples per key, freed after the build
+    hipError_t e = tmp.reserve((size_t)nkeys * cbft_ed25519_comb_tmp_words_per_unit() * sizeof(uint32_t));
+    if (e != hipSuccess) {
+      kt.pk.release();
+      kt.comb.release();
+      kt.aok.release();
+      return fail(e, "hipMalloc(comb tmp)", __LINE__);
+    }
+    e = hipMemcpyAsync(kt.pk.p, pk, (size_t)nkeys * 32, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess)
+      e = cbft_ed25519_launch_comb_tables(kt.pk.as<uint8_t>(), nkeys, 1, kt.comb.as<uint32_t>(), tmp.as<uint32_t>(),
+                                          kt.aok.as<uint8_t>(), c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    tmp.release();
+    if (e != hipSuccess) {
+      kt.pk.release();
+      kt.comb.release();
+      kt.aok.release();
+      return fail(e, "comb table build", __LINE__);
+    }
   }
   uint32_t id = c->next_table_id++;
   if (id == CBFT_NO_KEY_TABLE) id = c->next_table_id++;
@@ -248,7 +287,7 @@ int cbft_ed25519_unload_keys(cbft_ctx* c, uint32_t id) {
   (void)hipSetDevice(c->device);
   (void)hipStreamSynchronize(c->stream);
   it->second.pk.release();
-  it->second.tbl.release();
+  it->second.comb.release();
   it->second.aok.release();
   c->tables.erase(it);
   return CBFT_OK;
@@ -279,7 +318,8 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     auto it = c->tables.find(table_id);
     if (it == c->tables.end() || !d_kidx) return CBFT_EINVAL;
     b.pk = it->second.pk.as<uint8_t>();
-    w.tbl = it->second.tbl.as<uint32_t>();
+    w.comb_tbl = it->second.comb.as<uint32_t>();
+    w.base_comb = c->base_comb.as<uint32_t>();
     w.aok = it->second.aok.as<uint8_t>();
   }
   CBFT_HIP(cbft_ed25519_launch_verify(b, w, s, c->profiling ? c->ev : nullptr));

@@ -58,6 +58,7 @@ class EdDSAVerifier : public IVerifier {
   // accepted here and every signature under it verifies false (OpenSSL does the same).
   EdDSAVerifier(const std::string& str_pub_key, KeyFormat fmt);
   ~EdDSAVerifier() override;
+  EdDSAVerifier(const EdDSAVerifier&) = default;
 
   bool verify(const std::string& data, const std::string& sig) const override;
   uint32_t signatureLength() const override { return 64; }
@@ -81,6 +82,9 @@ class EdDSASigner : public ISigner {
   // str_priv_key: 32-byte RFC 8032 seed, hex (HexaDecimalStrippedFormat) or PKCS#8 PEM.
   EdDSASigner(const std::string& str_priv_key, KeyFormat fmt);
   ~EdDSASigner() override;
+  EdDSASigner(const EdDSASigner&) = delete;  // owns an EVP_PKEY
+  EdDSASigner& operator=(const EdDSASigner&) = delete;
+  EdDSASigner(EdDSASigner&& o) noexcept : key_str_(std::move(o.key_str_)), pkey_(o.pkey_) { o.pkey_ = nullptr; }
   std::string sign(const std::string& data) override;
   uint32_t signatureLength() const override { return 64; }
   std::string getPrivKey() const override { return key_str_; }

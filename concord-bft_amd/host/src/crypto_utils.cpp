@@ -7,6 +7,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <shared_mutex>
 #include <stdexcept>
 
 #include "cbft_hipcrypto.h"
@@ -171,13 +172,23 @@ class Ed25519Engine {
       if (r.dataLength) std::memcpy(&msg[o], r.data, r.dataLength);
       o += r.dataLength;
     }
-    uint32_t table;
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      ensureTableLocked();
-      table = table_;
+    // the device table must cover every registered key; a rebuild (new key) takes the table
+    // lock exclusively, verifies hold it shared for the duration of the GPU call
+    std::shared_lock<std::shared_mutex> rd(tbl_mu_);
+    while (true) {
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (loaded_ == keys_.size() / 32 && table_ != CBFT_NO_KEY_TABLE) break;
+      }
+      rd.unlock();
+      {
+        std::unique_lock<std::shared_mutex> wr(tbl_mu_);
+        std::lock_guard<std::mutex> g(mu_);
+        ensureTableLocked();
+      }
+      rd.lock();
     }
-    int rc = cbft_ed25519_verify_batch(ctx_, table, kidx.data(), sig.data(), msg.data(), off.data(), len.data(), n,
+    int rc = cbft_ed25519_verify_batch(ctx_, table_, kidx.data(), sig.data(), msg.data(), off.data(), len.data(), n,
                                        bitmap.data());
     if (rc != CBFT_OK)
       throw std::runtime_error(std::string("cbft_ed25519_verify_batch: ") + cbft_strerror(rc) + " " +
@@ -211,7 +222,8 @@ class Ed25519Engine {
   }
 
   cbft_ctx* ctx_ = nullptr;
-  std::mutex mu_;
+  std::mutex mu_;                // guards keys_, index_, table_, loaded_
+  std::shared_mutex tbl_mu_;     // device table lifetime vs in-flight verifies
   std::vector<uint8_t> keys_;
   std::map<std::string, uint32_t> index_;
   uint32_t table_ = CBFT_NO_KEY_TABLE;
@@ -265,7 +277,9 @@ EdDSASigner::EdDSASigner(const std::string& str_priv_key, KeyFormat fmt) : key_s
   if (!pkey_) throw std::invalid_argument("EdDSASigner: key rejected");
 }
 
-EdDSASigner::~EdDSASigner() { EVP_PKEY_free(static_cast<EVP_PKEY*>(pkey_)); }
+EdDSASigner::~EdDSASigner() {
+  if (pkey_) EVP_PKEY_free(static_cast<EVP_PKEY*>(pkey_));
+}
 
 std::string EdDSASigner::sign(const std::string& data) {
   EVP_MD_CTX* ctx = EVP_MD_CTX_new();

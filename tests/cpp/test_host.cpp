@@ -62,6 +62,7 @@ int main() {
   ri.numReplicas = 4;
   std::vector<std::pair<std::set<PrincipalId>, std::string>> keys;
   std::vector<EdDSASigner> signers;
+  signers.reserve(16);
   for (int r = 0; r < 4; r++) {
     signers.emplace_back(seedHex(10 + r), KeyFormat::HexaDecimalStrippedFormat);
     keys.push_back({{(PrincipalId)r}, signers.back().getPubKeyHex()});
