@@ -147,6 +147,15 @@ class Context:
                                                    _ptr(lens), n, _ptr(out)), "cbft_ed25519_verify_batch")
         return out.tobytes()[: (n + 7) // 8]
 
+    def verify_packed(self, tid: int, key_idx: np.ndarray, sigs: np.ndarray, blob: np.ndarray, offs: np.ndarray,
+                      lens: np.ndarray) -> bytes:
+        """verify() with messages already packed as (blob, offsets u64, lengths u32)."""
+        n = int(lens.shape[0])
+        out = np.zeros(max(1, (n + 7) // 8), dtype=np.uint8)
+        _check(self.lib.cbft_ed25519_verify_batch(self.handle, tid, _ptr(key_idx), _ptr(sigs), _ptr(blob), _ptr(offs),
+                                                   _ptr(lens), n, _ptr(out)), "cbft_ed25519_verify_batch")
+        return out.tobytes()[: (n + 7) // 8]
+
     def verify_pk(self, pks, sigs, msgs: Sequence[bytes]) -> bytes:
         n = len(msgs)
         p = _as_rows(pks, 32)
