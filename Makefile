@@ -6,18 +6,24 @@ LIB     := concord-bft_amd/libcbft_hipcrypto.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall -Wno-unused-function
 ORACLE_LIB := oracle/libcbft_oracle.so
 
-.PHONY: all lib oracle clean
-all: lib oracle cpu host
+.PHONY: all lib oracle clean shim
+all: lib oracle cpu host shim
 
 lib: $(LIB)
 
 $(CSRC)/ed25519_verify.o: $(CSRC)/ed25519_verify.hip $(CSRC)/*.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(CSRC)/cbft_hipcrypto.o: $(CSRC)/cbft_hipcrypto.cpp include/cbft_hipcrypto.h $(CSRC)/ed25519_verify.h
+$(CSRC)/cbft_hipcrypto.o: $(CSRC)/cbft_hipcrypto.cpp include/cbft_hipcrypto.h $(CSRC)/ed25519_verify.h $(CSRC)/cbft_internal.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(CSRC)/ed25519_verify.o $(CSRC)/cbft_hipcrypto.o
+$(CSRC)/bls_kernels.o: $(CSRC)/bls_kernels.hip $(CSRC)/bls_kernels.h $(CSRC)/bn254_*.h $(CSRC)/bls_ops.h $(CSRC)/sha256.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/cbft_bls.o: $(CSRC)/cbft_bls.cpp $(CSRC)/cbft_internal.h include/cbft_hipcrypto.h $(CSRC)/bls_kernels.h
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(CSRC)/ed25519_verify.o $(CSRC)/cbft_hipcrypto.o $(CSRC)/bls_kernels.o $(CSRC)/cbft_bls.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle: $(ORACLE_LIB)
@@ -41,3 +47,9 @@ $(HOST_LIB): $(HOST_SRC) concord-bft_amd/host/include/*.hpp $(LIB)
 	g++ -O2 -std=c++17 -fPIC -shared -Wall $(HOST_INC) -o $@ $(HOST_SRC) -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN'
 tests/cpp/test_host: tests/cpp/test_host.cpp $(HOST_LIB)
 	g++ -O2 -std=c++17 -Wall $(HOST_INC) -o $@ $< -Lconcord-bft_amd -lcbft_host -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN/../../concord-bft_amd'
+
+# host build of the BN-P254 device code, for the CPU tests (and the "not RELIC" CPU baseline)
+SHIM := tests/cpp/libbn254_shim.so
+shim: $(SHIM)
+$(SHIM): tests/cpp/bn254_shim.cpp $(CSRC)/bn254_*.h $(CSRC)/bls_ops.h $(CSRC)/sha256.h
+	g++ -O3 -funroll-loops -std=c++17 -fPIC -shared -Wall -Wno-unknown-pragmas -I$(CSRC) -o $@ $< -lpthread

@@ -46,6 +46,20 @@ ABI = [
     ("cbft_sync", ctypes.c_int, [ctypes.c_void_p]),
     ("cbft_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("cbft_stage_times_ms", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
+    ("cbft_bls_load_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, _u32p]),
+    ("cbft_bls_unload_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
+    ("cbft_bls_key_status", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    ("cbft_bls_hash_to_g1", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p]),
+    ("cbft_bls_verify_shares", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
+      ctypes.c_void_p]),
+    ("cbft_bls_combine", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int,
+                                        ctypes.c_void_p]),
+    ("cbft_bls_verify", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
+                                       ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
+    ("cbft_bls_verify_multisig", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p,
+      ctypes.POINTER(ctypes.c_int)]),
 ]
 
 _lib = None
@@ -177,6 +191,50 @@ class Context:
 
     def sync(self):
         _check(self.lib.cbft_sync(self.handle), "cbft_sync")
+
+    # ------------------------------------------------------------------ BLS BN-P254
+    def bls_load_keys(self, pk65: bytes, vks65: Sequence[bytes]) -> int:
+        kid = ctypes.c_uint32()
+        _check(self.lib.cbft_bls_load_keys(self.handle, pk65, b"".join(vks65), len(vks65), ctypes.byref(kid)),
+               "cbft_bls_load_keys")
+        return kid.value
+
+    def bls_unload_keys(self, kid: int):
+        _check(self.lib.cbft_bls_unload_keys(self.handle, kid), "cbft_bls_unload_keys")
+
+    def bls_key_status(self, kid: int, n: int) -> bytes:
+        out = ctypes.create_string_buffer(n + 1)
+        _check(self.lib.cbft_bls_key_status(self.handle, kid, out), "cbft_bls_key_status")
+        return out.raw
+
+    def bls_hash_to_g1(self, msg: bytes) -> bytes:
+        out = ctypes.create_string_buffer(33)
+        _check(self.lib.cbft_bls_hash_to_g1(self.handle, msg, len(msg), out), "cbft_bls_hash_to_g1")
+        return out.raw
+
+    def bls_verify_shares(self, kid: int, msg: bytes, shares: Sequence[bytes]) -> np.ndarray:
+        k = len(shares)
+        out = ctypes.create_string_buffer(max(1, (k + 7) // 8))
+        _check(self.lib.cbft_bls_verify_shares(self.handle, kid, msg, len(msg), b"".join(shares), k, out),
+               "cbft_bls_verify_shares")
+        return bitmap_to_bools(out.raw, k)
+
+    def bls_combine(self, shares: Sequence[bytes], multisig: bool = False) -> bytes:
+        out = ctypes.create_string_buffer(33)
+        _check(self.lib.cbft_bls_combine(self.handle, b"".join(shares), len(shares), 1 if multisig else 0, out),
+               "cbft_bls_combine")
+        return out.raw
+
+    def bls_verify(self, kid: int, msg: bytes, sig33: bytes) -> bool:
+        ok = ctypes.c_int()
+        _check(self.lib.cbft_bls_verify(self.handle, kid, msg, len(msg), sig33, ctypes.byref(ok)), "cbft_bls_verify")
+        return bool(ok.value)
+
+    def bls_verify_multisig(self, kid: int, msg: bytes, sig33: bytes, signers256: bytes) -> bool:
+        ok = ctypes.c_int()
+        _check(self.lib.cbft_bls_verify_multisig(self.handle, kid, msg, len(msg), sig33, signers256,
+                                                  ctypes.byref(ok)), "cbft_bls_verify_multisig")
+        return bool(ok.value)
 
     def set_profiling(self, on: bool = True):
         _check(self.lib.cbft_set_profiling(self.handle, 1 if on else 0), "cbft_set_profiling")

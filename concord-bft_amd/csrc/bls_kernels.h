@@ -1,0 +1,26 @@
+// Launch interface of the BLS BN-P254 kernels (internal to libcbft_hipcrypto).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#define BLS_SIG_WORDS 19     // affine G1 (x, y, inf flag) per parsed share
+#define BLS_JAC_WORDS 27     // Jacobian G1 partial sum
+
+size_t cbft_bls_lines_words_per_key();
+hipError_t cbft_bls_launch_keys(const uint8_t* d_keys65, uint32_t nkeys, uint32_t* d_lines, uint8_t* d_ok,
+                                hipStream_t s);
+hipError_t cbft_bls_launch_gen_lines(uint32_t* d_lines, hipStream_t s);
+hipError_t cbft_bls_launch_hash(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, hipStream_t s);
+hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uint32_t n, const uint32_t* d_H,
+                                        const uint32_t* d_vk_lines, const uint8_t* d_vk_ok,
+                                        const uint32_t* d_gen_lines, int do_verify, uint8_t* d_valid,
+                                        uint32_t* d_sig, uint32_t* d_ids, hipStream_t s);
+hipError_t cbft_bls_launch_combine(const uint32_t* d_sig, const uint32_t* d_ids, const uint8_t* d_use, uint32_t k,
+                                   int multisig, uint32_t* d_lambda, uint32_t* d_partial, uint8_t* d_out33,
+                                   uint32_t* d_sig_aff, hipStream_t s);
+hipError_t cbft_bls_launch_g2_sum(const uint8_t* d_keys65, uint32_t n, const uint8_t* d_bitmap, uint32_t* d_lines,
+                                  uint8_t* d_ok, hipStream_t s);
+hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, const uint32_t* d_pk_lines,
+                                  const uint8_t* d_pk_ok, const uint32_t* d_gen_lines, uint8_t* d_result,
+                                  hipStream_t s);

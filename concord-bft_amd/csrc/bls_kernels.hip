@@ -1,0 +1,297 @@
+// BLS BN-P254 threshold-signature kernels for gfx950 (threshsign path).
+//
+//   bls_keys_kernel          per G2 key: decompress + subgroup check + 70 Miller-loop lines
+//                            (BlsThresholdVerifier ctor; lines make per-share work G2-free)
+//   bls_hash_kernel          H = g1_map(digest)            (BlsAccumulatorBase.cpp:55-60)
+//   bls_share_verify_kernel  lane per share: parse, e(H, vk_id) e(-sigma, g2) == 1
+//                            (BlsAccumulatorBase::verifyShare, BlsAccumulatorBase.cpp:62-84)
+//   bls_lagrange_kernel      lane per share: lambda_i = prod_{j!=i} j/(j-i) mod r
+//                            (lagrangeCoeffAccumReduced, LagrangeInterpolation.cpp:202-292)
+//   bls_msm_kernel           lane per share: lambda_i sigma_i, LDS tree sum per block
+//                            (fastMultExp, FastMultExp.cpp:26-59; multisig: lambda = 1)
+//   bls_msm_finish_kernel    sum of block partials -> 33-byte compressed G1
+//   bls_g2_sum_kernel        multisig PK = sum vk_i over the signer bitmap, + its lines
+//   bls_verify_kernel        e(H, PK) e(-sigma, g2) == 1   (BlsThresholdVerifier.cpp:69-96)
+// One lane per pairing check: the per-lane state (an Fp12 accumulator + temporaries) lives in
+// VGPRs/scratch; the G2 side is entirely precomputed.
+#include <hip/hip_runtime.h>
+
+#include "bls_kernels.h"
+#include "bls_ops.h"
+
+#define LINES_PER_KEY (BN_ATE_LINES * BN_LINE_WORDS)
+
+__device__ __forceinline__ void g1a_store(uint32_t* o, const g1a& a) {
+  for (int i = 0; i < 9; i++) {
+    o[i] = a.x.v[i];
+    o[9 + i] = a.y.v[i];
+  }
+  o[18] = a.inf ? 1u : 0u;
+}
+__device__ __forceinline__ void g1a_load(g1a& a, const uint32_t* o) {
+  for (int i = 0; i < 9; i++) {
+    a.x.v[i] = o[i];
+    a.y.v[i] = o[9 + i];
+  }
+  a.inf = o[18] != 0;
+}
+
+__global__ void __launch_bounds__(64) bls_keys_kernel(const uint8_t* keys65, uint32_t nkeys, uint32_t* lines,
+                                                      uint8_t* ok) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nkeys) return;
+  g2a q;
+  bool good = g2_decompress(q, keys65 + 65 * (size_t)k) && !q.inf;
+  ok[k] = good ? 1 : 0;
+  if (good) g2_precompute_lines(lines + (size_t)k * LINES_PER_KEY, q);
+}
+
+__global__ void bls_gen_lines_kernel(uint32_t* lines) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  g2a q;
+  fp2_load(q.x, Bn254Consts::G2X);
+  fp2_load(q.y, Bn254Consts::G2Y);
+  q.inf = false;
+  g2_precompute_lines(lines, q);
+}
+
+__global__ void bls_hash_kernel(const uint8_t* msg, uint32_t len, uint32_t* H) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  g1a h;
+  g1_map(h, msg, len);
+  g1a_store(H, h);
+}
+
+// shares: k x 37 bytes.  out: valid[k] (1 = verified), sig[k] (parsed affine point, 19 words),
+// ids[k].  A share whose id is outside [1, n] or whose point does not decode is invalid.
+__global__ void __launch_bounds__(64) bls_share_verify_kernel(const uint8_t* shares, uint32_t k, uint32_t n,
+                                                              const uint32_t* H, const uint32_t* vk_lines,
+                                                              const uint8_t* vk_ok, const uint32_t* gen_lines,
+                                                              int do_verify, uint8_t* valid, uint32_t* sig,
+                                                              uint32_t* ids) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= k) return;
+  uint32_t id;
+  g1a s;
+  bool good = bls_parse_share(id, s, shares + 37 * (size_t)j);
+  good = good && id >= 1 && id <= n;
+  ids[j] = id;
+  g1a_store(sig + 19 * (size_t)j, s);
+  if (good && do_verify) {
+    good = vk_ok[id - 1] != 0;
+    if (good) {
+      g1a P[2];
+      g1a_load(P[0], H);
+      P[1] = s;
+      if (!s.inf) f_neg(P[1].y, s.y);
+      const uint32_t* l[2] = {vk_lines + (size_t)(id - 1) * LINES_PER_KEY, gen_lines};
+      // e(O, Q) = 1: an infinite sigma checks against e(H, vk) alone
+      if (P[1].inf)
+        good = pairing_check<1>(P, l);
+      else
+        good = pairing_check<2>(P, l);
+    }
+  }
+  valid[j] = good ? 1 : 0;
+}
+
+// lambda_i = prod_{j != i} j / (j - i) mod r over the shares with use[j] != 0; words out (LE)
+__global__ void __launch_bounds__(64) bls_lagrange_kernel(const uint32_t* ids, const uint8_t* use, uint32_t k,
+                                                          uint32_t* lambda) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k) return;
+  uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (use[i]) {
+    fr num, den, t, d;
+    f_one(num);
+    f_one(den);
+    const uint32_t me = ids[i];
+    for (uint32_t j = 0; j < k; j++) {
+      if (j == i || !use[j]) continue;
+      const uint32_t o = ids[j];
+      uint32_t v[8] = {o, 0, 0, 0, 0, 0, 0, 0};
+      f_from_words(t, v);
+      f_mul(num, num, t);
+      uint32_t dv[8] = {o > me ? o - me : me - o, 0, 0, 0, 0, 0, 0, 0};
+      f_from_words(d, dv);
+      if (o < me) f_neg(d, d);
+      f_mul(den, den, d);
+    }
+    fr_inv(den, den);
+    f_mul(num, num, den);
+    f_to_words(w, num);
+  }
+  for (int q = 0; q < 8; q++) lambda[8 * (size_t)i + q] = w[q];
+}
+
+#define MSM_BLOCK 64
+// partial[b] = sum over this block's lanes of lambda_j * sig_j (Jacobian, 27 words)
+__global__ void __launch_bounds__(MSM_BLOCK) bls_msm_kernel(const uint32_t* sig, const uint32_t* lambda,
+                                                            const uint8_t* use, uint32_t k, int unit_scalars,
+                                                            uint32_t* partial) {
+  __shared__ uint32_t sp[MSM_BLOCK][27];
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  g1j acc;
+  g1_set_inf(acc);
+  if (j < k && use[j]) {
+    g1a s;
+    g1a_load(s, sig + 19 * (size_t)j);
+    g1j p;
+    g1_from_affine(p, s);
+    if (unit_scalars) {
+      acc = p;
+    } else {
+      uint32_t lw[8];
+      for (int q = 0; q < 8; q++) lw[q] = lambda[8 * (size_t)j + q];
+      g1_mul(acc, p, lw);
+    }
+  }
+  for (int stride = MSM_BLOCK / 2; stride >= 1; stride >>= 1) {
+    const int t = threadIdx.x;
+    if (t >= stride && t < 2 * stride) {
+      for (int q = 0; q < 9; q++) {
+        sp[t - stride][q] = acc.X.v[q];
+        sp[t - stride][9 + q] = acc.Y.v[q];
+        sp[t - stride][18 + q] = acc.Z.v[q];
+      }
+    }
+    __syncthreads();
+    if (t < stride) {
+      g1j o;
+      for (int q = 0; q < 9; q++) {
+        o.X.v[q] = sp[t][q];
+        o.Y.v[q] = sp[t][9 + q];
+        o.Z.v[q] = sp[t][18 + q];
+      }
+      g1_add(acc, acc, o);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    uint32_t* o = partial + 27 * (size_t)blockIdx.x;
+    for (int q = 0; q < 9; q++) {
+      o[q] = acc.X.v[q];
+      o[9 + q] = acc.Y.v[q];
+      o[18 + q] = acc.Z.v[q];
+    }
+  }
+}
+
+__global__ void bls_msm_finish_kernel(const uint32_t* partial, uint32_t nparts, uint8_t* out33, uint32_t* sig_aff) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  g1j acc;
+  g1_set_inf(acc);
+  for (uint32_t b = 0; b < nparts; b++) {
+    g1j o;
+    for (int q = 0; q < 9; q++) {
+      o.X.v[q] = partial[27 * b + q];
+      o.Y.v[q] = partial[27 * b + 9 + q];
+      o.Z.v[q] = partial[27 * b + 18 + q];
+    }
+    g1_add(acc, acc, o);
+  }
+  g1a a;
+  g1_to_affine(a, acc);
+  g1_compress(out33, a);
+  if (sig_aff) g1a_store(sig_aff, a);
+}
+
+// multisig public key = sum of vk_i for set bits (bit id-1, LSB first) of the 256-byte bitmap;
+// then its Miller-loop lines.  Single lane (the G2 sum is <= 2048 additions).
+__global__ void bls_g2_sum_kernel(const uint8_t* keys65, uint32_t n, const uint8_t* bitmap, uint32_t* lines,
+                                  uint8_t* ok) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  g2j acc;
+  fp2_one(acc.X);
+  fp2_one(acc.Y);
+  fp2_zero(acc.Z);
+  bool good = true;
+  for (uint32_t id = 1; id <= n; id++) {
+    if (!((bitmap[(id - 1) >> 3] >> ((id - 1) & 7)) & 1)) continue;
+    g2a q;
+    if (!g2_decompress(q, keys65 + 65 * (size_t)(id - 1))) {
+      good = false;
+      continue;
+    }
+    g2j p;
+    p.X = q.x;
+    p.Y = q.y;
+    fp2_one(p.Z);
+    g2_add_j(acc, acc, p);
+  }
+  g2a s;
+  g2_to_affine(s, acc);
+  good = good && !s.inf;
+  ok[0] = good ? 1 : 0;
+  if (good) g2_precompute_lines(lines, s);
+}
+
+// e(H, PK) * e(-sigma, g2) == 1 for a combined signature (33 bytes)
+__global__ void bls_verify_kernel(const uint32_t* H, const uint8_t* sig33, const uint32_t* pk_lines,
+                                  const uint8_t* pk_ok, const uint32_t* gen_lines, uint8_t* result) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  g1a P[2];
+  g1a_load(P[0], H);
+  bool good = pk_ok[0] && g1_decompress(P[1], sig33);
+  if (good) {
+    const uint32_t* l[2] = {pk_lines, gen_lines};
+    if (P[1].inf) {
+      good = pairing_check<1>(P, l);
+    } else {
+      f_neg(P[1].y, P[1].y);
+      good = pairing_check<2>(P, l);
+    }
+  }
+  result[0] = good ? 1 : 0;
+}
+
+// ------------------------------------------------------------------------------ launchers
+size_t cbft_bls_lines_words_per_key() { return (size_t)LINES_PER_KEY; }
+
+hipError_t cbft_bls_launch_keys(const uint8_t* d_keys65, uint32_t nkeys, uint32_t* d_lines, uint8_t* d_ok,
+                                hipStream_t s) {
+  if (!nkeys) return hipSuccess;
+  hipLaunchKernelGGL(bls_keys_kernel, dim3((nkeys + 63) / 64), dim3(64), 0, s, d_keys65, nkeys, d_lines, d_ok);
+  return hipGetLastError();
+}
+hipError_t cbft_bls_launch_gen_lines(uint32_t* d_lines, hipStream_t s) {
+  hipLaunchKernelGGL(bls_gen_lines_kernel, dim3(1), dim3(64), 0, s, d_lines);
+  return hipGetLastError();
+}
+hipError_t cbft_bls_launch_hash(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, hipStream_t s) {
+  hipLaunchKernelGGL(bls_hash_kernel, dim3(1), dim3(64), 0, s, d_msg, len, d_H);
+  return hipGetLastError();
+}
+hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uint32_t n, const uint32_t* d_H,
+                                        const uint32_t* d_vk_lines, const uint8_t* d_vk_ok,
+                                        const uint32_t* d_gen_lines, int do_verify, uint8_t* d_valid,
+                                        uint32_t* d_sig, uint32_t* d_ids, hipStream_t s) {
+  if (!k) return hipSuccess;
+  hipLaunchKernelGGL(bls_share_verify_kernel, dim3((k + 63) / 64), dim3(64), 0, s, d_shares, k, n, d_H, d_vk_lines,
+                     d_vk_ok, d_gen_lines, do_verify, d_valid, d_sig, d_ids);
+  return hipGetLastError();
+}
+hipError_t cbft_bls_launch_combine(const uint32_t* d_sig, const uint32_t* d_ids, const uint8_t* d_use, uint32_t k,
+                                   int multisig, uint32_t* d_lambda, uint32_t* d_partial, uint8_t* d_out33,
+                                   uint32_t* d_sig_aff, hipStream_t s) {
+  if (!multisig && k)
+    hipLaunchKernelGGL(bls_lagrange_kernel, dim3((k + 63) / 64), dim3(64), 0, s, d_ids, d_use, k, d_lambda);
+  const uint32_t nparts = (k + MSM_BLOCK - 1) / MSM_BLOCK;
+  if (k)
+    hipLaunchKernelGGL(bls_msm_kernel, dim3(nparts), dim3(MSM_BLOCK), 0, s, d_sig, d_lambda, d_use, k, multisig,
+                       d_partial);
+  hipLaunchKernelGGL(bls_msm_finish_kernel, dim3(1), dim3(64), 0, s, d_partial, nparts, d_out33, d_sig_aff);
+  return hipGetLastError();
+}
+hipError_t cbft_bls_launch_g2_sum(const uint8_t* d_keys65, uint32_t n, const uint8_t* d_bitmap, uint32_t* d_lines,
+                                  uint8_t* d_ok, hipStream_t s) {
+  hipLaunchKernelGGL(bls_g2_sum_kernel, dim3(1), dim3(64), 0, s, d_keys65, n, d_bitmap, d_lines, d_ok);
+  return hipGetLastError();
+}
+hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, const uint32_t* d_pk_lines,
+                                  const uint8_t* d_pk_ok, const uint32_t* d_gen_lines, uint8_t* d_result,
+                                  hipStream_t s) {
+  hipLaunchKernelGGL(bls_verify_kernel, dim3(1), dim3(64), 0, s, d_H, d_sig33, d_pk_lines, d_pk_ok, d_gen_lines,
+                     d_result);
+  return hipGetLastError();
+}

@@ -1,0 +1,325 @@
+// BN-P254 prime fields (Fp: base field, Fr: group order) for gfx950 and for the host, one
+// element per lane.  Same source compiles as HIP device code and as plain C++ (the host build
+// is used for tests and for the labelled "not RELIC" CPU baseline).
+//
+// Representation: Montgomery form, 9 limbs x 29 bits (R = 2^261), limbs normalised (< 2^29),
+// value < 2q ("reduced", q = the modulus).  Multiplication is FIPS (finely integrated product
+// scanning): column k accumulates every a_i b_j and m_j q_(k-j) into one 64-bit accumulator
+// with v_mad_u64_u32, so there is no per-product carry chain: 81 + 81 mads per multiply,
+// 45 + 81 per square.  Column bound: 18 products < 2^58 plus carry < 2^63 (normalised inputs).
+// Output of mont_mul for inputs < 2q is < 2q (R = 2^261 > 4q).
+#pragma once
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define BN_HD __host__ __device__ __forceinline__
+// Heavy tower/curve/pairing routines are compiled once and called (objects pass through
+// scratch): fully inlining the pairing into its kernels makes the code object explode
+// (a > 40 min compile measured); field-level ops stay inlined inside each routine.
+#define BN_HDN __host__ __device__ __noinline__
+#else
+#define BN_HD inline
+#define BN_HDN inline
+#endif
+
+#define BN_LIMBS 9
+#define BN_MASK 0x1fffffffu
+
+struct FpParams {  // p = 36u^4 + 36u^3 + 24u^2 + 6u + 1, u = -(2^62 + 2^55 + 1)
+  static constexpr uint32_t Q[9] = {0x00000013u, 0x18000000u, 0x000004e9u, 0x02000000u, 0x00008612u,
+                                    0x06c00000u, 0x0006e8d1u, 0x10480000u, 0x00252364u};
+  static constexpr uint32_t NPRIME = 0x179435e5u;  // -q^-1 mod 2^29
+  static constexpr uint32_t R2[9] = {0x011cbcb5u, 0x18ce8a6eu, 0x03e367a8u, 0x097460e6u, 0x124f515fu,
+                                     0x123f0d2au, 0x1e665acbu, 0x19981d1du, 0x0014cc78u};
+  static constexpr uint32_t ONE[9] = {0x1fffefacu, 0x1fffffffu, 0x1ffbc71eu, 0x07ffffffu, 0x1f8cc87au,
+                                      0x12ffffffu, 0x1a0fec35u, 0x021fffffu, 0x001595a0u};
+};
+struct FrParams {  // r = 36u^4 + 36u^3 + 18u^2 + 6u + 1 (the order of G1, G2, GT)
+  static constexpr uint32_t Q[9] = {0x0000000du, 0x08000000u, 0x00000428u, 0x1f000000u, 0x00007ff9u,
+                                    0x06c00000u, 0x0006e8d1u, 0x10480000u, 0x00252364u};
+  static constexpr uint32_t NPRIME = 0x1b13b13bu;
+  static constexpr uint32_t R2[9] = {0x0a9e505bu, 0x0ad6de81u, 0x1eb35b9fu, 0x1d971118u, 0x1c3bba09u,
+                                     0x05eebab4u, 0x00bd2046u, 0x0b27c81au, 0x001934a7u};
+  static constexpr uint32_t ONE[9] = {0x1ffff4d4u, 0x1fffffffu, 0x1ffc6d68u, 0x1bffffffu, 0x1f92052eu,
+                                      0x12ffffffu, 0x1a0fec35u, 0x021fffffu, 0x001595a0u};
+};
+
+template <class F>
+struct Fe {
+  uint32_t v[BN_LIMBS];
+};
+using fp = Fe<FpParams>;
+using fr = Fe<FrParams>;
+
+BN_HD uint64_t bn_mad(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * (uint64_t)b + c; }
+
+template <class F>
+BN_HD void f_zero(Fe<F>& r) {
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) r.v[i] = 0;
+}
+template <class F>
+BN_HD void f_one(Fe<F>& r) {
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) r.v[i] = F::ONE[i];
+}
+
+// r = a * b * 2^-261 mod q (a, b < 2q, normalised)  ->  r < 2q, normalised
+template <class F>
+BN_HD void f_mul(Fe<F>& r, const Fe<F>& a, const Fe<F>& b) {
+  uint32_t m[BN_LIMBS], o[BN_LIMBS];
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * BN_LIMBS - 1; k++) {
+#pragma unroll
+    for (int i = 0; i < BN_LIMBS; i++) {
+      const int j = k - i;
+      if (j >= 0 && j < BN_LIMBS) acc = bn_mad(a.v[i], b.v[j], acc);
+    }
+#pragma unroll
+    for (int j = 0; j < BN_LIMBS; j++) {
+      const int i = k - j;
+      if (j < k && j < BN_LIMBS && i >= 0 && i < BN_LIMBS) acc = bn_mad(m[j], F::Q[i], acc);
+    }
+    if (k < BN_LIMBS) {
+      m[k] = ((uint32_t)acc * F::NPRIME) & BN_MASK;
+      acc = bn_mad(m[k], F::Q[0], acc);  // low 29 bits become 0
+      acc >>= 29;
+    } else {
+      o[k - BN_LIMBS] = (uint32_t)acc & BN_MASK;
+      acc >>= 29;
+    }
+  }
+  o[BN_LIMBS - 1] = (uint32_t)acc;  // final carry = top limb (value < 2q < 2^255)
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) r.v[i] = o[i];
+}
+
+template <class F>
+BN_HD void f_sqr(Fe<F>& r, const Fe<F>& a) {
+  uint32_t a2[BN_LIMBS], m[BN_LIMBS], o[BN_LIMBS];
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) a2[i] = a.v[i] << 1;
+  uint64_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < 2 * BN_LIMBS - 1; k++) {
+#pragma unroll
+    for (int i = 0; i < BN_LIMBS; i++) {
+      const int j = k - i;
+      if (j > i && j < BN_LIMBS) acc = bn_mad(a2[i], a.v[j], acc);
+    }
+    if ((k & 1) == 0 && (k >> 1) < BN_LIMBS) acc = bn_mad(a.v[k >> 1], a.v[k >> 1], acc);
+#pragma unroll
+    for (int j = 0; j < BN_LIMBS; j++) {
+      const int i = k - j;
+      if (j < k && j < BN_LIMBS && i >= 0 && i < BN_LIMBS) acc = bn_mad(m[j], F::Q[i], acc);
+    }
+    if (k < BN_LIMBS) {
+      m[k] = ((uint32_t)acc * F::NPRIME) & BN_MASK;
+      acc = bn_mad(m[k], F::Q[0], acc);
+      acc >>= 29;
+    } else {
+      o[k - BN_LIMBS] = (uint32_t)acc & BN_MASK;
+      acc >>= 29;
+    }
+  }
+  o[BN_LIMBS - 1] = (uint32_t)acc;  // final carry = top limb (value < 2q < 2^255)
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) r.v[i] = o[i];
+}
+
+// t = a - c*q for the selected c (c = 0 or 1 times q or 2q via `sub`), keep if non-negative
+template <class F>
+BN_HD void f_csub(Fe<F>& a, const uint32_t* s) {  // a -= s if a >= s (a, s normalised)
+  uint32_t t[BN_LIMBS];
+  int32_t br = 0;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    int32_t d = (int32_t)a.v[i] - (int32_t)s[i] + br;
+    t[i] = (uint32_t)d & BN_MASK;
+    br = d >> 29;  // 0 or -1
+  }
+  const bool keep = br == 0;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) a.v[i] = keep ? t[i] : a.v[i];
+}
+
+template <class F>
+BN_HD void f_2q(uint32_t* s) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    uint32_t x = (F::Q[i] << 1) + c;
+    s[i] = x & BN_MASK;
+    c = x >> 29;
+  }
+}
+
+// r = a + b mod (2q range): a, b < 2q -> r < 2q
+template <class F>
+BN_HD void f_add(Fe<F>& r, const Fe<F>& a, const Fe<F>& b) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    uint32_t x = a.v[i] + b.v[i] + c;
+    r.v[i] = x & BN_MASK;
+    c = x >> 29;
+  }
+  uint32_t q2[BN_LIMBS];
+  f_2q<F>(q2);
+  f_csub(r, q2);
+}
+
+// r = a - b: a, b < 2q -> r < 2q
+template <class F>
+BN_HD void f_sub(Fe<F>& r, const Fe<F>& a, const Fe<F>& b) {
+  uint32_t q2[BN_LIMBS];
+  f_2q<F>(q2);
+  int32_t br = 0;
+  uint32_t t[BN_LIMBS];
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    int32_t d = (int32_t)a.v[i] - (int32_t)b.v[i] + br;
+    t[i] = (uint32_t)d & BN_MASK;
+    br = d >> 29;
+  }
+  // if negative add 2q
+  const uint32_t msk = br ? BN_MASK : 0u;
+  uint32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    uint32_t x = t[i] + (q2[i] & msk) + c;
+    r.v[i] = x & BN_MASK;
+    c = x >> 29;
+  }
+}
+
+template <class F>
+BN_HD void f_neg(Fe<F>& r, const Fe<F>& a) {
+  Fe<F> z;
+  f_zero(z);
+  f_sub(r, z, a);
+}
+
+template <class F>
+BN_HD void f_dbl(Fe<F>& r, const Fe<F>& a) {
+  f_add(r, a, a);
+}
+
+// canonical value in [0, q) (still Montgomery form)
+template <class F>
+BN_HD void f_canon(Fe<F>& a) {
+  f_csub(a, F::Q);
+}
+
+template <class F>
+BN_HD bool f_eq(const Fe<F>& a, const Fe<F>& b) {
+  Fe<F> x = a, y = b;
+  f_canon(x);
+  f_canon(y);
+  uint32_t d = 0;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) d |= x.v[i] ^ y.v[i];
+  return d == 0;
+}
+
+template <class F>
+BN_HD bool f_is_zero(const Fe<F>& a) {
+  Fe<F> x = a;
+  f_canon(x);
+  uint32_t d = 0;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) d |= x.v[i];
+  return d == 0;
+}
+
+// integer (8 little-endian 32-bit words, < q) -> Montgomery
+template <class F>
+BN_HD void f_from_words(Fe<F>& r, const uint32_t* w) {
+  Fe<F> t, r2;
+  t.v[0] = w[0] & BN_MASK;
+  t.v[1] = ((w[0] >> 29) | (w[1] << 3)) & BN_MASK;
+  t.v[2] = ((w[1] >> 26) | (w[2] << 6)) & BN_MASK;
+  t.v[3] = ((w[2] >> 23) | (w[3] << 9)) & BN_MASK;
+  t.v[4] = ((w[3] >> 20) | (w[4] << 12)) & BN_MASK;
+  t.v[5] = ((w[4] >> 17) | (w[5] << 15)) & BN_MASK;
+  t.v[6] = ((w[5] >> 14) | (w[6] << 18)) & BN_MASK;
+  t.v[7] = ((w[6] >> 11) | (w[7] << 21)) & BN_MASK;
+  t.v[8] = (w[7] >> 8);
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) r2.v[i] = F::R2[i];
+  f_mul(r, t, r2);
+}
+
+// Montgomery -> canonical integer words
+template <class F>
+BN_HD void f_to_words(uint32_t* w, const Fe<F>& a) {
+  Fe<F> one, t;
+  f_zero(one);
+  one.v[0] = 1;
+  f_mul(t, a, one);
+  f_canon(t);
+  w[0] = t.v[0] | (t.v[1] << 29);
+  w[1] = (t.v[1] >> 3) | (t.v[2] << 26);
+  w[2] = (t.v[2] >> 6) | (t.v[3] << 23);
+  w[3] = (t.v[3] >> 9) | (t.v[4] << 20);
+  w[4] = (t.v[4] >> 12) | (t.v[5] << 17);
+  w[5] = (t.v[5] >> 15) | (t.v[6] << 14);
+  w[6] = (t.v[6] >> 18) | (t.v[7] << 11);
+  w[7] = (t.v[7] >> 21) | (t.v[8] << 8);
+}
+
+// r = a^e, e given as 8 little-endian words (left-to-right binary, runtime loop)
+template <class F>
+BN_HDN void f_pow(Fe<F>& r, const Fe<F>& a, const uint32_t* e) {
+  Fe<F> acc;
+  f_one(acc);
+  for (int i = 255; i >= 0; i--) {
+    f_sqr(acc, acc);
+    if ((e[i >> 5] >> (i & 31)) & 1) f_mul(acc, acc, a);
+  }
+  r = acc;
+}
+
+// exponents as words
+struct FpExp {
+  // p - 2
+  static constexpr uint32_t PM2[8] = {0x00000011u, 0xa7000000u, 0x00000013u, 0x61210000u,
+                                      0x00000008u, 0xba344d80u, 0x40000001u, 0x25236482u};
+  // (p + 1) / 4
+  static constexpr uint32_t SQRT[8] = {0x00000005u, 0xe9c00000u, 0x00000004u, 0x18484000u,
+                                       0x00000002u, 0x6e8d1360u, 0x90000000u, 0x0948d920u};
+  // r - 2 (inversion in Fr)
+  static constexpr uint32_t RM2[8] = {0x0000000bu, 0xa1000000u, 0x00000010u, 0xff9f8000u,
+                                      0x00000007u, 0xba344d80u, 0x40000001u, 0x25236482u};
+};
+
+// exponent word arrays must live in registers on the device: copy from the constexpr table
+template <class F>
+BN_HD void f_inv_fp(Fe<F>& r, const Fe<F>& a) {
+  uint32_t e[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) e[i] = FpExp::PM2[i];
+  f_pow(r, a, e);
+}
+
+// square root for p = 3 mod 4: y = a^((p+1)/4); returns false if a is not a square
+BN_HDN bool fp_sqrt(fp& y, const fp& a) {
+  uint32_t e[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) e[i] = FpExp::SQRT[i];
+  f_pow(y, a, e);
+  fp t;
+  f_sqr(t, y);
+  return f_eq(t, a);
+}
+
+BN_HDN void fp_inv(fp& r, const fp& a) { f_inv_fp(r, a); }
+
+BN_HDN void fr_inv(fr& r, const fr& a) {
+  uint32_t e[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) e[i] = FpExp::RM2[i];
+  f_pow(r, a, e);
+}

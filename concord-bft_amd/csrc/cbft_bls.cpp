@@ -1,0 +1,219 @@
+// libcbft_hipcrypto, BLS BN-P254 half of the C ABI (include/cbft_hipcrypto.h).
+//
+// Mirrors threshsign's verifier/accumulator work: key sets are
+// decoded and their G2 Miller-loop lines precomputed once (cbft_bls_load_keys, like
+// BlsThresholdVerifier's constructor holding the decoded keys); every per-certificate call
+// runs on the GPU: hash-to-G1, share decompression + pairing checks, Lagrange coefficients,
+// the multi-scalar multiplication, the combined-signature check.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "bls_kernels.h"
+#include "cbft_internal.h"
+
+#define BLS_MAX_SHARES 2048  // IThresholdVerifier::maxSize_ (IThresholdVerifier.h:36)
+
+static int bls_gen_lines(cbft_ctx* c) {
+  if (c->bls_gen_lines.p) return CBFT_OK;
+  CBFT_HIP(c->bls_gen_lines.reserve(cbft_bls_lines_words_per_key() * 4));
+  CBFT_HIP(cbft_bls_launch_gen_lines(c->bls_gen_lines.as<uint32_t>(), c->stream));
+  return CBFT_OK;
+}
+
+static int bls_upload_msg_hash(cbft_ctx* c, const uint8_t* msg, uint32_t len) {
+  CBFT_HIP(c->bls_msg.reserve(len + 1));
+  CBFT_HIP(c->bls_H.reserve(19 * 4));
+  if (len) CBFT_HIP(hipMemcpyAsync(c->bls_msg.p, msg, len, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_hash(c->bls_msg.as<uint8_t>(), len, c->bls_H.as<uint32_t>(), c->stream));
+  return CBFT_OK;
+}
+
+static BlsKeySet* find_set(cbft_ctx* c, uint32_t id) {
+  auto it = c->bls_sets.find(id);
+  return it == c->bls_sets.end() ? nullptr : &it->second;
+}
+
+extern "C" {
+
+int cbft_bls_load_keys(cbft_ctx* c, const uint8_t* pk65, const uint8_t* vks65, uint32_t n, uint32_t* out_id) {
+  if (!c || !pk65 || !out_id || (n && !vks65) || n > BLS_MAX_SHARES) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  CBFT_HIP(hipSetDevice(c->device));
+  int rc = bls_gen_lines(c);
+  if (rc) return rc;
+  BlsKeySet ks;
+  ks.n = n;
+  const size_t nk = (size_t)n + 1;  // slot 0 = group PK
+  CBFT_HIP(ks.keys65.reserve(nk * 65));
+  CBFT_HIP(ks.lines.reserve(nk * cbft_bls_lines_words_per_key() * 4));
+  CBFT_HIP(ks.ok.reserve(nk));
+  CBFT_HIP(hipMemcpyAsync(ks.keys65.p, pk65, 65, hipMemcpyHostToDevice, c->stream));
+  if (n)
+    CBFT_HIP(hipMemcpyAsync(ks.keys65.as<uint8_t>() + 65, vks65, (size_t)n * 65, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_keys(ks.keys65.as<uint8_t>(), (uint32_t)nk, ks.lines.as<uint32_t>(), ks.ok.as<uint8_t>(),
+                                c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  uint32_t id = c->next_bls_id++;
+  c->bls_sets.emplace(id, std::move(ks));
+  *out_id = id;
+  return CBFT_OK;
+}
+
+int cbft_bls_unload_keys(cbft_ctx* c, uint32_t id) {
+  if (!c) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  BlsKeySet* ks = find_set(c, id);
+  if (!ks) return CBFT_EINVAL;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  ks->keys65.release();
+  ks->lines.release();
+  ks->ok.release();
+  c->bls_sets.erase(id);
+  return CBFT_OK;
+}
+
+int cbft_bls_key_status(cbft_ctx* c, uint32_t id, uint8_t* out_ok) {
+  if (!c || !out_ok) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  BlsKeySet* ks = find_set(c, id);
+  if (!ks) return CBFT_EINVAL;
+  CBFT_HIP(hipSetDevice(c->device));
+  CBFT_HIP(hipMemcpy(out_ok, ks->ok.p, ks->n + 1, hipMemcpyDeviceToHost));
+  return CBFT_OK;
+}
+
+int cbft_bls_hash_to_g1(cbft_ctx* c, const uint8_t* msg, uint32_t len, uint8_t* out33) {
+  if (!c || !out33 || (len && !msg)) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  CBFT_HIP(hipSetDevice(c->device));
+  int rc = bls_upload_msg_hash(c, msg, len);
+  if (rc) return rc;
+  // compress through the MSM finish kernel path: reuse combine with one unit share is
+  // overkill; instead read H back and compress on the device via a 1-share multisig combine
+  CBFT_HIP(c->bls_use.reserve(1));
+  CBFT_HIP(c->bls_partial.reserve(27 * 4));
+  CBFT_HIP(c->bls_out.reserve(33));
+  uint8_t one = 1;
+  CBFT_HIP(hipMemcpyAsync(c->bls_use.p, &one, 1, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_combine(c->bls_H.as<uint32_t>(), nullptr, c->bls_use.as<uint8_t>(), 1, 1, nullptr,
+                                   c->bls_partial.as<uint32_t>(), c->bls_out.as<uint8_t>(), nullptr, c->stream));
+  CBFT_HIP(hipMemcpyAsync(out33, c->bls_out.p, 33, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  return CBFT_OK;
+}
+
+// Stage k shares on the device and run the parse (+ verify) kernel.
+static int bls_shares(cbft_ctx* c, BlsKeySet* ks, const uint8_t* shares37, uint32_t k, int do_verify) {
+  CBFT_HIP(c->bls_shares.reserve((size_t)k * 37));
+  CBFT_HIP(c->bls_valid.reserve(k));
+  CBFT_HIP(c->bls_sig.reserve((size_t)k * BLS_SIG_WORDS * 4));
+  CBFT_HIP(c->bls_ids.reserve((size_t)k * 4));
+  CBFT_HIP(hipMemcpyAsync(c->bls_shares.p, shares37, (size_t)k * 37, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_share_verify(
+      c->bls_shares.as<uint8_t>(), k, ks ? ks->n : BLS_MAX_SHARES, c->bls_H.as<uint32_t>(),
+      ks ? ks->lines.as<uint32_t>() + cbft_bls_lines_words_per_key() : nullptr, ks ? ks->ok.as<uint8_t>() + 1 : nullptr,
+      c->bls_gen_lines.as<uint32_t>(), do_verify, c->bls_valid.as<uint8_t>(), c->bls_sig.as<uint32_t>(),
+      c->bls_ids.as<uint32_t>(), c->stream));
+  return CBFT_OK;
+}
+
+int cbft_bls_verify_shares(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, const uint8_t* shares37,
+                           uint32_t k, uint8_t* valid_bitmap) {
+  if (!c || (k && (!shares37 || !valid_bitmap)) || (len && !msg) || k > BLS_MAX_SHARES) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  BlsKeySet* ks = find_set(c, id);
+  if (!ks) return CBFT_EINVAL;
+  if (!k) return CBFT_OK;
+  CBFT_HIP(hipSetDevice(c->device));
+  int rc = bls_gen_lines(c);
+  if (!rc) rc = bls_upload_msg_hash(c, msg, len);
+  if (!rc) rc = bls_shares(c, ks, shares37, k, 1);
+  if (rc) return rc;
+  std::vector<uint8_t> v(k);
+  CBFT_HIP(hipMemcpyAsync(v.data(), c->bls_valid.p, k, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  std::memset(valid_bitmap, 0, (k + 7) / 8);
+  for (uint32_t j = 0; j < k; j++)
+    if (v[j]) valid_bitmap[j >> 3] |= (uint8_t)(1u << (j & 7));
+  return CBFT_OK;
+}
+
+int cbft_bls_combine(cbft_ctx* c, const uint8_t* shares37, uint32_t k, int multisig, uint8_t* out33) {
+  if (!c || !out33 || !k || !shares37 || k > BLS_MAX_SHARES) return CBFT_EINVAL;
+  // distinct ids (the accumulators never hold two shares of one signer)
+  std::vector<uint8_t> seen(1u << 16, 0);
+  for (uint32_t j = 0; j < k; j++) {
+    const uint8_t* s = shares37 + 37 * (size_t)j;
+    const uint32_t sid = ((uint32_t)s[0] << 24) | ((uint32_t)s[1] << 16) | ((uint32_t)s[2] << 8) | s[3];
+    if (sid == 0 || sid > BLS_MAX_SHARES || seen[sid]) return CBFT_EINVAL;
+    seen[sid] = 1;
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  CBFT_HIP(hipSetDevice(c->device));
+  int rc = bls_shares(c, nullptr, shares37, k, 0);
+  if (rc) return rc;
+  CBFT_HIP(c->bls_lambda.reserve((size_t)k * 8 * 4));
+  CBFT_HIP(c->bls_partial.reserve((size_t)((k + 63) / 64) * BLS_JAC_WORDS * 4));
+  CBFT_HIP(c->bls_out.reserve(33));
+  // every share decoded? (the parse kernel wrote valid = decodable && id in range)
+  std::vector<uint8_t> v(k);
+  CBFT_HIP(hipMemcpyAsync(v.data(), c->bls_valid.p, k, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  for (uint32_t j = 0; j < k; j++)
+    if (!v[j]) return CBFT_EINVAL;
+  CBFT_HIP(cbft_bls_launch_combine(c->bls_sig.as<uint32_t>(), c->bls_ids.as<uint32_t>(), c->bls_valid.as<uint8_t>(),
+                                   k, multisig, c->bls_lambda.as<uint32_t>(), c->bls_partial.as<uint32_t>(),
+                                   c->bls_out.as<uint8_t>(), nullptr, c->stream));
+  CBFT_HIP(hipMemcpyAsync(out33, c->bls_out.p, 33, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  return CBFT_OK;
+}
+
+static int bls_verify_with_lines(cbft_ctx* c, const uint8_t* sig33, const uint32_t* d_lines, const uint8_t* d_ok,
+                                 int* out_ok) {
+  CBFT_HIP(c->bls_shares.reserve(33));
+  CBFT_HIP(c->bls_out.reserve(33));
+  CBFT_HIP(hipMemcpyAsync(c->bls_shares.p, sig33, 33, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_verify(c->bls_H.as<uint32_t>(), c->bls_shares.as<uint8_t>(), d_lines, d_ok,
+                                  c->bls_gen_lines.as<uint32_t>(), c->bls_out.as<uint8_t>(), c->stream));
+  uint8_t r = 0;
+  CBFT_HIP(hipMemcpyAsync(&r, c->bls_out.p, 1, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  *out_ok = r ? 1 : 0;
+  return CBFT_OK;
+}
+
+int cbft_bls_verify(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, const uint8_t* sig33, int* out_ok) {
+  if (!c || !sig33 || !out_ok || (len && !msg)) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  BlsKeySet* ks = find_set(c, id);
+  if (!ks) return CBFT_EINVAL;
+  CBFT_HIP(hipSetDevice(c->device));
+  int rc = bls_gen_lines(c);
+  if (!rc) rc = bls_upload_msg_hash(c, msg, len);
+  if (rc) return rc;
+  return bls_verify_with_lines(c, sig33, ks->lines.as<uint32_t>(), ks->ok.as<uint8_t>(), out_ok);
+}
+
+int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, const uint8_t* sig33,
+                             const uint8_t* signers256, int* out_ok) {
+  if (!c || !sig33 || !signers256 || !out_ok || (len && !msg)) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  BlsKeySet* ks = find_set(c, id);
+  if (!ks) return CBFT_EINVAL;
+  CBFT_HIP(hipSetDevice(c->device));
+  int rc = bls_gen_lines(c);
+  if (!rc) rc = bls_upload_msg_hash(c, msg, len);
+  if (rc) return rc;
+  CBFT_HIP(c->bls_bitmap.reserve(256));
+  CBFT_HIP(c->bls_ms_lines.reserve(cbft_bls_lines_words_per_key() * 4));
+  CBFT_HIP(c->bls_ms_ok.reserve(1));
+  CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_g2_sum(ks->keys65.as<uint8_t>() + 65, ks->n, c->bls_bitmap.as<uint8_t>(),
+                                  c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), c->stream));
+  return bls_verify_with_lines(c, sig33, c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), out_ok);
+}
+
+}  // extern "C"

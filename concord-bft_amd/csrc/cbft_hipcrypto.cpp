@@ -16,81 +16,18 @@
 #include <unordered_map>
 #include <vector>
 
+#include "cbft_internal.h"
 #include "ed25519_verify.h"
-
-namespace {
-
-struct DevBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  // (re)allocate to at least `bytes`; contents are not preserved
-  hipError_t reserve(size_t bytes) {
-    if (bytes <= cap) return hipSuccess;
-    if (p) {
-      (void)hipDeviceSynchronize();  // an earlier async launch may still read the old buffer
-      (void)hipFree(p);
-    }
-    p = nullptr;
-    cap = 0;
-    size_t want = std::max<size_t>(bytes, 4096);
-    hipError_t e = hipMalloc(&p, want);
-    if (e != hipSuccess) {
-      p = nullptr;
-      return e;
-    }
-    cap = want;
-    return hipSuccess;
-  }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-  }
-  template <class T>
-  T* as() const {
-    return static_cast<T*>(p);
-  }
-};
-
-struct KeyTable {
-  uint32_t nkeys = 0;
-  DevBuf pk, comb, aok;  // raw keys, per-key comb tables of -A, decode status
-};
-
-}  // namespace
-
-struct cbft_ctx {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  std::mutex mu;
-  DevBuf base_table, base_comb;
-  std::unordered_map<uint32_t, KeyTable> tables;
-  uint32_t next_table_id = 1;
-  // per-batch work buffers
-  DevBuf h, flags, xyz, verdicts;
-  DevBuf sig, msg, off, len, kidx, pk, ps_tbl, ps_aok;
-  std::vector<uint64_t> host_verdicts;
-  // profiling: events around K1 (hash), K3 (ladder), K4 (finish) of the last verify
-  bool profiling = false;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
-  bool ev_valid = false;
-};
 
 // Last failure of this thread, for cbft_last_error() (diagnostics only).
 static thread_local char g_last_error[256];
 
-static int fail(hipError_t e, const char* what, int line) {
-  snprintf(g_last_error, sizeof g_last_error, "%s failed at cbft_hipcrypto.cpp:%d: %s (%d)", what, line,
-           hipGetErrorString(e), (int)e);
+int cbft_fail(hipError_t e, const char* what, const char* file, int line) {
+  snprintf(g_last_error, sizeof g_last_error, "%s failed at %s:%d: %s (%d)", what, file, line, hipGetErrorString(e),
+           (int)e);
   (void)hipGetLastError();
   return e == hipErrorOutOfMemory ? CBFT_ENOMEM : CBFT_EIO;
 }
-
-#define CBFT_HIP(expr)                                          \
-  do {                                                          \
-    hipError_t _e = (expr);                                     \
-    if (_e != hipSuccess) return fail(_e, #expr, __LINE__);     \
-  } while (0)
 
 static int reserve_work(cbft_ctx* c, size_t n) {
   CBFT_HIP(c->h.reserve(n * 8 * sizeof(uint32_t)));
@@ -203,6 +140,15 @@ void cbft_close(cbft_ctx* c) {
     kv.second.comb.release();
     kv.second.aok.release();
   }
+  for (auto& kv : c->bls_sets) {
+    kv.second.keys65.release();
+    kv.second.lines.release();
+    kv.second.ok.release();
+  }
+  for (DevBuf* b : {&c->bls_gen_lines, &c->bls_msg, &c->bls_H, &c->bls_shares, &c->bls_valid, &c->bls_sig,
+                    &c->bls_ids, &c->bls_use, &c->bls_lambda, &c->bls_partial, &c->bls_out, &c->bls_ms_lines,
+                    &c->bls_ms_ok, &c->bls_bitmap})
+    b->release();
   for (DevBuf* b : {&c->base_table, &c->base_comb, &c->h, &c->flags, &c->xyz, &c->verdicts, &c->sig, &c->msg, &c->off, &c->len,
                     &c->kidx, &c->pk, &c->ps_tbl, &c->ps_aok})
     b->release();
@@ -257,7 +203,7 @@ int cbft_ed25519_load_keys(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, uint3
       kt.pk.release();
       kt.comb.release();
       kt.aok.release();
-      return fail(e, "hipMalloc(comb tmp)", __LINE__);
+      return cbft_fail(e, "hipMalloc(comb tmp)", __FILE__, __LINE__);
     }
     e = hipMemcpyAsync(kt.pk.p, pk, (size_t)nkeys * 32, hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess)
@@ -269,7 +215,7 @@ int cbft_ed25519_load_keys(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, uint3
       kt.pk.release();
       kt.comb.release();
       kt.aok.release();
-      return fail(e, "comb table build", __LINE__);
+      return cbft_fail(e, "comb table build", __FILE__, __LINE__);
     }
   }
   uint32_t id = c->next_table_id++;

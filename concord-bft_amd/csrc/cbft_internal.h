@@ -1,0 +1,87 @@
+// Internal state of libcbft_hipcrypto shared by the Ed25519 (cbft_hipcrypto.cpp) and BLS
+// (cbft_bls.cpp) halves of the C ABI.  Not installed; not part of the ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <unordered_map>
+#include <vector>
+
+#include "cbft_hipcrypto.h"
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  // (re)allocate to at least `bytes`; contents are not preserved
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) {
+      (void)hipDeviceSynchronize();  // an earlier async launch may still read the old buffer
+      (void)hipFree(p);
+    }
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 4096);
+    hipError_t e = hipMalloc(&p, want);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    cap = want;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+struct KeyTable {
+  uint32_t nkeys = 0;
+  DevBuf pk, comb, aok;  // raw keys, per-key comb tables of -A, decode status
+};
+
+// BLS verifier key set: group public key + n share verification keys, decoded and with their
+// Miller-loop lines precomputed (slot 0 = PK, slot i = vk_i)
+struct BlsKeySet {
+  uint32_t n = 0;
+  DevBuf keys65, lines, ok;
+};
+
+struct cbft_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  DevBuf base_table, base_comb;
+  std::unordered_map<uint32_t, KeyTable> tables;
+  uint32_t next_table_id = 1;
+  // per-batch work buffers
+  DevBuf h, flags, xyz, verdicts;
+  DevBuf sig, msg, off, len, kidx, pk, ps_tbl, ps_aok;
+  std::vector<uint64_t> host_verdicts;
+  // profiling: events around K1 (hash), K3 (ladder), K4 (finish) of the last verify
+  bool profiling = false;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  bool ev_valid = false;
+  // BLS
+  std::unordered_map<uint32_t, BlsKeySet> bls_sets;
+  uint32_t next_bls_id = 1;
+  DevBuf bls_gen_lines, bls_msg, bls_H, bls_shares, bls_valid, bls_sig, bls_ids, bls_use, bls_lambda,
+      bls_partial, bls_out, bls_ms_lines, bls_ms_ok, bls_bitmap;
+};
+
+int cbft_fail(hipError_t e, const char* what, const char* file, int line);
+
+#define CBFT_HIP(expr)                                                          \
+  do {                                                                          \
+    hipError_t _e = (expr);                                                     \
+    if (_e != hipSuccess) return cbft_fail(_e, #expr, __FILE__, __LINE__);      \
+  } while (0)

@@ -106,6 +106,49 @@ int cbft_sync(cbft_ctx* ctx);
 int cbft_set_profiling(cbft_ctx* ctx, int enable);
 int cbft_stage_times_ms(cbft_ctx* ctx, float* out, int nout);
 
+/* ------------------------------------------------------------- BLS BN-P254 (threshsign) ------
+ * RELIC "BN_P254" curve (threshsign/src/bls/relic/Library.cpp:51,72): G1 compressed = 33 bytes,
+ * G2 compressed = 65 bytes, share = 4-byte big-endian id || 33-byte G1 (BlsThresholdSigner.cpp:
+ * 32-47), signer bitmap = 256 bytes, bit (id-1) LSB-first (VectorOfShares.cpp:136-161).
+ * Encodings and hash-to-G1 follow RELIC as restated in oracle/bn254_ref.py (parity with RELIC
+ * itself is unpinned: RELIC is not available offline). */
+#define CBFT_BLS_G1_BYTES 33
+#define CBFT_BLS_G2_BYTES 65
+#define CBFT_BLS_SHARE_BYTES 37
+#define CBFT_BLS_SIGNERS_BYTES 256
+
+/* Load a verifier key set: the group public key and n share verification keys vk_1..vk_n
+ * (65 bytes each).  Decoding, subgroup checks and Miller-loop line precomputation run once
+ * here (BlsThresholdVerifier's constructor, BlsThresholdVerifier.cpp:36-51).  Keys that do not
+ * decode are accepted and make every check against them fail (see cbft_bls_key_status). */
+int cbft_bls_load_keys(cbft_ctx* ctx, const uint8_t* pk65, const uint8_t* vks65, uint32_t n, uint32_t* out_keyset);
+int cbft_bls_unload_keys(cbft_ctx* ctx, uint32_t keyset);
+/* out_ok: n + 1 bytes, [0] = PK decoded, [i] = vk_i decoded */
+int cbft_bls_key_status(cbft_ctx* ctx, uint32_t keyset, uint8_t* out_ok);
+
+/* H = g1_map(msg) as 33 bytes (RELIC ep_map, 2019: SHA-256, try-and-increment). */
+int cbft_bls_hash_to_g1(cbft_ctx* ctx, const uint8_t* msg, uint32_t len, uint8_t* out33);
+
+/* Verify k shares against msg: bit j of valid_bitmap (ceil(k/8) bytes) = 1 iff share j decodes,
+ * its id is in [1, n] and e(H(msg), vk_id) == e(sigma, g2)
+ * (BlsAccumulatorBase::verifyShare, BlsAccumulatorBase.cpp:62-84). */
+int cbft_bls_verify_shares(cbft_ctx* ctx, uint32_t keyset, const uint8_t* msg, uint32_t len, const uint8_t* shares37,
+                           uint32_t k, uint8_t* valid_bitmap);
+
+/* Combine k shares with distinct ids: threshold (multisig = 0): sum lambda_i sigma_i with
+ * lambda_i = prod_{j != i} j/(j - i) mod r over the given ids (BlsThresholdAccumulator,
+ * LagrangeInterpolation.cpp:202-292, FastMultExp.cpp:26-59); multisig (multisig = 1):
+ * sum sigma_i (BlsMultisigAccumulator.cpp:57-65).  out33 = compressed G1.  CBFT_EINVAL if an id
+ * repeats or a share does not decode. */
+int cbft_bls_combine(cbft_ctx* ctx, const uint8_t* shares37, uint32_t k, int multisig, uint8_t* out33);
+
+/* e(H(msg), PK) == e(sig, g2) with the key set's group PK (BlsThresholdVerifier.cpp:69-96). */
+int cbft_bls_verify(cbft_ctx* ctx, uint32_t keyset, const uint8_t* msg, uint32_t len, const uint8_t* sig33,
+                    int* out_ok);
+/* Multisig: PK = sum of vk_i over the signer bitmap (BlsMultisigVerifier.cpp:75-105). */
+int cbft_bls_verify_multisig(cbft_ctx* ctx, uint32_t keyset, const uint8_t* msg, uint32_t len, const uint8_t* sig33,
+                             const uint8_t* signers256, int* out_ok);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,148 @@
+// Host build of the BN-P254 device code (concord-bft_amd/csrc/bn254_*.h), exposed to the
+// Python tests through ctypes: the SAME source that runs on gfx950, checked on the CPU against
+// oracle/bn254_ref.py.  Test infrastructure; also the labelled "not RELIC" CPU baseline.
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "bls_ops.h"
+
+static void fp12_flat(uint8_t* out, const fp12& x) {  // 12 x 32-byte big-endian, oracle basis
+  const fp2* e[6] = {&x.c0.c0, &x.c1.c0, &x.c0.c1, &x.c1.c1, &x.c0.c2, &x.c1.c2};
+  for (int k = 0; k < 6; k++) {
+    fp lo;
+    f_sub(lo, e[k]->a, e[k]->b);
+    uint32_t w[8];
+    f_to_words(w, lo);
+    words_to_be32(out + 32 * k, w);
+    f_to_words(w, e[k]->b);
+    words_to_be32(out + 32 * (k + 6), w);
+  }
+}
+
+extern "C" {
+
+int shim_g1_decompress(const uint8_t* in33, uint8_t* out64) {
+  g1a a;
+  if (!g1_decompress(a, in33)) return 0;
+  uint32_t w[8];
+  f_to_words(w, a.x);
+  words_to_be32(out64, w);
+  f_to_words(w, a.y);
+  words_to_be32(out64 + 32, w);
+  return a.inf ? 2 : 1;
+}
+
+void shim_g1_mul(const uint8_t* in33, const uint8_t* kbe, uint8_t* out33) {
+  g1a a;
+  g1_decompress(a, in33);
+  g1j p, r;
+  g1_from_affine(p, a);
+  uint32_t k[8];
+  be32_to_words(k, kbe);
+  g1_mul(r, p, k);
+  g1a o;
+  g1_to_affine(o, r);
+  g1_compress(out33, o);
+}
+
+int shim_g2_decompress(const uint8_t* in65, uint8_t* out65) {
+  g2a q;
+  if (!g2_decompress(q, in65)) return 0;
+  g2_compress(out65, q);
+  return 1;
+}
+
+void shim_g1_map(const uint8_t* msg, uint32_t len, uint8_t* out33) {
+  g1a h;
+  g1_map(h, msg, len);
+  g1_compress(out33, h);
+}
+
+// full pairing value e(P, Q) in the oracle's flat Fp12 basis (12 x 32 bytes)
+int shim_pairing(const uint8_t* p33, const uint8_t* q65, uint8_t* out384) {
+  g1a P;
+  g2a Q;
+  if (!g1_decompress(P, p33) || !g2_decompress(Q, q65)) return 0;
+  std::vector<uint32_t> lines(BN_ATE_LINES * BN_LINE_WORDS);
+  g2_precompute_lines(lines.data(), Q);
+  const uint32_t* l[1] = {lines.data()};
+  fp12 f, e;
+  miller_multi<1>(f, &P, l);
+  final_exp(e, f);
+  fp12_flat(out384, e);
+  return 1;
+}
+
+// e(P1, Q1) * e(P2, Q2) == 1 ?
+int shim_pairing_check2(const uint8_t* p1, const uint8_t* q1, const uint8_t* p2, const uint8_t* q2) {
+  g1a P[2];
+  g2a Q[2];
+  if (!g1_decompress(P[0], p1) || !g1_decompress(P[1], p2) || !g2_decompress(Q[0], q1) ||
+      !g2_decompress(Q[1], q2))
+    return -1;
+  std::vector<uint32_t> l0(BN_ATE_LINES * BN_LINE_WORDS), l1(BN_ATE_LINES * BN_LINE_WORDS);
+  g2_precompute_lines(l0.data(), Q[0]);
+  g2_precompute_lines(l1.data(), Q[1]);
+  const uint32_t* l[2] = {l0.data(), l1.data()};
+  return pairing_check<2>(P, l) ? 1 : 0;
+}
+
+// vk = sk * g2 (65 bytes), sk big-endian 32 bytes
+void shim_g2_mul_gen(const uint8_t* skbe, uint8_t* out65) {
+  uint32_t k[8];
+  be32_to_words(k, skbe);
+  g2j P, acc;
+  fp2_load(P.X, Bn254Consts::G2X);
+  fp2_load(P.Y, Bn254Consts::G2Y);
+  fp2_one(P.Z);
+  fp2_one(acc.X);
+  fp2_one(acc.Y);
+  fp2_zero(acc.Z);
+  for (int i = 255; i >= 0; i--) {
+    g2_dbl_j(acc, acc);
+    if ((k[i >> 5] >> (i & 31)) & 1) g2_add_j(acc, acc, P);
+  }
+  g2a a;
+  g2_to_affine(a, acc);
+  g2_compress(out65, a);
+}
+
+// BlsThresholdSigner::signData: id (4 B big-endian) || sk * g1_map(msg)
+void shim_sign_share(const uint8_t* skbe, uint32_t id, const uint8_t* msg, uint32_t len, uint8_t* out37) {
+  g1a h;
+  g1_map(h, msg, len);
+  g1j p, r;
+  g1_from_affine(p, h);
+  uint32_t k[8];
+  be32_to_words(k, skbe);
+  g1_mul(r, p, k);
+  g1a a;
+  g1_to_affine(a, r);
+  out37[0] = (uint8_t)(id >> 24);
+  out37[1] = (uint8_t)(id >> 16);
+  out37[2] = (uint8_t)(id >> 8);
+  out37[3] = (uint8_t)id;
+  g1_compress(out37 + 4, a);
+}
+
+// many shares / keys on host threads (test-set generation)
+void shim_sign_shares_mt(const uint8_t* sks, const uint32_t* ids, uint32_t k, const uint8_t* msg, uint32_t len,
+                         uint8_t* out, int threads) {
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; t++)
+    th.emplace_back([=] {
+      for (uint32_t j = t; j < k; j += threads) shim_sign_share(sks + 32 * j, ids[j], msg, len, out + 37 * j);
+    });
+  for (auto& x : th) x.join();
+}
+void shim_g2_mul_gen_mt(const uint8_t* sks, uint32_t n, uint8_t* out, int threads) {
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; t++)
+    th.emplace_back([=] {
+      for (uint32_t j = t; j < n; j += threads) shim_g2_mul_gen(sks + 32 * j, out + 65 * j);
+    });
+  for (auto& x : th) x.join();
+}
+
+}  // extern "C"

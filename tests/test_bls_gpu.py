@@ -1,0 +1,125 @@
+"""GPU parity tests of the BLS BN-P254 path (threshsign) through the C ABI, against the Python
+oracle (oracle/bn254_ref.py) and the host build of the same code.  RELIC parity itself is
+unpinned; verdicts and combined signatures are fixed by the mathematics."""
+import random
+
+import numpy as np
+import pytest
+
+import bn254_ref as B
+import blsgen
+import cbft_hipcrypto as cb
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    c = cb.Context(device=0)
+    yield c
+    c.close()
+
+
+def test_hash_to_g1_matches_oracle(ctx):
+    for m in (b"", b"abc", bytes(32), bytes(range(32)), b"\xff" * 100):
+        assert ctx.bls_hash_to_g1(m) == B.g1_to_bytes(B.g1_map(m))
+
+
+def test_share_verification_verdicts(ctx):
+    n, k = 16, 11
+    sk, sks, pk, vks = blsgen.keyset(n, k, seed=11)
+    msg = bytes(range(100, 132))
+    good = blsgen.shares(sks, range(1, n + 1), msg)
+    cases = list(good)
+    cases.append(blsgen.doubled(good[2]))                       # Double() -> invalid
+    cases.append((4).to_bytes(4, "big") + good[2][4:])          # sk_3's point labelled id 4
+    cases.append(b"\x00\x00\x00\x00" + good[0][4:])             # id 0
+    cases.append((17).to_bytes(4, "big") + good[0][4:])         # id > n
+    cases.append(good[5][:4] + b"\x05" + good[5][5:])           # bad prefix
+    cases.append(good[5][:4] + b"\x02" + B.P.to_bytes(32, "big"))  # x >= p
+    kid = ctx.bls_load_keys(pk, vks)
+    try:
+        assert all(ctx.bls_key_status(kid, n))
+        got = ctx.bls_verify_shares(kid, msg, cases)
+    finally:
+        ctx.bls_unload_keys(kid)
+    H = B.g1_map(msg)
+    exp = []
+    for s in cases:
+        i = int.from_bytes(s[:4], "big")
+        try:
+            p = B.g1_from_bytes(s[4:])
+        except ValueError:
+            exp.append(False)
+            continue
+        exp.append(1 <= i <= n and B.verify_share(H, p, B.g2_from_bytes(vks[i - 1])))
+    assert got.tolist() == exp
+    assert sum(exp) == n
+
+
+@pytest.mark.parametrize("n,k", [(1, 1), (4, 3), (7, 5), (16, 11), (16, 16)])
+def test_threshold_combine_byte_identical(ctx, n, k):
+    sk, sks, pk, vks = blsgen.keyset(n, k, seed=n * 100 + k)
+    msg = bytes([n, k]) * 16
+    rng = random.Random(n + k)
+    ids = sorted(rng.sample(range(1, n + 1), k))
+    sh = blsgen.shares(sks, ids, msg)
+    comb = ctx.bls_combine(sh)
+    want = B.g1_to_bytes(B.combine_threshold({i: B.parse_share(s)[1] for i, s in zip(ids, sh)}))
+    assert comb == want == blsgen.sign_point(sk, msg)
+    kid = ctx.bls_load_keys(pk, vks)
+    try:
+        assert ctx.bls_verify(kid, msg, comb)
+        assert not ctx.bls_verify(kid, msg + b"x", comb)
+        assert not ctx.bls_verify(kid, msg, blsgen.doubled(b"\0\0\0\1" + comb)[4:])
+    finally:
+        ctx.bls_unload_keys(kid)
+
+
+def test_multisig_combine_and_verify(ctx):
+    n = 10
+    sk, sks, pk, vks = blsgen.keyset(n, n, seed=5)
+    msg = b"multisig digest 0123456789abcdef"
+    ids = [1, 2, 4, 5, 7, 9, 10]
+    sh = blsgen.shares(sks, ids, msg)
+    comb = ctx.bls_combine(sh, multisig=True)
+    acc = None
+    for s in sh:
+        acc = B.ec_add(acc, B.parse_share(s)[1], None)
+    assert comb == B.g1_to_bytes(acc)
+    kid = ctx.bls_load_keys(pk, vks)
+    try:
+        assert ctx.bls_verify_multisig(kid, msg, comb, B.signers_bitmap(ids))
+        assert not ctx.bls_verify_multisig(kid, msg, comb, B.signers_bitmap(ids[:-1]))
+    finally:
+        ctx.bls_unload_keys(kid)
+
+
+def test_combine_rejects_duplicate_ids(ctx):
+    sk, sks, pk, vks = blsgen.keyset(4, 3, seed=1)
+    sh = blsgen.shares(sks, [1, 2], b"m" * 32)
+    with pytest.raises(cb.CbftError):
+        ctx.bls_combine([sh[0], sh[0], sh[1]])
+
+
+def test_full_size_commit_certificate(ctx):
+    # BASELINE config #4: n = 1024 replicas, k = 2f+1 = 683, 10% of the shares doubled
+    n, k = 1024, 683
+    sk, sks, pk, vks = blsgen.keyset(n, k, seed=2024)
+    msg = bytes(range(32))
+    rng = random.Random(7)
+    ids = sorted(rng.sample(range(1, n + 1), 760))
+    sh = blsgen.shares(sks, ids, msg)
+    bad = set(rng.sample(range(len(sh)), 76))
+    for j in bad:
+        sh[j] = blsgen.doubled(sh[j])
+    kid = ctx.bls_load_keys(pk, vks)
+    try:
+        valid = ctx.bls_verify_shares(kid, msg, sh)
+        assert valid.tolist() == [j not in bad for j in range(len(sh))]
+        use = [s for j, s in enumerate(sh) if valid[j]][:k]
+        comb = ctx.bls_combine(use)
+        assert comb == blsgen.sign_point(sk, msg)
+        assert ctx.bls_verify(kid, msg, comb)
+    finally:
+        ctx.bls_unload_keys(kid)
