@@ -170,7 +170,7 @@ def main():
     ladder_ms = statistics.median(stage["ladder"])
     pipe_ms = sum(statistics.median(v) for v in stage.values())
     achieved = OPS_DSM * n / (ladder_ms * 1e-3)
-    kname = "ed25519_comb_ladder_kernel" if args.key_mode == "keytable" else "ed25519_ladder_kernel"
+    kname = "ed25519_comb8_ladder_kernel" if args.key_mode == "keytable" else "ed25519_ladder_kernel"
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_ladder.json")
     if os.path.exists(pmc):

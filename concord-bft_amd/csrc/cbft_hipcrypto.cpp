@@ -29,6 +29,9 @@ int cbft_fail(hipError_t e, const char* what, const char* file, int line) {
   return e == hipErrorOutOfMemory ? CBFT_ENOMEM : CBFT_EIO;
 }
 
+// keys per launch of the comb-table build (bounds the 589,824-B-per-key staging buffer)
+static const uint32_t kCombBuildChunk = 256;
+
 static int reserve_work(cbft_ctx* c, size_t n) {
   CBFT_HIP(c->h.reserve(n * 8 * sizeof(uint32_t)));
   CBFT_HIP(c->flags.reserve(n));
@@ -102,15 +105,15 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
                                      0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
                                      0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
       DevBuf enc, tmp;
-      if (c->base_comb.reserve(cbft_ed25519_comb_words_per_unit() * 4) != hipSuccess ||
-          enc.reserve(32) != hipSuccess || tmp.reserve(cbft_ed25519_comb_tmp_words_per_unit() * 4) != hipSuccess) {
+      if (c->base_comb.reserve(cbft_ed25519_comb8_words_per_unit() * 4) != hipSuccess ||
+          enc.reserve(32) != hipSuccess || tmp.reserve(cbft_ed25519_comb8_tmp_words_per_unit() * 4) != hipSuccess) {
         enc.release();
         tmp.release();
         rc = CBFT_ENOMEM;
         break;
       }
       bool okb = hipMemcpy(enc.p, kB, 32, hipMemcpyHostToDevice) == hipSuccess &&
-                 cbft_ed25519_launch_comb_tables(enc.as<uint8_t>(), 1, 0, c->base_comb.as<uint32_t>(),
+                 cbft_ed25519_launch_comb8_tables(enc.as<uint8_t>(), 1, 0, c->base_comb.as<uint32_t>(),
                                                  tmp.as<uint32_t>(), nullptr, c->stream) == hipSuccess &&
                  hipStreamSynchronize(c->stream) == hipSuccess;
       enc.release();
@@ -194,11 +197,14 @@ int cbft_ed25519_load_keys(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, uint3
   kt.nkeys = nkeys;
   const size_t n = std::max<uint32_t>(nkeys, 1);
   CBFT_HIP(kt.pk.reserve(n * 32));
-  CBFT_HIP(kt.comb.reserve(n * cbft_ed25519_comb_words_per_unit() * sizeof(uint32_t)));
+  CBFT_HIP(kt.comb.reserve(n * cbft_ed25519_comb8_words_per_unit() * sizeof(uint32_t)));
   CBFT_HIP(kt.aok.reserve(n));
   if (nkeys) {
-    DevBuf tmp;  // projective staging of the 256 multiples per key, freed after the build
-    hipError_t e = tmp.reserve((size_t)nkeys * cbft_ed25519_comb_tmp_words_per_unit() * sizeof(uint32_t));
+    // the radix-256 comb tables are built in chunks of keys so the projective staging buffer
+    // stays bounded (each key stages 32 x 128 points)
+    const uint32_t chunk = std::min<uint32_t>(nkeys, kCombBuildChunk);
+    DevBuf tmp;
+    hipError_t e = tmp.reserve((size_t)chunk * cbft_ed25519_comb8_tmp_words_per_unit() * sizeof(uint32_t));
     if (e != hipSuccess) {
       kt.pk.release();
       kt.comb.release();
@@ -206,9 +212,12 @@ int cbft_ed25519_load_keys(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, uint3
       return cbft_fail(e, "hipMalloc(comb tmp)", __FILE__, __LINE__);
     }
     e = hipMemcpyAsync(kt.pk.p, pk, (size_t)nkeys * 32, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess)
-      e = cbft_ed25519_launch_comb_tables(kt.pk.as<uint8_t>(), nkeys, 1, kt.comb.as<uint32_t>(), tmp.as<uint32_t>(),
-                                          kt.aok.as<uint8_t>(), c->stream);
+    for (uint32_t k0 = 0; e == hipSuccess && k0 < nkeys; k0 += chunk) {
+      const uint32_t m = std::min(chunk, nkeys - k0);
+      e = cbft_ed25519_launch_comb8_tables(kt.pk.as<uint8_t>() + (size_t)k0 * 32, m, 1,
+                                           kt.comb.as<uint32_t>() + (size_t)k0 * cbft_ed25519_comb8_words_per_unit(),
+                                           tmp.as<uint32_t>(), kt.aok.as<uint8_t>() + k0, c->stream);
+    }
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
     tmp.release();
     if (e != hipSuccess) {

@@ -46,7 +46,7 @@ struct DevBuf {
 
 struct KeyTable {
   uint32_t nkeys = 0;
-  DevBuf pk, comb, aok;  // raw keys, per-key comb tables of -A, decode status
+  DevBuf pk, comb, aok;  // raw keys, per-key radix-256 comb tables of -A, decode status
 };
 
 // BLS verifier key set: group public key + n share verification keys, decoded and with their

@@ -33,8 +33,8 @@ struct Ed25519Batch {
 struct Ed25519Work {
   const uint32_t* base_table;  // cbft_ed25519_base_table_words() words
   const uint32_t* tbl;         // windowed -A tables, indexed like pk (per-signature key mode)
-  const uint32_t* comb_tbl;    // comb -A tables per key (key-table mode; then tbl is unused)
-  const uint32_t* base_comb;   // comb table of B
+  const uint32_t* comb_tbl;    // radix-256 comb tables of -A per key (key-table mode; tbl unused)
+  const uint32_t* base_comb;   // radix-256 comb table of B
   const uint8_t* aok;          // A decoded OK, indexed like pk
   uint32_t* h_soa;             // 8 x n words
   uint8_t* flags;              // n bytes
@@ -43,9 +43,9 @@ struct Ed25519Work {
 };
 
 size_t cbft_ed25519_table_words_per_unit();
-size_t cbft_ed25519_comb_words_per_unit();
-size_t cbft_ed25519_comb_tmp_words_per_unit();
-hipError_t cbft_ed25519_launch_comb_tables(const uint8_t* d_pk, size_t nunits, int negate, uint32_t* d_tbl,
+size_t cbft_ed25519_comb8_words_per_unit();
+size_t cbft_ed25519_comb8_tmp_words_per_unit();
+hipError_t cbft_ed25519_launch_comb8_tables(const uint8_t* d_pk, size_t nunits, int negate, uint32_t* d_tbl,
                                            uint32_t* d_tmp, uint8_t* d_aok, hipStream_t stream);
 size_t cbft_ed25519_base_table_words();
 hipError_t cbft_ed25519_build_base_table(uint32_t* d_tbl, hipStream_t stream);

@@ -350,89 +350,82 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_finish_kernel(const
 }
 
 // ---------------------------------------------------------------------------------------
-// Fixed-base comb path (key-table mode).
+// Radix-256 fixed-base comb ("comb8"), four lanes per signature (key-table mode).
 //
-// For a point P known ahead of the signatures (the base point B, or a loaded key's -A) the table
-//   C_P[j][k] = k * 256^j * P,   j = 0..31, k = 0..8   (affine niels form, k = 0 = identity)
-// turns [s]P, with s written in 64 signed radix-16 digits d_i in [-8, 7]
-// (s + 0x88..8 nibble-wise minus 8), into
-//   [s]P = sum_j C_P[j][d_(2j)] + 16 * sum_j C_P[j][d_(2j+1)]
-// i.e. 64 mixed additions and 4 doublings, with no per-bit doubling chain.  R' = [S]B + [h](-A)
-// runs both sums jointly: 128 additions + 4 doublings, against 252 doublings + 88 additions of
-// the windowed ladder.  The per-key tables (32 x 9 x 112 B = 32,256 B per key) are built once
-// in cbft_ed25519_load_keys (the decoded key cached exactly like SigManager's per-key verifier);
-// the B table (same size) is built once per context and staged into LDS by every workgroup.
+// At the headline batch (64K signatures) one lane per signature gives 1,024 waves: one wave per
+// SIMD, and a lone wave issues VALU at half the SIMD's rate (MI355X_MICROARCH.md, constants
+// table).  The comb sum is split instead:
+//   C8_P[j][e] = e * 256^j * P,  j = 0..31, e = 0..128 (affine niels, 128-B entries, e = 0 =
+//   identity);  s + 0x8080..80 has bytes b_j, digit d_j = b_j - 128 in [-128, 127], and
+//   [s]P = sum_j sign(d_j) C8_P[j][|d_j|]   (32 mixed additions, no doublings).
+// Lane q of each quad (4 adjacent lanes) sums 16 positions of one scalar:
+//   q = 0: h positions 0..15 on -A,  q = 1: h positions 16..31,  q = 2, 3: S on B likewise,
+// then two DPP butterfly levels (xor 1, xor 2) add the partial sums: every lane of the quad ends
+// with R' = [S]B + [h](-A).  4,096 waves at 64K: 4 waves per SIMD.
+// The per-key table (32 x 129 x 128 B = 528,384 B) lives in HBM; B's table (same size) is read
+// through L2 by every lane.
 // ---------------------------------------------------------------------------------------
-#define COMB_POS 32
-#define COMB_ENT 9
-#define COMB_WORDS_PER_UNIT (COMB_POS * COMB_ENT * NIELS_WORDS)
+#define C8_POS 32
+#define C8_ENT 129
+#define C8_STRIDE 32  // words per entry: one 128-B line
+#define C8_WORDS_PER_UNIT (C8_POS * C8_ENT * C8_STRIDE)
+#define C8_TMP_WORDS_PER_LANE (128 * CACHED_WORDS)
+#define C8_TABLE_BLOCK 64
 
-// One lane per unit (key): decode, 256 projective multiples in tmp, Montgomery batch
-// inversion, affine niels entries in tbl.  tmp: 256 x 36 words per unit (Z-prefix products
-// reuse the T slot).
-__global__ void __launch_bounds__(64) ed25519_comb_table_kernel(const uint8_t* pk, size_t nunits, int negate,
-                                                                 uint32_t* tbl, uint32_t* tmp, uint8_t* aok) {
-  const size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+// One lane per (unit, position j): P_j = 256^j P (8j doublings), multiples 1..128 of P_j
+// projectively into tmp, Montgomery batch inversion, affine niels into tbl[unit][j][1..128].
+__global__ void __launch_bounds__(C8_TABLE_BLOCK) ed25519_comb8_table_kernel(const uint8_t* pk, size_t nunits,
+                                                                             int negate, uint32_t* tbl,
+                                                                             uint32_t* tmp, uint8_t* aok) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t u = g / C8_POS;
+  const int j = (int)(g % C8_POS);
   if (u >= nunits) return;
   uint32_t Aw[8];
   load_words8(Aw, pk + u * 32);
   ge_p3 Pj;
   const bool ok = ge_frombytes(Pj, Aw);
-  if (aok) aok[u] = ok ? 1 : 0;
+  if (aok && j == 0) aok[u] = ok ? 1 : 0;
   if (negate) {
     fe_neg(Pj.X, Pj.X);
     fe_neg(Pj.T, Pj.T);
   }
-  uint32_t* t = tmp + u * (size_t)(COMB_POS * 8 * CACHED_WORDS);
-  uint32_t* out = tbl + u * (size_t)COMB_WORDS_PER_UNIT;
-  // pass 1: k * 256^j * P, k = 1..8, projective, into tmp[(8j + k - 1)]
 #pragma nounroll
-  for (int j = 0; j < COMB_POS; j++) {
-    ge_cached cj;
-    ge_p3_to_cached(cj, Pj);
-    ge_p3 Q = Pj;
-#pragma nounroll
-    for (int k = 1; k <= 8; k++) {
-      uint32_t* e = t + (size_t)(8 * j + k - 1) * CACHED_WORDS;
-      fe_store(e, Q.X);
-      fe_store(e + 9, Q.Y);
-      fe_store(e + 18, Q.Z);
-      if (k < 8) {
-        ge_p1p1 r;
-        ge_add(r, Q, cj, false);
-        ge_p1p1_to_p3(Q, r);
-      }
-    }
-    if (j + 1 < COMB_POS) {  // P_{j+1} = 256 * P_j: 8 doublings
-      ge_p1p1 r;
-#pragma nounroll
-      for (int d = 0; d < 8; d++) {
-        ge_dbl(r, Pj.X, Pj.Y, Pj.Z);
-        ge_p1p1_to_p3(Pj, r);
-      }
-    }
+  for (int d = 0; d < 8 * j; d++) {
+    ge_p1p1 r;
+    ge_dbl(r, Pj.X, Pj.Y, Pj.Z);
+    ge_p1p1_to_p3(Pj, r);
   }
-  // pass 2: prefix products of Z into the T slot
+  uint32_t* t = tmp + g * (size_t)C8_TMP_WORDS_PER_LANE;
+  uint32_t* out = tbl + (u * C8_POS + j) * (size_t)(C8_ENT * C8_STRIDE);
+  ge_cached cj;
+  ge_p3_to_cached(cj, Pj);
+  ge_p3 Q = Pj;
   fe acc;
   fe_1(acc);
 #pragma nounroll
-  for (int i = 0; i < COMB_POS * 8; i++) {
-    uint32_t* e = t + (size_t)i * CACHED_WORDS;
-    fe z;
-    fe_load(z, e + 18);
-    fe_mul(acc, acc, z);
-    fe_store(e + 27, acc);
+  for (int k = 1; k <= 128; k++) {
+    uint32_t* e = t + (size_t)(k - 1) * CACHED_WORDS;
+    fe_store(e, Q.X);
+    fe_store(e + 9, Q.Y);
+    fe_store(e + 18, Q.Z);
+    fe_mul(acc, acc, Q.Z);
+    fe_store(e + 27, acc);  // prefix product Z_1 .. Z_k
+    if (k < 128) {
+      ge_p1p1 r;
+      ge_add(r, Q, cj, false);
+      ge_p1p1_to_p3(Q, r);
+    }
   }
-  // pass 3: backwards, inv = 1/(Z_0..Z_i); zi = inv * prefix_{i-1}; inv *= Z_i
   fe inv;
   fe_invert(inv, acc);
   fe d2;
   fe_load_const(d2, kFeD2);
 #pragma nounroll
-  for (int i = COMB_POS * 8 - 1; i >= 0; i--) {
-    uint32_t* e = t + (size_t)i * CACHED_WORDS;
+  for (int k = 128; k >= 1; k--) {
+    uint32_t* e = t + (size_t)(k - 1) * CACHED_WORDS;
     fe zi, x, y, z, xy, ypx, ymx, t2d;
-    if (i > 0) {
+    if (k > 1) {
       fe pre;
       fe_load(pre, e - CACHED_WORDS + 27);
       fe_mul(zi, inv, pre);
@@ -450,124 +443,121 @@ __global__ void __launch_bounds__(64) ed25519_comb_table_kernel(const uint8_t* p
     fe_carry(ypx);
     fe_sub(ymx, y, x);
     fe_mul(t2d, xy, d2);
-    const int j = i >> 3, k = (i & 7) + 1;
-    uint32_t* o = out + (size_t)(j * COMB_ENT + k) * NIELS_WORDS;
+    uint32_t* o = out + (size_t)k * C8_STRIDE;
     fe_store(o, ypx);
     fe_store(o + 9, ymx);
     fe_store(o + 18, t2d);
-    o[27] = 0;
-  }
-  // identity entries k = 0: (y+x, y-x, 2dxy) = (1, 1, 0)
-#pragma nounroll
-  for (int j = 0; j < COMB_POS; j++) {
-    uint32_t* o = out + (size_t)(j * COMB_ENT) * NIELS_WORDS;
-    for (int w = 0; w < NIELS_WORDS; w++) o[w] = (w == 0 || w == 9) ? 1u : 0u;
-  }
-}
-
-// Signed radix-16 recoding of k < 2^253: k' = k + 0x88..8; digit i = nibble_i(k') - 8.
-// Even-indexed and odd-indexed nibbles are packed separately (4 words each) so each comb pass
-// pops its digits from the bottom with a 4-bit shift.
-__device__ __forceinline__ uint32_t even_nibbles16(uint32_t x) {
-  return (x & 0xFu) | ((x >> 4) & 0xF0u) | ((x >> 8) & 0xF00u) | ((x >> 12) & 0xF000u);
-}
-__device__ __forceinline__ void sc_recode16(uint32_t* ev, uint32_t* od, const uint32_t* k) {
-  uint32_t s[8];
-  uint64_t c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint64_t t = (uint64_t)k[i] + 0x88888888u + c;
-    s[i] = (uint32_t)t;
-    c = t >> 32;
+    for (int w = 27; w < C8_STRIDE; w++) o[w] = 0;
   }
 #pragma unroll
-  for (int m = 0; m < 4; m++) {
-    ev[m] = even_nibbles16(s[2 * m]) | (even_nibbles16(s[2 * m + 1]) << 16);
-    od[m] = even_nibbles16(s[2 * m] >> 4) | (even_nibbles16(s[2 * m + 1] >> 4) << 16);
-  }
-}
-__device__ __forceinline__ int pop_digit16(uint32_t* w) {
-  const int d = (int)(w[0] & 15u) - 8;
-  w[0] = (w[0] >> 4) | (w[1] << 28);
-  w[1] = (w[1] >> 4) | (w[2] << 28);
-  w[2] = (w[2] >> 4) | (w[3] << 28);
-  w[3] >>= 4;
-  return d;
+  for (int w = 0; w < C8_STRIDE; w++) out[w] = (w == 0 || w == 9) ? 1u : 0u;  // identity (1, 1, 0)
 }
 
-#ifndef CBFT_COMB_MIN_WAVES
-#define CBFT_COMB_MIN_WAVES 4
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ void fe_dpp(fe& r, const fe& a) {
+#pragma unroll
+  for (int k = 0; k < FE_LIMBS; k++) r.v[k] = dpp_u32<CTRL>(a.v[k]);
+}
+
+// P += (partner lane's P): quad_perm CTRL = 0xB1 (lane ^ 1) or 0x4E (lane ^ 2).  9M.
+template <int CTRL>
+__device__ __forceinline__ void quad_combine(ge_p3& P, bool needT) {
+  ge_p3 Q;
+  fe_dpp<CTRL>(Q.X, P.X);
+  fe_dpp<CTRL>(Q.Y, P.Y);
+  fe_dpp<CTRL>(Q.Z, P.Z);
+  fe_dpp<CTRL>(Q.T, P.T);
+  ge_cached c;
+  ge_p3_to_cached(c, Q);
+  ge_p1p1 t;
+  ge_add(t, P, c, false);
+  if (needT) fe_mul(P.T, t.X, t.Y);
+  fe_mul(P.X, t.X, t.T);
+  fe_mul(P.Y, t.Y, t.Z);
+  fe_mul(P.Z, t.Z, t.T);
+}
+
+#ifndef CBFT_COMB8_MIN_WAVES
+#define CBFT_COMB8_MIN_WAVES 4
 #endif
 
-__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
-    ed25519_comb_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* tbl,
-                               const uint32_t* base_comb, uint32_t* xyz_soa) {
-  __shared__ uint32_t sB[COMB_WORDS_PER_UNIT];
-  {
-    const uint4* src = reinterpret_cast<const uint4*>(base_comb);
-    uint4* dst = reinterpret_cast<uint4*>(sB);
-    for (int k = threadIdx.x; k < COMB_WORDS_PER_UNIT / 4; k += blockDim.x) dst[k] = src[k];
-  }
-  __syncthreads();
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= b.n) return;
-  const uint32_t* ta = tbl + (size_t)b.key_idx[i] * COMB_WORDS_PER_UNIT;
-  uint32_t hE[4], hO[4], sE[4], sO[4];
-  {
-    uint32_t w[8];
+__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB8_MIN_WAVES)
+    ed25519_comb8_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* tbl,
+                                const uint32_t* base8, uint32_t* xyz_soa) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t q = threadIdx.x & 3u;
+  size_t i = g >> 2;
+  const bool live = i < b.n;
+  if (!live) i = b.n - 1;  // tail quads compute a copy (all lanes stay active for the DPP)
+  const bool onB = (q & 2u) != 0;
+  const uint32_t half = q & 1u;
+  uint32_t w[8];
+  if (onB) {
+    load_words8(w, b.sig + i * 64 + 32);
+  } else {
 #pragma unroll
     for (int k = 0; k < 8; k++) w[k] = h_soa[k * b.n + i];
-    sc_recode16(hE, hO, w);
-    load_words8(w, b.sig + i * 64 + 32);
-    sc_recode16(sE, sO, w);
   }
+  // s' = s + 0x8080..80; this lane's 16 bytes (words 4*half .. 4*half+3)
+  uint32_t dw[4];
+  {
+    uint64_t c = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      const uint64_t s = (uint64_t)w[k] + 0x80808080u + c;
+      w[k] = (uint32_t)s;
+      c = s >> 32;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; k++) dw[k] = half ? w[4 + k] : w[k];
+  }
+  const uint32_t* base = onB ? base8 : tbl + (size_t)b.key_idx[i] * C8_WORDS_PER_UNIT;
+  base += (size_t)half * 16 * (C8_ENT * C8_STRIDE);
   ge_p3 P;
   ge_p3_0(P);
-  // pass 0: odd digits, then 4 doublings; pass 1: even digits
 #pragma nounroll
-  for (int pass = 0; pass < 2; pass++) {
-#pragma nounroll
-    for (int j = 0; j < COMB_POS; j++) {
-#pragma nounroll
-      for (int src = 0; src < 2; src++) {
-        int d;
-        const uint32_t* e;
-        if (src == 0) {
-          d = pop_digit16(pass == 0 ? hO : hE);
-          e = ta + (j * COMB_ENT + (d < 0 ? -d : d)) * NIELS_WORDS;
-        } else {
-          d = pop_digit16(pass == 0 ? sO : sE);
-          e = sB + (j * COMB_ENT + (d < 0 ? -d : d)) * NIELS_WORDS;
-        }
-        ge_p1p1 t;
-        ge_add_mem<true>(t, P, e, d < 0);
-        const bool last = (pass == 1 && j == COMB_POS - 1 && src == 1);
-        if (!last) fe_mul(P.T, t.X, t.Y);
-        fe_mul(P.X, t.X, t.T);
-        fe_mul(P.Y, t.Y, t.Z);
-        fe_mul(P.Z, t.Z, t.T);
-      }
-    }
-    if (pass == 0) {
-#pragma nounroll
-      for (int k = 0; k < 4; k++) {
-        ge_p1p1 t;
-        ge_dbl(t, P.X, P.Y, P.Z);
-        if (k == 3) fe_mul(P.T, t.X, t.Y);
-        fe_mul(P.X, t.X, t.T);
-        fe_mul(P.Y, t.Y, t.Z);
-        fe_mul(P.Z, t.Z, t.T);
-      }
-    }
+  for (int jj = 0; jj < 16; jj++) {
+    const int d = (int)(dw[0] & 0xffu) - 128;
+    dw[0] = (dw[0] >> 8) | (dw[1] << 24);
+    dw[1] = (dw[1] >> 8) | (dw[2] << 24);
+    dw[2] = (dw[2] >> 8) | (dw[3] << 24);
+    dw[3] >>= 8;
+    const uint32_t* e = base + (jj * C8_ENT + (d < 0 ? -d : d)) * C8_STRIDE;
+    ge_p1p1 t;
+    ge_add_mem<true>(t, P, e, d < 0);
+    fe_mul(P.T, t.X, t.Y);
+    fe_mul(P.X, t.X, t.T);
+    fe_mul(P.Y, t.Y, t.Z);
+    fe_mul(P.Z, t.Z, t.T);
   }
-  fe_store_soa(xyz_soa, b.n, i, P.X);
-  fe_store_soa(xyz_soa + 9 * b.n, b.n, i, P.Y);
-  fe_store_soa(xyz_soa + 18 * b.n, b.n, i, P.Z);
+  quad_combine<0xB1>(P, true);
+  quad_combine<0x4E>(P, false);
+  if (live && q == 0) {
+    fe_store_soa(xyz_soa, b.n, i, P.X);
+    fe_store_soa(xyz_soa + 9 * b.n, b.n, i, P.Y);
+    fe_store_soa(xyz_soa + 18 * b.n, b.n, i, P.Z);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
 // host-side launch helpers (used by cbft_hipcrypto.cpp)
 // ---------------------------------------------------------------------------------------
+size_t cbft_ed25519_comb8_words_per_unit() { return (size_t)C8_WORDS_PER_UNIT; }
+size_t cbft_ed25519_comb8_tmp_words_per_unit() { return (size_t)C8_POS * C8_TMP_WORDS_PER_LANE; }
+
+hipError_t cbft_ed25519_launch_comb8_tables(const uint8_t* d_pk, size_t nunits, int negate, uint32_t* d_tbl,
+                                            uint32_t* d_tmp, uint8_t* d_aok, hipStream_t stream) {
+  if (nunits == 0) return hipSuccess;
+  const size_t lanes = nunits * C8_POS;
+  hipLaunchKernelGGL(ed25519_comb8_table_kernel, dim3((unsigned)((lanes + C8_TABLE_BLOCK - 1) / C8_TABLE_BLOCK)),
+                     dim3(C8_TABLE_BLOCK), 0, stream, d_pk, nunits, negate, d_tbl, d_tmp, d_aok);
+  return hipGetLastError();
+}
 size_t cbft_ed25519_table_words_per_unit() { return (size_t)Shape::TA * CACHED_WORDS; }
 size_t cbft_ed25519_base_table_words() { return (size_t)Shape::TB * NIELS_WORDS; }
 
@@ -586,17 +576,6 @@ hipError_t cbft_ed25519_launch_prep(const uint8_t* d_pk, size_t nunits, uint32_t
   return hipGetLastError();
 }
 
-size_t cbft_ed25519_comb_words_per_unit() { return (size_t)COMB_WORDS_PER_UNIT; }
-size_t cbft_ed25519_comb_tmp_words_per_unit() { return (size_t)COMB_POS * 8 * CACHED_WORDS; }
-
-hipError_t cbft_ed25519_launch_comb_tables(const uint8_t* d_pk, size_t nunits, int negate, uint32_t* d_tbl,
-                                           uint32_t* d_tmp, uint8_t* d_aok, hipStream_t stream) {
-  if (nunits == 0) return hipSuccess;
-  hipLaunchKernelGGL(ed25519_comb_table_kernel, dim3((unsigned)((nunits + 63) / 64)), dim3(64), 0, stream, d_pk,
-                     nunits, negate, d_tbl, d_tmp, d_aok);
-  return hipGetLastError();
-}
-
 hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& w, hipStream_t stream,
                                       hipEvent_t* ev) {
   if (b.n == 0) return hipSuccess;
@@ -605,8 +584,8 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   hipLaunchKernelGGL(ed25519_hash_kernel, grid, block, 0, stream, b, w.h_soa, w.flags);
   if (ev) (void)hipEventRecord(ev[1], stream);
   if (w.comb_tbl && w.base_comb && b.key_idx)
-    hipLaunchKernelGGL(ed25519_comb_ladder_kernel, grid, block, 0, stream, b, w.h_soa, w.comb_tbl, w.base_comb,
-                       w.xyz_soa);
+    hipLaunchKernelGGL(ed25519_comb8_ladder_kernel, dim3((unsigned)((4 * b.n + CBFT_VERIFY_BLOCK - 1) / CBFT_VERIFY_BLOCK)),
+                       block, 0, stream, b, w.h_soa, w.comb_tbl, w.base_comb, w.xyz_soa);
   else
     hipLaunchKernelGGL(ed25519_ladder_kernel, grid, block, 0, stream, b, w.h_soa, w.tbl, w.base_table, w.xyz_soa);
   if (ev) (void)hipEventRecord(ev[2], stream);
