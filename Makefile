@@ -40,12 +40,15 @@ $(CPU_LIB): tools/cpu_baseline/openssl_ed25519.c
 	gcc -O2 -std=gnu11 -fPIC -shared -Wall -o $@ $< -lcrypto -lpthread
 
 HOST_LIB := concord-bft_amd/libcbft_host.so
-HOST_SRC := concord-bft_amd/host/src/crypto_utils.cpp concord-bft_amd/host/src/sig_manager.cpp
+HOST_SRC := concord-bft_amd/host/src/crypto_utils.cpp concord-bft_amd/host/src/sig_manager.cpp concord-bft_amd/host/src/bls_hip.cpp
 HOST_INC := -Iinclude -Iconcord-bft_amd/host/include
-host: $(HOST_LIB) tests/cpp/test_host
-$(HOST_LIB): $(HOST_SRC) concord-bft_amd/host/include/*.hpp $(LIB)
+host: $(HOST_LIB) tests/cpp/test_host tests/cpp/test_bls_host
+$(HOST_LIB): $(HOST_SRC) concord-bft_amd/host/include/*.hpp concord-bft_amd/host/include/threshsign/*.h* $(LIB)
 	g++ -O2 -std=c++17 -fPIC -shared -Wall $(HOST_INC) -o $@ $(HOST_SRC) -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN'
 tests/cpp/test_host: tests/cpp/test_host.cpp $(HOST_LIB)
+	g++ -O2 -std=c++17 -Wall $(HOST_INC) -o $@ $< -Lconcord-bft_amd -lcbft_host -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN/../../concord-bft_amd'
+
+tests/cpp/test_bls_host: tests/cpp/test_bls_host.cpp $(HOST_LIB)
 	g++ -O2 -std=c++17 -Wall $(HOST_INC) -o $@ $< -Lconcord-bft_amd -lcbft_host -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN/../../concord-bft_amd'
 
 # host build of the BN-P254 device code, for the CPU tests (and the "not RELIC" CPU baseline)

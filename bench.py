@@ -58,6 +58,9 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-runs", type=int, default=200)
+    ap.add_argument("--inflight", type=int, default=2, help="batches in flight (streams) in the timed loop")
+    ap.add_argument("--no-extras", dest="extras", action="store_false",
+                    help="skip the config #3 (mixed) and config #4 (BLS) side measurements")
     return ap.parse_args()
 
 
@@ -99,27 +102,41 @@ def main():
         d_pk = to_dev(ss.per_sig_pk().reshape(-1), np.uint8)
         d_kidx = None
     nwords = (n + 63) // 64
-    d_verdict = torch.zeros(nwords, dtype=torch.int64, device=dev)
-    gathered = torch.zeros(world * nwords, dtype=torch.int64, device=dev) if world > 1 else None
-    stream = torch.cuda.current_stream().cuda_stream
+    # two batches in flight (the library rotates two work slots): batch i's finish kernel and
+    # batch i+1's hash kernel share the SIMDs instead of each running at one wave per SIMD
+    inflight = max(1, args.inflight)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(inflight)]
+    d_verdicts = [torch.zeros(nwords, dtype=torch.int64, device=dev) for _ in range(inflight)]
+    gathered = [torch.zeros(world * nwords, dtype=torch.int64, device=dev) for _ in range(inflight)] \
+        if world > 1 else None
+    d_verdict = d_verdicts[0]
+    stream = streams[0].cuda_stream
+    counter = [0]
 
-    def step():
+    def step(single: bool = False):
+        j = 0 if single else counter[0] % inflight
+        counter[0] += 0 if single else 1
+        s = streams[j]
         ctx.verify_device(tid, d_pk.data_ptr() if d_pk is not None else 0,
                           d_kidx.data_ptr() if d_kidx is not None else 0, d_sig.data_ptr(), d_blob.data_ptr(),
-                          d_off.data_ptr(), d_len.data_ptr(), n, d_verdict.data_ptr(), stream)
+                          d_off.data_ptr(), d_len.data_ptr(), n, d_verdicts[j].data_ptr(), s.cuda_stream)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, d_verdict)
+            with torch.cuda.stream(s):
+                dist.all_gather_into_tensor(gathered[j], d_verdicts[j])
 
     # ---- parity gate: bit-exact vs host OpenSSL before any number is reported
-    step()
+    step(single=True)
     torch.cuda.synchronize()
     got = cb.bitmap_to_bools(d_verdict.cpu().numpy().view(np.uint8).tobytes(), n)
     if not np.array_equal(got, ss.expected):
         raise SystemExit(f"rank {rank}: GPU verdicts differ from OpenSSL on {(got != ss.expected).sum()} sigs")
     if world > 1:
         torch.cuda.synchronize()
-        mine = gathered.view(world, nwords)[rank]
+        mine = gathered[0].view(world, nwords)[rank]
         assert torch.equal(mine, d_verdict), "all-gather lost this rank's bitmap"
+    for d in d_verdicts:
+        d.zero_()
+    torch.cuda.synchronize()
 
     for _ in range(args.warmup):
         step()
@@ -138,6 +155,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     value = world * n * args.steps / elapsed
+    for d in d_verdicts:  # every in-flight slot produced the exact verdicts
+        got = cb.bitmap_to_bools(d.cpu().numpy().view(np.uint8).tobytes(), n)
+        if not np.array_equal(got, ss.expected):
+            raise SystemExit(f"rank {rank}: pipelined verdicts differ from OpenSSL")
 
     # ---- secondary: per-signature key mode (keys decoded per signature, windowed ladder)
     perkey_value = None
@@ -163,7 +184,7 @@ def main():
     ctx.set_profiling(True)
     stage = {"hash": [], "ladder": [], "finish": []}
     for _ in range(5):
-        step()
+        step(single=True)  # one batch at a time: kernel durations without overlap
         for k, v in ctx.stage_times_ms().items():
             stage[k].append(v)
     ctx.set_profiling(False)
@@ -230,24 +251,127 @@ def main():
                 ht.append(time.perf_counter() - c0)
             assert np.array_equal(cb.bitmap_to_bools(bm, n), ss.expected)
             host_path = n / statistics.median(ht)
+        mixed = bench_mixed(ctx, args) if (args.extras and world == 1) else None
+        bls = bench_bls(ctx, args) if (args.extras and world == 1) else None
         out = {
             "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": "ed25519_verify_64k_256B_4096keys (BASELINE config #2)", "batch_per_gpu": n,
                        "msg_len": args.msg_len, "nkeys": args.nkeys, "key_mode": args.key_mode,
+                       "inflight_batches": inflight,
                        "parallelism": f"static shard x{world}, RCCL all-gather of verdict bitmaps"},
             "roofline": roofline, "cpu_baseline": cpu,
             "p50_latency_ms_batch1k": lat,
             "perkey_mode_value": perkey_value,
             "host_path_value": host_path,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
+            "mixed_config3": mixed,
+            "bls_config4": bls,
             "verdicts": "bit-exact vs host OpenSSL (checked before timing)",
         }
         print(json.dumps(out), flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def _median_ms(fn, runs: int) -> float:
+    ts = []
+    for _ in range(runs):
+        c0 = time.perf_counter()
+        fn()
+        ts.append((time.perf_counter() - c0) * 1e3)
+    return statistics.median(ts)
+
+
+def bench_mixed(ctx, args):
+    """BASELINE config #3 (SigManager mixed): 4,096 keys, lengths log-uniform in [64, 4096] B,
+    10 % invalid (R/S bit flips, S + L, message byte, wrong key).  Host buffers in, bitmap out
+    (what SigManager::verifySigBatch does); exact-match count against OpenSSL."""
+    n = args.batch
+    ss = workload.make_sigset(n, nkeys=args.nkeys, msg_len=(64, 4096), seed=0xBADC0DE, invalid_frac=0.10,
+                              threads=args.cpu_threads)
+    tid = ctx.load_keys(ss.pk)
+    try:
+        bm = ctx.verify_packed(tid, ss.key_idx, ss.sig, ss.blob, ss.off, ss.len)
+        got = cb.bitmap_to_bools(bm, n)
+        match = int((got == ss.expected).sum())
+        ms = _median_ms(lambda: ctx.verify_packed(tid, ss.key_idx, ss.sig, ss.blob, ss.off, ss.len), 5)
+    finally:
+        ctx.unload_keys(tid)
+    return {"config": f"config #3: {n} sigs, 4096 keys, msg 64-4096 B log-uniform, 10% invalid",
+            "value": n / (ms * 1e-3), "unit": "verifies/s (host buffers in, PCIe included)",
+            "exact_match": match, "n": n, "invalid": int((~ss.expected).sum()),
+            "msg_bytes_total": int(ss.len.sum())}
+
+
+def bench_bls(ctx, args):
+    """BASELINE config #4: threshold BLS on BN-P254, n = 1,024 replicas, k = 2f+1 = 683, 32-byte
+    digest.  Unit = one commit certificate: verify 760 shares (10 % of them doubled, i.e. bad),
+    Lagrange-combine 683 valid ones, verify the combined signature.  Also the multisig variant
+    (sum of shares, signer bitmap, 1 verify) and the 0 %-bad optimistic path (combine + verify)."""
+    n, k = 1024, 683
+    cert = workload.make_bls_cert(n, k, extra=77, bad_frac=0.10, seed=2024, threads=args.cpu_threads)
+    kid = ctx.bls_load_keys(cert.pk, cert.vks)
+    try:
+        h33 = ctx.bls_hash_to_g1(cert.msg)
+        valid = ctx.bls_verify_shares(kid, cert.msg, cert.shares)
+        exp = np.array([j not in cert.bad for j in range(len(cert.shares))])
+        if not np.array_equal(np.asarray(valid, dtype=bool), exp):
+            raise SystemExit("BLS share verdicts differ from the expected bad set")
+        use = [s for j, s in enumerate(cert.shares) if valid[j]][:k]
+        comb = ctx.bls_combine(use)
+        if comb != cert.expected_sig or not ctx.bls_verify(kid, cert.msg, comb):
+            raise SystemExit("BLS combined signature differs from sk * H(m)")
+        ids = [int.from_bytes(s[:4], "big") for s in use]
+        bitmap = bytearray(256)
+        for i in ids:
+            bitmap[(i - 1) // 8] |= 1 << ((i - 1) % 8)
+        msig = ctx.bls_combine(use, multisig=True)
+        if not ctx.bls_verify_multisig(kid, cert.msg, msig, bytes(bitmap)):
+            raise SystemExit("BLS multisig does not verify")
+        runs = 5
+        t_share = _median_ms(lambda: ctx.bls_verify_shares(kid, cert.msg, cert.shares), runs)
+        t_comb = _median_ms(lambda: ctx.bls_combine(use), runs)
+        t_ver = _median_ms(lambda: ctx.bls_verify(kid, cert.msg, comb), runs)
+
+        def certificate():
+            v = ctx.bls_verify_shares(kid, cert.msg, cert.shares)
+            u = [s for j, s in enumerate(cert.shares) if v[j]][:k]
+            c = ctx.bls_combine(u)
+            assert ctx.bls_verify(kid, cert.msg, c)
+
+        def optimistic():
+            c = ctx.bls_combine(use)
+            assert ctx.bls_verify(kid, cert.msg, c)
+
+        def multisig():
+            c = ctx.bls_combine(use, multisig=True)
+            assert ctx.bls_verify_multisig(kid, cert.msg, c, bytes(bitmap))
+
+        t_cert = _median_ms(certificate, runs)
+        t_opt = _median_ms(optimistic, runs)
+        t_ms = _median_ms(multisig, runs)
+    finally:
+        ctx.bls_unload_keys(kid)
+    nsh = len(cert.shares)
+    out = {"config": f"config #4: n={n}, k={k}, {nsh} shares ({len(cert.bad)} bad, doubled), 32-B digest",
+           "certificate_ms": t_cert, "certificates_per_s": 1e3 / t_cert,
+           "share_verify_ms": t_share, "shares_per_s": nsh / (t_share * 1e-3),
+           "pairings_per_s": 2 * nsh / (t_share * 1e-3),
+           "combine_ms": t_comb, "verify_ms": t_ver, "optimistic_ms": t_opt, "multisig_ms": t_ms,
+           "verdicts": "share verdicts == planted bad set; combined sig == sk*H(m) byte-exact"}
+    if not args.no_cpu:
+        workload.cpu_bls_verify_shares(cert, h33, threads=args.cpu_threads)  # warm-up
+        c0 = time.perf_counter()
+        v = workload.cpu_bls_verify_shares(cert, h33, threads=args.cpu_threads)
+        dt = time.perf_counter() - c0
+        assert np.array_equal(v.astype(bool), exp)
+        out["cpu_baseline"] = {"value": nsh / dt, "unit": "shares/s", "cores": args.cpu_threads, "kind": "port",
+                               "sample": f"{nsh} share verifies (2 pairings + G2 lines each) with the library's "
+                                         f"own BN-P254 code built for the host (not RELIC: RELIC is absent)"}
+    return out
 
 
 def _openssl_version():

@@ -60,6 +60,9 @@ ABI = [
     ("cbft_bls_verify_multisig", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p,
       ctypes.POINTER(ctypes.c_int)]),
+    ("cbft_bls_sum_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_void_p]),
+    ("cbft_bls_sign", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
+                                     ctypes.c_uint32, ctypes.c_void_p]),
 ]
 
 _lib = None
@@ -235,6 +238,17 @@ class Context:
         _check(self.lib.cbft_bls_verify_multisig(self.handle, kid, msg, len(msg), sig33, signers256,
                                                   ctypes.byref(ok)), "cbft_bls_verify_multisig")
         return bool(ok.value)
+
+    def bls_sum_keys(self, kid: int, signers256: bytes) -> bytes:
+        out = ctypes.create_string_buffer(65)
+        _check(self.lib.cbft_bls_sum_keys(self.handle, kid, signers256, out), "cbft_bls_sum_keys")
+        return out.raw
+
+    def bls_sign(self, sk: int, share_id: int, msg: bytes) -> bytes:
+        out = ctypes.create_string_buffer(37)
+        _check(self.lib.cbft_bls_sign(self.handle, sk.to_bytes(32, "big"), share_id, msg, len(msg), out),
+               "cbft_bls_sign")
+        return out.raw
 
     def set_profiling(self, on: bool = True):
         _check(self.lib.cbft_set_profiling(self.handle, 1 if on else 0), "cbft_set_profiling")

@@ -20,7 +20,9 @@ hipError_t cbft_bls_launch_combine(const uint32_t* d_sig, const uint32_t* d_ids,
                                    int multisig, uint32_t* d_lambda, uint32_t* d_partial, uint8_t* d_out33,
                                    uint32_t* d_sig_aff, hipStream_t s);
 hipError_t cbft_bls_launch_g2_sum(const uint8_t* d_keys65, uint32_t n, const uint8_t* d_bitmap, uint32_t* d_lines,
-                                  uint8_t* d_ok, hipStream_t s);
+                                  uint8_t* d_ok, uint8_t* d_out65, hipStream_t s);
 hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, const uint32_t* d_pk_lines,
                                   const uint8_t* d_pk_ok, const uint32_t* d_gen_lines, uint8_t* d_result,
                                   hipStream_t s);
+hipError_t cbft_bls_launch_sign(const uint8_t* d_msg, uint32_t len, const uint32_t* d_sk, uint32_t id,
+                                uint8_t* d_out37, hipStream_t s);

@@ -199,7 +199,7 @@ __global__ void bls_msm_finish_kernel(const uint32_t* partial, uint32_t nparts, 
 // multisig public key = sum of vk_i for set bits (bit id-1, LSB first) of the 256-byte bitmap;
 // then its Miller-loop lines.  Single lane (the G2 sum is <= 2048 additions).
 __global__ void bls_g2_sum_kernel(const uint8_t* keys65, uint32_t n, const uint8_t* bitmap, uint32_t* lines,
-                                  uint8_t* ok) {
+                                  uint8_t* ok, uint8_t* out65) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   g2j acc;
   fp2_one(acc.X);
@@ -221,9 +221,16 @@ __global__ void bls_g2_sum_kernel(const uint8_t* keys65, uint32_t n, const uint8
   }
   g2a s;
   g2_to_affine(s, acc);
+  if (out65) {
+    if (good) {
+      g2_compress(out65, s);
+    } else {
+      for (int q = 0; q < 65; q++) out65[q] = 0;
+    }
+  }
   good = good && !s.inf;
   ok[0] = good ? 1 : 0;
-  if (good) g2_precompute_lines(lines, s);
+  if (good && lines) g2_precompute_lines(lines, s);
 }
 
 // e(H, PK) * e(-sigma, g2) == 1 for a combined signature (33 bytes)
@@ -243,6 +250,26 @@ __global__ void bls_verify_kernel(const uint32_t* H, const uint8_t* sig33, const
     }
   }
   result[0] = good ? 1 : 0;
+}
+
+// sigma_i = sk_i * g1_map(msg) as a 37-byte share (BlsThresholdSigner::signData,
+// BlsThresholdSigner.cpp:32-47): 4-byte big-endian id || 33-byte compressed G1.  sk: 8 LE words.
+__global__ void bls_sign_kernel(const uint8_t* msg, uint32_t len, const uint32_t* sk, uint32_t id, uint8_t* out37) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  g1a h;
+  g1_map(h, msg, len);
+  g1j p, r;
+  g1_from_affine(p, h);
+  uint32_t k[8];
+  for (int q = 0; q < 8; q++) k[q] = sk[q];
+  g1_mul(r, p, k);
+  g1a a;
+  g1_to_affine(a, r);
+  out37[0] = (uint8_t)(id >> 24);
+  out37[1] = (uint8_t)(id >> 16);
+  out37[2] = (uint8_t)(id >> 8);
+  out37[3] = (uint8_t)id;
+  g1_compress(out37 + 4, a);
 }
 
 // ------------------------------------------------------------------------------ launchers
@@ -284,8 +311,8 @@ hipError_t cbft_bls_launch_combine(const uint32_t* d_sig, const uint32_t* d_ids,
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_g2_sum(const uint8_t* d_keys65, uint32_t n, const uint8_t* d_bitmap, uint32_t* d_lines,
-                                  uint8_t* d_ok, hipStream_t s) {
-  hipLaunchKernelGGL(bls_g2_sum_kernel, dim3(1), dim3(64), 0, s, d_keys65, n, d_bitmap, d_lines, d_ok);
+                                  uint8_t* d_ok, uint8_t* d_out65, hipStream_t s) {
+  hipLaunchKernelGGL(bls_g2_sum_kernel, dim3(1), dim3(64), 0, s, d_keys65, n, d_bitmap, d_lines, d_ok, d_out65);
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, const uint32_t* d_pk_lines,
@@ -293,5 +320,10 @@ hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, c
                                   hipStream_t s) {
   hipLaunchKernelGGL(bls_verify_kernel, dim3(1), dim3(64), 0, s, d_H, d_sig33, d_pk_lines, d_pk_ok, d_gen_lines,
                      d_result);
+  return hipGetLastError();
+}
+hipError_t cbft_bls_launch_sign(const uint8_t* d_msg, uint32_t len, const uint32_t* d_sk, uint32_t id,
+                                uint8_t* d_out37, hipStream_t s) {
+  hipLaunchKernelGGL(bls_sign_kernel, dim3(1), dim3(64), 0, s, d_msg, len, d_sk, id, d_out37);
   return hipGetLastError();
 }

@@ -212,8 +212,45 @@ int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint3
   CBFT_HIP(c->bls_ms_ok.reserve(1));
   CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(cbft_bls_launch_g2_sum(ks->keys65.as<uint8_t>() + 65, ks->n, c->bls_bitmap.as<uint8_t>(),
-                                  c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), c->stream));
+                                  c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), nullptr, c->stream));
   return bls_verify_with_lines(c, sig33, c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), out_ok);
+}
+
+int cbft_bls_sum_keys(cbft_ctx* c, uint32_t id, const uint8_t* signers256, uint8_t* out65) {
+  if (!c || !signers256 || !out65) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  BlsKeySet* ks = find_set(c, id);
+  if (!ks) return CBFT_EINVAL;
+  CBFT_HIP(hipSetDevice(c->device));
+  CBFT_HIP(c->bls_bitmap.reserve(256));
+  CBFT_HIP(c->bls_ms_ok.reserve(1));
+  CBFT_HIP(c->bls_out.reserve(65));
+  CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_g2_sum(ks->keys65.as<uint8_t>() + 65, ks->n, c->bls_bitmap.as<uint8_t>(), nullptr,
+                                  c->bls_ms_ok.as<uint8_t>(), c->bls_out.as<uint8_t>(), c->stream));
+  CBFT_HIP(hipMemcpyAsync(out65, c->bls_out.p, 65, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  return CBFT_OK;
+}
+
+int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* msg, uint32_t len, uint8_t* out37) {
+  if (!c || !sk32 || !out37 || (len && !msg)) return CBFT_EINVAL;
+  uint32_t w[8];
+  for (int q = 0; q < 8; q++)
+    w[q] = ((uint32_t)sk32[31 - 4 * q - 3] << 24) | ((uint32_t)sk32[31 - 4 * q - 2] << 16) |
+           ((uint32_t)sk32[31 - 4 * q - 1] << 8) | sk32[31 - 4 * q];
+  std::lock_guard<std::mutex> g(c->mu);
+  CBFT_HIP(hipSetDevice(c->device));
+  CBFT_HIP(c->bls_msg.reserve(len + 1));
+  CBFT_HIP(c->bls_lambda.reserve(8 * 4));
+  CBFT_HIP(c->bls_out.reserve(37));
+  if (len) CBFT_HIP(hipMemcpyAsync(c->bls_msg.p, msg, len, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(hipMemcpyAsync(c->bls_lambda.p, w, sizeof(w), hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_sign(c->bls_msg.as<uint8_t>(), len, c->bls_lambda.as<uint32_t>(), id,
+                                c->bls_out.as<uint8_t>(), c->stream));
+  CBFT_HIP(hipMemcpyAsync(out37, c->bls_out.p, 37, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  return CBFT_OK;
 }
 
 }  // extern "C"

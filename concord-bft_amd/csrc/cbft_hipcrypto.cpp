@@ -32,10 +32,19 @@ int cbft_fail(hipError_t e, const char* what, const char* file, int line) {
 // keys per launch of the comb-table build (bounds the 589,824-B-per-key staging buffer)
 static const uint32_t kCombBuildChunk = 256;
 
+static int reserve_slot(WorkSlot& w, size_t n) {
+  CBFT_HIP(w.h.reserve(n * 8 * sizeof(uint32_t)));
+  CBFT_HIP(w.flags.reserve(n));
+  CBFT_HIP(w.xyz.reserve(n * 27 * sizeof(uint32_t)));
+  if (!w.done) CBFT_HIP(hipEventCreateWithFlags(&w.done, hipEventDisableTiming));
+  return CBFT_OK;
+}
+
 static int reserve_work(cbft_ctx* c, size_t n) {
-  CBFT_HIP(c->h.reserve(n * 8 * sizeof(uint32_t)));
-  CBFT_HIP(c->flags.reserve(n));
-  CBFT_HIP(c->xyz.reserve(n * 27 * sizeof(uint32_t)));
+  for (WorkSlot& w : c->slots) {
+    int rc = reserve_slot(w, n);
+    if (rc) return rc;
+  }
   CBFT_HIP(c->verdicts.reserve(((n + 63) / 64) * sizeof(uint64_t)));
   return CBFT_OK;
 }
@@ -152,9 +161,13 @@ void cbft_close(cbft_ctx* c) {
                     &c->bls_ids, &c->bls_use, &c->bls_lambda, &c->bls_partial, &c->bls_out, &c->bls_ms_lines,
                     &c->bls_ms_ok, &c->bls_bitmap})
     b->release();
-  for (DevBuf* b : {&c->base_table, &c->base_comb, &c->h, &c->flags, &c->xyz, &c->verdicts, &c->sig, &c->msg, &c->off, &c->len,
-                    &c->kidx, &c->pk, &c->ps_tbl, &c->ps_aok})
+  (void)hipDeviceSynchronize();  // device-path batches may still run on caller streams
+  for (DevBuf* b : {&c->base_table, &c->base_comb, &c->verdicts, &c->sig, &c->msg, &c->off, &c->len, &c->kidx, &c->pk})
     b->release();
+  for (WorkSlot& w : c->slots) {
+    for (DevBuf* b : {&w.h, &w.flags, &w.xyz, &w.ps_tbl, &w.ps_aok}) b->release();
+    if (w.done) (void)hipEventDestroy(w.done);
+  }
   for (hipEvent_t& e : c->ev)
     if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -240,7 +253,7 @@ int cbft_ed25519_unload_keys(cbft_ctx* c, uint32_t id) {
   auto it = c->tables.find(id);
   if (it == c->tables.end()) return CBFT_EINVAL;
   (void)hipSetDevice(c->device);
-  (void)hipStreamSynchronize(c->stream);
+  (void)hipDeviceSynchronize();  // in-flight device-path batches on caller streams read it
   it->second.pk.release();
   it->second.comb.release();
   it->second.aok.release();
@@ -254,30 +267,40 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
                          size_t n, uint64_t* d_verdicts, hipStream_t s) {
   int rc = reserve_work(c, n);
   if (rc) return rc;
+  auto it = c->tables.end();
+  if (table_id != CBFT_NO_KEY_TABLE) {
+    it = c->tables.find(table_id);
+    if (it == c->tables.end() || !d_kidx) return CBFT_EINVAL;
+  }
+  WorkSlot& slot = c->slots[c->next_slot++ % CBFT_WORK_SLOTS];
+  if (table_id == CBFT_NO_KEY_TABLE) {
+    CBFT_HIP(slot.ps_tbl.reserve(n * cbft_ed25519_table_words_per_unit() * sizeof(uint32_t)));
+    CBFT_HIP(slot.ps_aok.reserve(n));
+  }
+  // the slot's previous batch (maybe on another stream) must be done with its buffers
+  if (slot.used) CBFT_HIP(hipStreamWaitEvent(s, slot.done, 0));
   Ed25519Batch b{n, d_pk, d_kidx, d_sig, d_msg, d_off, d_len};
   Ed25519Work w{};
   w.base_table = c->base_table.as<uint32_t>();
-  w.h_soa = c->h.as<uint32_t>();
-  w.flags = c->flags.as<uint8_t>();
-  w.xyz_soa = c->xyz.as<uint32_t>();
+  w.h_soa = slot.h.as<uint32_t>();
+  w.flags = slot.flags.as<uint8_t>();
+  w.xyz_soa = slot.xyz.as<uint32_t>();
   w.verdict_words = d_verdicts;
   if (table_id == CBFT_NO_KEY_TABLE) {
     // per-signature keys: decode + precompute per signature
-    CBFT_HIP(c->ps_tbl.reserve(n * cbft_ed25519_table_words_per_unit() * sizeof(uint32_t)));
-    CBFT_HIP(c->ps_aok.reserve(n));
-    CBFT_HIP(cbft_ed25519_launch_prep(d_pk, n, c->ps_tbl.as<uint32_t>(), c->ps_aok.as<uint8_t>(), s));
+    CBFT_HIP(cbft_ed25519_launch_prep(d_pk, n, slot.ps_tbl.as<uint32_t>(), slot.ps_aok.as<uint8_t>(), s));
     b.key_idx = nullptr;
-    w.tbl = c->ps_tbl.as<uint32_t>();
-    w.aok = c->ps_aok.as<uint8_t>();
+    w.tbl = slot.ps_tbl.as<uint32_t>();
+    w.aok = slot.ps_aok.as<uint8_t>();
   } else {
-    auto it = c->tables.find(table_id);
-    if (it == c->tables.end() || !d_kidx) return CBFT_EINVAL;
     b.pk = it->second.pk.as<uint8_t>();
     w.comb_tbl = it->second.comb.as<uint32_t>();
     w.base_comb = c->base_comb.as<uint32_t>();
     w.aok = it->second.aok.as<uint8_t>();
   }
   CBFT_HIP(cbft_ed25519_launch_verify(b, w, s, c->profiling ? c->ev : nullptr));
+  CBFT_HIP(hipEventRecord(slot.done, s));
+  slot.used = true;
   c->ev_valid = c->profiling;
   return CBFT_OK;
 }

@@ -56,6 +56,18 @@ struct BlsKeySet {
   DevBuf keys65, lines, ok;
 };
 
+// Per-batch intermediate state of one in-flight verify (h, S<L flags, R' coordinates, the
+// per-signature key tables).  A context rotates over CBFT_WORK_SLOTS of them so that
+// consecutive device-path batches on different streams overlap (batch i's finish and batch
+// i+1's hash run together, each alone would leave the SIMDs half idle); a slot's `done` event
+// orders its reuse after its previous batch.
+#define CBFT_WORK_SLOTS 2
+struct WorkSlot {
+  DevBuf h, flags, xyz, ps_tbl, ps_aok;
+  hipEvent_t done = nullptr;
+  bool used = false;
+};
+
 struct cbft_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -64,8 +76,10 @@ struct cbft_ctx {
   std::unordered_map<uint32_t, KeyTable> tables;
   uint32_t next_table_id = 1;
   // per-batch work buffers
-  DevBuf h, flags, xyz, verdicts;
-  DevBuf sig, msg, off, len, kidx, pk, ps_tbl, ps_aok;
+  WorkSlot slots[CBFT_WORK_SLOTS];
+  unsigned next_slot = 0;
+  DevBuf verdicts;
+  DevBuf sig, msg, off, len, kidx, pk;
   std::vector<uint64_t> host_verdicts;
   // profiling: events around K1 (hash), K3 (ladder), K4 (finish) of the last verify
   bool profiling = false;

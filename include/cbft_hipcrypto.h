@@ -149,6 +149,14 @@ int cbft_bls_verify(cbft_ctx* ctx, uint32_t keyset, const uint8_t* msg, uint32_t
 int cbft_bls_verify_multisig(cbft_ctx* ctx, uint32_t keyset, const uint8_t* msg, uint32_t len, const uint8_t* sig33,
                              const uint8_t* signers256, int* out_ok);
 
+/* out65 = sum of vk_i over the signer bitmap, compressed (65 zero bytes if a selected key does
+ * not decode).  The n-of-n multisig public key (BlsMultisigVerifier.cpp:33-38). */
+int cbft_bls_sum_keys(cbft_ctx* ctx, uint32_t keyset, const uint8_t* signers256, uint8_t* out65);
+
+/* Sign a share: out37 = 4-byte big-endian id || sk * g1_map(msg) compressed, sk = 32 bytes
+ * big-endian (< r) (IThresholdSigner::signData; BlsThresholdSigner.cpp:32-47). */
+int cbft_bls_sign(cbft_ctx* ctx, const uint8_t* sk32, uint32_t id, const uint8_t* msg, uint32_t len, uint8_t* out37);
+
 #ifdef __cplusplus
 }
 #endif

@@ -136,6 +136,45 @@ void shim_sign_shares_mt(const uint8_t* sks, const uint32_t* ids, uint32_t k, co
     });
   for (auto& x : th) x.join();
 }
+// CPU baseline of share verification (labelled "not RELIC"): per share, decompress, G2 line
+// precomputation for vk_id (as RELIC's pc_map recomputes the G2 side every call) and the
+// 2-pairing check e(H, vk) e(-sigma, g2) == 1, shares split over host threads.
+void shim_verify_shares_mt(const uint8_t* h33, const uint8_t* vks65, uint32_t n, const uint8_t* shares37,
+                           uint32_t k, uint8_t* out, int threads) {
+  g1a H;
+  g1_decompress(H, h33);
+  g2a G;
+  fp2_load(G.x, Bn254Consts::G2X);
+  fp2_load(G.y, Bn254Consts::G2Y);
+  G.inf = false;
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; t++)
+    th.emplace_back([=] {
+      std::vector<uint32_t> l0(BN_ATE_LINES * BN_LINE_WORDS), l1(BN_ATE_LINES * BN_LINE_WORDS);
+      for (uint32_t j = t; j < k; j += threads) {
+        uint32_t id;
+        g1a P[2];
+        g2a Q;
+        bool ok = bls_parse_share(id, P[1], shares37 + 37 * (size_t)j) && id >= 1 && id <= n &&
+                  g2_decompress(Q, vks65 + 65 * (size_t)(id - 1)) && !Q.inf;
+        if (ok) {
+          P[0] = H;
+          g2_precompute_lines(l0.data(), Q);
+          g2_precompute_lines(l1.data(), G);
+          const uint32_t* l[2] = {l0.data(), l1.data()};
+          if (P[1].inf) {
+            ok = pairing_check<1>(P, l);
+          } else {
+            f_neg(P[1].y, P[1].y);
+            ok = pairing_check<2>(P, l);
+          }
+        }
+        out[j] = ok ? 1 : 0;
+      }
+    });
+  for (auto& x : th) x.join();
+}
+
 void shim_g2_mul_gen_mt(const uint8_t* sks, uint32_t n, uint8_t* out, int threads) {
   std::vector<std::thread> th;
   for (int t = 0; t < threads; t++)

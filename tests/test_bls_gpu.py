@@ -123,3 +123,26 @@ def test_full_size_commit_certificate(ctx):
         assert ctx.bls_verify(kid, msg, comb)
     finally:
         ctx.bls_unload_keys(kid)
+
+
+def test_sign_matches_oracle(ctx):
+    # IThresholdSigner::signData: id (4 B big-endian) || sk * g1_map(msg) (BlsThresholdSigner.cpp:32-47)
+    rng = random.Random(5)
+    for sid, msg in ((1, b""), (7, bytes(32)), (2048, b"commit digest" * 3)):
+        sk = rng.randrange(1, B.R)
+        assert ctx.bls_sign(sk, sid, msg) == B.sign_share(sk, sid, msg)
+
+
+def test_sum_keys_is_multisig_pk(ctx):
+    # n-of-n multisig PK = sum of vk_i (BlsMultisigVerifier.cpp:33-38)
+    n, k = 9, 9
+    sk, sks, pk, vks = blsgen.keyset(n, k, seed=21)
+    kid = ctx.bls_load_keys(pk, vks)
+    try:
+        for ids in (range(1, n + 1), [2, 5, 9], [4]):
+            acc = None
+            for i in ids:
+                acc = B.ec_add(acc, B.g2_from_bytes(vks[i - 1]), None)
+            assert ctx.bls_sum_keys(kid, B.signers_bitmap(ids)) == B.g2_to_bytes(acc)
+    finally:
+        ctx.bls_unload_keys(kid)

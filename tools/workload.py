@@ -127,3 +127,80 @@ def cpu_verify(ss: SigSet, threads: int = 8, keycache=None) -> np.ndarray:
     if own:
         lib.cbft_cpu_keys_free(keycache, ss.pk.shape[0])
     return out
+
+
+# ------------------------------------------------------------------ BLS BN-P254 (config #4)
+# Host build of the library's own BN-P254 code (tests/cpp/libbn254_shim.so, `make shim`): used
+# here only to generate key sets and shares, and as the labelled "not RELIC" CPU baseline.
+BN_R = 0x2523648240000001BA344D8000000007FF9F800000000010A10000000000000D
+SHIM_SO = os.path.join(ROOT, "tests", "cpp", "libbn254_shim.so")
+_shim = None
+
+
+def bn_lib():
+    global _shim
+    if _shim is None:
+        if not os.path.exists(SHIM_SO):
+            raise RuntimeError(f"{SHIM_SO} missing: run `make shim`")
+        _shim = ctypes.CDLL(SHIM_SO)
+    return _shim
+
+
+@dataclass
+class BlsCert:
+    n: int
+    k: int
+    pk: bytes          # 65-byte group public key
+    vks: list          # n x 65-byte share verification keys
+    msg: bytes         # 32-byte digest
+    shares: list       # 37-byte shares (id || G1), some "doubled" (bad)
+    bad: set           # indices into shares
+    expected_sig: bytes
+
+
+def make_bls_cert(n: int = 1024, k: int = 683, extra: int = 0, bad_frac: float = 0.0, seed: int = 2024,
+                  threads: int = 8) -> BlsCert:
+    """Shamir key set (degree k-1 polynomial, as BlsThresholdKeygen), shares of k + extra
+    random signers over a 32-byte digest; bad shares are sigma doubled (TestBlsBatchVerifier.cpp:84-90)."""
+    import random
+    rng = random.Random(seed)
+    coeffs = [rng.randrange(1, BN_R) for _ in range(k)]
+
+    def f(x):
+        acc = 0
+        for c in reversed(coeffs):
+            acc = (acc * x + c) % BN_R
+        return acc
+
+    lib = bn_lib()
+    sks = {i: f(i) for i in range(1, n + 1)}
+    buf = b"".join(sks[i].to_bytes(32, "big") for i in range(1, n + 1))
+    out = ctypes.create_string_buffer(65 * n)
+    lib.shim_g2_mul_gen_mt(buf, n, out, threads)
+    vks = [out.raw[65 * i:65 * i + 65] for i in range(n)]
+    pkb = ctypes.create_string_buffer(65)
+    lib.shim_g2_mul_gen(coeffs[0].to_bytes(32, "big"), pkb)
+    msg = bytes(rng.randrange(256) for _ in range(32))
+    ids = sorted(rng.sample(range(1, n + 1), k + extra))
+    sbuf = b"".join(sks[i].to_bytes(32, "big") for i in ids)
+    arr = (ctypes.c_uint32 * len(ids))(*ids)
+    so = ctypes.create_string_buffer(37 * len(ids))
+    lib.shim_sign_shares_mt(sbuf, arr, len(ids), msg, len(msg), so, threads)
+    shares = [so.raw[37 * j:37 * j + 37] for j in range(len(ids))]
+    bad = set(rng.sample(range(len(shares)), int(round(bad_frac * len(shares)))))
+    two = (2).to_bytes(32, "big")
+    for j in bad:
+        d = ctypes.create_string_buffer(33)
+        lib.shim_g1_mul(shares[j][4:], two, d)
+        shares[j] = shares[j][:4] + d.raw
+    es = ctypes.create_string_buffer(37)
+    lib.shim_sign_share(coeffs[0].to_bytes(32, "big"), 0, msg, len(msg), es)
+    return BlsCert(n, k, pkb.raw, vks, msg, shares, bad, es.raw[4:])
+
+
+def cpu_bls_verify_shares(cert: BlsCert, h33: bytes, threads: int = 16) -> np.ndarray:
+    lib = bn_lib()
+    k = len(cert.shares)
+    out = np.zeros(k, dtype=np.uint8)
+    lib.shim_verify_shares_mt(h33, b"".join(cert.vks), cert.n, b"".join(cert.shares), k, _p(out), threads)
+    return out
