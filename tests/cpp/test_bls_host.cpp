@@ -135,7 +135,11 @@ static int testThreshold(const KeySet& ks) {
       threw = true;
     }
     CHECK(threw);
-    if (!almost) {
+    if (!almost && ks.n - 1 < ks.k) {  // n-of-n: one bad share leaves the set short
+      CHECK(acc->getNumValidShares() == ks.n - 1);
+      auto inv = acc->getInvalidShareIds();
+      CHECK(inv.size() == 1 && *inv.begin() == bad);
+    } else if (!almost) {
       CHECK(acc->getNumValidShares() == ks.k);
       auto inv = acc->getInvalidShareIds();
       CHECK(inv.size() == 1 && *inv.begin() == bad);
