@@ -279,6 +279,7 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   }
   // the slot's previous batch (maybe on another stream) must be done with its buffers
   if (slot.used) CBFT_HIP(hipStreamWaitEvent(s, slot.done, 0));
+
   Ed25519Batch b{n, d_pk, d_kidx, d_sig, d_msg, d_off, d_len};
   Ed25519Work w{};
   w.base_table = c->base_table.as<uint32_t>();

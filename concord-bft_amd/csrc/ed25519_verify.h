@@ -14,6 +14,9 @@
 #ifndef CBFT_VERIFY_BLOCK
 #define CBFT_VERIFY_BLOCK 256
 #endif
+#ifndef CBFT_COMB8_LDS
+#define CBFT_COMB8_LDS 1  // stage comb-table entries through LDS with global_load_lds
+#endif
 #ifndef CBFT_LADDER_MIN_WAVES
 #define CBFT_LADDER_MIN_WAVES 4  // waves/SIMD the ladder is register-allocated for
 #endif

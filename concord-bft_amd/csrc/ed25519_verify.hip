@@ -520,6 +520,81 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB8_MIN_WAVES)
   base += (size_t)half * 16 * (C8_ENT * C8_STRIDE);
   ge_p3 P;
   ge_p3_0(P);
+#if CBFT_COMB8_LDS
+  // Table entries are staged through LDS with global_load_lds (no VGPR destination): entry
+  // jj+1's 7 x 16 B are requested as soon as entry jj has been read out of LDS, so its HBM /
+  // L2 latency overlaps the rest of addition jj (the key tables, 2 GB at 4,096 keys, are read
+  // at random; B's table is L2-resident).  LDS image per wave: [chunk 0..6][lane][16 B]
+  // (lane-linear, as one global_load_lds_dwordx4 writes it), 7 KB per wave.
+  __shared__ uint4 stage[CBFT_VERIFY_BLOCK / 64][7][64];
+  uint4(*st)[64] = stage[threadIdx.x >> 6];
+  const uint32_t ln = threadIdx.x & 63u;
+  auto pop = [&]() {
+    const int d = (int)(dw[0] & 0xffu) - 128;
+    dw[0] = (dw[0] >> 8) | (dw[1] << 24);
+    dw[1] = (dw[1] >> 8) | (dw[2] << 24);
+    dw[2] = (dw[2] >> 8) | (dw[3] << 24);
+    dw[3] >>= 8;
+    return d;
+  };
+  auto request = [&](const uint32_t* e) {
+#pragma unroll
+    for (int c = 0; c < 7; c++)
+      __builtin_amdgcn_global_load_lds(e + 4 * c, (__attribute__((address_space(3))) void*)&st[c][0], 16, 0, 0);
+  };
+  int d = pop();
+  request(base + (d < 0 ? -d : d) * C8_STRIDE);
+#pragma nounroll
+  for (int jj = 0; jj < 16; jj++) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t ew[28];
+#pragma unroll
+    for (int c = 0; c < 7; c++) {
+      const uint4 v = st[c][ln];
+      ew[4 * c] = v.x;
+      ew[4 * c + 1] = v.y;
+      ew[4 * c + 2] = v.z;
+      ew[4 * c + 3] = v.w;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry jj is in VGPRs: the slot is free
+    const bool neg = d < 0;
+    if (jj < 15) {
+      d = pop();
+      request(base + ((jj + 1) * C8_ENT + (d < 0 ? -d : d)) * C8_STRIDE);
+    }
+    ge_p1p1 t;
+    {
+      // niels (y+x, y-x, 2dxy), negated by swapping y+x <-> y-x and C <-> -C (ge_add_mem)
+      fe A, B, C, D, s, e;
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) e.v[k] = neg ? ew[9 + k] : ew[k];
+      fe_add(s, P.Y, P.X);
+      fe_mul(A, s, e);
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) e.v[k] = neg ? ew[k] : ew[9 + k];
+      fe_sub(s, P.Y, P.X);
+      fe_mul(B, s, e);
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) e.v[k] = ew[18 + k];
+      fe_mul(C, e, P.T);
+      fe_add(D, P.Z, P.Z);
+      fe_sub(t.X, A, B);
+      fe_add(t.Y, A, B);
+      fe_add(s, D, C);
+      fe_carry(s);
+      fe_sub(e, D, C);
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        t.Z.v[k] = neg ? e.v[k] : s.v[k];
+        t.T.v[k] = neg ? s.v[k] : e.v[k];
+      }
+    }
+    fe_mul(P.T, t.X, t.Y);
+    fe_mul(P.X, t.X, t.T);
+    fe_mul(P.Y, t.Y, t.Z);
+    fe_mul(P.Z, t.Z, t.T);
+  }
+#else
 #pragma nounroll
   for (int jj = 0; jj < 16; jj++) {
     const int d = (int)(dw[0] & 0xffu) - 128;
@@ -535,6 +610,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB8_MIN_WAVES)
     fe_mul(P.Y, t.Y, t.Z);
     fe_mul(P.Z, t.Z, t.T);
   }
+#endif
   quad_combine<0xB1>(P, true);
   quad_combine<0x4E>(P, false);
   if (live && q == 0) {
