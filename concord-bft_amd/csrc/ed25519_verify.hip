@@ -164,33 +164,35 @@ __global__ void __launch_bounds__(64) ed25519_base_table_kernel(uint32_t* tbl, i
 // NW big-endian 64-bit words of (M || 0x80 || 0 ...) starting at M-relative offset base.
 // Only dwords that overlap [m, m+len) are loaded (an aligned dword holding >= 1 message byte
 // never faults), so callers need no padding after the blob.
+//
+// Branch-free: dword k is read from index min(k, kmax) (kmax = last dword holding a byte of
+// M), or from `safe` (any readable dword) when no dword of this window holds one; bytes at or
+// past len are then masked off arithmetically, so a wave never splits on message length.
 template <int NW>
-__device__ __forceinline__ void load_msg_words(uint64_t* W, const uint8_t* m, uint32_t len, uint32_t base) {
+__device__ __forceinline__ void load_msg_words(uint64_t* W, const uint8_t* m, uint32_t len, uint32_t base,
+                                               const uint32_t* safe) {
   const uintptr_t a = (uintptr_t)(m + base);
   const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
   const uint32_t sh = (uint32_t)(a & 3);
+  const int kmax = ((int)len - 1 - (int)base + (int)sh) >> 2;  // < 0: window is past M
   uint32_t d[2 * NW + 1];
 #pragma unroll
   for (int k = 0; k < 2 * NW + 1; k++) {
-    const int s = (int)(base + 4 * k) - (int)sh;  // M-relative start of dword k
-    d[k] = (s < (int)len) ? q[k] : 0u;
+    const uint32_t* src = kmax >= 0 ? q + (k < kmax ? k : kmax) : safe;
+    d[k] = *src;
   }
 #pragma unroll
   for (int j = 0; j < NW; j++) {
     const uint32_t lo = __builtin_amdgcn_alignbyte(d[2 * j + 1], d[2 * j], sh);
     const uint32_t hi = __builtin_amdgcn_alignbyte(d[2 * j + 2], d[2 * j + 1], sh);
     uint64_t w = ((uint64_t)bswap32(lo) << 32) | bswap32(hi);
-    const uint32_t q0 = base + 8u * j;
-    if (q0 + 8u > len) {  // this word holds the end of M: zero the tail, 0x80 marker
-#pragma unroll
-      for (int b = 0; b < 8; b++) {
-        const uint32_t pos = q0 + b;
-        const int shb = 56 - 8 * b;
-        if (pos >= len) w &= ~(0xffull << shb);
-        if (pos == len) w |= 0x80ull << shb;
-      }
-    }
-    W[j] = w;
+    // rem = bytes of M left at this word: keep the first min(rem, 8) (big-endian, high bytes
+    // first), then the 0x80 marker right after M's last byte
+    const int rem = (int)len - (int)(base + 8u * j);
+    const int keep = rem < 0 ? 0 : (rem > 8 ? 8 : rem);
+    const uint64_t mask = keep == 0 ? 0ull : (~0ull << (64 - 8 * keep));
+    const uint64_t mark = (rem >= 0 && rem < 8) ? (0x80ull << (56 - 8 * rem)) : 0ull;
+    W[j] = (w & mask) | mark;
   }
 }
 
@@ -205,6 +207,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const E
   load_words8(Sw, b.sig + i * 64 + 32);
   const uint8_t* m = b.msg + b.msg_off[i];
   const uint32_t len = b.msg_len[i];
+  const uint32_t* safe = reinterpret_cast<const uint32_t*>(b.sig + i * 64);  // readable dword
 
   uint64_t H[8], W[16];
   sha512_init(H);
@@ -216,9 +219,9 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const E
       for (int j = 0; j < 4; j++) W[j] = ((uint64_t)bswap32(Rw[2 * j]) << 32) | bswap32(Rw[2 * j + 1]);
 #pragma unroll
       for (int j = 0; j < 4; j++) W[4 + j] = ((uint64_t)bswap32(Aw[2 * j]) << 32) | bswap32(Aw[2 * j + 1]);
-      load_msg_words<8>(W + 8, m, len, 0u);
+      load_msg_words<8>(W + 8, m, len, 0u, safe);
     } else {
-      load_msg_words<16>(W, m, len, 128u * blk - 64u);
+      load_msg_words<16>(W, m, len, 128u * blk - 64u, safe);
     }
     if (blk == nblocks - 1) {
       W[14] = 0;

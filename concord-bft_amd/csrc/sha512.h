@@ -23,38 +23,70 @@ __device__ __constant__ const uint64_t kSha512K[80] = {
     0x113f9804bef90daeull, 0x1b710b35131c471bull, 0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull,
     0x431d67c49c100d4cull, 0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull};
 
-__device__ __forceinline__ uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-// 80 rounds as 5 x (16 unrolled rounds): full unrolling lets the scheduler hoist the whole
-// message schedule ahead of the rounds (180 VGPRs measured); one 16-round window keeps
-// W[16] + state live only.  K is read with uniform scalar loads per window.
+// 64-bit rotate as two v_alignbit_b32 on the 32-bit halves (N is a compile-time constant)
+template <int N>
+__device__ __forceinline__ uint64_t rotr64(uint64_t x) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  uint32_t rl, rh;
+  if (N < 32) {
+    rl = __builtin_amdgcn_alignbit(hi, lo, N);
+    rh = __builtin_amdgcn_alignbit(lo, hi, N);
+  } else {
+    rl = __builtin_amdgcn_alignbit(lo, hi, N - 32);
+    rh = __builtin_amdgcn_alignbit(hi, lo, N - 32);
+  }
+  return ((uint64_t)rh << 32) | rl;
+}
+
+#define SHA512_ROUND(a, b, c, d, e, f, g, h, kw)                                          \
+  do {                                                                                    \
+    const uint64_t S1_ = rotr64<14>(e) ^ rotr64<18>(e) ^ rotr64<41>(e);                   \
+    const uint64_t ch_ = (e & f) ^ (~e & g);                                              \
+    const uint64_t t1_ = h + S1_ + ch_ + (kw);                                            \
+    const uint64_t S0_ = rotr64<28>(a) ^ rotr64<34>(a) ^ rotr64<39>(a);                   \
+    const uint64_t mj_ = (a & b) ^ (c & (a ^ b));                                         \
+    d += t1_;                                                                             \
+    h = t1_ + S0_ + mj_;                                                                  \
+  } while (0)
+
+// Rounds 0-15 straight from the block, then 4 x 16 rounds with the message schedule in a
+// 16-word ring (no data-dependent control flow: an `if (r > 0)` inside the unrolled window
+// made the compiler copy the whole ring every round).  The 8 working variables rotate by
+// renaming (8 divides 16), so the window loop has no moves at its back edge.
 __device__ __forceinline__ void sha512_compress(uint64_t* H, uint64_t* W) {
   uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+#pragma unroll
+  for (int j = 0; j < 16; j += 8) {
+    SHA512_ROUND(a, b, c, d, e, f, g, h, kSha512K[j + 0] + W[j + 0]);
+    SHA512_ROUND(h, a, b, c, d, e, f, g, kSha512K[j + 1] + W[j + 1]);
+    SHA512_ROUND(g, h, a, b, c, d, e, f, kSha512K[j + 2] + W[j + 2]);
+    SHA512_ROUND(f, g, h, a, b, c, d, e, kSha512K[j + 3] + W[j + 3]);
+    SHA512_ROUND(e, f, g, h, a, b, c, d, kSha512K[j + 4] + W[j + 4]);
+    SHA512_ROUND(d, e, f, g, h, a, b, c, kSha512K[j + 5] + W[j + 5]);
+    SHA512_ROUND(c, d, e, f, g, h, a, b, kSha512K[j + 6] + W[j + 6]);
+    SHA512_ROUND(b, c, d, e, f, g, h, a, kSha512K[j + 7] + W[j + 7]);
+  }
 #pragma nounroll
-  for (int r = 0; r < 80; r += 16) {
+  for (int r = 16; r < 80; r += 16) {
 #pragma unroll
     for (int j = 0; j < 16; j++) {
-      if (r > 0) {
-        uint64_t w15 = W[(j + 1) & 15], w2 = W[(j + 14) & 15];
-        uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-        uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-        W[j] = W[j] + s0 + W[(j + 9) & 15] + s1;
-      }
-      uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-      uint64_t ch = (e & f) ^ (~e & g);
-      uint64_t t1 = h + S1 + ch + kSha512K[r + j] + W[j];
-      uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-      uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
-      uint64_t t2 = S0 + mj;
-      h = g;
-      g = f;
-      f = e;
-      e = d + t1;
-      d = c;
-      c = b;
-      b = a;
-      a = t1 + t2;
+      const uint64_t w15 = W[(j + 1) & 15], w2 = W[(j + 14) & 15];
+      const uint64_t s0 = rotr64<1>(w15) ^ rotr64<8>(w15) ^ (w15 >> 7);
+      const uint64_t s1 = rotr64<19>(w2) ^ rotr64<61>(w2) ^ (w2 >> 6);
+      W[j] = W[j] + s0 + W[(j + 9) & 15] + s1;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; j += 8) {
+      SHA512_ROUND(a, b, c, d, e, f, g, h, kSha512K[r + j + 0] + W[j + 0]);
+      SHA512_ROUND(h, a, b, c, d, e, f, g, kSha512K[r + j + 1] + W[j + 1]);
+      SHA512_ROUND(g, h, a, b, c, d, e, f, kSha512K[r + j + 2] + W[j + 2]);
+      SHA512_ROUND(f, g, h, a, b, c, d, e, kSha512K[r + j + 3] + W[j + 3]);
+      SHA512_ROUND(e, f, g, h, a, b, c, d, kSha512K[r + j + 4] + W[j + 4]);
+      SHA512_ROUND(d, e, f, g, h, a, b, c, kSha512K[r + j + 5] + W[j + 5]);
+      SHA512_ROUND(c, d, e, f, g, h, a, b, kSha512K[r + j + 6] + W[j + 6]);
+      SHA512_ROUND(b, c, d, e, f, g, h, a, kSha512K[r + j + 7] + W[j + 7]);
     }
   }
   H[0] += a;
