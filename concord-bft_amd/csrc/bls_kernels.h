@@ -6,10 +6,11 @@
 
 #define BLS_SIG_WORDS 19     // affine G1 (x, y, inf flag) per parsed share
 #define BLS_JAC_WORDS 27     // Jacobian G1 partial sum
+#define BLS_G2A_WORDS 37     // affine G2 (x.a, x.b, y.a, y.b, inf flag) of a decoded key
 
 size_t cbft_bls_lines_words_per_key();
 hipError_t cbft_bls_launch_keys(const uint8_t* d_keys65, uint32_t nkeys, uint32_t* d_lines, uint8_t* d_ok,
-                                hipStream_t s);
+                                uint32_t* d_aff, hipStream_t s);
 hipError_t cbft_bls_launch_gen_lines(uint32_t* d_lines, hipStream_t s);
 hipError_t cbft_bls_launch_hash(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, hipStream_t s);
 hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uint32_t n, const uint32_t* d_H,
@@ -19,8 +20,8 @@ hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uin
 hipError_t cbft_bls_launch_combine(const uint32_t* d_sig, const uint32_t* d_ids, const uint8_t* d_use, uint32_t k,
                                    int multisig, uint32_t* d_lambda, uint32_t* d_partial, uint8_t* d_out33,
                                    uint32_t* d_sig_aff, hipStream_t s);
-hipError_t cbft_bls_launch_g2_sum(const uint8_t* d_keys65, uint32_t n, const uint8_t* d_bitmap, uint32_t* d_lines,
-                                  uint8_t* d_ok, uint8_t* d_out65, hipStream_t s);
+hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok, uint32_t n, const uint8_t* d_bitmap,
+                                  uint32_t* d_lines, uint8_t* d_ok, uint8_t* d_out65, hipStream_t s);
 hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, const uint32_t* d_pk_lines,
                                   const uint8_t* d_pk_ok, const uint32_t* d_gen_lines, uint8_t* d_result,
                                   hipStream_t s);

@@ -36,13 +36,34 @@ __device__ __forceinline__ void g1a_load(g1a& a, const uint32_t* o) {
   a.inf = o[18] != 0;
 }
 
+__device__ __forceinline__ void g2a_store(uint32_t* o, const g2a& a) {
+  for (int i = 0; i < 9; i++) {
+    o[i] = a.x.a.v[i];
+    o[9 + i] = a.x.b.v[i];
+    o[18 + i] = a.y.a.v[i];
+    o[27 + i] = a.y.b.v[i];
+  }
+  o[36] = a.inf ? 1u : 0u;
+}
+__device__ __forceinline__ void g2a_load(g2a& a, const uint32_t* o) {
+  for (int i = 0; i < 9; i++) {
+    a.x.a.v[i] = o[i];
+    a.x.b.v[i] = o[9 + i];
+    a.y.a.v[i] = o[18 + i];
+    a.y.b.v[i] = o[27 + i];
+  }
+  a.inf = o[36] != 0;
+}
+
 __global__ void __launch_bounds__(64) bls_keys_kernel(const uint8_t* keys65, uint32_t nkeys, uint32_t* lines,
-                                                      uint8_t* ok) {
+                                                      uint8_t* ok, uint32_t* aff) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nkeys) return;
   g2a q;
   bool good = g2_decompress(q, keys65 + 65 * (size_t)k) && !q.inf;
   ok[k] = good ? 1 : 0;
+  if (!good) q.inf = true;
+  g2a_store(aff + (size_t)k * BLS_G2A_WORDS, q);
   if (good) g2_precompute_lines(lines + (size_t)k * LINES_PER_KEY, q);
 }
 
@@ -196,31 +217,66 @@ __global__ void bls_msm_finish_kernel(const uint32_t* partial, uint32_t nparts, 
   if (sig_aff) g1a_store(sig_aff, a);
 }
 
-// multisig public key = sum of vk_i for set bits (bit id-1, LSB first) of the 256-byte bitmap;
-// then its Miller-loop lines.  Single lane (the G2 sum is <= 2048 additions).
-__global__ void bls_g2_sum_kernel(const uint8_t* keys65, uint32_t n, const uint8_t* bitmap, uint32_t* lines,
-                                  uint8_t* ok, uint8_t* out65) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// multisig public key = sum of vk_i for set bits (bit id-1, LSB first) of the 256-byte bitmap,
+// then its Miller-loop lines (BlsMultisigVerifier.cpp:33-38, 89-95).  One block: each of the
+// SUM_THREADS lanes adds its strided share of the (already decoded, at load) keys in Jacobian
+// form, then an LDS tree halves the partial sums; lane 0 normalises, compresses and computes
+// the lines.  A selected key that did not decode makes the result invalid (ok = 0).
+#define SUM_THREADS 256
+__global__ void __launch_bounds__(SUM_THREADS) bls_g2_sum_kernel(const uint32_t* aff, const uint8_t* key_ok,
+                                                                 uint32_t n, const uint8_t* bitmap, uint32_t* lines,
+                                                                 uint8_t* ok, uint8_t* out65) {
+  __shared__ uint32_t sp[SUM_THREADS / 2][54];
+  __shared__ int bad;
+  const int t = threadIdx.x;
+  if (t == 0) bad = 0;
+  __syncthreads();
   g2j acc;
   fp2_one(acc.X);
   fp2_one(acc.Y);
   fp2_zero(acc.Z);
-  bool good = true;
-  for (uint32_t id = 1; id <= n; id++) {
+  bool mine_bad = false;
+  for (uint32_t id = 1 + t; id <= n; id += SUM_THREADS) {
     if (!((bitmap[(id - 1) >> 3] >> ((id - 1) & 7)) & 1)) continue;
-    g2a q;
-    if (!g2_decompress(q, keys65 + 65 * (size_t)(id - 1))) {
-      good = false;
+    if (!key_ok[id - 1]) {
+      mine_bad = true;
       continue;
     }
+    g2a q;
+    g2a_load(q, aff + (size_t)(id - 1) * BLS_G2A_WORDS);
     g2j p;
     p.X = q.x;
     p.Y = q.y;
     fp2_one(p.Z);
     g2_add_j(acc, acc, p);
   }
+  if (mine_bad) atomicOr(&bad, 1);
+  for (int stride = SUM_THREADS / 2; stride >= 1; stride >>= 1) {
+    if (t >= stride && t < 2 * stride) {
+      const fp2* src[3] = {&acc.X, &acc.Y, &acc.Z};
+      for (int c = 0; c < 3; c++)
+        for (int q = 0; q < 9; q++) {
+          sp[t - stride][18 * c + q] = src[c]->a.v[q];
+          sp[t - stride][18 * c + 9 + q] = src[c]->b.v[q];
+        }
+    }
+    __syncthreads();
+    if (t < stride) {
+      g2j o;
+      fp2* dst[3] = {&o.X, &o.Y, &o.Z};
+      for (int c = 0; c < 3; c++)
+        for (int q = 0; q < 9; q++) {
+          dst[c]->a.v[q] = sp[t][18 * c + q];
+          dst[c]->b.v[q] = sp[t][18 * c + 9 + q];
+        }
+      g2_add_j(acc, acc, o);
+    }
+    __syncthreads();
+  }
+  if (t != 0) return;
   g2a s;
   g2_to_affine(s, acc);
+  const bool good = !bad;
   if (out65) {
     if (good) {
       g2_compress(out65, s);
@@ -228,9 +284,9 @@ __global__ void bls_g2_sum_kernel(const uint8_t* keys65, uint32_t n, const uint8
       for (int q = 0; q < 65; q++) out65[q] = 0;
     }
   }
-  good = good && !s.inf;
-  ok[0] = good ? 1 : 0;
-  if (good && lines) g2_precompute_lines(lines, s);
+  const bool usable = good && !s.inf;
+  ok[0] = usable ? 1 : 0;
+  if (usable && lines) g2_precompute_lines(lines, s);
 }
 
 // e(H, PK) * e(-sigma, g2) == 1 for a combined signature (33 bytes)
@@ -276,9 +332,10 @@ __global__ void bls_sign_kernel(const uint8_t* msg, uint32_t len, const uint32_t
 size_t cbft_bls_lines_words_per_key() { return (size_t)LINES_PER_KEY; }
 
 hipError_t cbft_bls_launch_keys(const uint8_t* d_keys65, uint32_t nkeys, uint32_t* d_lines, uint8_t* d_ok,
-                                hipStream_t s) {
+                                uint32_t* d_aff, hipStream_t s) {
   if (!nkeys) return hipSuccess;
-  hipLaunchKernelGGL(bls_keys_kernel, dim3((nkeys + 63) / 64), dim3(64), 0, s, d_keys65, nkeys, d_lines, d_ok);
+  hipLaunchKernelGGL(bls_keys_kernel, dim3((nkeys + 63) / 64), dim3(64), 0, s, d_keys65, nkeys, d_lines, d_ok,
+                     d_aff);
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_gen_lines(uint32_t* d_lines, hipStream_t s) {
@@ -310,9 +367,10 @@ hipError_t cbft_bls_launch_combine(const uint32_t* d_sig, const uint32_t* d_ids,
   hipLaunchKernelGGL(bls_msm_finish_kernel, dim3(1), dim3(64), 0, s, d_partial, nparts, d_out33, d_sig_aff);
   return hipGetLastError();
 }
-hipError_t cbft_bls_launch_g2_sum(const uint8_t* d_keys65, uint32_t n, const uint8_t* d_bitmap, uint32_t* d_lines,
-                                  uint8_t* d_ok, uint8_t* d_out65, hipStream_t s) {
-  hipLaunchKernelGGL(bls_g2_sum_kernel, dim3(1), dim3(64), 0, s, d_keys65, n, d_bitmap, d_lines, d_ok, d_out65);
+hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok, uint32_t n, const uint8_t* d_bitmap,
+                                  uint32_t* d_lines, uint8_t* d_ok, uint8_t* d_out65, hipStream_t s) {
+  hipLaunchKernelGGL(bls_g2_sum_kernel, dim3(1), dim3(SUM_THREADS), 0, s, d_aff, d_key_ok, n, d_bitmap, d_lines, d_ok,
+                     d_out65);
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, const uint32_t* d_pk_lines,

@@ -65,68 +65,70 @@ BN_HD void f_one(Fe<F>& r) {
   for (int i = 0; i < BN_LIMBS; i++) r.v[i] = F::ONE[i];
 }
 
-// r = a * b * 2^-261 mod q (a, b < 2q, normalised)  ->  r < 2q, normalised
+// Montgomery reduction of 17 product columns c[0..16] (each < 2^61.2, c[17] = 0 spare):
+// word-serial REDC, m_k = c_k * (-q^-1) mod 2^29, then m_k q added into columns k..k+8.  The
+// only serial dependency is column k -> m_k -> column k+1 (about 4 instructions per step);
+// the 9 mads of each step are independent.  Columns stay < 2^62.2 + carries.
 template <class F>
-BN_HD void f_mul(Fe<F>& r, const Fe<F>& a, const Fe<F>& b) {
-  uint32_t m[BN_LIMBS], o[BN_LIMBS];
+BN_HD void f_redc(Fe<F>& r, uint64_t* c) {
+#pragma unroll
+  for (int k = 0; k < BN_LIMBS; k++) {
+    const uint32_t mk = ((uint32_t)c[k] * F::NPRIME) & BN_MASK;
+    c[k] = bn_mad(mk, F::Q[0], c[k]);  // low 29 bits become 0
+    c[k + 1] = bn_mad(mk, F::Q[1], c[k + 1]) + (c[k] >> 29);
+#pragma unroll
+    for (int i = 2; i < BN_LIMBS; i++) c[k + i] = bn_mad(mk, F::Q[i], c[k + i]);
+  }
   uint64_t acc = 0;
 #pragma unroll
+  for (int i = 0; i < BN_LIMBS - 1; i++) {
+    acc += c[BN_LIMBS + i];
+    r.v[i] = (uint32_t)acc & BN_MASK;
+    acc >>= 29;
+  }
+  r.v[BN_LIMBS - 1] = (uint32_t)(acc + c[2 * BN_LIMBS - 1]);  // value < 2q < 2^255
+}
+
+// r = a * b * 2^-261 mod q (a, b < 2q, normalised)  ->  r < 2q, normalised.  Product columns
+// first (17 independent mad chains), then f_redc: bit-identical to the interleaved FIPS form
+// (the same m_k), but with a dependency chain ~4x shorter, which is what a pairing running on
+// few lanes waits on.
+template <class F>
+BN_HD void f_mul(Fe<F>& r, const Fe<F>& a, const Fe<F>& b) {
+  uint64_t c[2 * BN_LIMBS];
+#pragma unroll
   for (int k = 0; k < 2 * BN_LIMBS - 1; k++) {
+    uint64_t acc = 0;
 #pragma unroll
     for (int i = 0; i < BN_LIMBS; i++) {
       const int j = k - i;
       if (j >= 0 && j < BN_LIMBS) acc = bn_mad(a.v[i], b.v[j], acc);
     }
-#pragma unroll
-    for (int j = 0; j < BN_LIMBS; j++) {
-      const int i = k - j;
-      if (j < k && j < BN_LIMBS && i >= 0 && i < BN_LIMBS) acc = bn_mad(m[j], F::Q[i], acc);
-    }
-    if (k < BN_LIMBS) {
-      m[k] = ((uint32_t)acc * F::NPRIME) & BN_MASK;
-      acc = bn_mad(m[k], F::Q[0], acc);  // low 29 bits become 0
-      acc >>= 29;
-    } else {
-      o[k - BN_LIMBS] = (uint32_t)acc & BN_MASK;
-      acc >>= 29;
-    }
+    c[k] = acc;
   }
-  o[BN_LIMBS - 1] = (uint32_t)acc;  // final carry = top limb (value < 2q < 2^255)
-#pragma unroll
-  for (int i = 0; i < BN_LIMBS; i++) r.v[i] = o[i];
+  c[2 * BN_LIMBS - 1] = 0;
+  f_redc(r, c);
 }
 
 template <class F>
 BN_HD void f_sqr(Fe<F>& r, const Fe<F>& a) {
-  uint32_t a2[BN_LIMBS], m[BN_LIMBS], o[BN_LIMBS];
+  uint32_t a2[BN_LIMBS];
 #pragma unroll
   for (int i = 0; i < BN_LIMBS; i++) a2[i] = a.v[i] << 1;
-  uint64_t acc = 0;
+  uint64_t c[2 * BN_LIMBS];
 #pragma unroll
   for (int k = 0; k < 2 * BN_LIMBS - 1; k++) {
+    uint64_t acc = 0;
 #pragma unroll
     for (int i = 0; i < BN_LIMBS; i++) {
       const int j = k - i;
       if (j > i && j < BN_LIMBS) acc = bn_mad(a2[i], a.v[j], acc);
     }
     if ((k & 1) == 0 && (k >> 1) < BN_LIMBS) acc = bn_mad(a.v[k >> 1], a.v[k >> 1], acc);
-#pragma unroll
-    for (int j = 0; j < BN_LIMBS; j++) {
-      const int i = k - j;
-      if (j < k && j < BN_LIMBS && i >= 0 && i < BN_LIMBS) acc = bn_mad(m[j], F::Q[i], acc);
-    }
-    if (k < BN_LIMBS) {
-      m[k] = ((uint32_t)acc * F::NPRIME) & BN_MASK;
-      acc = bn_mad(m[k], F::Q[0], acc);
-      acc >>= 29;
-    } else {
-      o[k - BN_LIMBS] = (uint32_t)acc & BN_MASK;
-      acc >>= 29;
-    }
+    c[k] = acc;
   }
-  o[BN_LIMBS - 1] = (uint32_t)acc;  // final carry = top limb (value < 2q < 2^255)
-#pragma unroll
-  for (int i = 0; i < BN_LIMBS; i++) r.v[i] = o[i];
+  c[2 * BN_LIMBS - 1] = 0;
+  f_redc(r, c);
 }
 
 // t = a - c*q for the selected c (c = 0 or 1 times q or 2q via `sub`), keep if non-negative

@@ -48,11 +48,12 @@ int cbft_bls_load_keys(cbft_ctx* c, const uint8_t* pk65, const uint8_t* vks65, u
   CBFT_HIP(ks.keys65.reserve(nk * 65));
   CBFT_HIP(ks.lines.reserve(nk * cbft_bls_lines_words_per_key() * 4));
   CBFT_HIP(ks.ok.reserve(nk));
+  CBFT_HIP(ks.aff.reserve(nk * BLS_G2A_WORDS * 4));
   CBFT_HIP(hipMemcpyAsync(ks.keys65.p, pk65, 65, hipMemcpyHostToDevice, c->stream));
   if (n)
     CBFT_HIP(hipMemcpyAsync(ks.keys65.as<uint8_t>() + 65, vks65, (size_t)n * 65, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(cbft_bls_launch_keys(ks.keys65.as<uint8_t>(), (uint32_t)nk, ks.lines.as<uint32_t>(), ks.ok.as<uint8_t>(),
-                                c->stream));
+                                ks.aff.as<uint32_t>(), c->stream));
   CBFT_HIP(hipStreamSynchronize(c->stream));
   uint32_t id = c->next_bls_id++;
   c->bls_sets.emplace(id, std::move(ks));
@@ -70,6 +71,7 @@ int cbft_bls_unload_keys(cbft_ctx* c, uint32_t id) {
   ks->keys65.release();
   ks->lines.release();
   ks->ok.release();
+  ks->aff.release();
   c->bls_sets.erase(id);
   return CBFT_OK;
 }
@@ -211,7 +213,8 @@ int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint3
   CBFT_HIP(c->bls_ms_lines.reserve(cbft_bls_lines_words_per_key() * 4));
   CBFT_HIP(c->bls_ms_ok.reserve(1));
   CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
-  CBFT_HIP(cbft_bls_launch_g2_sum(ks->keys65.as<uint8_t>() + 65, ks->n, c->bls_bitmap.as<uint8_t>(),
+  CBFT_HIP(cbft_bls_launch_g2_sum(ks->aff.as<uint32_t>() + BLS_G2A_WORDS, ks->ok.as<uint8_t>() + 1, ks->n,
+                                  c->bls_bitmap.as<uint8_t>(),
                                   c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), nullptr, c->stream));
   return bls_verify_with_lines(c, sig33, c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), out_ok);
 }
@@ -226,7 +229,8 @@ int cbft_bls_sum_keys(cbft_ctx* c, uint32_t id, const uint8_t* signers256, uint8
   CBFT_HIP(c->bls_ms_ok.reserve(1));
   CBFT_HIP(c->bls_out.reserve(65));
   CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
-  CBFT_HIP(cbft_bls_launch_g2_sum(ks->keys65.as<uint8_t>() + 65, ks->n, c->bls_bitmap.as<uint8_t>(), nullptr,
+  CBFT_HIP(cbft_bls_launch_g2_sum(ks->aff.as<uint32_t>() + BLS_G2A_WORDS, ks->ok.as<uint8_t>() + 1, ks->n,
+                                  c->bls_bitmap.as<uint8_t>(), nullptr,
                                   c->bls_ms_ok.as<uint8_t>(), c->bls_out.as<uint8_t>(), c->stream));
   CBFT_HIP(hipMemcpyAsync(out65, c->bls_out.p, 65, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipStreamSynchronize(c->stream));

@@ -156,6 +156,7 @@ void cbft_close(cbft_ctx* c) {
     kv.second.keys65.release();
     kv.second.lines.release();
     kv.second.ok.release();
+    kv.second.aff.release();
   }
   for (DevBuf* b : {&c->bls_gen_lines, &c->bls_msg, &c->bls_H, &c->bls_shares, &c->bls_valid, &c->bls_sig,
                     &c->bls_ids, &c->bls_use, &c->bls_lambda, &c->bls_partial, &c->bls_out, &c->bls_ms_lines,

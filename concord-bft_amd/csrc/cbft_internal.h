@@ -53,7 +53,7 @@ struct KeyTable {
 // Miller-loop lines precomputed (slot 0 = PK, slot i = vk_i)
 struct BlsKeySet {
   uint32_t n = 0;
-  DevBuf keys65, lines, ok;
+  DevBuf keys65, lines, ok, aff;  // aff: decoded affine keys (BLS_G2A_WORDS each)
 };
 
 // Per-batch intermediate state of one in-flight verify (h, S<L flags, R' coordinates, the
