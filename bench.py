@@ -55,6 +55,8 @@ def parse():
     ap.add_argument("--msg-len", type=int, default=256)
     ap.add_argument("--nkeys", type=int, default=4096)
     ap.add_argument("--key-mode", choices=["keytable", "perkey"], default="keytable")
+    ap.add_argument("--comb-radix", type=int, default=11,
+                    help="radix 2^r of the per-key comb tables (8..13; 11 = 3 MB per key)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-runs", type=int, default=200)
@@ -94,7 +96,7 @@ def main():
     d_off = to_dev(ss.off.view(np.int64), np.int64)
     d_len = to_dev(ss.len.view(np.int32), np.int32)
     if args.key_mode == "keytable":
-        tid = ctx.load_keys(ss.pk)  # key table resident, like SigManager's per-key verifiers
+        tid = ctx.load_keys(ss.pk, radix=args.comb_radix)  # key tables resident, like SigManager's verifiers
         d_kidx = to_dev(ss.key_idx.view(np.int32), np.int32)
         d_pk = None
     else:
@@ -191,12 +193,14 @@ def main():
     ladder_ms = statistics.median(stage["ladder"])
     pipe_ms = sum(statistics.median(v) for v in stage.values())
     achieved = OPS_DSM * n / (ladder_ms * 1e-3)
-    kname = "ed25519_comb8_ladder_kernel" if args.key_mode == "keytable" else "ed25519_ladder_kernel"
+    kname = "ed25519_comb_ladder_kernel" if args.key_mode == "keytable" else "ed25519_ladder_kernel"
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "pmc_ladder.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            rec = json.load(open(pmc))
+            if rec.get("kernel") == kname and rec.get("batch") == n and rec.get("comb_radix") == args.comb_radix:
+                traffic = rec.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
     roofline = {"bound": "valu_int32", "achieved": achieved / 1e12, "peak": INT32_PEAK / 1e12, "unit": "TOP/s",
@@ -258,7 +262,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "u32", "data": "synthetic",
             "config": {"workload": "ed25519_verify_64k_256B_4096keys (BASELINE config #2)", "batch_per_gpu": n,
-                       "msg_len": args.msg_len, "nkeys": args.nkeys, "key_mode": args.key_mode,
+                       "msg_len": args.msg_len, "nkeys": args.nkeys, "key_mode": args.key_mode, "comb_radix": args.comb_radix if args.key_mode == "keytable" else None,
                        "inflight_batches": inflight,
                        "parallelism": f"static shard x{world}, RCCL all-gather of verdict bitmaps"},
             "roofline": roofline, "cpu_baseline": cpu,

@@ -33,6 +33,8 @@ ABI = [
     ("cbft_open", ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_size_t]),
     ("cbft_close", None, [ctypes.c_void_p]),
     ("cbft_ed25519_load_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, _u32p]),
+    ("cbft_ed25519_load_keys_ex", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, _u32p]),
     ("cbft_ed25519_unload_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
     ("cbft_ed25519_verify_batch", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -142,11 +144,12 @@ class Context:
             pass
 
     # ------------------------------------------------------------------ keys
-    def load_keys(self, pks: Iterable[bytes] | np.ndarray) -> int:
+    def load_keys(self, pks: Iterable[bytes] | np.ndarray, radix: int = 0) -> int:
+        """Upload a key table; radix = comb radix 2^radix of the per-key tables (8..13, 0 = default)."""
         arr = _as_rows(pks, 32)
         tid = ctypes.c_uint32()
-        _check(self.lib.cbft_ed25519_load_keys(self.handle, _ptr(arr), arr.shape[0], ctypes.byref(tid)),
-               "cbft_ed25519_load_keys")
+        _check(self.lib.cbft_ed25519_load_keys_ex(self.handle, _ptr(arr), arr.shape[0], radix, ctypes.byref(tid)),
+               "cbft_ed25519_load_keys_ex")
         return tid.value
 
     def unload_keys(self, tid: int):

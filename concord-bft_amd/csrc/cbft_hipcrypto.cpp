@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
@@ -29,8 +30,37 @@ int cbft_fail(hipError_t e, const char* what, const char* file, int line) {
   return e == hipErrorOutOfMemory ? CBFT_ENOMEM : CBFT_EIO;
 }
 
-// keys per launch of the comb-table build (bounds the 589,824-B-per-key staging buffer)
-static const uint32_t kCombBuildChunk = 256;
+// table-build lanes per launch (bounds the projective staging buffer: 18 KB per lane)
+static const size_t kCombBuildLanes = 131072;
+
+// comb radix of a key table: explicit (8..16), else CBFT_COMB_RADIX from the environment, else
+// CBFT_COMB_A_RADIX_DEF
+static int key_radix(int requested) {
+  if (requested) return requested;
+  if (const char* e = getenv("CBFT_COMB_RADIX")) {
+    const int r = atoi(e);
+    if (cbft_comb_npos(r)) return r;
+  }
+  return CBFT_COMB_A_RADIX_DEF;
+}
+
+// Build comb tables for nunits encoded points (d_pk, 32 B each) into d_tbl, in launches of at
+// most kCombBuildLanes lanes; synchronous.
+static hipError_t build_comb(const uint8_t* d_pk, size_t nunits, int negate, const CombGeom& g, uint32_t* d_tbl,
+                             uint8_t* d_aok, hipStream_t s) {
+  const size_t lanes_per_unit = (size_t)g.npos * g.chunks();
+  const size_t chunk = std::max<size_t>(1, std::min(nunits, kCombBuildLanes / lanes_per_unit));
+  DevBuf tmp;
+  hipError_t e = tmp.reserve(cbft_ed25519_comb_tmp_words(g, chunk) * sizeof(uint32_t));
+  for (size_t k0 = 0; e == hipSuccess && k0 < nunits; k0 += chunk) {
+    const size_t m = std::min(chunk, nunits - k0);
+    e = cbft_ed25519_launch_comb_tables(d_pk + k0 * 32, m, negate, g, d_tbl + k0 * g.words_per_unit(),
+                                        tmp.as<uint32_t>(), d_aok ? d_aok + k0 : nullptr, s);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  tmp.release();
+  return e;
+}
 
 static int reserve_slot(WorkSlot& w, size_t n) {
   CBFT_HIP(w.h.reserve(n * 8 * sizeof(uint32_t)));
@@ -113,20 +143,16 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
       static const uint8_t kB[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
                                      0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
                                      0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
-      DevBuf enc, tmp;
-      if (c->base_comb.reserve(cbft_ed25519_comb8_words_per_unit() * 4) != hipSuccess ||
-          enc.reserve(32) != hipSuccess || tmp.reserve(cbft_ed25519_comb8_tmp_words_per_unit() * 4) != hipSuccess) {
+      const CombGeom gb = cbft_comb_geom(CBFT_COMB_B_RADIX);
+      DevBuf enc;
+      if (c->base_comb.reserve(gb.words_per_unit() * 4) != hipSuccess || enc.reserve(32) != hipSuccess) {
         enc.release();
-        tmp.release();
         rc = CBFT_ENOMEM;
         break;
       }
       bool okb = hipMemcpy(enc.p, kB, 32, hipMemcpyHostToDevice) == hipSuccess &&
-                 cbft_ed25519_launch_comb8_tables(enc.as<uint8_t>(), 1, 0, c->base_comb.as<uint32_t>(),
-                                                 tmp.as<uint32_t>(), nullptr, c->stream) == hipSuccess &&
-                 hipStreamSynchronize(c->stream) == hipSuccess;
+                 build_comb(enc.as<uint8_t>(), 1, 0, gb, c->base_comb.as<uint32_t>(), nullptr, c->stream) == hipSuccess;
       enc.release();
-      tmp.release();
       if (!okb) {
         rc = CBFT_EIO;
         break;
@@ -203,37 +229,21 @@ int cbft_sync(cbft_ctx* c) {
   return CBFT_OK;
 }
 
-int cbft_ed25519_load_keys(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, uint32_t* out_id) {
+int cbft_ed25519_load_keys_ex(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, int comb_radix, uint32_t* out_id) {
   if (!c || !out_id || (nkeys && !pk)) return CBFT_EINVAL;
+  if (comb_radix && (comb_radix < 8 || comb_radix > 13)) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
   KeyTable kt;
   kt.nkeys = nkeys;
+  kt.geo = cbft_comb_geom(key_radix(comb_radix));
   const size_t n = std::max<uint32_t>(nkeys, 1);
   CBFT_HIP(kt.pk.reserve(n * 32));
-  CBFT_HIP(kt.comb.reserve(n * cbft_ed25519_comb8_words_per_unit() * sizeof(uint32_t)));
+  CBFT_HIP(kt.comb.reserve(n * kt.geo.words_per_unit() * sizeof(uint32_t)));
   CBFT_HIP(kt.aok.reserve(n));
   if (nkeys) {
-    // the radix-256 comb tables are built in chunks of keys so the projective staging buffer
-    // stays bounded (each key stages 32 x 128 points)
-    const uint32_t chunk = std::min<uint32_t>(nkeys, kCombBuildChunk);
-    DevBuf tmp;
-    hipError_t e = tmp.reserve((size_t)chunk * cbft_ed25519_comb8_tmp_words_per_unit() * sizeof(uint32_t));
-    if (e != hipSuccess) {
-      kt.pk.release();
-      kt.comb.release();
-      kt.aok.release();
-      return cbft_fail(e, "hipMalloc(comb tmp)", __FILE__, __LINE__);
-    }
-    e = hipMemcpyAsync(kt.pk.p, pk, (size_t)nkeys * 32, hipMemcpyHostToDevice, c->stream);
-    for (uint32_t k0 = 0; e == hipSuccess && k0 < nkeys; k0 += chunk) {
-      const uint32_t m = std::min(chunk, nkeys - k0);
-      e = cbft_ed25519_launch_comb8_tables(kt.pk.as<uint8_t>() + (size_t)k0 * 32, m, 1,
-                                           kt.comb.as<uint32_t>() + (size_t)k0 * cbft_ed25519_comb8_words_per_unit(),
-                                           tmp.as<uint32_t>(), kt.aok.as<uint8_t>() + k0, c->stream);
-    }
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    tmp.release();
+    hipError_t e = hipMemcpyAsync(kt.pk.p, pk, (size_t)nkeys * 32, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = build_comb(kt.pk.as<uint8_t>(), nkeys, 1, kt.geo, kt.comb.as<uint32_t>(), kt.aok.as<uint8_t>(), c->stream);
     if (e != hipSuccess) {
       kt.pk.release();
       kt.comb.release();
@@ -246,6 +256,10 @@ int cbft_ed25519_load_keys(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, uint3
   c->tables.emplace(id, std::move(kt));
   *out_id = id;
   return CBFT_OK;
+}
+
+int cbft_ed25519_load_keys(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, uint32_t* out_id) {
+  return cbft_ed25519_load_keys_ex(c, pk, nkeys, 0, out_id);
 }
 
 int cbft_ed25519_unload_keys(cbft_ctx* c, uint32_t id) {
@@ -298,6 +312,7 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     b.pk = it->second.pk.as<uint8_t>();
     w.comb_tbl = it->second.comb.as<uint32_t>();
     w.base_comb = c->base_comb.as<uint32_t>();
+    w.comb = cbft_comb_ladder(it->second.geo.w, CBFT_COMB_B_RADIX);
     w.aok = it->second.aok.as<uint8_t>();
   }
   CBFT_HIP(cbft_ed25519_launch_verify(b, w, s, c->profiling ? c->ev : nullptr));

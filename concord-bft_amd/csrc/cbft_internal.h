@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "cbft_hipcrypto.h"
+#include "ed25519_verify.h"
 
 struct DevBuf {
   void* p = nullptr;
@@ -46,7 +47,8 @@ struct DevBuf {
 
 struct KeyTable {
   uint32_t nkeys = 0;
-  DevBuf pk, comb, aok;  // raw keys, per-key radix-256 comb tables of -A, decode status
+  CombGeom geo{};        // radix of the per-key comb tables
+  DevBuf pk, comb, aok;  // raw keys, per-key comb tables of -A, decode status
 };
 
 // BLS verifier key set: group public key + n share verification keys, decoded and with their

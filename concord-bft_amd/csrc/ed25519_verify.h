@@ -32,12 +32,56 @@ struct Ed25519Batch {
   const uint32_t* msg_len;  // n lengths
 };
 
+// Geometry of a fixed-base comb table with signed radix-2^w digits (8 <= w <= 16):
+// npos positions of entries() = 2^(w-1) + 1 affine niels points (e * 2^(w j) * P, e = 0 ..
+// 2^(w-1)), 32 words each.  npos is the least count whose top digit stays <= 2^(w-1) for every
+// scalar < L (tests/test_comb_recode.py).
+struct CombGeom {
+  int w;
+  int npos;
+  __host__ __device__ int entries() const { return (1 << (w - 1)) + 1; }
+  __host__ __device__ int chunks() const { return (1 << (w - 1)) / 128; }  // table-build lanes per position
+  __host__ __device__ size_t words_per_unit() const { return (size_t)npos * entries() * 32; }
+};
+inline int cbft_comb_npos(int w) {
+  static const int kPos[17] = {0, 0, 0, 0, 0, 0, 0, 0, 32, 29, 26, 23, 22, 20, 19, 17, 16};
+  return (w >= 8 && w <= 16) ? kPos[w] : 0;
+}
+inline CombGeom cbft_comb_geom(int w) { return CombGeom{w, cbft_comb_npos(w)}; }
+
+// Ladder parameters of the comb verify: -A tables (a), B's table (b), the recoding offsets
+// 2^(w-1) sum_{j < npos-1} 2^(w j) as 8 little-endian words, and additions per lane.
+struct CombLadder {
+  CombGeom a, b;
+  uint32_t offA[8], offB[8];
+  int nper;
+};
+inline void cbft_comb_offset(const CombGeom& g, uint32_t* off) {
+  for (int k = 0; k < 8; k++) off[k] = 0;
+  for (int j = 0; j + 1 < g.npos; j++) {
+    const int bit = g.w * j + g.w - 1;
+    off[bit >> 5] |= 1u << (bit & 31);
+  }
+}
+inline CombLadder cbft_comb_ladder(int wa, int wb) {
+  CombLadder c{};
+  c.a = cbft_comb_geom(wa);
+  c.b = cbft_comb_geom(wb);
+  cbft_comb_offset(c.a, c.offA);
+  cbft_comb_offset(c.b, c.offB);
+  c.nper = (c.a.npos + c.b.npos + 3) / 4;
+  return c;
+}
+#define CBFT_COMB_B_RADIX 16     // B's table: 16 positions x 32,769 entries (67 MB per context)
+#define CBFT_COMB_A_RADIX_DEF 11  // default per-key table: 23 positions x 1,025 entries (3.0 MB/key)
+
 // Device work buffers of one verify launch.
 struct Ed25519Work {
   const uint32_t* base_table;  // cbft_ed25519_base_table_words() words
   const uint32_t* tbl;         // windowed -A tables, indexed like pk (per-signature key mode)
-  const uint32_t* comb_tbl;    // radix-256 comb tables of -A per key (key-table mode; tbl unused)
-  const uint32_t* base_comb;   // radix-256 comb table of B
+  const uint32_t* comb_tbl;    // comb tables of -A per key (key-table mode; tbl unused)
+  const uint32_t* base_comb;   // comb table of B
+  CombLadder comb;             // their geometry
   const uint8_t* aok;          // A decoded OK, indexed like pk
   uint32_t* h_soa;             // 8 x n words
   uint8_t* flags;              // n bytes
@@ -46,10 +90,9 @@ struct Ed25519Work {
 };
 
 size_t cbft_ed25519_table_words_per_unit();
-size_t cbft_ed25519_comb8_words_per_unit();
-size_t cbft_ed25519_comb8_tmp_words_per_unit();
-hipError_t cbft_ed25519_launch_comb8_tables(const uint8_t* d_pk, size_t nunits, int negate, uint32_t* d_tbl,
-                                           uint32_t* d_tmp, uint8_t* d_aok, hipStream_t stream);
+size_t cbft_ed25519_comb_tmp_words(const CombGeom& g, size_t nunits);
+hipError_t cbft_ed25519_launch_comb_tables(const uint8_t* d_pk, size_t nunits, int negate, const CombGeom& g,
+                                           uint32_t* d_tbl, uint32_t* d_tmp, uint8_t* d_aok, hipStream_t stream);
 size_t cbft_ed25519_base_table_words();
 hipError_t cbft_ed25519_build_base_table(uint32_t* d_tbl, hipStream_t stream);
 hipError_t cbft_ed25519_launch_prep(const uint8_t* d_pk, size_t nunits, uint32_t* d_tbl, uint8_t* d_aok,

@@ -353,68 +353,87 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_finish_kernel(const
 }
 
 // ---------------------------------------------------------------------------------------
-// Radix-256 fixed-base comb ("comb8"), four lanes per signature (key-table mode).
+// Wide fixed-base combs, four lanes per signature (key-table mode).
 //
-// At the headline batch (64K signatures) one lane per signature gives 1,024 waves: one wave per
-// SIMD, and a lone wave issues VALU at half the SIMD's rate (MI355X_MICROARCH.md, constants
-// table).  The comb sum is split instead:
-//   C8_P[j][e] = e * 256^j * P,  j = 0..31, e = 0..128 (affine niels, 128-B entries, e = 0 =
-//   identity);  s + 0x8080..80 has bytes b_j, digit d_j = b_j - 128 in [-128, 127], and
-//   [s]P = sum_j sign(d_j) C8_P[j][|d_j|]   (32 mixed additions, no doublings).
-// Lane q of each quad (4 adjacent lanes) sums 16 positions of one scalar:
-//   q = 0: h positions 0..15 on -A,  q = 1: h positions 16..31,  q = 2, 3: S on B likewise,
-// then two DPP butterfly levels (xor 1, xor 2) add the partial sums: every lane of the quad ends
-// with R' = [S]B + [h](-A).  4,096 waves at 64K: 4 waves per SIMD.
-// The per-key table (32 x 129 x 128 B = 528,384 B) lives in HBM; B's table (same size) is read
-// through L2 by every lane.
+// For a point P known before the signatures arrive (B, or a loaded key's -A) the table
+//   C_P[j][e] = e * 2^(w j) * P,   j = 0..npos-1, e = 0..2^(w-1)   (affine niels, 128-B entries,
+//   e = 0 = identity)
+// turns [s]P into sum_j sign(d_j) C_P[j][|d_j|] with signed radix-2^w digits: s' = s + offset,
+// offset = 2^(w-1) sum_{j < npos-1} 2^(w j); d_j = chunk_j(s') - 2^(w-1) below the top position,
+// d_top = chunk_top(s') in [0, 2^(w-1)] (CombGeom in ed25519_verify.h; tests/test_comb_recode.py
+// checks the recoding exhaustively at the range edges).  One mixed addition per position and no
+// doublings: B's table is radix 2^16 (16 positions, 67 MB: Infinity-Cache resident), a key's
+// table radix 2^w_A (default 2^11: 23 positions, 3.0 MB per key, 12.4 GB for 4,096 keys -- HBM
+// is 288 GB and keys are long-lived, SigManager.cpp:139-150), so a verify is 16 + 23 = 39 mixed
+// additions (the radix-256 comb of the first round: 64).
+//
+// The 39 additions are dealt to the 4 lanes of a quad in order (lane q takes additions
+// q*nper .. q*nper+nper-1, the A positions first), then two DPP butterfly levels (quad_perm
+// xor 1, xor 2) add the four partial sums: every lane of the quad ends with
+// R' = [S]B + [h](-A).  4,096 waves at 64K signatures: 4 waves per SIMD.
 // ---------------------------------------------------------------------------------------
-#define C8_POS 32
-#define C8_ENT 129
-#define C8_STRIDE 32  // words per entry: one 128-B line
-#define C8_WORDS_PER_UNIT (C8_POS * C8_ENT * C8_STRIDE)
-#define C8_TMP_WORDS_PER_LANE (128 * CACHED_WORDS)
-#define C8_TABLE_BLOCK 64
+#define COMB_STRIDE 32  // words per entry: one 128-B line (y+x | y-x | 2dxy, 9 limbs each, + pad)
+#define COMB_CHUNK 128  // multiples built per table-build lane
+#define COMB_TMP_WORDS_PER_LANE (COMB_CHUNK * CACHED_WORDS)
+#define COMB_TABLE_BLOCK 64
+#define COMB_MAX_STEPS 12  // additions per lane (nper) the ladder supports
 
-// One lane per (unit, position j): P_j = 256^j P (8j doublings), multiples 1..128 of P_j
-// projectively into tmp, Montgomery batch inversion, affine niels into tbl[unit][j][1..128].
-__global__ void __launch_bounds__(C8_TABLE_BLOCK) ed25519_comb8_table_kernel(const uint8_t* pk, size_t nunits,
-                                                                             int negate, uint32_t* tbl,
+// One lane per (unit, position j, chunk c): P_j = 2^(w j) P (w j doublings), then the multiples
+// 128c+1 .. 128c+128 of P_j projectively into tmp, Montgomery batch inversion, affine niels into
+// tbl[unit][j][128c+1 .. 128c+128]; the c = 0 lane also writes the identity entry 0.
+__global__ void __launch_bounds__(COMB_TABLE_BLOCK) ed25519_comb_table_kernel(const uint8_t* pk, size_t nunits,
+                                                                             int negate, CombGeom geo, uint32_t* tbl,
                                                                              uint32_t* tmp, uint8_t* aok) {
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const size_t u = g / C8_POS;
-  const int j = (int)(g % C8_POS);
+  const int chunks = geo.chunks();
+  const size_t u = g / ((size_t)geo.npos * chunks);
+  const int j = (int)((g / chunks) % geo.npos);
+  const int c = (int)(g % chunks);
   if (u >= nunits) return;
   uint32_t Aw[8];
   load_words8(Aw, pk + u * 32);
   ge_p3 Pj;
   const bool ok = ge_frombytes(Pj, Aw);
-  if (aok && j == 0) aok[u] = ok ? 1 : 0;
+  if (aok && j == 0 && c == 0) aok[u] = ok ? 1 : 0;
   if (negate) {
     fe_neg(Pj.X, Pj.X);
     fe_neg(Pj.T, Pj.T);
   }
 #pragma nounroll
-  for (int d = 0; d < 8 * j; d++) {
+  for (int d = 0; d < geo.w * j; d++) {
     ge_p1p1 r;
     ge_dbl(r, Pj.X, Pj.Y, Pj.Z);
     ge_p1p1_to_p3(Pj, r);
   }
-  uint32_t* t = tmp + g * (size_t)C8_TMP_WORDS_PER_LANE;
-  uint32_t* out = tbl + (u * C8_POS + j) * (size_t)(C8_ENT * C8_STRIDE);
   ge_cached cj;
   ge_p3_to_cached(cj, Pj);
-  ge_p3 Q = Pj;
+  // Q = (128c + 1) P_j, MSB first over the 15 bits a chunk index can have (w <= 16)
+  ge_p3 Q;
+  ge_p3_0(Q);
+  const uint32_t k0 = (uint32_t)c * COMB_CHUNK + 1u;
+#pragma nounroll
+  for (int bit = 14; bit >= 0; bit--) {
+    ge_p1p1 r;
+    ge_dbl(r, Q.X, Q.Y, Q.Z);
+    ge_p1p1_to_p3(Q, r);
+    if ((k0 >> bit) & 1u) {
+      ge_add(r, Q, cj, false);
+      ge_p1p1_to_p3(Q, r);
+    }
+  }
+  uint32_t* t = tmp + g * (size_t)COMB_TMP_WORDS_PER_LANE;
+  uint32_t* out = tbl + (u * geo.npos + j) * (size_t)geo.entries() * COMB_STRIDE;
   fe acc;
   fe_1(acc);
 #pragma nounroll
-  for (int k = 1; k <= 128; k++) {
+  for (int k = 1; k <= COMB_CHUNK; k++) {
     uint32_t* e = t + (size_t)(k - 1) * CACHED_WORDS;
     fe_store(e, Q.X);
     fe_store(e + 9, Q.Y);
     fe_store(e + 18, Q.Z);
     fe_mul(acc, acc, Q.Z);
     fe_store(e + 27, acc);  // prefix product Z_1 .. Z_k
-    if (k < 128) {
+    if (k < COMB_CHUNK) {
       ge_p1p1 r;
       ge_add(r, Q, cj, false);
       ge_p1p1_to_p3(Q, r);
@@ -425,7 +444,7 @@ __global__ void __launch_bounds__(C8_TABLE_BLOCK) ed25519_comb8_table_kernel(con
   fe d2;
   fe_load_const(d2, kFeD2);
 #pragma nounroll
-  for (int k = 128; k >= 1; k--) {
+  for (int k = COMB_CHUNK; k >= 1; k--) {
     uint32_t* e = t + (size_t)(k - 1) * CACHED_WORDS;
     fe zi, x, y, z, xy, ypx, ymx, t2d;
     if (k > 1) {
@@ -446,15 +465,17 @@ __global__ void __launch_bounds__(C8_TABLE_BLOCK) ed25519_comb8_table_kernel(con
     fe_carry(ypx);
     fe_sub(ymx, y, x);
     fe_mul(t2d, xy, d2);
-    uint32_t* o = out + (size_t)k * C8_STRIDE;
+    uint32_t* o = out + ((size_t)c * COMB_CHUNK + k) * COMB_STRIDE;
     fe_store(o, ypx);
     fe_store(o + 9, ymx);
     fe_store(o + 18, t2d);
 #pragma unroll
-    for (int w = 27; w < C8_STRIDE; w++) o[w] = 0;
+    for (int w = 27; w < COMB_STRIDE; w++) o[w] = 0;
   }
+  if (c == 0) {
 #pragma unroll
-  for (int w = 0; w < C8_STRIDE; w++) out[w] = (w == 0 || w == 9) ? 1u : 0u;  // identity (1, 1, 0)
+    for (int w = 0; w < COMB_STRIDE; w++) out[w] = (w == 0 || w == 9) ? 1u : 0u;  // identity (1, 1, 0)
+  }
 }
 
 template <int CTRL>
@@ -485,70 +506,101 @@ __device__ __forceinline__ void quad_combine(ge_p3& P, bool needT) {
   fe_mul(P.Z, t.Z, t.T);
 }
 
-#ifndef CBFT_COMB8_MIN_WAVES
-#define CBFT_COMB8_MIN_WAVES 4
+// w-bit chunk of a 256-bit little-endian word array at a runtime bit offset (bits >= 256 read
+// as 0); the word selects are cndmask chains, so no scratch indexing.
+__device__ __forceinline__ uint32_t chunk_at(const uint32_t* s, uint32_t off, uint32_t w) {
+  const uint32_t wi = off >> 5, sh = off & 31u;
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (uint32_t t = 0; t < 8; t++) {
+    lo = wi == t ? s[t] : lo;
+    hi = wi + 1 == t ? s[t] : hi;
+  }
+  const uint64_t v = (((uint64_t)hi << 32) | lo) >> sh;
+  return (uint32_t)v & ((1u << w) - 1u);
+}
+
+// s + off (mod 2^256) in place
+__device__ __forceinline__ void add256(uint32_t* s, const uint32_t* off) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const uint64_t t = (uint64_t)s[k] + off[k] + c;
+    s[k] = (uint32_t)t;
+    c = t >> 32;
+  }
+}
+
+#ifndef CBFT_COMB_MIN_WAVES
+#define CBFT_COMB_MIN_WAVES 4
 #endif
 
-__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB8_MIN_WAVES)
-    ed25519_comb8_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* tbl,
-                                const uint32_t* base8, uint32_t* xyz_soa) {
+__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
+    ed25519_comb_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* atbl,
+                               const uint32_t* btbl, const CombLadder cl, uint32_t* xyz_soa) {
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t q = threadIdx.x & 3u;
   size_t i = g >> 2;
   const bool live = i < b.n;
   if (!live) i = b.n - 1;  // tail quads compute a copy (all lanes stay active for the DPP)
-  const bool onB = (q & 2u) != 0;
-  const uint32_t half = q & 1u;
-  uint32_t w[8];
-  if (onB) {
-    load_words8(w, b.sig + i * 64 + 32);
-  } else {
-#pragma unroll
-    for (int k = 0; k < 8; k++) w[k] = h_soa[k * b.n + i];
-  }
-  // s' = s + 0x8080..80; this lane's 16 bytes (words 4*half .. 4*half+3)
-  uint32_t dw[4];
+  const uint32_t ntot = cl.a.npos + cl.b.npos;
+  const uint32_t first = q * cl.nper;
+  // Digits of this lane's additions, 16-bit offset binary (d + 2^15), kept in LDS
+  // ([step][thread]: conflict-free) so the addition loop holds no digit registers.
+  __shared__ uint16_t sdig[COMB_MAX_STEPS][CBFT_VERIFY_BLOCK];
   {
-    uint64_t c = 0;
+    uint32_t hs[8], ss[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) {
-      const uint64_t s = (uint64_t)w[k] + 0x80808080u + c;
-      w[k] = (uint32_t)s;
-      c = s >> 32;
+    for (int k = 0; k < 8; k++) hs[k] = h_soa[k * b.n + i];
+    load_words8(ss, b.sig + i * 64 + 32);
+    add256(hs, cl.offA);
+    add256(ss, cl.offB);
+#pragma unroll
+    for (int jj = 0; jj < COMB_MAX_STEPS; jj++) {
+      const uint32_t k = first + jj;
+      const bool isA = k < (uint32_t)cl.a.npos;
+      const uint32_t pos = isA ? k : k - cl.a.npos;
+      const uint32_t w = isA ? cl.a.w : cl.b.w;
+      const uint32_t top = (isA ? cl.a.npos : cl.b.npos) - 1;
+      uint32_t s[8];
+#pragma unroll
+      for (int t = 0; t < 8; t++) s[t] = isA ? hs[t] : ss[t];
+      const uint32_t ch = chunk_at(s, pos * w, w);
+      const uint32_t half = 1u << (w - 1);
+      // top digit in [0, 2^(w-1)]; only S >= L (flagged, rejected in K4) can exceed it
+      const uint32_t tmax = half - (w == 16 ? 1u : 0u);
+      int d = pos == top ? (int)(ch < tmax ? ch : tmax) : (int)ch - (int)half;
+      if (jj >= cl.nper || k >= ntot) d = 0;
+      sdig[jj][threadIdx.x] = (uint16_t)(d + 32768);
     }
-#pragma unroll
-    for (int k = 0; k < 4; k++) dw[k] = half ? w[4 + k] : w[k];
   }
-  const uint32_t* base = onB ? base8 : tbl + (size_t)b.key_idx[i] * C8_WORDS_PER_UNIT;
-  base += (size_t)half * 16 * (C8_ENT * C8_STRIDE);
+  const uint32_t* akey = atbl + (size_t)b.key_idx[i] * cl.a.words_per_unit();
+  auto entry = [&](uint32_t jj, int d) {
+    const uint32_t k = first + jj;
+    const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+    if (k < (uint32_t)cl.a.npos) return akey + ((size_t)k * cl.a.entries() + ad) * COMB_STRIDE;
+    const uint32_t pos = k < ntot ? k - cl.a.npos : 0u;  // past the last position: identity
+    return btbl + ((size_t)pos * cl.b.entries() + ad) * COMB_STRIDE;
+  };
+  auto digit = [&](int jj) { return (int)sdig[jj][threadIdx.x] - 32768; };
   ge_p3 P;
   ge_p3_0(P);
-#if CBFT_COMB8_LDS
   // Table entries are staged through LDS with global_load_lds (no VGPR destination): entry
   // jj+1's 7 x 16 B are requested as soon as entry jj has been read out of LDS, so its HBM /
-  // L2 latency overlaps the rest of addition jj (the key tables, 2 GB at 4,096 keys, are read
-  // at random; B's table is L2-resident).  LDS image per wave: [chunk 0..6][lane][16 B]
-  // (lane-linear, as one global_load_lds_dwordx4 writes it), 7 KB per wave.
+  // Infinity-Cache latency overlaps the rest of addition jj.  LDS image per wave:
+  // [chunk 0..6][lane][16 B] (lane-linear, as one global_load_lds_dwordx4 writes it), 7 KB.
   __shared__ uint4 stage[CBFT_VERIFY_BLOCK / 64][7][64];
   uint4(*st)[64] = stage[threadIdx.x >> 6];
   const uint32_t ln = threadIdx.x & 63u;
-  auto pop = [&]() {
-    const int d = (int)(dw[0] & 0xffu) - 128;
-    dw[0] = (dw[0] >> 8) | (dw[1] << 24);
-    dw[1] = (dw[1] >> 8) | (dw[2] << 24);
-    dw[2] = (dw[2] >> 8) | (dw[3] << 24);
-    dw[3] >>= 8;
-    return d;
-  };
   auto request = [&](const uint32_t* e) {
 #pragma unroll
     for (int c = 0; c < 7; c++)
       __builtin_amdgcn_global_load_lds(e + 4 * c, (__attribute__((address_space(3))) void*)&st[c][0], 16, 0, 0);
   };
-  int d = pop();
-  request(base + (d < 0 ? -d : d) * C8_STRIDE);
+  int d = digit(0);
+  request(entry(0, d));
 #pragma nounroll
-  for (int jj = 0; jj < 16; jj++) {
+  for (int jj = 0; jj < cl.nper; jj++) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t ew[28];
 #pragma unroll
@@ -561,9 +613,9 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB8_MIN_WAVES)
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry jj is in VGPRs: the slot is free
     const bool neg = d < 0;
-    if (jj < 15) {
-      d = pop();
-      request(base + ((jj + 1) * C8_ENT + (d < 0 ? -d : d)) * C8_STRIDE);
+    if (jj + 1 < cl.nper) {
+      d = digit(jj + 1);
+      request(entry(jj + 1, d));
     }
     ge_p1p1 t;
     {
@@ -597,23 +649,6 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB8_MIN_WAVES)
     fe_mul(P.Y, t.Y, t.Z);
     fe_mul(P.Z, t.Z, t.T);
   }
-#else
-#pragma nounroll
-  for (int jj = 0; jj < 16; jj++) {
-    const int d = (int)(dw[0] & 0xffu) - 128;
-    dw[0] = (dw[0] >> 8) | (dw[1] << 24);
-    dw[1] = (dw[1] >> 8) | (dw[2] << 24);
-    dw[2] = (dw[2] >> 8) | (dw[3] << 24);
-    dw[3] >>= 8;
-    const uint32_t* e = base + (jj * C8_ENT + (d < 0 ? -d : d)) * C8_STRIDE;
-    ge_p1p1 t;
-    ge_add_mem<true>(t, P, e, d < 0);
-    fe_mul(P.T, t.X, t.Y);
-    fe_mul(P.X, t.X, t.T);
-    fe_mul(P.Y, t.Y, t.Z);
-    fe_mul(P.Z, t.Z, t.T);
-  }
-#endif
   quad_combine<0xB1>(P, true);
   quad_combine<0x4E>(P, false);
   if (live && q == 0) {
@@ -626,15 +661,17 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB8_MIN_WAVES)
 // ---------------------------------------------------------------------------------------
 // host-side launch helpers (used by cbft_hipcrypto.cpp)
 // ---------------------------------------------------------------------------------------
-size_t cbft_ed25519_comb8_words_per_unit() { return (size_t)C8_WORDS_PER_UNIT; }
-size_t cbft_ed25519_comb8_tmp_words_per_unit() { return (size_t)C8_POS * C8_TMP_WORDS_PER_LANE; }
+size_t cbft_ed25519_comb_tmp_words(const CombGeom& g, size_t nunits) {
+  return nunits * (size_t)g.npos * g.chunks() * COMB_TMP_WORDS_PER_LANE;
+}
 
-hipError_t cbft_ed25519_launch_comb8_tables(const uint8_t* d_pk, size_t nunits, int negate, uint32_t* d_tbl,
-                                            uint32_t* d_tmp, uint8_t* d_aok, hipStream_t stream) {
+hipError_t cbft_ed25519_launch_comb_tables(const uint8_t* d_pk, size_t nunits, int negate, const CombGeom& g,
+                                           uint32_t* d_tbl, uint32_t* d_tmp, uint8_t* d_aok, hipStream_t stream) {
   if (nunits == 0) return hipSuccess;
-  const size_t lanes = nunits * C8_POS;
-  hipLaunchKernelGGL(ed25519_comb8_table_kernel, dim3((unsigned)((lanes + C8_TABLE_BLOCK - 1) / C8_TABLE_BLOCK)),
-                     dim3(C8_TABLE_BLOCK), 0, stream, d_pk, nunits, negate, d_tbl, d_tmp, d_aok);
+  if (g.w < 8 || g.w > 16) return hipErrorInvalidValue;
+  const size_t lanes = nunits * g.npos * g.chunks();
+  hipLaunchKernelGGL(ed25519_comb_table_kernel, dim3((unsigned)((lanes + COMB_TABLE_BLOCK - 1) / COMB_TABLE_BLOCK)),
+                     dim3(COMB_TABLE_BLOCK), 0, stream, d_pk, nunits, negate, g, d_tbl, d_tmp, d_aok);
   return hipGetLastError();
 }
 size_t cbft_ed25519_table_words_per_unit() { return (size_t)Shape::TA * CACHED_WORDS; }
@@ -658,15 +695,19 @@ hipError_t cbft_ed25519_launch_prep(const uint8_t* d_pk, size_t nunits, uint32_t
 hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& w, hipStream_t stream,
                                       hipEvent_t* ev) {
   if (b.n == 0) return hipSuccess;
+  const bool comb = w.comb_tbl && w.base_comb && b.key_idx;
+  if (comb && (w.comb.nper < 1 || w.comb.nper > COMB_MAX_STEPS || 4 * w.comb.nper < w.comb.a.npos + w.comb.b.npos))
+    return hipErrorInvalidValue;
   const dim3 grid(grid_for(b.n)), block(CBFT_VERIFY_BLOCK);
   if (ev) (void)hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(ed25519_hash_kernel, grid, block, 0, stream, b, w.h_soa, w.flags);
   if (ev) (void)hipEventRecord(ev[1], stream);
-  if (w.comb_tbl && w.base_comb && b.key_idx)
-    hipLaunchKernelGGL(ed25519_comb8_ladder_kernel, dim3((unsigned)((4 * b.n + CBFT_VERIFY_BLOCK - 1) / CBFT_VERIFY_BLOCK)),
-                       block, 0, stream, b, w.h_soa, w.comb_tbl, w.base_comb, w.xyz_soa);
-  else
+  if (comb) {
+    hipLaunchKernelGGL(ed25519_comb_ladder_kernel, dim3((unsigned)((4 * b.n + CBFT_VERIFY_BLOCK - 1) / CBFT_VERIFY_BLOCK)),
+                       block, 0, stream, b, w.h_soa, w.comb_tbl, w.base_comb, w.comb, w.xyz_soa);
+  } else {
     hipLaunchKernelGGL(ed25519_ladder_kernel, grid, block, 0, stream, b, w.h_soa, w.tbl, w.base_table, w.xyz_soa);
+  }
   if (ev) (void)hipEventRecord(ev[2], stream);
   hipLaunchKernelGGL(ed25519_finish_kernel, grid, block, 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words);
   if (ev) (void)hipEventRecord(ev[3], stream);

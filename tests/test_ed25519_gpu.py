@@ -53,6 +53,30 @@ def test_golden_key_table(ctx, golden):
         ctx.unload_keys(tid)
 
 
+@pytest.mark.parametrize("radix", [8, 9, 10, 12, 13])
+def test_golden_key_table_radix(ctx, golden, radix):
+    """Every comb radix gives the golden verdicts (the default radix is covered above)."""
+    keys = sorted({v.pk for v in golden})
+    index = {k: i for i, k in enumerate(keys)}
+    tid = ctx.load_keys(keys, radix=radix)
+    try:
+        n = len(golden)
+        got = _bools(ctx.verify(tid, [index[v.pk] for v in golden], [v.sig for v in golden],
+                                [v.msg for v in golden]), n)
+        exp = np.array([bool(v.verdict) for v in golden])
+        assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
+    finally:
+        ctx.unload_keys(tid)
+
+
+def test_load_keys_bad_radix(ctx):
+    lib = ctx.lib
+    tid = ctypes.c_uint32()
+    key = (ctypes.c_uint8 * 32)()
+    for r in (7, 14, -1):
+        assert lib.cbft_ed25519_load_keys_ex(ctx.handle, key, 1, r, ctypes.byref(tid)) == -22
+
+
 @pytest.mark.parametrize("n", [1, 7, 63, 64, 65, 200, 1000])
 def test_ragged_batch_sizes(ctx, golden, n):
     vs = [golden[i % len(golden)] for i in range(n)]
