@@ -55,8 +55,8 @@ def parse():
     ap.add_argument("--msg-len", type=int, default=256)
     ap.add_argument("--nkeys", type=int, default=4096)
     ap.add_argument("--key-mode", choices=["keytable", "perkey"], default="keytable")
-    ap.add_argument("--comb-radix", type=int, default=11,
-                    help="radix 2^r of the per-key comb tables (8..13; 11 = 3 MB per key)")
+    ap.add_argument("--comb-radix", type=int, default=13,
+                    help="radix 2^r of the per-key comb tables (8..13; 13 = 10.5 MB per key, 43 GB at 4,096 keys)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-runs", type=int, default=200)
@@ -192,23 +192,36 @@ def main():
     ctx.set_profiling(False)
     ladder_ms = statistics.median(stage["ladder"])
     pipe_ms = sum(statistics.median(v) for v in stage.values())
-    achieved = OPS_DSM * n / (ladder_ms * 1e-3)
     kname = "ed25519_comb_ladder_kernel" if args.key_mode == "keytable" else "ed25519_ladder_kernel"
-    traffic = None
+    # Executed VALU work of one ladder launch, from this configuration's own rocprofv3 --pmc passes
+    # (profiles/pmc_ladder.json, tools/pmc_summary.py): every VALU wave-instruction is 64 lane-ops,
+    # and the INT64-class ones (v_mad_u64_u32, measured half rate) take two issue slots, so
+    # slot_ops / kernel time against the INT32 lane-op peak is the VALU-busy fraction.
+    traffic = slot_ops = valu_ops = None
     pmc = os.path.join(ROOT, "profiles", "pmc_ladder.json")
     if os.path.exists(pmc):
         try:
             rec = json.load(open(pmc))
             if rec.get("kernel") == kname and rec.get("batch") == n and rec.get("comb_radix") == args.comb_radix:
                 traffic = rec.get("hbm_bytes_per_launch")
+                k = rec["counters"][kname]
+                valu_ops = k["SQ_INSTS_VALU"] * 64
+                slot_ops = (k["SQ_INSTS_VALU"] + k["SQ_INSTS_VALU_INT64"]) * 64
         except Exception:
-            traffic = None
-    roofline = {"bound": "valu_int32", "achieved": achieved / 1e12, "peak": INT32_PEAK / 1e12, "unit": "TOP/s",
-                "frac": achieved / INT32_PEAK, "traffic": traffic,
-                "kernel": kname, "kernel_ms": ladder_ms,
-                "ops_per_unit": OPS_DSM, "units_per_launch": n,
+            traffic = slot_ops = valu_ops = None
+    model = OPS_DSM * n / (ladder_ms * 1e-3)  # SURVEY.md §8(d) ref10 model, work-equivalent
+    achieved = slot_ops / (ladder_ms * 1e-3) if slot_ops else None
+    roofline = {"bound": "valu_int32", "achieved": achieved / 1e12 if achieved else None,
+                "peak": INT32_PEAK / 1e12, "unit": "TOP/s",
+                "frac": achieved / INT32_PEAK if achieved else None, "traffic": traffic,
+                "kernel": kname, "kernel_ms": ladder_ms, "units_per_launch": n,
+                "achieved_basis": "executed VALU issue slots per launch (PMC, INT64-class x2) / kernel time",
+                "valu_lane_ops_per_launch": valu_ops, "issue_slot_ops_per_launch": slot_ops,
+                "model_ref10": {"ops_per_unit": OPS_DSM, "work_equivalent_TOPs": model / 1e12,
+                                "note": "SURVEY.md 8(d) op model of a ref10 double-scalar mult; the comb "
+                                        "executes fewer field ops, so this exceeds the issue peak"},
                 "stage_ms": {k: statistics.median(v) for k, v in stage.items()},
-                "pipeline_frac": (n / (pipe_ms * 1e-3)) * ops_per_verify(args.msg_len) / INT32_PEAK}
+                "pipeline_frac_ref10": (n / (pipe_ms * 1e-3)) * ops_per_verify(args.msg_len) / INT32_PEAK}
 
     out = None
     if rank == 0:

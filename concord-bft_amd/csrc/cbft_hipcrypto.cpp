@@ -33,15 +33,22 @@ int cbft_fail(hipError_t e, const char* what, const char* file, int line) {
 // table-build lanes per launch (bounds the projective staging buffer: 18 KB per lane)
 static const size_t kCombBuildLanes = 131072;
 
-// comb radix of a key table: explicit (8..16), else CBFT_COMB_RADIX from the environment, else
-// CBFT_COMB_A_RADIX_DEF
-static int key_radix(int requested) {
+// comb radix of a key table: explicit (8..13), else $CBFT_COMB_RADIX, else the widest radix
+// whose tables for nkeys keys fit the per-table budget ($CBFT_COMB_BUDGET_GB, default 64 GB of
+// the 288 GB HBM): 13 (10.5 MB/key, 9 additions per lane) up to ~6,100 keys, 11 (3.0 MB/key,
+// 10) up to ~21,000, then 8 (0.53 MB/key, 12).
+static int key_radix(int requested, uint32_t nkeys) {
   if (requested) return requested;
   if (const char* e = getenv("CBFT_COMB_RADIX")) {
     const int r = atoi(e);
-    if (cbft_comb_npos(r)) return r;
+    if (r >= 8 && r <= 13) return r;
   }
-  return CBFT_COMB_A_RADIX_DEF;
+  double budget = 64.0;
+  if (const char* e = getenv("CBFT_COMB_BUDGET_GB")) budget = atof(e);
+  for (int r : {13, 11}) {
+    if ((double)nkeys * cbft_comb_geom(r).words_per_unit() * 4.0 <= budget * 1e9) return r;
+  }
+  return 8;
 }
 
 // Build comb tables for nunits encoded points (d_pk, 32 B each) into d_tbl, in launches of at
@@ -120,6 +127,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   cbft_ctx* c = new (std::nothrow) cbft_ctx();
   if (!c) return CBFT_ENOMEM;
   c->device = device;
+  if (const char* e = getenv("CBFT_FINISH_BATCH")) c->finish_batch = atoi(e);
   int rc = CBFT_OK;
   do {
     if (hipSetDevice(device) != hipSuccess) {
@@ -236,7 +244,7 @@ int cbft_ed25519_load_keys_ex(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, in
   CBFT_HIP(hipSetDevice(c->device));
   KeyTable kt;
   kt.nkeys = nkeys;
-  kt.geo = cbft_comb_geom(key_radix(comb_radix));
+  kt.geo = cbft_comb_geom(key_radix(comb_radix, nkeys));
   const size_t n = std::max<uint32_t>(nkeys, 1);
   CBFT_HIP(kt.pk.reserve(n * 32));
   CBFT_HIP(kt.comb.reserve(n * kt.geo.words_per_unit() * sizeof(uint32_t)));
@@ -297,6 +305,9 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
 
   Ed25519Batch b{n, d_pk, d_kidx, d_sig, d_msg, d_off, d_len};
   Ed25519Work w{};
+  // one inversion per 8 signatures per lane only where the batch keeps >= 64 finish waves; a
+  // small (latency-bound) batch inverts per signature
+  w.finish_batch = c->finish_batch ? c->finish_batch : (n >= 32768 ? 8 : 1);
   w.base_table = c->base_table.as<uint32_t>();
   w.h_soa = slot.h.as<uint32_t>();
   w.flags = slot.flags.as<uint8_t>();

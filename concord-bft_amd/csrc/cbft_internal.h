@@ -80,6 +80,7 @@ struct cbft_ctx {
   // per-batch work buffers
   WorkSlot slots[CBFT_WORK_SLOTS];
   unsigned next_slot = 0;
+  int finish_batch = 0;  // K4: signatures per lane sharing one inversion ($CBFT_FINISH_BATCH; 0 = by batch size)
   DevBuf verdicts;
   DevBuf sig, msg, off, len, kidx, pk;
   std::vector<uint64_t> host_verdicts;

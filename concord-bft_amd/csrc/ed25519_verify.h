@@ -73,7 +73,6 @@ inline CombLadder cbft_comb_ladder(int wa, int wb) {
   return c;
 }
 #define CBFT_COMB_B_RADIX 16     // B's table: 16 positions x 32,769 entries (67 MB per context)
-#define CBFT_COMB_A_RADIX_DEF 11  // default per-key table: 23 positions x 1,025 entries (3.0 MB/key)
 
 // Device work buffers of one verify launch.
 struct Ed25519Work {
@@ -82,6 +81,7 @@ struct Ed25519Work {
   const uint32_t* comb_tbl;    // comb tables of -A per key (key-table mode; tbl unused)
   const uint32_t* base_comb;   // comb table of B
   CombLadder comb;             // their geometry
+  int finish_batch;            // signatures per lane sharing one inversion in K4 (2/4/8/16; else 1)
   const uint8_t* aok;          // A decoded OK, indexed like pk
   uint32_t* h_soa;             // 8 x n words
   uint8_t* flags;              // n bytes

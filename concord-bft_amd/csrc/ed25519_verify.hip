@@ -352,6 +352,80 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_finish_kernel(const
   if ((threadIdx.x & 63) == 0 && i < b.n) verdict_words[i >> 6] = ballot;
 }
 
+// K4' (batched): the same verdicts with one field inversion per K signatures per lane
+// (Montgomery's trick).  Lane l of block w handles signatures w*64K + 64j + l, j = 0..K-1:
+//   up:   acc_j = prod_{t <= j} Z_t  (prefix products kept in LDS, [j][limb][lane])
+//   inv = acc_{K-1}^-1  (254 S + 11 M, once per K signatures instead of once per signature)
+//   down: 1/Z_j = inv * acc_{j-1},  inv <- inv * Z_j;  x = X/Z, y = Y/Z, encode, compare with R.
+// A signature already rejected (S >= L, A not decodable) or with Z = 0 enters the product as 1,
+// so it cannot disturb its neighbours' inverses.  At 64K signatures and K = 8 the kernel is 128
+// waves: it does a quarter of K4's VALU work and leaves most SIMDs to the next batch's hash and
+// ladder (two batches in flight on two streams).
+template <int K>
+__global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519Batch b, const uint32_t* xyz_soa,
+                                                                  const uint8_t* flags, const uint8_t* aok,
+                                                                  uint64_t* verdict_words) {
+  __shared__ uint32_t pre[K][FE_LIMBS][64];
+  const uint32_t ln = threadIdx.x;
+  const size_t base = (size_t)blockIdx.x * 64 * K;
+  fe acc;
+  fe_1(acc);
+  uint32_t okmask = 0;
+#pragma nounroll
+  for (int j = 0; j < K; j++) {
+    const size_t i = base + (size_t)j * 64 + ln;
+    fe Z;
+    fe_1(Z);
+    bool ok = false;
+    if (i < b.n) {
+      fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
+      const uint32_t unit = b.key_idx ? b.key_idx[i] : (uint32_t)i;
+      ok = flags[i] && aok[unit] && !fe_iszero(Z);
+      if (!ok) fe_1(Z);
+    }
+    okmask |= (ok ? 1u : 0u) << j;
+    fe_mul(acc, acc, Z);
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) pre[j][k][ln] = acc.v[k];
+  }
+  fe inv;
+  fe_invert(inv, acc);
+#pragma nounroll
+  for (int j = K - 1; j >= 0; j--) {
+    const size_t i = base + (size_t)j * 64 + ln;
+    const bool ok = (okmask >> j) & 1u;
+    fe zi, Z;
+    if (j > 0) {
+      fe p;
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) p.v[k] = pre[j - 1][k][ln];
+      fe_mul(zi, inv, p);
+    } else {
+      fe_copy(zi, inv);
+    }
+    bool verdict = false;
+    if (ok) {
+      fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
+      fe_mul(inv, inv, Z);
+      fe X, Y, x, y;
+      fe_load_soa(X, xyz_soa, b.n, i);
+      fe_load_soa(Y, xyz_soa + 9 * b.n, b.n, i);
+      fe_mul(x, X, zi);
+      fe_mul(y, Y, zi);
+      uint32_t Rp[8], Rw[8];
+      fe_to_words(Rp, y);
+      Rp[7] ^= fe_isnegative(x) << 31;
+      load_words8(Rw, b.sig + i * 64);
+      uint32_t diff = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) diff |= Rp[k] ^ Rw[k];
+      verdict = diff == 0;
+    }
+    const uint64_t ballot = __ballot(verdict);
+    if (ln == 0 && base + (size_t)j * 64 < b.n) verdict_words[blockIdx.x * K + j] = ballot;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Wide fixed-base combs, four lanes per signature (key-table mode).
 //
@@ -363,11 +437,11 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_finish_kernel(const
 // d_top = chunk_top(s') in [0, 2^(w-1)] (CombGeom in ed25519_verify.h; tests/test_comb_recode.py
 // checks the recoding exhaustively at the range edges).  One mixed addition per position and no
 // doublings: B's table is radix 2^16 (16 positions, 67 MB: Infinity-Cache resident), a key's
-// table radix 2^w_A (default 2^11: 23 positions, 3.0 MB per key, 12.4 GB for 4,096 keys -- HBM
-// is 288 GB and keys are long-lived, SigManager.cpp:139-150), so a verify is 16 + 23 = 39 mixed
-// additions (the radix-256 comb of the first round: 64).
+// table radix 2^w_A (default 2^13 while the tables fit the budget: 20 positions, 10.5 MB per key,
+// 43 GB for 4,096 keys -- HBM is 288 GB and keys are long-lived, SigManager.cpp:139-150), so a
+// verify is 16 + 20 = 36 mixed additions (the radix-256 comb of the first round: 64).
 //
-// The 39 additions are dealt to the 4 lanes of a quad in order (lane q takes additions
+// The additions are dealt to the 4 lanes of a quad in order (lane q takes additions
 // q*nper .. q*nper+nper-1, the A positions first), then two DPP butterfly levels (quad_perm
 // xor 1, xor 2) add the four partial sums: every lane of the quad ends with
 // R' = [S]B + [h](-A).  4,096 waves at 64K signatures: 4 waves per SIMD.
@@ -709,7 +783,20 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
     hipLaunchKernelGGL(ed25519_ladder_kernel, grid, block, 0, stream, b, w.h_soa, w.tbl, w.base_table, w.xyz_soa);
   }
   if (ev) (void)hipEventRecord(ev[2], stream);
-  hipLaunchKernelGGL(ed25519_finish_kernel, grid, block, 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words);
+  switch (w.finish_batch) {
+#define CBFT_FINISH_CASE(K)                                                                                     \
+  case K:                                                                                                       \
+    hipLaunchKernelGGL(ed25519_finish_batch_kernel<K>, dim3((unsigned)((b.n + 64 * K - 1) / (64 * K))), dim3(64), \
+                       0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words);                               \
+    break;
+    CBFT_FINISH_CASE(2)
+    CBFT_FINISH_CASE(4)
+    CBFT_FINISH_CASE(8)
+    CBFT_FINISH_CASE(16)
+#undef CBFT_FINISH_CASE
+    default:
+      hipLaunchKernelGGL(ed25519_finish_kernel, grid, block, 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words);
+  }
   if (ev) (void)hipEventRecord(ev[3], stream);
   return hipGetLastError();
 }

@@ -70,8 +70,9 @@ void cbft_close(cbft_ctx* ctx);
  * decode is accepted into the table; every signature under it verifies false. */
 int cbft_ed25519_load_keys(cbft_ctx* ctx, const uint8_t* pk /* nkeys x 32 */, uint32_t nkeys,
                            uint32_t* out_key_table_id);
-/* Same, choosing the radix 2^comb_radix of the per-key fixed-base comb tables (8..13; 0 = the
- * default: $CBFT_COMB_RADIX if set, else 11).  Memory per key = npos x (2^(radix-1) + 1) x 128 B:
+/* Same, choosing the radix 2^comb_radix of the per-key fixed-base comb tables (8..13).  0 = the
+ * default: $CBFT_COMB_RADIX if set, else the widest of 13 / 11 / 8 whose tables fit
+ * $CBFT_COMB_BUDGET_GB (default 64).  Memory per key = npos x (2^(radix-1) + 1) x 128 B:
  * radix 8: 0.53 MB (32 additions per [h]A), 11: 3.0 MB (23), 13: 10.5 MB (20).  The verdicts do
  * not depend on the radix. */
 int cbft_ed25519_load_keys_ex(cbft_ctx* ctx, const uint8_t* pk, uint32_t nkeys, int comb_radix,

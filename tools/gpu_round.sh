@@ -25,7 +25,7 @@ if [[ $step == all || $step == pmc ]]; then
              "SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_WAIT_INST_LDS" \
              "FETCH_SIZE" "WRITE_SIZE"; do
     i=$((i+1))
-    timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --pmc $grp -d "$GRAFT_REPO_ROOT/gpurun_out/pmc$i" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --latency-runs 0 > "$GRAFT_REPO_ROOT/gpurun_out/pmc$i.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/pmc$i.err" || { echo "pmc pass $i failed"; tail -20 "$GRAFT_REPO_ROOT/gpurun_out/pmc$i.err"; exit 1; }
+    timeout -s KILL 120 rocprofv3 --kernel-trace --output-format csv --pmc $grp -d "$GRAFT_REPO_ROOT/gpurun_out/pmc$i" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --latency-runs 0 --no-extras > "$GRAFT_REPO_ROOT/gpurun_out/pmc$i.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/pmc$i.err" || { echo "pmc pass $i failed"; tail -20 "$GRAFT_REPO_ROOT/gpurun_out/pmc$i.err"; exit 1; }
   done
   cd "$GRAFT_REPO_ROOT"; find gpurun_out -name "*counter_collection.csv" | head
 fi
