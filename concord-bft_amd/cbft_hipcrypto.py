@@ -65,7 +65,19 @@ ABI = [
     ("cbft_bls_sum_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_void_p]),
     ("cbft_bls_sign", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                      ctypes.c_uint32, ctypes.c_void_p]),
+    ("cbft_bls_combine_partial", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
+      ctypes.c_void_p]),
+    ("cbft_bls_combine_finish", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p]),
+    ("cbft_bls_sum_keys_partial", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]),
+    ("cbft_bls_verify_multisig_partials", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32,
+      ctypes.POINTER(ctypes.c_int)]),
 ]
+
+BLS_G1_PARTIAL_BYTES = 108
+BLS_G2_PARTIAL_BYTES = 220
 
 _lib = None
 
@@ -246,6 +258,32 @@ class Context:
         out = ctypes.create_string_buffer(65)
         _check(self.lib.cbft_bls_sum_keys(self.handle, kid, signers256, out), "cbft_bls_sum_keys")
         return out.raw
+
+    # sharded combine / multisig key sum (partials are exchanged between ranks, cbft_multigpu)
+    def bls_combine_partial(self, shares: Sequence[bytes], lo: int, hi: int, multisig: bool = False) -> bytes:
+        out = ctypes.create_string_buffer(BLS_G1_PARTIAL_BYTES)
+        _check(self.lib.cbft_bls_combine_partial(self.handle, b"".join(shares), len(shares), lo, hi,
+                                                  1 if multisig else 0, out), "cbft_bls_combine_partial")
+        return out.raw
+
+    def bls_combine_finish(self, partials: Sequence[bytes]) -> bytes:
+        out = ctypes.create_string_buffer(33)
+        _check(self.lib.cbft_bls_combine_finish(self.handle, b"".join(partials), len(partials), out),
+               "cbft_bls_combine_finish")
+        return out.raw
+
+    def bls_sum_keys_partial(self, kid: int, signers256: bytes, lo_id: int, hi_id: int) -> bytes:
+        out = ctypes.create_string_buffer(BLS_G2_PARTIAL_BYTES)
+        _check(self.lib.cbft_bls_sum_keys_partial(self.handle, kid, signers256, lo_id, hi_id, out),
+               "cbft_bls_sum_keys_partial")
+        return out.raw
+
+    def bls_verify_multisig_partials(self, msg: bytes, sig33: bytes, key_partials: Sequence[bytes]) -> bool:
+        ok = ctypes.c_int()
+        _check(self.lib.cbft_bls_verify_multisig_partials(self.handle, msg, len(msg), sig33, b"".join(key_partials),
+                                                           len(key_partials), ctypes.byref(ok)),
+               "cbft_bls_verify_multisig_partials")
+        return bool(ok.value)
 
     def bls_sign(self, sk: int, share_id: int, msg: bytes) -> bytes:
         out = ctypes.create_string_buffer(37)

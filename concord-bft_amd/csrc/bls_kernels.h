@@ -17,11 +17,18 @@ hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uin
                                         const uint32_t* d_vk_lines, const uint8_t* d_vk_ok,
                                         const uint32_t* d_gen_lines, int do_verify, uint8_t* d_valid,
                                         uint32_t* d_sig, uint32_t* d_ids, hipStream_t s);
+// lambda over all k shares; the MSM over shares [lo, hi); d_out_jac (nullable): write the sum as
+// one Jacobian partial (BLS_JAC_WORDS) instead of compressing it into d_out33
 hipError_t cbft_bls_launch_combine(const uint32_t* d_sig, const uint32_t* d_ids, const uint8_t* d_use, uint32_t k,
-                                   int multisig, uint32_t* d_lambda, uint32_t* d_partial, uint8_t* d_out33,
-                                   uint32_t* d_sig_aff, hipStream_t s);
+                                   uint32_t lo, uint32_t hi, int multisig, uint32_t* d_lambda, uint32_t* d_partial,
+                                   uint8_t* d_out33, uint32_t* d_sig_aff, uint32_t* d_out_jac, hipStream_t s);
+hipError_t cbft_bls_launch_g1_parts(const uint32_t* d_parts, uint32_t count, uint8_t* d_out33, hipStream_t s);
+#define BLS_G2_PART_WORDS 55  // Jacobian G2 partial key sum + bad-key flag
 hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok, uint32_t n, const uint8_t* d_bitmap,
-                                  uint32_t* d_lines, uint8_t* d_ok, uint8_t* d_out65, hipStream_t s);
+                                  uint32_t lo_id, uint32_t hi_id, uint32_t* d_lines, uint8_t* d_ok, uint8_t* d_out65,
+                                  uint32_t* d_out_part, hipStream_t s);
+hipError_t cbft_bls_launch_g2_parts(const uint32_t* d_parts, uint32_t count, uint32_t* d_lines, uint8_t* d_ok,
+                                    uint8_t* d_out65, hipStream_t s);
 hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, const uint32_t* d_pk_lines,
                                   const uint8_t* d_pk_ok, const uint32_t* d_gen_lines, uint8_t* d_result,
                                   hipStream_t s);

@@ -205,7 +205,10 @@ __global__ void __launch_bounds__(MSM_BLOCK) bls_msm_kernel(const uint32_t* sig,
   }
 }
 
-__global__ void bls_msm_finish_kernel(const uint32_t* partial, uint32_t nparts, uint8_t* out33, uint32_t* sig_aff) {
+// Sum of nparts Jacobian partials (27 words each): compressed into out33, or (out_jac) left as
+// one Jacobian partial -- the form ranks exchange when a combine is sharded across GPUs.
+__global__ void bls_msm_finish_kernel(const uint32_t* partial, uint32_t nparts, uint8_t* out33, uint32_t* sig_aff,
+                                      uint32_t* out_jac) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   g1j acc;
   g1_set_inf(acc);
@@ -217,6 +220,14 @@ __global__ void bls_msm_finish_kernel(const uint32_t* partial, uint32_t nparts, 
       o.Z.v[q] = partial[27 * b + 18 + q];
     }
     g1_add(acc, acc, o);
+  }
+  if (out_jac) {
+    for (int q = 0; q < 9; q++) {
+      out_jac[q] = acc.X.v[q];
+      out_jac[9 + q] = acc.Y.v[q];
+      out_jac[18 + q] = acc.Z.v[q];
+    }
+    return;
   }
   g1a a;
   g1_to_affine(a, acc);
@@ -230,9 +241,47 @@ __global__ void bls_msm_finish_kernel(const uint32_t* partial, uint32_t nparts, 
 // form, then an LDS tree halves the partial sums; lane 0 normalises, compresses and computes
 // the lines.  A selected key that did not decode makes the result invalid (ok = 0).
 #define SUM_THREADS 256
+// normalise, compress (out65) and compute the Miller lines of a summed key; bad = a selected
+// key did not decode
+__device__ void g2_sum_tail(const g2j& acc, bool bad, uint32_t* lines, uint8_t* ok, uint8_t* out65) {
+  g2a s;
+  g2_to_affine(s, acc);
+  const bool good = !bad;
+  if (out65) {
+    if (good) {
+      g2_compress(out65, s);
+    } else {
+      for (int q = 0; q < 65; q++) out65[q] = 0;
+    }
+  }
+  const bool usable = good && !s.inf;
+  ok[0] = usable ? 1 : 0;
+  if (usable && lines) g2_precompute_lines(lines, s);
+}
+
+__device__ __forceinline__ void g2j_store(uint32_t* o, const g2j& a) {
+  const fp2* src[3] = {&a.X, &a.Y, &a.Z};
+  for (int c = 0; c < 3; c++)
+    for (int q = 0; q < 9; q++) {
+      o[18 * c + q] = src[c]->a.v[q];
+      o[18 * c + 9 + q] = src[c]->b.v[q];
+    }
+}
+__device__ __forceinline__ void g2j_load(g2j& a, const uint32_t* o) {
+  fp2* dst[3] = {&a.X, &a.Y, &a.Z};
+  for (int c = 0; c < 3; c++)
+    for (int q = 0; q < 9; q++) {
+      dst[c]->a.v[q] = o[18 * c + q];
+      dst[c]->b.v[q] = o[18 * c + 9 + q];
+    }
+}
+
+// Signer ids [lo_id, hi_id) only (a rank's slice of a sharded multisig key sum).  With out_part
+// the block writes its Jacobian sum (54 words) + the bad-key flag (1 word) and stops there.
 __global__ void __launch_bounds__(SUM_THREADS) bls_g2_sum_kernel(const uint32_t* aff, const uint8_t* key_ok,
-                                                                 uint32_t n, const uint8_t* bitmap, uint32_t* lines,
-                                                                 uint8_t* ok, uint8_t* out65) {
+                                                                 uint32_t n, const uint8_t* bitmap, uint32_t lo_id,
+                                                                 uint32_t hi_id, uint32_t* lines, uint8_t* ok,
+                                                                 uint8_t* out65, uint32_t* out_part) {
   __shared__ uint32_t sp[SUM_THREADS / 2][54];
   __shared__ int bad;
   const int t = threadIdx.x;
@@ -243,7 +292,8 @@ __global__ void __launch_bounds__(SUM_THREADS) bls_g2_sum_kernel(const uint32_t*
   fp2_one(acc.Y);
   fp2_zero(acc.Z);
   bool mine_bad = false;
-  for (uint32_t id = 1 + t; id <= n; id += SUM_THREADS) {
+  const uint32_t lo = lo_id < 1 ? 1 : lo_id, hi = hi_id > n + 1 ? n + 1 : hi_id;
+  for (uint32_t id = lo + t; id < hi; id += SUM_THREADS) {
     if (!((bitmap[(id - 1) >> 3] >> ((id - 1) & 7)) & 1)) continue;
     if (!key_ok[id - 1]) {
       mine_bad = true;
@@ -259,41 +309,40 @@ __global__ void __launch_bounds__(SUM_THREADS) bls_g2_sum_kernel(const uint32_t*
   }
   if (mine_bad) atomicOr(&bad, 1);
   for (int stride = SUM_THREADS / 2; stride >= 1; stride >>= 1) {
-    if (t >= stride && t < 2 * stride) {
-      const fp2* src[3] = {&acc.X, &acc.Y, &acc.Z};
-      for (int c = 0; c < 3; c++)
-        for (int q = 0; q < 9; q++) {
-          sp[t - stride][18 * c + q] = src[c]->a.v[q];
-          sp[t - stride][18 * c + 9 + q] = src[c]->b.v[q];
-        }
-    }
+    if (t >= stride && t < 2 * stride) g2j_store(sp[t - stride], acc);
     __syncthreads();
     if (t < stride) {
       g2j o;
-      fp2* dst[3] = {&o.X, &o.Y, &o.Z};
-      for (int c = 0; c < 3; c++)
-        for (int q = 0; q < 9; q++) {
-          dst[c]->a.v[q] = sp[t][18 * c + q];
-          dst[c]->b.v[q] = sp[t][18 * c + 9 + q];
-        }
+      g2j_load(o, sp[t]);
       g2_add_j(acc, acc, o);
     }
     __syncthreads();
   }
   if (t != 0) return;
-  g2a s;
-  g2_to_affine(s, acc);
-  const bool good = !bad;
-  if (out65) {
-    if (good) {
-      g2_compress(out65, s);
-    } else {
-      for (int q = 0; q < 65; q++) out65[q] = 0;
-    }
+  if (out_part) {
+    g2j_store(out_part, acc);
+    out_part[54] = bad ? 1u : 0u;
+    return;
   }
-  const bool usable = good && !s.inf;
-  ok[0] = usable ? 1 : 0;
-  if (usable && lines) g2_precompute_lines(lines, s);
+  g2_sum_tail(acc, bad != 0, lines, ok, out65);
+}
+
+// Sum of count G2 partials (55 words each, from bls_g2_sum_kernel's out_part) + the tail.
+__global__ void bls_g2_parts_kernel(const uint32_t* parts, uint32_t count, uint32_t* lines, uint8_t* ok,
+                                    uint8_t* out65) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  g2j acc;
+  fp2_one(acc.X);
+  fp2_one(acc.Y);
+  fp2_zero(acc.Z);
+  bool bad = false;
+  for (uint32_t b = 0; b < count; b++) {
+    g2j o;
+    g2j_load(o, parts + 55 * (size_t)b);
+    bad |= parts[55 * (size_t)b + 54] != 0;
+    g2_add_j(acc, acc, o);
+  }
+  g2_sum_tail(acc, bad, lines, ok, out65);
 }
 
 // e(H, PK) * e(-sigma, g2) == 1 for a combined signature (33 bytes); one 8-lane group
@@ -365,21 +414,35 @@ hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uin
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_combine(const uint32_t* d_sig, const uint32_t* d_ids, const uint8_t* d_use, uint32_t k,
-                                   int multisig, uint32_t* d_lambda, uint32_t* d_partial, uint8_t* d_out33,
-                                   uint32_t* d_sig_aff, hipStream_t s) {
+                                   uint32_t lo, uint32_t hi, int multisig, uint32_t* d_lambda, uint32_t* d_partial,
+                                   uint8_t* d_out33, uint32_t* d_sig_aff, uint32_t* d_out_jac, hipStream_t s) {
   if (!multisig && k)
     hipLaunchKernelGGL(bls_lagrange_kernel, dim3((k + 63) / 64), dim3(64), 0, s, d_ids, d_use, k, d_lambda);
-  const uint32_t nparts = (k + MSM_BLOCK - 1) / MSM_BLOCK;
-  if (k)
-    hipLaunchKernelGGL(bls_msm_kernel, dim3(nparts), dim3(MSM_BLOCK), 0, s, d_sig, d_lambda, d_use, k, multisig,
-                       d_partial);
-  hipLaunchKernelGGL(bls_msm_finish_kernel, dim3(1), dim3(64), 0, s, d_partial, nparts, d_out33, d_sig_aff);
+  hi = hi < k ? hi : k;
+  lo = lo < hi ? lo : hi;
+  const uint32_t m = hi - lo;  // the MSM runs over shares [lo, hi) only
+  const uint32_t nparts = (m + MSM_BLOCK - 1) / MSM_BLOCK;
+  if (m)
+    hipLaunchKernelGGL(bls_msm_kernel, dim3(nparts), dim3(MSM_BLOCK), 0, s, d_sig + 19 * (size_t)lo,
+                       d_lambda + 8 * (size_t)lo, d_use + lo, m, multisig, d_partial);
+  hipLaunchKernelGGL(bls_msm_finish_kernel, dim3(1), dim3(64), 0, s, d_partial, nparts, d_out33, d_sig_aff,
+                     d_out_jac);
+  return hipGetLastError();
+}
+hipError_t cbft_bls_launch_g1_parts(const uint32_t* d_parts, uint32_t count, uint8_t* d_out33, hipStream_t s) {
+  hipLaunchKernelGGL(bls_msm_finish_kernel, dim3(1), dim3(64), 0, s, d_parts, count, d_out33, nullptr, nullptr);
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok, uint32_t n, const uint8_t* d_bitmap,
-                                  uint32_t* d_lines, uint8_t* d_ok, uint8_t* d_out65, hipStream_t s) {
-  hipLaunchKernelGGL(bls_g2_sum_kernel, dim3(1), dim3(SUM_THREADS), 0, s, d_aff, d_key_ok, n, d_bitmap, d_lines, d_ok,
-                     d_out65);
+                                  uint32_t lo_id, uint32_t hi_id, uint32_t* d_lines, uint8_t* d_ok, uint8_t* d_out65,
+                                  uint32_t* d_out_part, hipStream_t s) {
+  hipLaunchKernelGGL(bls_g2_sum_kernel, dim3(1), dim3(SUM_THREADS), 0, s, d_aff, d_key_ok, n, d_bitmap, lo_id, hi_id,
+                     d_lines, d_ok, d_out65, d_out_part);
+  return hipGetLastError();
+}
+hipError_t cbft_bls_launch_g2_parts(const uint32_t* d_parts, uint32_t count, uint32_t* d_lines, uint8_t* d_ok,
+                                    uint8_t* d_out65, hipStream_t s) {
+  hipLaunchKernelGGL(bls_g2_parts_kernel, dim3(1), dim3(64), 0, s, d_parts, count, d_lines, d_ok, d_out65);
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, const uint32_t* d_pk_lines,

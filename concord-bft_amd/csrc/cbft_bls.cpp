@@ -12,6 +12,9 @@
 #include "bls_kernels.h"
 #include "cbft_internal.h"
 
+static_assert(CBFT_BLS_G1_PARTIAL_BYTES == BLS_JAC_WORDS * 4, "G1 partial layout");
+static_assert(CBFT_BLS_G2_PARTIAL_BYTES == BLS_G2_PART_WORDS * 4, "G2 partial layout");
+
 #define BLS_MAX_SHARES 2048  // IThresholdVerifier::maxSize_ (IThresholdVerifier.h:36)
 
 static int bls_gen_lines(cbft_ctx* c) {
@@ -99,8 +102,9 @@ int cbft_bls_hash_to_g1(cbft_ctx* c, const uint8_t* msg, uint32_t len, uint8_t* 
   CBFT_HIP(c->bls_out.reserve(33));
   uint8_t one = 1;
   CBFT_HIP(hipMemcpyAsync(c->bls_use.p, &one, 1, hipMemcpyHostToDevice, c->stream));
-  CBFT_HIP(cbft_bls_launch_combine(c->bls_H.as<uint32_t>(), nullptr, c->bls_use.as<uint8_t>(), 1, 1, nullptr,
-                                   c->bls_partial.as<uint32_t>(), c->bls_out.as<uint8_t>(), nullptr, c->stream));
+  CBFT_HIP(cbft_bls_launch_combine(c->bls_H.as<uint32_t>(), nullptr, c->bls_use.as<uint8_t>(), 1, 0, 1, 1, nullptr,
+                                   c->bls_partial.as<uint32_t>(), c->bls_out.as<uint8_t>(), nullptr, nullptr,
+                                   c->stream));
   CBFT_HIP(hipMemcpyAsync(out33, c->bls_out.p, 33, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipStreamSynchronize(c->stream));
   return CBFT_OK;
@@ -142,8 +146,10 @@ int cbft_bls_verify_shares(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_
   return CBFT_OK;
 }
 
-int cbft_bls_combine(cbft_ctx* c, const uint8_t* shares37, uint32_t k, int multisig, uint8_t* out33) {
-  if (!c || !out33 || !k || !shares37 || k > BLS_MAX_SHARES) return CBFT_EINVAL;
+// Parse k shares (distinct ids, all decodable) onto the device and launch lambda + the MSM over
+// [lo, hi): into out33 (compressed), or into out_part (one Jacobian partial) when non-null.
+static int bls_combine_range(cbft_ctx* c, const uint8_t* shares37, uint32_t k, uint32_t lo, uint32_t hi, int multisig,
+                             uint8_t* out33, uint8_t* out_part) {
   // distinct ids (the accumulators never hold two shares of one signer)
   std::vector<uint8_t> seen(1u << 16, 0);
   for (uint32_t j = 0; j < k; j++) {
@@ -157,8 +163,8 @@ int cbft_bls_combine(cbft_ctx* c, const uint8_t* shares37, uint32_t k, int multi
   int rc = bls_shares(c, nullptr, shares37, k, 0);
   if (rc) return rc;
   CBFT_HIP(c->bls_lambda.reserve((size_t)k * 8 * 4));
-  CBFT_HIP(c->bls_partial.reserve((size_t)((k + 63) / 64) * BLS_JAC_WORDS * 4));
-  CBFT_HIP(c->bls_out.reserve(33));
+  CBFT_HIP(c->bls_partial.reserve((size_t)((k + 63) / 64 + 1) * BLS_JAC_WORDS * 4));
+  CBFT_HIP(c->bls_out.reserve(BLS_JAC_WORDS * 4));
   // every share decoded? (the parse kernel wrote valid = decodable && id in range)
   std::vector<uint8_t> v(k);
   CBFT_HIP(hipMemcpyAsync(v.data(), c->bls_valid.p, k, hipMemcpyDeviceToHost, c->stream));
@@ -166,8 +172,37 @@ int cbft_bls_combine(cbft_ctx* c, const uint8_t* shares37, uint32_t k, int multi
   for (uint32_t j = 0; j < k; j++)
     if (!v[j]) return CBFT_EINVAL;
   CBFT_HIP(cbft_bls_launch_combine(c->bls_sig.as<uint32_t>(), c->bls_ids.as<uint32_t>(), c->bls_valid.as<uint8_t>(),
-                                   k, multisig, c->bls_lambda.as<uint32_t>(), c->bls_partial.as<uint32_t>(),
-                                   c->bls_out.as<uint8_t>(), nullptr, c->stream));
+                                   k, lo, hi, multisig, c->bls_lambda.as<uint32_t>(), c->bls_partial.as<uint32_t>(),
+                                   c->bls_out.as<uint8_t>(), nullptr,
+                                   out_part ? c->bls_out.as<uint32_t>() : nullptr, c->stream));
+  if (out_part)
+    CBFT_HIP(hipMemcpyAsync(out_part, c->bls_out.p, CBFT_BLS_G1_PARTIAL_BYTES, hipMemcpyDeviceToHost, c->stream));
+  else
+    CBFT_HIP(hipMemcpyAsync(out33, c->bls_out.p, 33, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  return CBFT_OK;
+}
+
+int cbft_bls_combine(cbft_ctx* c, const uint8_t* shares37, uint32_t k, int multisig, uint8_t* out33) {
+  if (!c || !out33 || !k || !shares37 || k > BLS_MAX_SHARES) return CBFT_EINVAL;
+  return bls_combine_range(c, shares37, k, 0, k, multisig, out33, nullptr);
+}
+
+int cbft_bls_combine_partial(cbft_ctx* c, const uint8_t* shares37, uint32_t k, uint32_t lo, uint32_t hi, int multisig,
+                             uint8_t* out_partial) {
+  if (!c || !out_partial || !k || !shares37 || k > BLS_MAX_SHARES || lo > hi || hi > k) return CBFT_EINVAL;
+  return bls_combine_range(c, shares37, k, lo, hi, multisig, nullptr, out_partial);
+}
+
+int cbft_bls_combine_finish(cbft_ctx* c, const uint8_t* partials, uint32_t count, uint8_t* out33) {
+  if (!c || !out33 || !count || !partials) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  CBFT_HIP(hipSetDevice(c->device));
+  CBFT_HIP(c->bls_partial.reserve((size_t)count * CBFT_BLS_G1_PARTIAL_BYTES));
+  CBFT_HIP(c->bls_out.reserve(33));
+  CBFT_HIP(hipMemcpyAsync(c->bls_partial.p, partials, (size_t)count * CBFT_BLS_G1_PARTIAL_BYTES,
+                          hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_g1_parts(c->bls_partial.as<uint32_t>(), count, c->bls_out.as<uint8_t>(), c->stream));
   CBFT_HIP(hipMemcpyAsync(out33, c->bls_out.p, 33, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipStreamSynchronize(c->stream));
   return CBFT_OK;
@@ -214,8 +249,8 @@ int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint3
   CBFT_HIP(c->bls_ms_ok.reserve(1));
   CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(cbft_bls_launch_g2_sum(ks->aff.as<uint32_t>() + BLS_G2A_WORDS, ks->ok.as<uint8_t>() + 1, ks->n,
-                                  c->bls_bitmap.as<uint8_t>(),
-                                  c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), nullptr, c->stream));
+                                  c->bls_bitmap.as<uint8_t>(), 1, ks->n + 1, c->bls_ms_lines.as<uint32_t>(),
+                                  c->bls_ms_ok.as<uint8_t>(), nullptr, nullptr, c->stream));
   return bls_verify_with_lines(c, sig33, c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), out_ok);
 }
 
@@ -230,11 +265,48 @@ int cbft_bls_sum_keys(cbft_ctx* c, uint32_t id, const uint8_t* signers256, uint8
   CBFT_HIP(c->bls_out.reserve(65));
   CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(cbft_bls_launch_g2_sum(ks->aff.as<uint32_t>() + BLS_G2A_WORDS, ks->ok.as<uint8_t>() + 1, ks->n,
-                                  c->bls_bitmap.as<uint8_t>(), nullptr,
-                                  c->bls_ms_ok.as<uint8_t>(), c->bls_out.as<uint8_t>(), c->stream));
+                                  c->bls_bitmap.as<uint8_t>(), 1, ks->n + 1, nullptr, c->bls_ms_ok.as<uint8_t>(),
+                                  c->bls_out.as<uint8_t>(), nullptr, c->stream));
   CBFT_HIP(hipMemcpyAsync(out65, c->bls_out.p, 65, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipStreamSynchronize(c->stream));
   return CBFT_OK;
+}
+
+int cbft_bls_sum_keys_partial(cbft_ctx* c, uint32_t id, const uint8_t* signers256, uint32_t lo_id, uint32_t hi_id,
+                              uint8_t* out_partial) {
+  if (!c || !signers256 || !out_partial || lo_id > hi_id) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  BlsKeySet* ks = find_set(c, id);
+  if (!ks) return CBFT_EINVAL;
+  CBFT_HIP(hipSetDevice(c->device));
+  CBFT_HIP(c->bls_bitmap.reserve(256));
+  CBFT_HIP(c->bls_ms_ok.reserve(1));
+  CBFT_HIP(c->bls_partial.reserve(CBFT_BLS_G2_PARTIAL_BYTES));
+  CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_g2_sum(ks->aff.as<uint32_t>() + BLS_G2A_WORDS, ks->ok.as<uint8_t>() + 1, ks->n,
+                                  c->bls_bitmap.as<uint8_t>(), lo_id, hi_id, nullptr, c->bls_ms_ok.as<uint8_t>(),
+                                  nullptr, c->bls_partial.as<uint32_t>(), c->stream));
+  CBFT_HIP(hipMemcpyAsync(out_partial, c->bls_partial.p, CBFT_BLS_G2_PARTIAL_BYTES, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  return CBFT_OK;
+}
+
+int cbft_bls_verify_multisig_partials(cbft_ctx* c, const uint8_t* msg, uint32_t len, const uint8_t* sig33,
+                                      const uint8_t* key_partials, uint32_t count, int* out_ok) {
+  if (!c || !sig33 || !key_partials || !count || !out_ok || (len && !msg)) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  CBFT_HIP(hipSetDevice(c->device));
+  int rc = bls_gen_lines(c);
+  if (!rc) rc = bls_upload_msg_hash(c, msg, len);
+  if (rc) return rc;
+  CBFT_HIP(c->bls_partial.reserve((size_t)count * CBFT_BLS_G2_PARTIAL_BYTES));
+  CBFT_HIP(c->bls_ms_lines.reserve(cbft_bls_lines_words_per_key() * 4));
+  CBFT_HIP(c->bls_ms_ok.reserve(1));
+  CBFT_HIP(hipMemcpyAsync(c->bls_partial.p, key_partials, (size_t)count * CBFT_BLS_G2_PARTIAL_BYTES,
+                          hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_g2_parts(c->bls_partial.as<uint32_t>(), count, c->bls_ms_lines.as<uint32_t>(),
+                                    c->bls_ms_ok.as<uint8_t>(), nullptr, c->stream));
+  return bls_verify_with_lines(c, sig33, c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), out_ok);
 }
 
 int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* msg, uint32_t len, uint8_t* out37) {

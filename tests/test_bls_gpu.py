@@ -146,3 +146,50 @@ def test_sum_keys_is_multisig_pk(ctx):
             assert ctx.bls_sum_keys(kid, B.signers_bitmap(ids)) == B.g2_to_bytes(acc)
     finally:
         ctx.bls_unload_keys(kid)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8])
+def test_sharded_combine_equals_combine(ctx, world):
+    """cbft_bls_combine_partial over each rank's slice + cbft_bls_combine_finish == one combine
+    (the multi-GPU path of cbft_multigpu.bls_combine_sharded, ranks simulated on one GPU)."""
+    import cbft_multigpu as mg
+
+    n, k = 24, 17
+    sk, sks, pk, vks = blsgen.keyset(n, k, seed=23)
+    msg = bytes(range(40, 72))
+    ids = random.Random(world).sample(range(1, n + 1), k)
+    shares = blsgen.shares(sks, ids, msg)
+    whole = ctx.bls_combine(shares)
+    assert whole == blsgen.sign_point(sk, msg)
+    parts = [ctx.bls_combine_partial(shares, *mg.share_slice(k, world, r)) for r in range(world)]
+    assert all(len(p) == cb.BLS_G1_PARTIAL_BYTES for p in parts)
+    assert ctx.bls_combine_finish(parts) == whole
+    # multisig (unit scalars): sum of the shares
+    parts_ms = [ctx.bls_combine_partial(shares, *mg.share_slice(k, world, r), multisig=True) for r in range(world)]
+    assert ctx.bls_combine_finish(parts_ms) == ctx.bls_combine(shares, multisig=True)
+
+
+@pytest.mark.parametrize("world", [1, 2, 4])
+def test_sharded_multisig_key_sum(ctx, world):
+    import cbft_multigpu as mg
+
+    n = 20
+    sk, sks, pk, vks = blsgen.keyset(n, n, seed=29)
+    msg = bytes(range(7, 39))
+    signers = [1, 2, 5, 6, 7, 11, 13, 17, 19, 20]
+    shares = blsgen.shares(sks, signers, msg)
+    sig = ctx.bls_combine(shares, multisig=True)
+    bm = B.signers_bitmap(signers)
+    kid = ctx.bls_load_keys(pk, vks)
+    try:
+        assert ctx.bls_verify_multisig(kid, msg, sig, bm)
+        parts = [ctx.bls_sum_keys_partial(kid, bm, *mg.id_slice(n, world, r)) for r in range(world)]
+        assert all(len(p) == cb.BLS_G2_PARTIAL_BYTES for p in parts)
+        assert ctx.bls_verify_multisig_partials(msg, sig, parts)
+        assert not ctx.bls_verify_multisig_partials(bytes(32), sig, parts)
+        # a signer missing from the key sum -> reject
+        bm2 = B.signers_bitmap(signers[:-1])
+        parts2 = [ctx.bls_sum_keys_partial(kid, bm2, *mg.id_slice(n, world, r)) for r in range(world)]
+        assert not ctx.bls_verify_multisig_partials(msg, sig, parts2)
+    finally:
+        ctx.bls_unload_keys(kid)
