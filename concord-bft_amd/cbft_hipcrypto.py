@@ -48,6 +48,16 @@ ABI = [
     ("cbft_sync", ctypes.c_int, [ctypes.c_void_p]),
     ("cbft_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("cbft_stage_times_ms", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
+    ("cbft_rsa_load_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, _u32p]),
+    ("cbft_rsa_unload_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
+    ("cbft_rsa_key_status", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
+    ("cbft_rsa_verify_batch", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
+    ("cbft_rsa_verify_batch_device", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
+    ("cbft_rsa_kernel_ms", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]),
     ("cbft_bls_load_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_uint32, _u32p]),
     ("cbft_bls_unload_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
     ("cbft_bls_key_status", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
@@ -209,6 +219,48 @@ class Context:
 
     def sync(self):
         _check(self.lib.cbft_sync(self.handle), "cbft_sync")
+
+    # ------------------------------------------------------------------ RSA-2048 PKCS#1 v1.5 / SHA-256
+    def rsa_load_keys(self, keys: Sequence[tuple]) -> int:
+        """keys: (n, e) integer pairs (2048-bit moduli, 32-bit exponents)."""
+        mods = np.frombuffer(b"".join(int(n).to_bytes(256, "big") for n, _ in keys), dtype=np.uint8) \
+            if keys else np.zeros(1, np.uint8)
+        exps = np.array([int(e) for _, e in keys] or [0], dtype=np.uint32)
+        tid = ctypes.c_uint32()
+        _check(self.lib.cbft_rsa_load_keys(self.handle, _ptr(mods), _ptr(exps), len(keys), ctypes.byref(tid)),
+               "cbft_rsa_load_keys")
+        return tid.value
+
+    def rsa_unload_keys(self, tid: int):
+        _check(self.lib.cbft_rsa_unload_keys(self.handle, tid), "cbft_rsa_unload_keys")
+
+    def rsa_key_status(self, tid: int, nkeys: int) -> np.ndarray:
+        out = np.zeros(max(1, nkeys), dtype=np.uint8)
+        _check(self.lib.cbft_rsa_key_status(self.handle, tid, _ptr(out)), "cbft_rsa_key_status")
+        return out[:nkeys].astype(bool)
+
+    def rsa_verify(self, tid: int, key_idx, sigs, msgs: Sequence[bytes]) -> bytes:
+        n = len(msgs)
+        kidx = np.ascontiguousarray(np.asarray(key_idx, dtype=np.uint32))
+        s = _as_rows(sigs, 256)
+        assert kidx.shape[0] == n and s.shape[0] == n
+        blob, offs, lens = pack_messages(msgs)
+        out = np.zeros(max(1, (n + 7) // 8), dtype=np.uint8)
+        _check(self.lib.cbft_rsa_verify_batch(self.handle, tid, _ptr(kidx), _ptr(s), _ptr(blob), _ptr(offs),
+                                               _ptr(lens), n, _ptr(out)), "cbft_rsa_verify_batch")
+        return out.tobytes()[: (n + 7) // 8]
+
+    def rsa_verify_device(self, tid: int, d_key_idx: int, d_sig: int, d_msg: int, d_off: int, d_len: int, n: int,
+                          d_verdict_words: int, stream: int = 0):
+        _check(self.lib.cbft_rsa_verify_batch_device(
+            self.handle, tid, ctypes.c_void_p(d_key_idx), ctypes.c_void_p(d_sig), ctypes.c_void_p(d_msg),
+            ctypes.c_void_p(d_off), ctypes.c_void_p(d_len), n, ctypes.c_void_p(d_verdict_words),
+            ctypes.c_void_p(stream)), "cbft_rsa_verify_batch_device")
+
+    def rsa_kernel_ms(self) -> float:
+        out = ctypes.c_float()
+        _check(self.lib.cbft_rsa_kernel_ms(self.handle, ctypes.byref(out)), "cbft_rsa_kernel_ms")
+        return out.value
 
     # ------------------------------------------------------------------ BLS BN-P254
     def bls_load_keys(self, pk65: bytes, vks65: Sequence[bytes]) -> int:

@@ -205,6 +205,10 @@ void cbft_close(cbft_ctx* c) {
   }
   for (hipEvent_t& e : c->ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto& kv : c->rsa_tables) kv.second.rec.release();
+  for (DevBuf* b : {&c->rsa_scratch, &c->rsa_sig, &c->rsa_kidx}) b->release();
+  for (hipEvent_t e : {c->rsa_done, c->rsa_ev[0], c->rsa_ev[1]})
+    if (e) (void)hipEventDestroy(e);
   if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
 }

@@ -12,6 +12,7 @@
 
 #include "cbft_hipcrypto.h"
 #include "ed25519_verify.h"
+#include "rsa_verify.h"
 
 struct DevBuf {
   void* p = nullptr;
@@ -70,6 +71,13 @@ struct WorkSlot {
   bool used = false;
 };
 
+// RSA verifier key table: per-key records (modulus, R^2 mod n, n0inv, e, validity) built on the
+// GPU at load time (one verifier per key, SigManager.cpp:139-150)
+struct RsaKeyTable {
+  uint32_t nkeys = 0;
+  DevBuf rec;
+};
+
 struct cbft_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -91,6 +99,14 @@ struct cbft_ctx {
   // BLS
   std::unordered_map<uint32_t, BlsKeySet> bls_sets;
   uint32_t next_bls_id = 1;
+  // RSA
+  std::unordered_map<uint32_t, RsaKeyTable> rsa_tables;
+  uint32_t next_rsa_id = 1;
+  DevBuf rsa_scratch, rsa_sig, rsa_kidx;
+  hipEvent_t rsa_done = nullptr;  // orders reuse of rsa_scratch across streams
+  bool rsa_used = false;
+  hipEvent_t rsa_ev[2] = {nullptr, nullptr};  // around the last RSA kernel when profiling
+  bool rsa_ev_valid = false;
   DevBuf bls_gen_lines, bls_msg, bls_H, bls_shares, bls_valid, bls_sig, bls_ids, bls_use, bls_lambda,
       bls_partial, bls_out, bls_ms_lines, bls_ms_ok, bls_bitmap;
 };

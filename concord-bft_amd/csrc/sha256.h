@@ -5,7 +5,14 @@
 #include <stddef.h>
 #include <stdint.h>
 
-#include "bn254_field.h"  // BN_HD
+#ifndef BN_HD  // same definition as bn254_field.h (identical redefinition is allowed)
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define BN_HD __host__ __device__ __forceinline__
+#else
+#define BN_HD inline
+#endif
+#endif
 
 BN_HD uint32_t sha256_rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
 

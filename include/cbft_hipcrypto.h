@@ -113,6 +113,40 @@ int cbft_sync(cbft_ctx* ctx);
 int cbft_set_profiling(cbft_ctx* ctx, int enable);
 int cbft_stage_times_ms(cbft_ctx* ctx, float* out, int nout);
 
+/* ------------------------------------------------------- RSA-2048 PKCS#1 v1.5 / SHA-256 ------
+ * Replaces concord::util::crypto::RSAVerifier (util/src/crypto_utils.cpp:101-117,155-168), i.e.
+ * Crypto++ 8.2.0 RSASS<PKCS1v15, SHA256>::Verifier::VerifyMessage, the verifier SigManager
+ * instantiates today for replica (e = 17) and client (e = 65537) keys (SigManager.cpp:138,146,255).
+ * Verdict = ((s mod n)^e mod n == 00 01 FF.. 00 || DigestInfo(SHA-256) || SHA-256(m)); as in
+ * Crypto++, s is NOT required to be < n (oracle/rsa_ref.py).  Moduli are exactly 2048 bits.
+ * A signature is 256 bytes big-endian (IVerifier::signatureLength() of a 2048-bit key). */
+#define CBFT_RSA_MODULUS_BYTES 256
+#define CBFT_RSA_SIGNATURE_BYTES 256
+
+/* Load nkeys public keys: moduli = nkeys x 256 bytes big-endian (top bit set), exponents = nkeys
+ * odd 32-bit public exponents (>= 3).  Per-key records (R^2 mod n, -n^-1 mod 2^32) are built on
+ * the GPU here, once.  A key that is not a 2048-bit odd modulus with an odd e >= 3 is accepted
+ * into the table and every signature under it verifies false (cbft_rsa_key_status). */
+int cbft_rsa_load_keys(cbft_ctx* ctx, const uint8_t* moduli, const uint32_t* exponents, uint32_t nkeys,
+                       uint32_t* out_key_table_id);
+int cbft_rsa_unload_keys(cbft_ctx* ctx, uint32_t key_table_id);
+/* out_ok: nkeys bytes, 1 = the key is usable */
+int cbft_rsa_key_status(cbft_ctx* ctx, uint32_t key_table_id, uint8_t* out_ok);
+
+/* Verify n signatures (sig = n x 256 bytes) against keys of a loaded table; message i =
+ * msg_blob[msg_off[i] .. + msg_len[i]); verdict_bitmap as for Ed25519.  key_idx[i] >= nkeys is
+ * CBFT_EINVAL. */
+int cbft_rsa_verify_batch(cbft_ctx* ctx, uint32_t key_table_id, const uint32_t* key_idx, const uint8_t* sig,
+                          const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
+                          uint8_t* verdict_bitmap);
+/* Device-resident variant (asynchronous on `stream`, ceil(n/64) verdict words); an out-of-range
+ * key index verifies false. */
+int cbft_rsa_verify_batch_device(cbft_ctx* ctx, uint32_t key_table_id, const uint32_t* d_key_idx,
+                                 const uint8_t* d_sig, const uint8_t* d_msg_blob, const uint64_t* d_msg_off,
+                                 const uint32_t* d_msg_len, size_t n, uint64_t* d_verdict_words, void* stream);
+/* With profiling enabled (cbft_set_profiling): the last RSA verify kernel's duration in ms. */
+int cbft_rsa_kernel_ms(cbft_ctx* ctx, float* out_ms);
+
 /* ------------------------------------------------------------- BLS BN-P254 (threshsign) ------
  * RELIC "BN_P254" curve (threshsign/src/bls/relic/Library.cpp:51,72): G1 compressed = 33 bytes,
  * G2 compressed = 65 bytes, share = 4-byte big-endian id || 33-byte G1 (BlsThresholdSigner.cpp:
