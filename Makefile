@@ -43,7 +43,7 @@ clean:
 CPU_LIB := tools/cpu_baseline/libcbft_cpu_openssl.so
 cpu: $(CPU_LIB)
 $(CPU_LIB): tools/cpu_baseline/openssl_ed25519.c
-	gcc -O2 -std=gnu11 -fPIC -shared -Wall -o $@ $< -lcrypto -lpthread
+	gcc -O2 -std=gnu11 -fPIC -shared -Wall -Wno-deprecated-declarations -o $@ $< -lcrypto -lpthread
 
 HOST_LIB := concord-bft_amd/libcbft_host.so
 HOST_SRC := concord-bft_amd/host/src/crypto_utils.cpp concord-bft_amd/host/src/sig_manager.cpp concord-bft_amd/host/src/bls_hip.cpp

@@ -62,7 +62,7 @@ def parse():
     ap.add_argument("--latency-runs", type=int, default=200)
     ap.add_argument("--inflight", type=int, default=2, help="batches in flight (streams) in the timed loop")
     ap.add_argument("--no-extras", dest="extras", action="store_false",
-                    help="skip the config #3 (mixed) and config #4 (BLS) side measurements")
+                    help="skip the config #3 (mixed), config #4 (BLS) and RSA-2048 side measurements")
     return ap.parse_args()
 
 
@@ -270,6 +270,7 @@ def main():
             host_path = n / statistics.median(ht)
         mixed = bench_mixed(ctx, args) if (args.extras and world == 1) else None
         bls = bench_bls(ctx, args) if (args.extras and world == 1) else None
+        rsa = bench_rsa(ctx, args) if (args.extras and world == 1) else None
         out = {
             "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -285,6 +286,7 @@ def main():
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
             "mixed_config3": mixed,
             "bls_config4": bls,
+            "rsa_2048": rsa,
             "verdicts": "bit-exact vs host OpenSSL (checked before timing)",
         }
         print(json.dumps(out), flush=True)
@@ -321,6 +323,108 @@ def bench_mixed(ctx, args):
             "value": n / (ms * 1e-3), "unit": "verifies/s (host buffers in, PCIe included)",
             "exact_match": match, "n": n, "invalid": int((~ss.expected).sum()),
             "msg_bytes_total": int(ss.len.sum())}
+
+
+# RSA: measured v_mad_u64_u32 issue rate of the chip (tools/microbench/intrate.hip,
+# profiles/r01_intrate_microbench.txt): the bound of a kernel that is all 32x32->64 MACs
+MAD64_PEAK = 3.277e13
+
+
+def bench_rsa(ctx, args):
+    """RSA-2048 PKCS#1 v1.5 / SHA-256 batch verify (the verifier SigManager
+    instantiates today).  64K signatures over 256-byte messages, inputs resident in HBM, client
+    keys (e = 65537) and replica keys (e = 17); verdicts checked against the host OpenSSL and the
+    host-buffer path before timing.  CPU baseline: OpenSSL RSA verify on 16 threads, same set."""
+    import torch
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import rsagen
+
+    n = args.batch
+    keys = rsagen.load_keys()
+    out = {"config": f"{n} x 256 B messages, RSA-2048, 256 distinct signed messages tiled", "unit": "verifies/s"}
+    dev = torch.device("cuda", torch.cuda.current_device())
+    mods = np.frombuffer(b"".join(k["n"].to_bytes(256, "big") for k in keys), dtype=np.uint8)
+    exps = np.array([k["e"] for k in keys], dtype=np.uint32)
+    tid = ctx.rsa_load_keys([(k["n"], k["e"]) for k in keys])
+    kc = workload.cpu_lib().cbft_cpu_rsa_keys_new(workload._p(mods), workload._p(exps), len(keys))
+    try:
+        for label, e in (("client_e65537", 65537), ("replica_e17", 17)):
+            ids = [i for i, k in enumerate(keys) if k["e"] == e]
+            _, kidx, sigs, msgs, _ = rsagen.signed_batch(n, nuniq=256, msg_len=args.msg_len, invalid_frac=0.0,
+                                                        seed=e, key_ids=ids)
+            blob, offs, lens = cb.pack_messages(msgs)
+            kidx_a = np.asarray(kidx, dtype=np.uint32)
+            sig_a = np.frombuffer(b"".join(sigs), dtype=np.uint8)
+            d_k = torch.from_numpy(kidx_a.view(np.int32).copy()).to(dev)
+            d_s = torch.from_numpy(sig_a.copy()).to(dev)
+            d_m = torch.from_numpy(blob.copy()).to(dev)
+            d_o = torch.from_numpy(offs.view(np.int64).copy()).to(dev)
+            d_l = torch.from_numpy(lens.view(np.int32).copy()).to(dev)
+            d_v = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+            torch.cuda.synchronize()
+            a = (tid, d_k.data_ptr(), d_s.data_ptr(), d_m.data_ptr(), d_o.data_ptr(), d_l.data_ptr(), n,
+                 d_v.data_ptr())
+            ctx.rsa_verify_device(*a)
+            ctx.sync()
+            words = d_v.cpu().numpy().view(np.uint64)
+            got = np.unpackbits(words.view(np.uint8), bitorder="little")[:n].astype(bool)
+            host = cb.bitmap_to_bools(ctx.rsa_verify(tid, kidx_a, sig_a, msgs), n)
+            cpu_v = np.zeros(n, dtype=np.uint8)
+            workload.cpu_lib().cbft_cpu_rsa_verify(kc, workload._p(kidx_a), workload._p(sig_a), workload._p(blob),
+                                                   workload._p(offs), workload._p(lens), n, workload._p(cpu_v),
+                                                   args.cpu_threads)
+            if not (got.all() and np.array_equal(got, host) and np.array_equal(got, cpu_v.astype(bool))):
+                raise SystemExit(f"RSA verdicts differ ({label})")
+            steps = max(5, args.steps // 2)
+            for _ in range(2):
+                ctx.rsa_verify_device(*a)
+            ctx.sync()
+            c0 = time.perf_counter()
+            for _ in range(steps):
+                ctx.rsa_verify_device(*a)
+            ctx.sync()
+            wall = (time.perf_counter() - c0) / steps
+            ctx.set_profiling(True)
+            kms = []
+            for _ in range(5):
+                ctx.rsa_verify_device(*a)
+                kms.append(ctx.rsa_kernel_ms())
+            ctx.set_profiling(False)
+            kms = statistics.median(kms)
+            nbits = e.bit_length()
+            products = 1 + (nbits - 1) + bin(e).count("1") + 1  # CONV + squarings + multiplies + REDC
+            macs = products * 64 * 128  # v_mad_u64_u32 per verify (64 rows x 2 x 64 columns)
+            ts = []
+            workload.cpu_lib().cbft_cpu_rsa_verify(kc, workload._p(kidx_a), workload._p(sig_a), workload._p(blob),
+                                                   workload._p(offs), workload._p(lens), n, workload._p(cpu_v),
+                                                   args.cpu_threads)
+            for _ in range(3):
+                c0 = time.perf_counter()
+                workload.cpu_lib().cbft_cpu_rsa_verify(kc, workload._p(kidx_a), workload._p(sig_a),
+                                                       workload._p(blob), workload._p(offs), workload._p(lens), n,
+                                                       workload._p(cpu_v), args.cpu_threads)
+                ts.append(time.perf_counter() - c0)
+            cpu_value = n / statistics.median(ts)
+            out[label] = {
+                "value": n / wall, "kernel_ms": kms, "kernel_value": n / (kms * 1e-3),
+                "roofline": {"bound": "valu_mad_u64_u32", "achieved": macs * n / (kms * 1e-3) / 1e12,
+                             "peak": MAD64_PEAK / 1e12, "unit": "T MAC/s",
+                             "frac": macs * n / (kms * 1e-3) / MAD64_PEAK, "macs_per_verify": macs,
+                             "kernel": "rsa_verify_kernel"},
+                "cpu_baseline": {"value": cpu_value, "unit": "verifies/s", "cores": args.cpu_threads,
+                                 "kind": "reference",
+                                 "sample": f"OpenSSL {_openssl_version()} EVP_DigestVerify(RSA PKCS#1 v1.5, "
+                                           f"SHA-256), EVP_PKEY per key, {args.cpu_threads} pthreads; median of "
+                                           f"3 passes over the same {n} signatures"},
+                "gpu_vs_cpu": (n / wall) / cpu_value,
+            }
+            del d_k, d_s, d_m, d_o, d_l, d_v
+    finally:
+        workload.cpu_lib().cbft_cpu_keys_free(kc, len(keys))
+        ctx.rsa_unload_keys(tid)
+    out["verdicts"] = "device path == host path == host OpenSSL, all accept"
+    return out
 
 
 def bench_bls(ctx, args):

@@ -1,19 +1,18 @@
 """Deterministic RSA-2048 test keys and signed batches for the RSA parity tests and bench.py.
 
 Keys are generated once (seeded Miller-Rabin prime search, pure Python) and cached in
-tests/golden/rsa_test_keys.json; signatures are PKCS#1 v1.5 / SHA-256 made with CRT through
-oracle/rsa_ref.py's encoding.  Test infrastructure only.
+tests/golden/rsa_test_keys.json; signatures are PKCS#1 v1.5 / SHA-256 made with CRT (the same
+encoding as oracle/rsa_ref.py, restated here so that bench.py's workload generation does not
+import the oracle).  Workload / fixture generation only.
 """
 from __future__ import annotations
 
+import hashlib
 import json
 import os
 import random
-import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(os.path.dirname(HERE), "oracle"))
-import rsa_ref as R  # noqa: E402
 
 KEYS_PATH = os.path.join(HERE, "golden", "rsa_test_keys.json")
 EXPONENTS = (65537, 17, 65537, 17, 3, 65537, 0xC0000001, 65537)
@@ -73,24 +72,32 @@ def load_keys():
     return [{k: (v if k == "e" else int(v, 16)) for k, v in key.items()} for key in raw]
 
 
+def emsa_sha256_2048(msg: bytes) -> bytes:
+    """EMSA-PKCS1-v1_5 for SHA-256 at 2048 bits: 00 01 FF*202 00 || DigestInfo || H(m)."""
+    t = bytes.fromhex("3031300d060960864801650304020105000420") + hashlib.sha256(msg).digest()
+    return b"\x00\x01" + b"\xff" * (256 - 3 - len(t)) + b"\x00" + t
+
+
 def sign(key, msg: bytes) -> bytes:
     """PKCS#1 v1.5 / SHA-256 signature with CRT (equal to rsa_ref.sign)."""
     n, d, p, q = key["n"], key["d"], key["p"], key["q"]
-    m = int.from_bytes(R.emsa_pkcs1_v15_sha256(msg, n.bit_length()), "big")
+    m = int.from_bytes(emsa_sha256_2048(msg), "big")
     sp = pow(m, d % (p - 1), p)
     sq = pow(m, d % (q - 1), q)
     h = (pow(q, -1, p) * (sp - sq)) % p
     return (sq + h * q).to_bytes(256, "big")
 
 
-def signed_batch(n: int, nuniq: int = 512, msg_len=256, invalid_frac: float = 0.1, seed: int = 7):
+def signed_batch(n: int, nuniq: int = 512, msg_len=256, invalid_frac: float = 0.1, seed: int = 7, key_ids=None):
     """n (key_idx, sig, msg, expected) entries over load_keys(): nuniq distinct honest signatures
-    tiled to n, then ~invalid_frac of the entries corrupted (bit flips in s or m, wrong key)."""
+    tiled to n, then ~invalid_frac of the entries corrupted (bit flips in s or m, wrong key).
+    key_ids restricts the signing keys (e.g. the e = 65537 client keys)."""
     keys = load_keys()
+    ids = list(key_ids) if key_ids is not None else list(range(len(keys)))
     rng = random.Random(seed)
     uniq = []
     for u in range(nuniq):
-        ki = u % len(keys)
+        ki = ids[u % len(ids)]
         ln = msg_len if isinstance(msg_len, int) else rng.randint(*msg_len)
         msg = bytes(rng.getrandbits(8) for _ in range(ln))
         uniq.append((ki, sign(keys[ki], msg), msg))

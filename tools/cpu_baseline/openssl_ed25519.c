@@ -116,3 +116,65 @@ int cbft_cpu_sign_many(const uint8_t* sk, uint32_t nkeys, const uint32_t* key_id
   free(jobs);
   return 0;
 }
+
+/* ---- RSA-2048 PKCS#1 v1.5 / SHA-256 (the verifier SigManager instantiates today,
+ * util/src/crypto_utils.cpp:101-117 — Crypto++ there, OpenSSL's RSA here as the host baseline;
+ * identical verdicts on modulus-length signatures with s < n). */
+#include <openssl/bn.h>
+#include <openssl/rsa.h>
+
+typedef struct {
+  EVP_PKEY** keys;
+  const uint32_t* key_idx;
+  const uint8_t* sig;
+  const uint8_t* blob;
+  const uint64_t* off;
+  const uint32_t* len;
+  size_t lo, hi;
+  uint8_t* out;
+} rjob_t;
+
+static void* rworker(void* arg) {
+  rjob_t* j = (rjob_t*)arg;
+  EVP_MD_CTX* ctx = EVP_MD_CTX_new();
+  for (size_t i = j->lo; i < j->hi; i++) {
+    EVP_PKEY* k = j->keys[j->key_idx[i]];
+    int ok = 0;
+    if (k && EVP_DigestVerifyInit(ctx, NULL, EVP_sha256(), NULL, k) == 1)
+      ok = EVP_DigestVerify(ctx, j->sig + 256 * i, 256, j->blob + j->off[i], j->len[i]) == 1;
+    j->out[i] = (uint8_t)ok;
+    EVP_MD_CTX_reset(ctx);
+  }
+  EVP_MD_CTX_free(ctx);
+  return NULL;
+}
+
+/* key cache from nkeys big-endian 256-byte moduli and 32-bit exponents */
+void* cbft_cpu_rsa_keys_new(const uint8_t* mod, const uint32_t* exps, uint32_t nkeys) {
+  EVP_PKEY** keys = (EVP_PKEY**)calloc(nkeys ? nkeys : 1, sizeof(EVP_PKEY*));
+  for (uint32_t i = 0; i < nkeys; i++) {
+    RSA* r = RSA_new();
+    BIGNUM* n = BN_bin2bn(mod + 256 * (size_t)i, 256, NULL);
+    BIGNUM* e = BN_new();
+    BN_set_word(e, exps[i]);
+    RSA_set0_key(r, n, e, NULL);
+    keys[i] = EVP_PKEY_new();
+    EVP_PKEY_assign_RSA(keys[i], r);
+  }
+  return keys;
+}
+
+int cbft_cpu_rsa_verify(void* keycache, const uint32_t* key_idx, const uint8_t* sig, const uint8_t* blob,
+                        const uint64_t* off, const uint32_t* len, size_t n, uint8_t* out, int threads) {
+  if (threads < 1) threads = 1;
+  pthread_t* th = (pthread_t*)calloc(threads, sizeof(pthread_t));
+  rjob_t* jobs = (rjob_t*)calloc(threads, sizeof(rjob_t));
+  for (int t = 0; t < threads; t++) {
+    jobs[t] = (rjob_t){(EVP_PKEY**)keycache, key_idx, sig, blob, off, len, n * t / threads, n * (t + 1) / threads, out};
+    pthread_create(&th[t], NULL, rworker, &jobs[t]);
+  }
+  for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+  free(th);
+  free(jobs);
+  return 0;
+}

@@ -29,6 +29,9 @@ def cpu_lib():
         lib.cbft_cpu_verify.argtypes = [vp, vp, vp, vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_int]
         lib.cbft_cpu_pubkey.argtypes = [vp, vp]
         lib.cbft_cpu_sign_many.argtypes = [vp, ctypes.c_uint32, vp, vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_int]
+        lib.cbft_cpu_rsa_keys_new.restype = vp
+        lib.cbft_cpu_rsa_keys_new.argtypes = [vp, vp, ctypes.c_uint32]
+        lib.cbft_cpu_rsa_verify.argtypes = [vp, vp, vp, vp, vp, vp, ctypes.c_size_t, vp, ctypes.c_int]
         _cpu = lib
     return _cpu
 
