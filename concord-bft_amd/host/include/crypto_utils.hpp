@@ -10,9 +10,15 @@
 //   EdDSASigner : ISigner          new; RFC 8032 signing through the host OpenSSL (not on the
 //                                  verify path; the reference signs on the host too)
 //
-// Batch side-API (the point of the engine): EdDSAVerifier::verifyBatch() verifies many
-// (verifier, data, sig) triples in one GPU launch; verdicts are identical to calling verify()
-// on each triple.
+//   RSAVerifier : IVerifier        crypto_utils.hpp:84-96 / crypto_utils.cpp:101-117,155-168:
+//                                  RSASS<PKCS1v15, SHA256> (Crypto++ 8.2.0 semantics, restated in
+//                                  oracle/rsa_ref.py) verified on the GPU (cbft_rsa_*); 2048-bit
+//                                  moduli, 32-bit public exponents
+//   RSASigner : ISigner            crypto_utils.hpp:98-110; host OpenSSL (not on the verify path)
+//
+// Batch side-API (the point of the engine): verifyBatch() verifies many (verifier, data, sig)
+// triples with one GPU launch per algorithm; verdicts are identical to calling verify() on each
+// triple.
 #pragma once
 
 #include <cstdint>
@@ -41,10 +47,11 @@ class ISigner {
 };
 
 class Ed25519Engine;  // per-GPU owner of the cbft_ctx and of the device key table
+class RsaEngine;      // same for RSA keys
 
 // One (verifier, message, signature) triple of a batch.  Pointers are borrowed.
 struct VerifyRequest {
-  const class EdDSAVerifier* verifier;
+  const IVerifier* verifier;
   const char* data;
   size_t dataLength;
   const char* sig;
@@ -67,7 +74,8 @@ class EdDSAVerifier : public IVerifier {
   const uint8_t* rawKey() const { return raw_; }
   uint32_t engineKeyIndex() const { return key_index_; }
 
-  // Verifies every request in one batch on the GPU; out[i] = verdict of reqs[i].
+  // Verifies every request whose verifier is an EdDSAVerifier in one GPU batch; out[i] = verdict
+  // of reqs[i] (false for other verifier types).
   static void verifyBatch(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out);
 
  private:
@@ -94,6 +102,57 @@ class EdDSASigner : public ISigner {
   std::string key_str_;
   void* pkey_;  // EVP_PKEY*
 };
+
+class RSAVerifier : public IVerifier {
+ public:
+  // str_pub_key: X.509 SubjectPublicKeyInfo, hex DER (HexaDecimalStrippedFormat, what
+  // Crypto++'s RSA::PublicKey::Save writes) or PEM.  Throws std::invalid_argument on a key that
+  // does not parse, is not RSA, or is not a 2048-bit modulus with a public exponent < 2^32.
+  RSAVerifier(const std::string& str_pub_key, KeyFormat fmt);
+  ~RSAVerifier() override;
+  RSAVerifier(const RSAVerifier&) = default;
+
+  // Crypto++ VerifyMessage semantics: the signature is read as a big-endian integer of any
+  // length (leading zero bytes are insignificant).  A signature with more than 256 significant
+  // bytes is rejected here (Crypto++ would reduce it mod n; such inputs are never produced by a
+  // signer and the reference's callers check signatureLength() first, ClientRequestMsg.cpp:156).
+  bool verify(const std::string& data, const std::string& sig) const override;
+  uint32_t signatureLength() const override { return 256; }
+  std::string getPubKey() const override { return key_str_; }
+
+  uint32_t engineKeyIndex() const { return key_index_; }
+  // Verifies every request whose verifier is an RSAVerifier in one GPU batch.
+  static void verifyBatch(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out);
+
+ private:
+  std::string key_str_;
+  uint32_t key_index_;
+  std::shared_ptr<RsaEngine> engine_;
+};
+
+class RSASigner : public ISigner {
+ public:
+  // str_priv_key: PKCS#8 / PKCS#1 private key, hex DER or PEM (crypto_utils.cpp:141-152).
+  RSASigner(const std::string& str_priv_key, KeyFormat fmt);
+  ~RSASigner() override;
+  RSASigner(const RSASigner&) = delete;
+  RSASigner& operator=(const RSASigner&) = delete;
+  std::string sign(const std::string& data) override;
+  uint32_t signatureLength() const override { return 256; }
+  std::string getPrivKey() const override { return key_str_; }
+
+ private:
+  std::string key_str_;
+  void* pkey_;  // EVP_PKEY*
+};
+
+// Builds the verifier a key string calls for: an Ed25519 key (raw 32 bytes or its
+// SubjectPublicKeyInfo) -> EdDSAVerifier, an RSA SubjectPublicKeyInfo -> RSAVerifier; throws
+// std::invalid_argument otherwise (SigManager.cpp:138,146,255 construct verifiers per key).
+std::shared_ptr<IVerifier> makeVerifier(const std::string& str_pub_key, KeyFormat fmt);
+
+// Verifies a mixed batch: one GPU launch per algorithm; other IVerifier types run verify().
+void verifyBatch(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out);
 
 // Helpers shared by the key parsers (hex <-> bytes, PEM SubjectPublicKeyInfo for Ed25519).
 std::string toHex(const uint8_t* p, size_t n);

@@ -49,8 +49,9 @@ class SigManager {
  public:
   using Key = std::string;
 
-  // publicKeys: (principal ids sharing the key, key string); all keys are Ed25519 here (the
-  // reference's key-format "version" tag would select EdDSAVerifier, SigManager.cpp:156).
+  // publicKeys: (principal ids sharing the key, key string); each key builds an EdDSAVerifier or
+  // an RSAVerifier by its type (makeVerifier; the reference builds RSAVerifiers,
+  // SigManager.cpp:138,146, and its key-format "version" tag would select Ed25519, :156).
   SigManager(PrincipalId myId, const std::pair<Key, concord::util::crypto::KeyFormat>& mySigPrivateKey,
              const std::vector<std::pair<std::set<PrincipalId>, Key>>& publicKeys,
              concord::util::crypto::KeyFormat keysFormat, const ReplicasInfo& replicasInfo);
@@ -79,7 +80,7 @@ class SigManager {
 
   const PrincipalId myId_;
   std::unique_ptr<concord::util::crypto::ISigner> mySigner_;
-  std::map<PrincipalId, std::shared_ptr<concord::util::crypto::EdDSAVerifier>> verifiers_;
+  std::map<PrincipalId, std::shared_ptr<concord::util::crypto::IVerifier>> verifiers_;
   ReplicasInfo replicasInfo_;
   mutable Metrics metrics_;
   mutable std::shared_mutex mutex_;

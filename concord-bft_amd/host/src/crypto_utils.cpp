@@ -152,11 +152,14 @@ class Ed25519Engine {
     std::vector<size_t> pos;
     pos.reserve(reqs.size());
     size_t blob = 0;
-    for (size_t i = 0; i < reqs.size(); i++)
-      if (reqs[i].sigLength == 64 && reqs[i].verifier) {
+    std::vector<const EdDSAVerifier*> ver(reqs.size(), nullptr);
+    for (size_t i = 0; i < reqs.size(); i++) {
+      ver[i] = dynamic_cast<const EdDSAVerifier*>(reqs[i].verifier);
+      if (reqs[i].sigLength == 64 && ver[i]) {
         pos.push_back(i);
         blob += reqs[i].dataLength;
       }
+    }
     if (pos.empty()) return;
     const size_t n = pos.size();
     std::vector<uint32_t> kidx(n), len(n);
@@ -165,7 +168,7 @@ class Ed25519Engine {
     size_t o = 0;
     for (size_t j = 0; j < n; j++) {
       const VerifyRequest& r = reqs[pos[j]];
-      kidx[j] = r.verifier->engineKeyIndex();
+      kidx[j] = ver[pos[j]]->engineKeyIndex();
       std::memcpy(&sig[64 * j], r.sig, 64);
       off[j] = o;
       len[j] = (uint32_t)r.dataLength;
@@ -251,10 +254,7 @@ void EdDSAVerifier::verifyBatch(const std::vector<VerifyRequest>& reqs, std::vec
   if (reqs.empty()) return;
   const EdDSAVerifier* any = nullptr;
   for (auto& r : reqs)
-    if (r.verifier) {
-      any = r.verifier;
-      break;
-    }
+    if ((any = dynamic_cast<const EdDSAVerifier*>(r.verifier))) break;
   if (!any) return;
   any->engine_->verify(reqs, out);
 }

@@ -9,6 +9,8 @@ namespace bftEngine::impl {
 
 using concord::util::crypto::EdDSASigner;
 using concord::util::crypto::EdDSAVerifier;
+using concord::util::crypto::IVerifier;
+using concord::util::crypto::RSASigner;
 using concord::util::crypto::KeyFormat;
 using concord::util::crypto::VerifyRequest;
 
@@ -16,12 +18,18 @@ SigManager::SigManager(PrincipalId myId, const std::pair<Key, KeyFormat>& mySigP
                        const std::vector<std::pair<std::set<PrincipalId>, Key>>& publicKeys, KeyFormat keysFormat,
                        const ReplicasInfo& replicasInfo)
     : myId_(myId), replicasInfo_(replicasInfo) {
-  if (!mySigPrivateKey.first.empty())
-    mySigner_ = std::make_unique<EdDSASigner>(mySigPrivateKey.first, mySigPrivateKey.second);
+  if (!mySigPrivateKey.first.empty()) {
+    // an Ed25519 seed (hex) or an RSA private key (the reference's replicas sign with RSA)
+    try {
+      mySigner_ = std::make_unique<EdDSASigner>(mySigPrivateKey.first, mySigPrivateKey.second);
+    } catch (const std::invalid_argument&) {
+      mySigner_ = std::make_unique<RSASigner>(mySigPrivateKey.first, mySigPrivateKey.second);
+    }
+  }
   // one verifier object per distinct key, shared by every principal mapped to it
-  // (SigManager.cpp:139-150)
+  // (SigManager.cpp:139-150); Ed25519 or RSA by key type
   for (const auto& [ids, key] : publicKeys) {
-    auto v = std::make_shared<EdDSAVerifier>(key, keysFormat);
+    auto v = concord::util::crypto::makeVerifier(key, keysFormat);
     for (PrincipalId id : ids) verifiers_[id] = v;
   }
 }
@@ -70,7 +78,7 @@ void SigManager::verifySigBatch(const std::vector<SigBatchItem>& items, std::vec
       known[i] = 1;
       reqs[i] = {it->second.get(), items[i].data, items[i].dataLength, items[i].sig, items[i].sigLength};
     }
-    EdDSAVerifier::verifyBatch(reqs, out);  // verifiers stay alive under the shared lock
+    concord::util::crypto::verifyBatch(reqs, out);  // verifiers stay alive under the shared lock
   }
   for (size_t i = 0; i < items.size(); i++) {
     if (!known[i]) {
@@ -91,7 +99,7 @@ void SigManager::sign(const char* data, size_t dataLength, char* outSig, uint16_
 uint16_t SigManager::getMySigLength() const { return mySigner_ ? (uint16_t)mySigner_->signatureLength() : 0; }
 
 void SigManager::setClientPublicKey(const std::string& key, PrincipalId id, KeyFormat fmt) {
-  auto v = std::make_shared<EdDSAVerifier>(key, fmt);  // throws on a bad key, like the reference
+  auto v = concord::util::crypto::makeVerifier(key, fmt);  // throws on a bad key, like the reference
   std::unique_lock lock(mutex_);
   verifiers_.insert_or_assign(id, std::move(v));
 }
