@@ -18,7 +18,7 @@ from typing import Iterable, List, Optional, Sequence
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libcbft_hipcrypto.so")
+LIB_PATH = os.environ.get("CBFT_LIB") or os.path.join(HERE, "libcbft_hipcrypto.so")  # CBFT_LIB: variant builds
 
 CBFT_NO_KEY_TABLE = 0xFFFFFFFF
 _u8p = ctypes.POINTER(ctypes.c_uint8)

@@ -131,6 +131,7 @@ int cbft_rsa_verify_batch_device(cbft_ctx* c, uint32_t id, const uint32_t* d_key
                                  const uint8_t* d_msg, const uint64_t* d_off, const uint32_t* d_len, size_t n,
                                  uint64_t* d_verdicts, void* stream) {
   if (!c || (n && (!d_key_idx || !d_sig || !d_off || !d_len || !d_verdicts))) return CBFT_EINVAL;
+  if (reinterpret_cast<uintptr_t>(d_sig) & 3) return CBFT_EINVAL;  // signatures are read as words
   if (n == 0) return CBFT_OK;
   std::lock_guard<std::mutex> g(c->mu);
   auto it = c->rsa_tables.find(id);

@@ -17,11 +17,18 @@
 #define RSA_KEY_N0INV 128
 #define RSA_KEY_E 129
 #define RSA_KEY_OK 130
+#ifndef CBFT_RSA_MIN_WAVES
+#define CBFT_RSA_MIN_WAVES 2  // waves/SIMD the verify kernel is register-allocated for
+#endif
+#ifndef CBFT_RSA_PREFETCH
+#define CBFT_RSA_PREFETCH 1  // software-pipeline the LDS reads of x one limb group ahead
+#endif
 #ifndef CBFT_RSA_BLOCK
-#define CBFT_RSA_BLOCK 128
+#define CBFT_RSA_BLOCK 64  // one wave per block: LDS (16 KB) then admits 2 waves/SIMD at any mix
 #endif
 
-// One batch, all pointers in device memory.  Signature i is sig[256 i .. 256 i + 256), big-endian.
+// One batch, all pointers in device memory.  Signature i is sig[256 i .. 256 i + 256), big-endian
+// (sig must be 4-byte aligned).
 struct RsaBatch {
   size_t n;
   const uint32_t* keys;     // key table (RSA_KEY_WORDS per key)

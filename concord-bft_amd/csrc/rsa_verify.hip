@@ -69,17 +69,27 @@ __device__ __forceinline__ void mont_mul(uint4 (*xl)[CBFT_RSA_BLOCK], uint32_t l
   uint32_t t[L + 1];
 #pragma unroll
   for (int j = 0; j <= L; j++) t[j] = 0;
+  uint32_t a_next = a(0);
 #pragma unroll 1
   for (int i = 0; i < L; i++) {
     // keep the x limbs streaming from LDS row by row (hoisting them out of the loop would need
     // 64 more VGPRs than a two-wave-per-SIMD budget has)
     asm volatile("" ::: "memory");
-    const uint32_t ai = a(i);
+    const uint32_t ai = a_next;
+    if (i + 1 < L) a_next = a(i + 1);  // the next row operand (maybe a global load) overlaps this row
     uint64_t c1 = 0, c2 = 0;
     uint32_t m = 0;
+#if CBFT_RSA_PREFETCH
+    uint4 nxt = xl[0][lane];
+#endif
 #pragma unroll
     for (int q = 0; q < L / 4; q++) {
+#if CBFT_RSA_PREFETCH
+      const uint4 b4 = nxt;  // x limbs 4q..4q+3; the next group's LDS read is in flight meanwhile
+      if (q + 1 < L / 4) nxt = xl[q + 1][lane];
+#else
       const uint4 b4 = xl[q][lane];
+#endif
       const uint32_t bv[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
       for (int r = 0; r < 4; r++) {
@@ -211,7 +221,7 @@ __global__ void __launch_bounds__(64) rsa_keys_kernel(const uint8_t* mod, const 
 }
 
 // ---------------------------------------------------------------- verify ---------------------
-__global__ void __launch_bounds__(CBFT_RSA_BLOCK, 2) rsa_verify_kernel(const RsaBatch b, uint32_t* scratch,
+__global__ void __launch_bounds__(CBFT_RSA_BLOCK, CBFT_RSA_MIN_WAVES) rsa_verify_kernel(const RsaBatch b, uint32_t* scratch,
                                                                     uint64_t* verdicts) {
   __shared__ uint4 xl[L / 4][CBFT_RSA_BLOCK];  // the running operand x, [limb/4][lane] (conflict-free)
   const uint32_t tid = threadIdx.x;
@@ -259,7 +269,8 @@ __global__ void __launch_bounds__(CBFT_RSA_BLOCK, 2) rsa_verify_kernel(const Rsa
         [&](int i) -> uint32_t {
           if (op == MUL) return scratch[(size_t)i * stride + idx];
           if (op == REDC) return i == 0 ? 1u : 0u;
-          if (op == CONV) return load_be32(sg + RSA_MOD_BYTES - 4 * (i + 1));
+          if (op == CONV)  // limb i of s: big-endian word 63 - i of the (4-byte aligned) signature
+            return __builtin_bswap32(*reinterpret_cast<const uint32_t*>(sg + RSA_MOD_BYTES - 4 * (i + 1)));
           const uint4 v = xl[i >> 2][tid];
           const int r = i & 3;
           return r == 0 ? v.x : r == 1 ? v.y : r == 2 ? v.z : v.w;

@@ -140,7 +140,7 @@ int cbft_rsa_verify_batch(cbft_ctx* ctx, uint32_t key_table_id, const uint32_t* 
                           const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
                           uint8_t* verdict_bitmap);
 /* Device-resident variant (asynchronous on `stream`, ceil(n/64) verdict words); an out-of-range
- * key index verifies false. */
+ * key index verifies false; d_sig must be 4-byte aligned (CBFT_EINVAL otherwise). */
 int cbft_rsa_verify_batch_device(cbft_ctx* ctx, uint32_t key_table_id, const uint32_t* d_key_idx,
                                  const uint8_t* d_sig, const uint8_t* d_msg_blob, const uint64_t* d_msg_off,
                                  const uint32_t* d_msg_len, size_t n, uint64_t* d_verdict_words, void* stream);

@@ -14,11 +14,9 @@ import rsagen
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 e_sel = sys.argv[2] if len(sys.argv) > 2 else "mixed"
-keys, kidx, sigs, msgs, _ = rsagen.signed_batch(n, nuniq=256, msg_len=256, invalid_frac=0.0, seed=1)
-if e_sel != "mixed":
-    want = int(e_sel)
-    kidx = [k if keys[k]["e"] == want else [i for i, kk in enumerate(keys) if kk["e"] == want][0] for k in kidx]
-    sigs = [rsagen.sign(keys[k], m) if keys[k]["e"] == want else s for k, s, m in zip(kidx, sigs, msgs)] if False else sigs
+keys = rsagen.load_keys()
+ids = None if e_sel == "mixed" else [i for i, k in enumerate(keys) if k["e"] == int(e_sel)]
+keys, kidx, sigs, msgs, _ = rsagen.signed_batch(n, nuniq=256, msg_len=256, invalid_frac=0.0, seed=1, key_ids=ids)
 torch.zeros(1, device="cuda:0")  # torch initialises HIP first (its runtime, then ours)
 with cb.Context(0) as ctx:
     tid = ctx.rsa_load_keys([(k["n"], k["e"]) for k in keys])
