@@ -394,7 +394,10 @@ def bench_rsa(ctx, args):
             kms = statistics.median(kms)
             nbits = e.bit_length()
             products = 1 + (nbits - 1) + bin(e).count("1") + 1  # CONV + squarings + multiplies + REDC
-            macs = products * 64 * 128  # v_mad_u64_u32 per verify (64 rows x 2 x 64 columns)
+            # v_mad_u64_u32 per verify of the running kernel's schedule: lane-pair radix-2^28 (74 rows x
+            # 2 x 74 columns) or, with CBFT_RSA_KERNEL=fios, 32-bit FIOS (64 rows x 2 x 64 columns)
+            fios = os.environ.get("CBFT_RSA_KERNEL") == "fios"
+            macs = products * (64 * 128 if fios else 74 * 148)
             ts = []
             workload.cpu_lib().cbft_cpu_rsa_verify(kc, workload._p(kidx_a), workload._p(sig_a), workload._p(blob),
                                                    workload._p(offs), workload._p(lens), n, workload._p(cpu_v),
@@ -411,7 +414,7 @@ def bench_rsa(ctx, args):
                 "roofline": {"bound": "valu_mad_u64_u32", "achieved": macs * n / (kms * 1e-3) / 1e12,
                              "peak": MAD64_PEAK / 1e12, "unit": "T MAC/s",
                              "frac": macs * n / (kms * 1e-3) / MAD64_PEAK, "macs_per_verify": macs,
-                             "kernel": "rsa_verify_kernel"},
+                             "kernel": "rsa_verify_kernel" if fios else "rsa_verify_pair_kernel"},
                 "cpu_baseline": {"value": cpu_value, "unit": "verifies/s", "cores": args.cpu_threads,
                                  "kind": "reference",
                                  "sample": f"OpenSSL {_openssl_version()} EVP_DigestVerify(RSA PKCS#1 v1.5, "

@@ -10,13 +10,23 @@
 
 #define RSA_LIMBS 64        // 2048-bit modulus as 64 little-endian 32-bit limbs
 #define RSA_MOD_BYTES 256
-// Key record in HBM (uint32 words): n[64] | R^2 mod n [64] | n0inv | e | ok | pad -> 136 words
-#define RSA_KEY_WORDS 136
+// Key record in HBM (uint32 words):
+//   [0, 136)   32-bit-limb form (FIOS kernel): n[64] | R^2 mod n [64] (R = 2^2048) | -n^-1 mod 2^32 |
+//              e | ok | pad
+//   [136, 384) 28-bit-limb form (lane-pair kernel, R' = 2^2072): n[80] | R'^2 mod n [80] |
+//              R' mod n [80] | -n^-1 mod 2^28 | pad   (limbs beyond 74 are zero)
+#define RSA_KEY_WORDS 384
 #define RSA_KEY_N 0
 #define RSA_KEY_R2 64
 #define RSA_KEY_N0INV 128
 #define RSA_KEY_E 129
 #define RSA_KEY_OK 130
+#define RSA_NL 74           // 28-bit limbs of a value < 2^2072
+#define RSA_PL 80           // 28-bit limbs stored per operand
+#define RSA_KEY_P_N 136
+#define RSA_KEY_P_R2 216
+#define RSA_KEY_P_R1 296
+#define RSA_KEY_P_N0INV 376
 #ifndef CBFT_RSA_MIN_WAVES
 #define CBFT_RSA_MIN_WAVES 2  // waves/SIMD the verify kernel is register-allocated for
 #endif
@@ -44,5 +54,7 @@ struct RsaBatch {
 hipError_t cbft_rsa_launch_keys(const uint8_t* d_mod, const uint32_t* d_exp, uint32_t nkeys, uint32_t* d_keys,
                                 hipStream_t stream);
 // Verify a batch; writes ceil(n/64) verdict words.  d_scratch: RSA_LIMBS * round_up(n, block) words.
-hipError_t cbft_rsa_launch_verify(const RsaBatch& b, uint32_t* d_scratch, uint64_t* d_verdicts, hipStream_t stream);
+// pair = 1: the lane-pair radix-2^28 kernel, 0: the one-lane FIOS kernel (same verdicts).
+hipError_t cbft_rsa_launch_verify(const RsaBatch& b, uint32_t* d_scratch, uint64_t* d_verdicts, hipStream_t stream,
+                                  int pair = 1);
 size_t cbft_rsa_scratch_words(size_t n);
