@@ -1,7 +1,9 @@
 """CPU tests of the RSA path's checker and host logic:
 the Crypto++-semantics restatement (oracle/rsa_ref.py) against OpenSSL-pinned golden vectors, the
-reference's own test key, and a Python model of the GPU kernel's Montgomery arithmetic (two-carry
-FIOS rows over 32-bit limbs, R = 2^2048) checked against exact big-integer results."""
+reference's own test key, and Python models of the GPU kernels' Montgomery arithmetic (the
+one-lane FIOS rows over 32-bit limbs, R = 2^2048, and the lane-pair radix-2^28 column
+accumulators, R' = 2^2072) checked against exact big-integer results, with every 64-bit
+intermediate bound asserted."""
 import json
 import os
 import random
@@ -133,3 +135,56 @@ def test_kernel_exponent_schedule_model():
                 x = mont_mul_fios(sm, x, n)
         x = mont_mul_fios(1, x, n)
         assert x == pow(s, e, n)
+
+
+def mont_mul_pair_model(a, b, n):
+    """The lane-pair radix-2^28 product of rsa_verify_pair_kernel: 74 limbs, R' = 2^2072, column
+    accumulators split over an even (positions 0..37) and odd (38..75) lane, two rows per
+    iteration then a two-column shift.  Checks every accumulator stays below 2^64 and returns
+    the fully carried value (< 2n)."""
+    M = (1 << 28) - 1
+    NL, PC = 74, 38
+    al = [(a >> (28 * i)) & M for i in range(NL)] + [0, 0]
+    xs = [0] + [(b >> (28 * i)) & M for i in range(NL)] + [0] * 5          # slot 1 + j = limb j
+    nl = [(n >> (28 * i)) & M for i in range(NL)]
+    n0inv = (-pow(nl[0], -1, 1 << 28)) % (1 << 28)
+    lanes = []
+    for hi in (0, 1):
+        P0 = PC if hi else 0
+        nreg = [nl[P0 + k - 1] if 0 <= P0 + k - 1 < NL else 0 for k in range(PC + 1)]
+        lanes.append({"P0": P0, "nreg": nreg, "A": [0] * PC})
+    for i in range(0, NL, 2):
+        for ln in lanes:
+            ln["xv"] = [xs[ln["P0"] + k] for k in range(PC + 1)]
+        L, H = lanes
+        for h, ai in ((0, al[i]), (1, al[i + 1])):
+            for ln in lanes:
+                for c in range(PC):
+                    ln["A"][c] += ai * ln["xv"][c + 1 - h]
+            m = (L["A"][h] & 0xFFFFFFFF) * n0inv & M
+            for ln in lanes:
+                for c in range(PC):
+                    ln["A"][c] += m * ln["nreg"][c + 1 - h]
+                    assert ln["A"][c] < 1 << 64
+            L["A"][h + 1] += L["A"][h] >> 28
+        u0, u1 = H["A"][0], H["A"][1]
+        for ln in lanes:
+            ln["A"] = ln["A"][2:] + [0, 0]
+        L["A"][PC - 2], L["A"][PC - 1] = u0, u1
+    v = sum(x << (28 * c) for c, x in enumerate(lanes[0]["A"]))
+    v += sum(x << (28 * (PC + c)) for c, x in enumerate(lanes[1]["A"]))
+    assert v < 2 * n
+    return v
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_kernel_pair_radix28_model(seed):
+    rng = random.Random(100 + seed)
+    keys = rsagen.load_keys()
+    R = 1 << 2072
+    for k in keys[:3]:
+        n = k["n"]
+        rinv = pow(R, -1, n)
+        for a, b in [(rng.randrange(2 * n), rng.randrange(2 * n)), (2 * n - 1, 2 * n - 1),
+                     ((1 << 2048) - 1, R * R % n), (1, n - 1)]:
+            assert mont_mul_pair_model(a, b, n) % n == a * b * rinv % n
