@@ -49,8 +49,8 @@ def ops_per_verify(m: int) -> int:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--msg-len", type=int, default=256)
     ap.add_argument("--nkeys", type=int, default=4096)

@@ -128,6 +128,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   if (!c) return CBFT_ENOMEM;
   c->device = device;
   if (const char* e = getenv("CBFT_FINISH_BATCH")) c->finish_batch = atoi(e);
+  if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e) != 0;
   int rc = CBFT_OK;
   do {
     if (hipSetDevice(device) != hipSuccess) {
@@ -204,6 +205,8 @@ void cbft_close(cbft_ctx* c) {
     if (w.done) (void)hipEventDestroy(w.done);
   }
   for (hipEvent_t& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t& e : c->stage_done)
     if (e) (void)hipEventDestroy(e);
   for (auto& kv : c->rsa_tables) kv.second.rec.release();
   for (DevBuf* b : {&c->rsa_scratch, &c->rsa_sig, &c->rsa_kidx}) b->release();
@@ -309,9 +312,11 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
 
   Ed25519Batch b{n, d_pk, d_kidx, d_sig, d_msg, d_off, d_len};
   Ed25519Work w{};
-  // one inversion per 8 signatures per lane only where the batch keeps >= 64 finish waves; a
-  // small (latency-bound) batch inverts per signature
-  w.finish_batch = c->finish_batch ? c->finish_batch : (n >= 32768 ? 8 : 1);
+  // one inversion per K signatures per lane only where the batch keeps >= 64 finish waves; a
+  // small (latency-bound) batch inverts per signature.  K = 16 at the 64K headline: the finish is
+  // then 64 waves that run beside the next batch's hash/ladder (stage order), 5 % of the VALU work
+  // of a per-signature inversion (A/B on MI355X: K = 8 327, K = 16 360, K = 32 273 M verifies/s)
+  w.finish_batch = c->finish_batch ? c->finish_batch : (n >= 65536 ? 16 : n >= 32768 ? 8 : 1);
   w.base_table = c->base_table.as<uint32_t>();
   w.h_soa = slot.h.as<uint32_t>();
   w.flags = slot.flags.as<uint8_t>();
@@ -330,7 +335,16 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     w.comb = cbft_comb_ladder(it->second.geo.w, CBFT_COMB_B_RADIX);
     w.aok = it->second.aok.as<uint8_t>();
   }
-  CBFT_HIP(cbft_ed25519_launch_verify(b, w, s, c->profiling ? c->ev : nullptr));
+  StageOrder order{};
+  if (c->stage_order) {
+    for (hipEvent_t& e : c->stage_done)
+      if (!e) CBFT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    order.wait = c->stage_used;
+    order.done[0] = c->stage_done[0];
+    order.done[1] = c->stage_done[1];
+  }
+  CBFT_HIP(cbft_ed25519_launch_verify(b, w, s, c->profiling ? c->ev : nullptr, c->stage_order ? &order : nullptr));
+  c->stage_used = c->stage_order;
   CBFT_HIP(hipEventRecord(slot.done, s));
   slot.used = true;
   c->ev_valid = c->profiling;

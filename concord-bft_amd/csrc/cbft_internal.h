@@ -89,6 +89,13 @@ struct cbft_ctx {
   WorkSlot slots[CBFT_WORK_SLOTS];
   unsigned next_slot = 0;
   int finish_batch = 0;  // K4: signatures per lane sharing one inversion ($CBFT_FINISH_BATCH; 0 = by batch size)
+  // Stage order across batches (any streams): batch i+1's hash starts after batch i's hash and
+  // its ladder after batch i's ladder, so the pipeline runs hash(i+1) / finish(i) beside
+  // ladder-to-ladder instead of two streams marching in phase (both finishes together, 7/8 of
+  // the SIMDs idle).  $CBFT_STAGE_ORDER=0 turns it off.
+  bool stage_order = true;
+  hipEvent_t stage_done[2] = {nullptr, nullptr};  // last hash, last ladder
+  bool stage_used = false;
   DevBuf verdicts;
   DevBuf sig, msg, off, len, kidx, pk;
   std::vector<uint64_t> host_verdicts;

@@ -98,5 +98,11 @@ hipError_t cbft_ed25519_build_base_table(uint32_t* d_tbl, hipStream_t stream);
 hipError_t cbft_ed25519_launch_prep(const uint8_t* d_pk, size_t nunits, uint32_t* d_tbl, uint8_t* d_aok,
                                     hipStream_t stream);
 // ev: nullable array of 4 events recorded before K1, K2->K3, K3->K4 and after K4 (profiling)
+// Cross-batch stage order: when `wait`, the hash waits for done[0] and the ladder for done[1]
+// (recorded by the previous batch, maybe on another stream); both are re-recorded here.
+struct StageOrder {
+  bool wait;
+  hipEvent_t done[2];
+};
 hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& w, hipStream_t stream,
-                                      hipEvent_t* ev = nullptr);
+                                      hipEvent_t* ev = nullptr, const StageOrder* order = nullptr);

@@ -767,14 +767,18 @@ hipError_t cbft_ed25519_launch_prep(const uint8_t* d_pk, size_t nunits, uint32_t
 }
 
 hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& w, hipStream_t stream,
-                                      hipEvent_t* ev) {
+                                      hipEvent_t* ev, const StageOrder* order) {
   if (b.n == 0) return hipSuccess;
   const bool comb = w.comb_tbl && w.base_comb && b.key_idx;
   if (comb && (w.comb.nper < 1 || w.comb.nper > COMB_MAX_STEPS || 4 * w.comb.nper < w.comb.a.npos + w.comb.b.npos))
     return hipErrorInvalidValue;
   const dim3 grid(grid_for(b.n)), block(CBFT_VERIFY_BLOCK);
+  hipError_t e;
+  if (order && order->wait && (e = hipStreamWaitEvent(stream, order->done[0], 0)) != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(ed25519_hash_kernel, grid, block, 0, stream, b, w.h_soa, w.flags);
+  if (order && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;
+  if (order && order->wait && (e = hipStreamWaitEvent(stream, order->done[1], 0)) != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[1], stream);
   if (comb) {
     hipLaunchKernelGGL(ed25519_comb_ladder_kernel, dim3((unsigned)((4 * b.n + CBFT_VERIFY_BLOCK - 1) / CBFT_VERIFY_BLOCK)),
@@ -782,6 +786,7 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   } else {
     hipLaunchKernelGGL(ed25519_ladder_kernel, grid, block, 0, stream, b, w.h_soa, w.tbl, w.base_table, w.xyz_soa);
   }
+  if (order && (e = hipEventRecord(order->done[1], stream)) != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[2], stream);
   switch (w.finish_batch) {
 #define CBFT_FINISH_CASE(K)                                                                                     \
@@ -793,6 +798,7 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
     CBFT_FINISH_CASE(4)
     CBFT_FINISH_CASE(8)
     CBFT_FINISH_CASE(16)
+    CBFT_FINISH_CASE(32)
 #undef CBFT_FINISH_CASE
     default:
       hipLaunchKernelGGL(ed25519_finish_kernel, grid, block, 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words);

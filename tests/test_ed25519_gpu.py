@@ -165,3 +165,96 @@ def test_fresh_context_without_presizing(golden):
         vs = golden  # grow
         got = _bools(c.verify_pk([v.pk for v in vs], [v.sig for v in vs], [v.msg for v in vs]), len(vs))
         assert np.array_equal(got, np.array([bool(v.verdict) for v in vs]))
+
+
+@pytest.mark.parametrize("k", [1, 2, 4, 8, 16, 32])
+def test_finish_inversion_batching(golden, monkeypatch, k):
+    # K4' shares one inversion among K signatures per lane (Montgomery's trick); rejected items
+    # (S >= L, undecodable A) enter the product as 1.  Every K must give the golden verdicts,
+    # including the ragged last block (1,145 vectors is not a multiple of 64 K).
+    monkeypatch.setenv("CBFT_FINISH_BATCH", str(k))
+    with cb.Context(device=0) as c:
+        got = _bools(c.verify_pk([v.pk for v in golden], [v.sig for v in golden], [v.msg for v in golden]),
+                     len(golden))
+    assert np.array_equal(got, np.array([bool(v.verdict) for v in golden]))
+
+
+class _Hip:
+    """Device buffers and streams from the HIP runtime libcbft_hipcrypto itself links (torch ships
+    its own HIP runtime; a second runtime in the same process sees no GPUs once the first owns it)."""
+
+    def __init__(self):
+        cb.load_library()
+        self.lib = ctypes.CDLL("libamdhip64.so.7")  # the soname libcbft_hipcrypto loaded
+        self.bufs, self.streams = [], []
+
+    def _ok(self, rc, what):
+        assert rc == 0, f"{what}: hipError {rc}"
+
+    def to_dev(self, a: np.ndarray) -> int:
+        p = ctypes.c_void_p()
+        self._ok(self.lib.hipMalloc(ctypes.byref(p), ctypes.c_size_t(max(a.nbytes, 1))), "hipMalloc")
+        self.bufs.append(p.value)
+        a = np.ascontiguousarray(a)
+        self._ok(self.lib.hipMemcpy(p, a.ctypes.data_as(ctypes.c_void_p), ctypes.c_size_t(a.nbytes), 1), "hipMemcpy")
+        return p.value
+
+    def from_dev(self, ptr: int, nbytes: int) -> bytes:
+        out = np.zeros(nbytes, dtype=np.uint8)
+        self._ok(self.lib.hipMemcpy(out.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(ptr), ctypes.c_size_t(nbytes),
+                                    2), "hipMemcpy")
+        return out.tobytes()
+
+    def stream(self) -> int:
+        s = ctypes.c_void_p()
+        self._ok(self.lib.hipStreamCreate(ctypes.byref(s)), "hipStreamCreate")
+        self.streams.append(s.value)
+        return s.value
+
+    def sync(self):
+        self._ok(self.lib.hipDeviceSynchronize(), "hipDeviceSynchronize")
+
+    def close(self):
+        self.sync()
+        for s in self.streams:
+            self.lib.hipStreamDestroy(ctypes.c_void_p(s))
+        for b in self.bufs:
+            self.lib.hipFree(ctypes.c_void_p(b))
+
+
+@pytest.mark.parametrize("order", ["1", "0"])
+def test_device_path_two_streams_stage_order(monkeypatch, order):
+    # the bench's schedule: device-resident batches alternating over two streams, the library's
+    # cross-batch stage order (hash after hash, ladder after ladder) and two rotating work slots.
+    # Batches with different corruption patterns must each keep their own verdicts.
+    monkeypatch.setenv("CBFT_STAGE_ORDER", order)
+    hip = _Hip()
+    n = 65536
+    nwords = (n + 63) // 64
+    base = sigsets.make_sigset(n, nkeys=512, msg_len=256, seed=23)
+    variants = []
+    for v in range(3):
+        sig = base.sig.copy()
+        bad = np.arange(v, n, 89 + 10 * v)
+        sig[bad, 33 + v] ^= 0x40
+        exp = np.ones(n, dtype=bool)
+        exp[bad] = False
+        variants.append((hip.to_dev(sig.reshape(-1)), exp))
+    try:
+        with cb.Context(device=0, max_batch=n) as c:
+            tid = c.load_keys(base.pk)
+            d_kidx = hip.to_dev(base.key_idx)
+            d_blob = hip.to_dev(base.blob)
+            d_off = hip.to_dev(base.off)
+            d_len = hip.to_dev(base.len)
+            streams = [hip.stream(), hip.stream()]
+            outs = [hip.to_dev(np.zeros(nwords, dtype=np.uint64)) for _ in range(6)]
+            for b in range(6):
+                c.verify_device(tid, 0, d_kidx, variants[b % 3][0], d_blob, d_off, d_len, n, outs[b], streams[b % 2])
+            hip.sync()
+            for b in range(6):
+                got = _bools(hip.from_dev(outs[b], nwords * 8), n)
+                assert np.array_equal(got, variants[b % 3][1]), f"batch {b}"
+            c.unload_keys(tid)
+    finally:
+        hip.close()
