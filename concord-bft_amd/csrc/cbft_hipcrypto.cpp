@@ -128,7 +128,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   if (!c) return CBFT_ENOMEM;
   c->device = device;
   if (const char* e = getenv("CBFT_FINISH_BATCH")) c->finish_batch = atoi(e);
-  if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e) != 0;
+  if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e);
   int rc = CBFT_OK;
   do {
     if (hipSetDevice(device) != hipSuccess) {
@@ -340,11 +340,12 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     for (hipEvent_t& e : c->stage_done)
       if (!e) CBFT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     order.wait = c->stage_used;
+    order.hash = c->stage_order != 2;
     order.done[0] = c->stage_done[0];
     order.done[1] = c->stage_done[1];
   }
   CBFT_HIP(cbft_ed25519_launch_verify(b, w, s, c->profiling ? c->ev : nullptr, c->stage_order ? &order : nullptr));
-  c->stage_used = c->stage_order;
+  c->stage_used = c->stage_order != 0;
   CBFT_HIP(hipEventRecord(slot.done, s));
   slot.used = true;
   c->ev_valid = c->profiling;

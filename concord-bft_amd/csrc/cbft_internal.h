@@ -92,8 +92,8 @@ struct cbft_ctx {
   // Stage order across batches (any streams): batch i+1's hash starts after batch i's hash and
   // its ladder after batch i's ladder, so the pipeline runs hash(i+1) / finish(i) beside
   // ladder-to-ladder instead of two streams marching in phase (both finishes together, 7/8 of
-  // the SIMDs idle).  $CBFT_STAGE_ORDER=0 turns it off.
-  bool stage_order = true;
+  // the SIMDs idle).  $CBFT_STAGE_ORDER: 0 off, 1 hash + ladder, 2 ladder only.
+  int stage_order = 1;
   hipEvent_t stage_done[2] = {nullptr, nullptr};  // last hash, last ladder
   bool stage_used = false;
   DevBuf verdicts;

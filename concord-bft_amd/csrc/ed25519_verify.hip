@@ -774,7 +774,8 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
     return hipErrorInvalidValue;
   const dim3 grid(grid_for(b.n)), block(CBFT_VERIFY_BLOCK);
   hipError_t e;
-  if (order && order->wait && (e = hipStreamWaitEvent(stream, order->done[0], 0)) != hipSuccess) return e;
+  if (order && order->wait && order->hash && (e = hipStreamWaitEvent(stream, order->done[0], 0)) != hipSuccess)
+    return e;
   if (ev) (void)hipEventRecord(ev[0], stream);
   hipLaunchKernelGGL(ed25519_hash_kernel, grid, block, 0, stream, b, w.h_soa, w.flags);
   if (order && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;
