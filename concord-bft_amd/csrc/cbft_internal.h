@@ -14,6 +14,34 @@
 #include "ed25519_verify.h"
 #include "rsa_verify.h"
 
+// Pinned host staging buffer (hipHostMalloc): the host-buffer entry points pack their inputs
+// into it and move them with one DMA copy instead of one pageable copy per array.
+struct HostBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  hipError_t reserve(size_t bytes) {
+    if (bytes <= cap) return hipSuccess;
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 1 << 16);
+    hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      p = nullptr;
+      return e;
+    }
+    cap = want;
+    return hipSuccess;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T* as(size_t off = 0) const { return reinterpret_cast<T*>(static_cast<uint8_t*>(p) + off); }
+};
+
 struct DevBuf {
   void* p = nullptr;
   size_t cap = 0;
@@ -99,6 +127,8 @@ struct cbft_ctx {
   DevBuf verdicts;
   DevBuf sig, msg, off, len, kidx, pk;
   std::vector<uint64_t> host_verdicts;
+  HostBuf hstage;  // packed host inputs + verdict words of the host-buffer path
+  DevBuf dstage;   // the same packing on the device
   // profiling: events around K1 (hash), K3 (ladder), K4 (finish) of the last verify
   bool profiling = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
