@@ -88,6 +88,22 @@ def test_ragged_batch_sizes(ctx, golden, n):
         assert bm[-1] >> (n % 8) == 0  # bits past n are zero
 
 
+@pytest.mark.parametrize("n", [8191, 8192, 8193, 20000])
+def test_host_staging_boundary(ctx, n):
+    # host-buffer batches up to 8,192 go through one packed pinned staging copy, larger ones
+    # through per-array copies (cbft_hipcrypto.cpp, CBFT_STAGE_MAX_N): both sides of the switch,
+    # key-table and per-signature keys, mixed lengths with 10 % invalid
+    ss = sigsets.make_sigset(n, nkeys=97, msg_len=(1, 700), seed=n, invalid_frac=0.10)
+    tid = ctx.load_keys(ss.pk)
+    try:
+        got = _bools(ctx.verify(tid, ss.key_idx, ss.sig, ss.msgs()), n)
+    finally:
+        ctx.unload_keys(tid)
+    assert np.array_equal(got, ss.expected)
+    got2 = _bools(ctx.verify_pk(ss.per_sig_pk(), ss.sig, ss.msgs()), n)
+    assert np.array_equal(got2, ss.expected)
+
+
 def test_empty_batch(ctx):
     assert ctx.verify_pk([], [], []) == b""
 
