@@ -190,8 +190,19 @@ def main():
         for k, v in ctx.stage_times_ms().items():
             stage[k].append(v)
     ctx.set_profiling(False)
-    ladder_ms = statistics.median(stage["ladder"])
+    iso_ladder_ms = statistics.median(stage["ladder"])
     pipe_ms = sum(statistics.median(v) for v in stage.values())
+    # ... and in the pipeline: the timed loop's schedule again (same steps, streams, slots) with
+    # per-batch events; each stage's events sit on its batch's stream after the cross-batch
+    # waits, so this is the mean launch duration while batches overlap (what rocprofv3 reports
+    # for the same command), and it is the duration the roofline divides by
+    ctx.set_profiling(True, per_batch=True)
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    pipe_stage, pipe_batches = ctx.stage_times_avg_ms()
+    ctx.set_profiling(False)
+    ladder_ms = pipe_stage["ladder"]
     kname = "ed25519_comb_ladder_kernel" if args.key_mode == "keytable" else "ed25519_ladder_kernel"
     # Executed VALU work of one ladder launch, from this configuration's own rocprofv3 --pmc passes
     # (profiles/pmc_ladder.json, tools/pmc_summary.py): every VALU wave-instruction is 64 lane-ops,
@@ -215,6 +226,10 @@ def main():
                 "peak": INT32_PEAK / 1e12, "unit": "TOP/s",
                 "frac": achieved / INT32_PEAK if achieved else None, "traffic": traffic,
                 "kernel": kname, "kernel_ms": ladder_ms, "units_per_launch": n,
+                "kernel_ms_basis": f"mean of {pipe_batches} pipelined launches (HIP events on the launch stream)",
+                "kernel_ms_isolated": iso_ladder_ms,
+                "frac_isolated": slot_ops / (iso_ladder_ms * 1e-3) / INT32_PEAK if slot_ops else None,
+                "stage_ms_pipelined": pipe_stage,
                 "achieved_basis": "executed VALU issue slots per launch (PMC, INT64-class x2) / kernel time",
                 "valu_lane_ops_per_launch": valu_ops, "issue_slot_ops_per_launch": slot_ops,
                 "model_ref10": {"ops_per_unit": OPS_DSM, "work_equivalent_TOPs": model / 1e12,

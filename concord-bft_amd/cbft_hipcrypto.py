@@ -48,6 +48,8 @@ ABI = [
     ("cbft_sync", ctypes.c_int, [ctypes.c_void_p]),
     ("cbft_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("cbft_stage_times_ms", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
+    ("cbft_stage_times_avg_ms", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
     ("cbft_rsa_load_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, _u32p]),
     ("cbft_rsa_unload_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
     ("cbft_rsa_key_status", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p]),
@@ -343,8 +345,17 @@ class Context:
                "cbft_bls_sign")
         return out.raw
 
-    def set_profiling(self, on: bool = True):
-        _check(self.lib.cbft_set_profiling(self.handle, 1 if on else 0), "cbft_set_profiling")
+    def set_profiling(self, on: bool = True, per_batch: bool = False):
+        mode = (2 if per_batch else 1) if on else 0
+        _check(self.lib.cbft_set_profiling(self.handle, mode), "cbft_set_profiling")
+
+    def stage_times_avg_ms(self):
+        """Mean {hash, ladder, finish} stage times (ms) over the batches since
+        set_profiling(per_batch=True), and the batch count."""
+        out = (ctypes.c_float * 3)()
+        cnt = ctypes.c_int(0)
+        _check(self.lib.cbft_stage_times_avg_ms(self.handle, out, 3, ctypes.byref(cnt)), "cbft_stage_times_avg_ms")
+        return {"hash": out[0], "ladder": out[1], "finish": out[2]}, cnt.value
 
     def stage_times_ms(self):
         """{hash, ladder, finish} kernel times (ms) of the last verify (needs set_profiling)."""

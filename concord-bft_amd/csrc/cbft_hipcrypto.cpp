@@ -69,6 +69,8 @@ static hipError_t build_comb(const uint8_t* d_pk, size_t nunits, int negate, con
   return e;
 }
 
+#define CBFT_PROF_RING 256  // batches whose stage events profiling mode 2 keeps
+
 static int reserve_slot(WorkSlot& w, size_t n) {
   CBFT_HIP(w.h.reserve(n * 8 * sizeof(uint32_t)));
   CBFT_HIP(w.flags.reserve(n));
@@ -210,6 +212,8 @@ void cbft_close(cbft_ctx* c) {
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t& e : c->stage_done)
     if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : c->ring)
+    if (e) (void)hipEventDestroy(e);
   for (auto& kv : c->rsa_tables) kv.second.rec.release();
   for (DevBuf* b : {&c->rsa_scratch, &c->rsa_sig, &c->rsa_kidx}) b->release();
   for (hipEvent_t e : {c->rsa_done, c->rsa_ev[0], c->rsa_ev[1]})
@@ -222,10 +226,38 @@ int cbft_set_profiling(cbft_ctx* c, int enable) {
   if (!c) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
+  if (enable < 0 || enable > 2) return CBFT_EINVAL;
   if (enable && !c->ev[0])
     for (hipEvent_t& e : c->ev) CBFT_HIP(hipEventCreate(&e));
+  if (enable == 2 && c->ring.empty()) {
+    c->ring.assign(CBFT_PROF_RING * 4, nullptr);
+    for (hipEvent_t& e : c->ring) CBFT_HIP(hipEventCreate(&e));
+  }
   c->profiling = enable != 0;
+  c->prof_mode = enable;
+  c->ring_n = 0;
   c->ev_valid = false;
+  return CBFT_OK;
+}
+
+int cbft_stage_times_avg_ms(cbft_ctx* c, float* out, int nout, int* nbatches) {
+  if (!c || !out || nout < 3) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  if (c->prof_mode != 2 || c->ring_n == 0) return CBFT_EINVAL;
+  CBFT_HIP(hipSetDevice(c->device));
+  const size_t cnt = std::min<size_t>(c->ring_n, CBFT_PROF_RING);
+  double sum[3] = {0, 0, 0};
+  for (size_t b = 0; b < cnt; b++) {
+    hipEvent_t* e = &c->ring[b * 4];
+    CBFT_HIP(hipEventSynchronize(e[3]));
+    for (int k = 0; k < 3; k++) {
+      float ms = 0;
+      CBFT_HIP(hipEventElapsedTime(&ms, e[k], e[k + 1]));
+      sum[k] += ms;
+    }
+  }
+  for (int k = 0; k < 3; k++) out[k] = (float)(sum[k] / (double)cnt);
+  if (nbatches) *nbatches = (int)cnt;
   return CBFT_OK;
 }
 
@@ -346,7 +378,9 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     order.done[0] = c->stage_done[0];
     order.done[1] = c->stage_done[1];
   }
-  CBFT_HIP(cbft_ed25519_launch_verify(b, w, s, c->profiling ? c->ev : nullptr, c->stage_order ? &order : nullptr));
+  hipEvent_t* evp = nullptr;
+  if (c->profiling) evp = c->prof_mode == 2 ? &c->ring[(c->ring_n++ % CBFT_PROF_RING) * 4] : c->ev;
+  CBFT_HIP(cbft_ed25519_launch_verify(b, w, s, evp, c->stage_order ? &order : nullptr));
   c->stage_used = c->stage_order != 0;
   CBFT_HIP(hipEventRecord(slot.done, s));
   slot.used = true;

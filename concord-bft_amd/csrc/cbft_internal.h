@@ -133,6 +133,11 @@ struct cbft_ctx {
   bool profiling = false;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   bool ev_valid = false;
+  // profiling mode 2: a ring of per-batch event quads, so pipelined batches keep their own
+  // timings (cbft_stage_times_avg_ms averages them)
+  std::vector<hipEvent_t> ring;
+  size_t ring_n = 0;
+  int prof_mode = 0;
   // BLS
   std::unordered_map<uint32_t, BlsKeySet> bls_sets;
   uint32_t next_bls_id = 1;

@@ -112,6 +112,13 @@ int cbft_sync(cbft_ctx* ctx);
  * {hash, ladder, finish} kernel times in ms into out[0..2] (nout >= 3). */
 int cbft_set_profiling(cbft_ctx* ctx, int enable);
 int cbft_stage_times_ms(cbft_ctx* ctx, float* out, int nout);
+/* enable = 2: every verify records its own events (a ring of the last 256 batches), so batches
+ * in flight on several streams keep separate timings; cbft_stage_times_avg_ms() waits for them
+ * and returns the mean {hash, ladder, finish} stage times (each stage's events sit on the
+ * batch's stream, after its cross-batch waits: the in-pipeline kernel durations) and, in
+ * *nbatches (nullable), how many batches were averaged.  -EINVAL unless in mode 2 with >= 1
+ * batch since cbft_set_profiling. */
+int cbft_stage_times_avg_ms(cbft_ctx* ctx, float* out, int nout, int* nbatches);
 
 /* ------------------------------------------------------- RSA-2048 PKCS#1 v1.5 / SHA-256 ------
  * Replaces concord::util::crypto::RSAVerifier (util/src/crypto_utils.cpp:101-117,155-168), i.e.
