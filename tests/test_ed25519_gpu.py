@@ -274,3 +274,23 @@ def test_device_path_two_streams_stage_order(monkeypatch, order):
             c.unload_keys(tid)
     finally:
         hip.close()
+
+
+def test_per_batch_profiling_ring(golden):
+    # cbft_set_profiling(ctx, 2): each verify keeps its own stage events; the average covers
+    # exactly the batches since enabling, and verdicts are unchanged by the instrumentation
+    with cb.Context(device=0) as c:
+        vs = golden[:512]
+        exp = np.array([bool(v.verdict) for v in vs])
+        c.set_profiling(True, per_batch=True)
+        for _ in range(3):
+            got = _bools(c.verify_pk([v.pk for v in vs], [v.sig for v in vs], [v.msg for v in vs]), len(vs))
+            assert np.array_equal(got, exp)
+        stage, cnt = c.stage_times_avg_ms()
+        assert cnt == 3
+        assert all(v > 0 for v in stage.values())
+        c.set_profiling(False)
+        with pytest.raises(cb.CbftError):
+            c.stage_times_avg_ms()
+        lib = cb.load_library()
+        assert lib.cbft_set_profiling(c.handle, 3) == -22
