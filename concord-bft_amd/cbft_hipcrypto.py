@@ -77,6 +77,7 @@ ABI = [
     ("cbft_bls_sum_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_void_p]),
     ("cbft_bls_sign", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p,
                                      ctypes.c_uint32, ctypes.c_void_p]),
+    ("cbft_bls_public_key", ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p]),
     ("cbft_bls_combine_partial", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int,
       ctypes.c_void_p]),
@@ -343,6 +344,12 @@ class Context:
         out = ctypes.create_string_buffer(37)
         _check(self.lib.cbft_bls_sign(self.handle, sk.to_bytes(32, "big"), share_id, msg, len(msg), out),
                "cbft_bls_sign")
+        return out.raw
+
+    def bls_public_key(self, sk: int) -> bytes:
+        """sk * g2, 65 compressed bytes (the signer's share verification key)."""
+        out = ctypes.create_string_buffer(65)
+        _check(self.lib.cbft_bls_public_key(self.handle, sk.to_bytes(32, "big"), out), "cbft_bls_public_key")
         return out.raw
 
     def set_profiling(self, on: bool = True, per_batch: bool = False):

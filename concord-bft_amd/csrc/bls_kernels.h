@@ -34,3 +34,4 @@ hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, c
                                   hipStream_t s);
 hipError_t cbft_bls_launch_sign(const uint8_t* d_msg, uint32_t len, const uint32_t* d_sk, uint32_t id,
                                 uint8_t* d_out37, hipStream_t s);
+hipError_t cbft_bls_launch_pubkey(const uint32_t* d_sk, uint8_t* d_out65, hipStream_t s);

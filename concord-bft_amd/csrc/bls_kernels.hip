@@ -386,6 +386,27 @@ __global__ void bls_sign_kernel(const uint8_t* msg, uint32_t len, const uint32_t
   g1_compress(out37 + 4, a);
 }
 
+// vk = sk * g2 as 65 compressed bytes: the signer's public key (BlsThresholdSigner's
+// publicKey_(secretKey) -> g2_mul_gen, BlsThresholdSigner.cpp:25; IThresholdSigner::
+// getShareVerificationKey).  sk: 8 LE words (< r).  One lane, double-and-add (a one-off per key).
+__global__ void bls_pubkey_kernel(const uint32_t* sk, uint8_t* out65) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  g2j G, acc;
+  fp2_load(G.X, Bn254Consts::G2X);
+  fp2_load(G.Y, Bn254Consts::G2Y);
+  fp2_one(G.Z);
+  fp2_one(acc.X);
+  fp2_one(acc.Y);
+  fp2_zero(acc.Z);
+  for (int i = 255; i >= 0; i--) {
+    g2_dbl_j(acc, acc);
+    if ((sk[i >> 5] >> (i & 31)) & 1) g2_add_j(acc, acc, G);
+  }
+  g2a a;
+  g2_to_affine(a, acc);
+  g2_compress(out65, a);
+}
+
 // ------------------------------------------------------------------------------ launchers
 size_t cbft_bls_lines_words_per_key() { return (size_t)LINES_PER_KEY; }
 
@@ -455,5 +476,9 @@ hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, c
 hipError_t cbft_bls_launch_sign(const uint8_t* d_msg, uint32_t len, const uint32_t* d_sk, uint32_t id,
                                 uint8_t* d_out37, hipStream_t s) {
   hipLaunchKernelGGL(bls_sign_kernel, dim3(1), dim3(64), 0, s, d_msg, len, d_sk, id, d_out37);
+  return hipGetLastError();
+}
+hipError_t cbft_bls_launch_pubkey(const uint32_t* d_sk, uint8_t* d_out65, hipStream_t s) {
+  hipLaunchKernelGGL(bls_pubkey_kernel, dim3(1), dim3(64), 0, s, d_sk, d_out65);
   return hipGetLastError();
 }

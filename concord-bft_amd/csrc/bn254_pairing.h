@@ -198,8 +198,25 @@ BN_HD bool words_lt_p(const uint32_t* w) {  // w < p ?
   return false;
 }
 
+// The y "parity" of RELIC's compressed encodings: fp_get_bit(y, 0) on RELIC's raw Montgomery
+// digits (R = 2^256 for FP_PRIME = 254 on 64-bit digits), i.e. lsb(y * 2^256 mod p) — not lsb(y).
+// Pinned for G2 by the reference's RELIC-generated key files (tests/simpleKVBC/scripts/
+// set{A,B}_replica_*, 40/40 vks, tests/golden/relic_bls_keys.json); G1 (ep_write_bin) uses the
+// same fp_get_bit rule (oracle/bn254_ref.py relic_bit).  Our own Montgomery radix is 2^261, so
+// y * (2^256 mod p) is formed with one field multiplication and read back canonically.
+BN_HDN uint32_t f_relic_bit(const fp& y) {
+  const uint32_t r256[8] = {0xffffff8eu, 0x15ffffffu, 0xffffff8au, 0xb939ffffu,
+                            0xffffffcdu, 0xa2c62effu, 0x7ffffff5u, 0x212ba4f2u};
+  fp c, t;
+  f_from_words(c, r256);
+  f_mul(t, y, c);
+  uint32_t w[8];
+  f_to_words(w, t);
+  return w[0] & 1u;
+}
+
 // RELIC ep_read_bin(pack = 1) semantics as restated in oracle/bn254_ref.py: 33 bytes,
-// 0x00 || 0^32 = infinity; prefix 2|parity(y); x < p; x^3 + 2 must be a square.
+// 0x00 || 0^32 = infinity; prefix 2 | f_relic_bit(y); x < p; x^3 + 2 must be a square.
 BN_HDN bool g1_decompress(g1a& r, const uint8_t* b) {
   r.inf = false;
   if (b[0] == 0) {
@@ -222,9 +239,7 @@ BN_HDN bool g1_decompress(g1a& r, const uint8_t* b) {
   f_from_words(b2, two);
   f_add(rhs, rhs, b2);
   if (!fp_sqrt(r.y, rhs)) return false;
-  uint32_t yw[8];
-  f_to_words(yw, r.y);
-  if ((yw[0] & 1u) != (uint32_t)(b[0] & 1)) f_neg(r.y, r.y);
+  if (f_relic_bit(r.y) != (uint32_t)(b[0] & 1)) f_neg(r.y, r.y);
   return true;
 }
 
@@ -233,10 +248,9 @@ BN_HDN void g1_compress(uint8_t* out, const g1a& a) {
     for (int i = 0; i < 33; i++) out[i] = 0;
     return;
   }
-  uint32_t xw[8], yw[8];
+  uint32_t xw[8];
   f_to_words(xw, a.x);
-  f_to_words(yw, a.y);
-  out[0] = (uint8_t)(2 | (yw[0] & 1));
+  out[0] = (uint8_t)(2 | f_relic_bit(a.y));
   words_to_be32(out + 1, xw);
 }
 
@@ -407,7 +421,7 @@ BN_HDN bool g2_in_subgroup(const g2a& q) {  // r * Q == O
   return fp2_is_zero(acc.Z);
 }
 
-// RELIC ep2_read_bin(pack = 1) as restated: 65 bytes, prefix 2 | parity(y.a), x0 || x1 < p,
+// RELIC ep2_read_bin(pack = 1) as restated: 65 bytes, prefix 2 | f_relic_bit(y.a), x0 || x1 < p,
 // on E', and (CHECK) in the order-r subgroup.
 BN_HDN bool g2_decompress(g2a& r, const uint8_t* b) {
   r.inf = false;
@@ -429,9 +443,7 @@ BN_HDN bool g2_decompress(g2a& r, const uint8_t* b) {
   fp2_load(b2, Bn254Consts::B2);
   fp2_add(rhs, rhs, b2);
   if (!fp2_sqrt(r.y, rhs)) return false;
-  uint32_t yw[8];
-  f_to_words(yw, r.y.a);
-  if ((yw[0] & 1u) != (uint32_t)(b[0] & 1)) fp2_neg(r.y, r.y);
+  if (f_relic_bit(r.y.a) != (uint32_t)(b[0] & 1)) fp2_neg(r.y, r.y);
   return g2_in_subgroup(r);
 }
 
@@ -441,8 +453,7 @@ BN_HDN void g2_compress(uint8_t* out, const g2a& a) {
     return;
   }
   uint32_t w[8];
-  f_to_words(w, a.y.a);
-  out[0] = (uint8_t)(2 | (w[0] & 1));
+  out[0] = (uint8_t)(2 | f_relic_bit(a.y.a));
   f_to_words(w, a.x.a);
   words_to_be32(out + 1, w);
   f_to_words(w, a.x.b);

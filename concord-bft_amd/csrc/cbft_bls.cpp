@@ -309,12 +309,32 @@ int cbft_bls_verify_multisig_partials(cbft_ctx* c, const uint8_t* msg, uint32_t 
   return bls_verify_with_lines(c, sig33, c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), out_ok);
 }
 
-int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* msg, uint32_t len, uint8_t* out37) {
-  if (!c || !sk32 || !out37 || (len && !msg)) return CBFT_EINVAL;
-  uint32_t w[8];
+// 32-byte big-endian scalar -> 8 little-endian words
+static void be32_scalar_words(uint32_t* w, const uint8_t* sk32) {
   for (int q = 0; q < 8; q++)
     w[q] = ((uint32_t)sk32[31 - 4 * q - 3] << 24) | ((uint32_t)sk32[31 - 4 * q - 2] << 16) |
            ((uint32_t)sk32[31 - 4 * q - 1] << 8) | sk32[31 - 4 * q];
+}
+
+int cbft_bls_public_key(cbft_ctx* c, const uint8_t* sk32, uint8_t* out65) {
+  if (!c || !sk32 || !out65) return CBFT_EINVAL;
+  uint32_t w[8];
+  be32_scalar_words(w, sk32);
+  std::lock_guard<std::mutex> g(c->mu);
+  CBFT_HIP(hipSetDevice(c->device));
+  CBFT_HIP(c->bls_lambda.reserve(8 * 4));
+  CBFT_HIP(c->bls_out.reserve(65));
+  CBFT_HIP(hipMemcpyAsync(c->bls_lambda.p, w, sizeof(w), hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_pubkey(c->bls_lambda.as<uint32_t>(), c->bls_out.as<uint8_t>(), c->stream));
+  CBFT_HIP(hipMemcpyAsync(out65, c->bls_out.p, 65, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  return CBFT_OK;
+}
+
+int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* msg, uint32_t len, uint8_t* out37) {
+  if (!c || !sk32 || !out37 || (len && !msg)) return CBFT_EINVAL;
+  uint32_t w[8];
+  be32_scalar_words(w, sk32);
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
   CBFT_HIP(c->bls_msg.reserve(len + 1));

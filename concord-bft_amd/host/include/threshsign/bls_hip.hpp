@@ -17,8 +17,8 @@
 //
 // Key encodings: PK and vk_i are 65-byte compressed G2 points as hex strings (130 characters,
 // ThresholdSignaturesTypes.cpp:220-228); share secret keys are decimal strings
-// (BlsSecretKey.h:37, BNT::toString base 10).  Encoding parity with RELIC is unpinned
-// (SURVEY.md §8(c)).
+// (BlsSecretKey.h:37, BNT::toString base 10).  The G2/G1 encodings are RELIC's (Montgomery-form
+// y parity), pinned by the reference's own key files (tests/golden/relic_bls_keys.json).
 #pragma once
 
 #include <array>
@@ -142,7 +142,9 @@ class BlsMultisigAccumulator : public BlsAccumulatorBase {
 
 class BlsThresholdSigner : public IThresholdSigner {
  public:
-  BlsThresholdSigner(ShareID id, const std::string& secretKeyDecimal, const std::string& vkHex);
+  // vkHex empty: the verification key is derived from the secret key on the GPU (sk * g2), as
+  // the reference's constructor does (BlsThresholdSigner.cpp:25)
+  BlsThresholdSigner(ShareID id, const std::string& secretKeyDecimal, const std::string& vkHex = "");
   int requiredLengthForSignedData() const override { return 37; }
   // outSig = 4-byte big-endian id || sk * H(hash); throws std::runtime_error if outSigLen < 37
   void signData(const char* hash, int hashLen, char* outSig, int outSigLen) override;

@@ -323,6 +323,11 @@ BlsThresholdSigner::BlsThresholdSigner(ShareID id, const std::string& secretKeyD
     : id_(id), sk_(secretKeyDecimal), vk_(vkHex.empty() ? BlsPublicKey() : BlsPublicKey(vkHex)) {
   if (id < 1 || id > MAX_NUM_OF_SHARES) throw std::invalid_argument("BLS signer: id out of range");
   engine_ = BlsEngine::get();
+  if (vkHex.empty()) {  // the reference derives it: publicKey_(secretKey) = sk * g2 (BlsThresholdSigner.cpp:25)
+    uint8_t vk65[65];
+    check(cbft_bls_public_key(engine_->ctx(), sk_.bytes().data(), vk65), "cbft_bls_public_key");
+    vk_ = BlsPublicKey(toHex(vk65, 65));
+  }
 }
 
 void BlsThresholdSigner::signData(const char* hash, int hashLen, char* outSig, int outSigLen) {

@@ -158,8 +158,12 @@ int cbft_rsa_kernel_ms(cbft_ctx* ctx, float* out_ms);
  * RELIC "BN_P254" curve (threshsign/src/bls/relic/Library.cpp:51,72): G1 compressed = 33 bytes,
  * G2 compressed = 65 bytes, share = 4-byte big-endian id || 33-byte G1 (BlsThresholdSigner.cpp:
  * 32-47), signer bitmap = 256 bytes, bit (id-1) LSB-first (VectorOfShares.cpp:136-161).
- * Encodings and hash-to-G1 follow RELIC as restated in oracle/bn254_ref.py (parity with RELIC
- * itself is unpinned: RELIC is not available offline). */
+ * Compressed encodings are RELIC's ep_write_bin / ep2_write_bin (pack = 1): prefix byte
+ * 2 | lsb(y * 2^256 mod p) — the parity bit of RELIC's Montgomery-form y (of y's real part in G2) —
+ * then x big-endian (G2: x0 || x1).  The G2 rule is pinned by the reference's RELIC-generated key
+ * files (tests/golden/relic_bls_keys.json, 40/40 vks); G1 uses the same RELIC fp_get_bit rule.
+ * Hash-to-G1 follows RELIC's 2019 ep_map as restated in oracle/bn254_ref.py (SHA-256,
+ * try-and-increment; parity with RELIC itself is unpinned there). */
 #define CBFT_BLS_G1_BYTES 33
 #define CBFT_BLS_G2_BYTES 65
 #define CBFT_BLS_SHARE_BYTES 37
@@ -220,6 +224,10 @@ int cbft_bls_sum_keys_partial(cbft_ctx* ctx, uint32_t keyset, const uint8_t* sig
                               uint32_t hi_id, uint8_t* out_partial);
 int cbft_bls_verify_multisig_partials(cbft_ctx* ctx, const uint8_t* msg, uint32_t len, const uint8_t* sig33,
                                       const uint8_t* key_partials, uint32_t count, int* out_ok);
+
+/* The signer's public (share verification) key: out65 = sk * g2 compressed, sk = 32 bytes
+ * big-endian (< r) (BlsThresholdSigner's publicKey_, IThresholdSigner::getShareVerificationKey). */
+int cbft_bls_public_key(cbft_ctx* ctx, const uint8_t* sk32, uint8_t* out65);
 
 /* Sign a share: out37 = 4-byte big-endian id || sk * g1_map(msg) compressed, sk = 32 bytes
  * big-endian (< r) (IThresholdSigner::signData; BlsThresholdSigner.cpp:32-47). */

@@ -4,8 +4,9 @@
 //                                   threshold and multisig schemes
 //   TestBlsBatchVerifier.cpp:42-106 a bad share is detected and reported by id
 //   ThresholdAccumulatorBase.cpp    pending/valid/invalid bookkeeping, digest immutability
-// Key sets and expected combined signatures: tests/golden/bls_sets.txt (gen_bls_fixtures.py,
-// from the Python oracle).
+// Key sets and expected combined signatures: tests/golden/bls_sets.txt (gen_bls_fixtures.py): the
+// reference's RELIC-generated cryptosystems (set{A,B}_replica_* key files) first, then larger
+// oracle-generated sets.
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -29,6 +30,7 @@ using namespace BLS::Hip;
 
 struct KeySet {
   int n = 0, k = 0;
+  bool multisig = false;  // independent keys, PK = sum of vks (no Lagrange combination)
   std::string sk, pk, msgHex, sigHex;
   std::vector<std::string> vk, ski;
 };
@@ -60,6 +62,10 @@ static std::vector<KeySet> load(const std::string& path) {
     if (tag == "set") {
       cur = KeySet();
       is >> cur.n >> cur.k;
+    } else if (tag == "scheme") {
+      std::string v;
+      is >> v;
+      cur.multisig = v == "multisig";
     } else if (tag == "sk") {
       is >> cur.sk;
     } else if (tag == "pk") {
@@ -100,6 +106,10 @@ static int testThreshold(const KeySet& ks) {
   CHECK(v.requiredLengthForSignedData() == 33);
   CHECK(v.getPublicKey().toString() == ks.pk);
   CHECK(v.getShareVerificationKey(1).toString() == ks.vk[0]);
+  {  // the signer derives its verification key on the GPU: sk_i * g2 == the fixture's vk_i
+    BlsThresholdSigner s(2, ks.ski[1]);
+    CHECK(s.getShareVerificationKey().toString() == ks.vk[1]);
+  }
 
   // signer output: 4-byte big-endian id || 33-byte point
   std::string s3 = share(ks, 3, msg);
@@ -228,13 +238,34 @@ static int testMultisig(const KeySet& ks) {
   return 0;
 }
 
+// A RELIC multisig cryptosystem (independent keys): the n-of-n verifier's key is the sum of the
+// vks and must equal the file's group key; the n-share aggregate equals group_sk * H(m) and
+// verifies under that key (BlsMultisigVerifier.cpp:33-38,75-105).
+static int testMultisigKeys(const KeySet& ks) {
+  const auto msg = unhex(ks.msgHex);
+  BlsMultisigVerifier v(ks.n, ks.n, ks.vk);
+  CHECK(v.getPublicKey().toString() == ks.pk);
+  std::unique_ptr<IThresholdAccumulator> acc(v.newAccumulator(true));
+  acc->setExpectedDigest(msg.data(), (int)msg.size());
+  for (int id = 1; id <= ks.n; id++) {
+    std::string sh = share(ks, id, msg);
+    CHECK(acc->add(sh.data(), (int)sh.size()) == id);
+  }
+  std::string sig(33, '\0');
+  acc->getFullSignedData(&sig[0], 33);
+  CHECK(hex(sig.data(), 33) == ks.sigHex);
+  CHECK(v.verify(reinterpret_cast<const char*>(msg.data()), (int)msg.size(), sig.data(), 33));
+  return 0;
+}
+
 int main(int argc, char** argv) {
   const std::string path = argc > 1 ? argv[1] : "tests/golden/bls_sets.txt";
   auto sets = load(path);
   CHECK(sets.size() >= 4);
   for (const auto& ks : sets) {
-    std::printf("set n=%d k=%d\n", ks.n, ks.k);
-    if (testThreshold(ks)) return 1;
+    std::printf("set n=%d k=%d %s\n", ks.n, ks.k, ks.multisig ? "multisig" : "threshold");
+    if (!ks.multisig && testThreshold(ks)) return 1;
+    if (ks.multisig && testMultisigKeys(ks)) return 1;
     if (testMultisig(ks)) return 1;
   }
   // key parsing errors throw
