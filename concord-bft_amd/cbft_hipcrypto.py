@@ -31,7 +31,23 @@ ABI = [
     ("cbft_strerror", ctypes.c_char_p, [ctypes.c_int]),
     ("cbft_last_error", ctypes.c_char_p, []),
     ("cbft_open", ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_size_t]),
+    ("cbft_open_mask", ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_uint32, ctypes.c_size_t]),
+    ("cbft_open_devices", ctypes.c_int,
+     [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_size_t]),
+    ("cbft_device_of", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ("cbft_close", None, [ctypes.c_void_p]),
+    ("cbft_host_alloc", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    ("cbft_host_free", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
+    ("cbft_ed25519_verify_batch_async", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    ("cbft_ed25519_verify_fixed_async", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32,
+      ctypes.c_size_t, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]),
+    ("cbft_wait", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint64]),
+    ("cbft_ed25519_batch_layout", ctypes.c_int,
+     [ctypes.c_size_t, ctypes.c_uint32, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t),
+      ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]),
     ("cbft_ed25519_load_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, _u32p]),
     ("cbft_ed25519_load_keys_ex", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, _u32p]),
@@ -145,11 +161,77 @@ def _ptr(a: np.ndarray):
 class Context:
     """One GPU context (cbft_open / cbft_close)."""
 
-    def __init__(self, device: int = 0, max_batch: int = 0):
+    def __init__(self, device: int = 0, max_batch: int = 0, device_mask: int = 0,
+                 devices: Optional[Sequence[int]] = None):
+        """device_mask != 0: one context over every GPU in the mask (cbft_open_mask); devices: an
+        explicit shard list, repeats allowed (cbft_open_devices)."""
         self.lib = load_library()
         self.handle = ctypes.c_void_p()
-        _check(self.lib.cbft_open(ctypes.byref(self.handle), device, max_batch), f"cbft_open(device={device})")
+        if devices:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            _check(self.lib.cbft_open_devices(ctypes.byref(self.handle), arr, len(devices), max_batch),
+                   f"cbft_open_devices({list(devices)})")
+            device = devices[0]
+        elif device_mask:
+            _check(self.lib.cbft_open_mask(ctypes.byref(self.handle), device_mask, max_batch),
+                   f"cbft_open_mask({device_mask:#x})")
+            device = (device_mask & -device_mask).bit_length() - 1
+        else:
+            _check(self.lib.cbft_open(ctypes.byref(self.handle), device, max_batch), f"cbft_open(device={device})")
         self.device = device
+
+    def devices(self) -> List[int]:
+        out = (ctypes.c_int * 32)()
+        n = self.lib.cbft_device_of(self.handle, out, 32)
+        if n < 0:
+            raise CbftError(n, "cbft_device_of")
+        return list(out[:n])
+
+    # ------------------------------------------------------------------ pinned host memory
+    def host_alloc(self, nbytes: int) -> np.ndarray:
+        """A uint8 numpy view of cbft_host_alloc memory (free with host_free(view))."""
+        p = ctypes.c_void_p()
+        _check(self.lib.cbft_host_alloc(self.handle, nbytes, ctypes.byref(p)), "cbft_host_alloc")
+        buf = (ctypes.c_uint8 * nbytes).from_address(p.value)
+        return np.frombuffer(buf, dtype=np.uint8)
+
+    def host_free(self, view: np.ndarray):
+        _check(self.lib.cbft_host_free(self.handle, ctypes.c_void_p(view.ctypes.data)), "cbft_host_free")
+
+    # ------------------------------------------------------------------ async host-buffer verify
+    def verify_async(self, tid: int, key_idx: np.ndarray, sigs: np.ndarray, blob: np.ndarray, out: np.ndarray,
+                     offs: Optional[np.ndarray] = None, lens: Optional[np.ndarray] = None,
+                     msg_len: Optional[int] = None, n: Optional[int] = None) -> int:
+        """Queue a batch; returns the ticket.  Either (offs, lens) or a fixed msg_len.  `out`
+        (uint8, >= ceil(n/8)) receives the bitmap by the time wait(ticket) returns; inputs and
+        out must stay alive until then."""
+        t = ctypes.c_uint64()
+        if msg_len is not None:
+            n = int(key_idx.shape[0]) if n is None else n
+            _check(self.lib.cbft_ed25519_verify_fixed_async(self.handle, tid, _ptr(key_idx), _ptr(sigs), _ptr(blob),
+                                                            msg_len, n, _ptr(out), ctypes.byref(t)),
+                   "cbft_ed25519_verify_fixed_async")
+        else:
+            n = int(lens.shape[0]) if n is None else n
+            _check(self.lib.cbft_ed25519_verify_batch_async(self.handle, tid, _ptr(key_idx), _ptr(sigs), _ptr(blob),
+                                                            _ptr(offs), _ptr(lens), n, _ptr(out), ctypes.byref(t)),
+                   "cbft_ed25519_verify_batch_async")
+        return t.value
+
+    def batch_views(self, n: int, msg_len: int):
+        """One pinned block laid out as cbft_ed25519_batch_layout says: returns (block, key_idx
+        u32[n], sig u8[n, 64], msgs u8[n * msg_len]) views; fill them and submit with
+        verify_async(..., msg_len=msg_len) for a single-DMA batch.  Free with host_free(block)."""
+        o = [ctypes.c_size_t() for _ in range(4)]
+        _check(self.lib.cbft_ed25519_batch_layout(n, msg_len, *[ctypes.byref(x) for x in o]),
+               "cbft_ed25519_batch_layout")
+        ok, osig, omsg, total = (x.value for x in o)
+        blk = self.host_alloc(total)
+        return (blk, blk[ok:ok + 4 * n].view(np.uint32), blk[osig:osig + 64 * n].reshape(n, 64),
+                blk[omsg:omsg + n * msg_len])
+
+    def wait(self, ticket: int):
+        _check(self.lib.cbft_wait(self.handle, ticket), "cbft_wait")
 
     def close(self):
         if self.handle:

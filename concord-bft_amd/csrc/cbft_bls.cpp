@@ -40,6 +40,7 @@ static BlsKeySet* find_set(cbft_ctx* c, uint32_t id) {
 extern "C" {
 
 int cbft_bls_load_keys(cbft_ctx* c, const uint8_t* pk65, const uint8_t* vks65, uint32_t n, uint32_t* out_id) {
+  c = cbft_dev0(c);
   if (!c || !pk65 || !out_id || (n && !vks65) || n > BLS_MAX_SHARES) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
@@ -65,6 +66,7 @@ int cbft_bls_load_keys(cbft_ctx* c, const uint8_t* pk65, const uint8_t* vks65, u
 }
 
 int cbft_bls_unload_keys(cbft_ctx* c, uint32_t id) {
+  c = cbft_dev0(c);
   if (!c) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   BlsKeySet* ks = find_set(c, id);
@@ -80,6 +82,7 @@ int cbft_bls_unload_keys(cbft_ctx* c, uint32_t id) {
 }
 
 int cbft_bls_key_status(cbft_ctx* c, uint32_t id, uint8_t* out_ok) {
+  c = cbft_dev0(c);
   if (!c || !out_ok) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   BlsKeySet* ks = find_set(c, id);
@@ -90,6 +93,7 @@ int cbft_bls_key_status(cbft_ctx* c, uint32_t id, uint8_t* out_ok) {
 }
 
 int cbft_bls_hash_to_g1(cbft_ctx* c, const uint8_t* msg, uint32_t len, uint8_t* out33) {
+  c = cbft_dev0(c);
   if (!c || !out33 || (len && !msg)) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
@@ -127,6 +131,7 @@ static int bls_shares(cbft_ctx* c, BlsKeySet* ks, const uint8_t* shares37, uint3
 
 int cbft_bls_verify_shares(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, const uint8_t* shares37,
                            uint32_t k, uint8_t* valid_bitmap) {
+  c = cbft_dev0(c);
   if (!c || (k && (!shares37 || !valid_bitmap)) || (len && !msg) || k > BLS_MAX_SHARES) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   BlsKeySet* ks = find_set(c, id);
@@ -184,17 +189,20 @@ static int bls_combine_range(cbft_ctx* c, const uint8_t* shares37, uint32_t k, u
 }
 
 int cbft_bls_combine(cbft_ctx* c, const uint8_t* shares37, uint32_t k, int multisig, uint8_t* out33) {
+  c = cbft_dev0(c);
   if (!c || !out33 || !k || !shares37 || k > BLS_MAX_SHARES) return CBFT_EINVAL;
   return bls_combine_range(c, shares37, k, 0, k, multisig, out33, nullptr);
 }
 
 int cbft_bls_combine_partial(cbft_ctx* c, const uint8_t* shares37, uint32_t k, uint32_t lo, uint32_t hi, int multisig,
                              uint8_t* out_partial) {
+  c = cbft_dev0(c);
   if (!c || !out_partial || !k || !shares37 || k > BLS_MAX_SHARES || lo > hi || hi > k) return CBFT_EINVAL;
   return bls_combine_range(c, shares37, k, lo, hi, multisig, nullptr, out_partial);
 }
 
 int cbft_bls_combine_finish(cbft_ctx* c, const uint8_t* partials, uint32_t count, uint8_t* out33) {
+  c = cbft_dev0(c);
   if (!c || !out33 || !count || !partials) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
@@ -223,6 +231,7 @@ static int bls_verify_with_lines(cbft_ctx* c, const uint8_t* sig33, const uint32
 }
 
 int cbft_bls_verify(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, const uint8_t* sig33, int* out_ok) {
+  c = cbft_dev0(c);
   if (!c || !sig33 || !out_ok || (len && !msg)) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   BlsKeySet* ks = find_set(c, id);
@@ -236,6 +245,7 @@ int cbft_bls_verify(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, 
 
 int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, const uint8_t* sig33,
                              const uint8_t* signers256, int* out_ok) {
+  c = cbft_dev0(c);
   if (!c || !sig33 || !signers256 || !out_ok || (len && !msg)) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   BlsKeySet* ks = find_set(c, id);
@@ -255,6 +265,7 @@ int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint3
 }
 
 int cbft_bls_sum_keys(cbft_ctx* c, uint32_t id, const uint8_t* signers256, uint8_t* out65) {
+  c = cbft_dev0(c);
   if (!c || !signers256 || !out65) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   BlsKeySet* ks = find_set(c, id);
@@ -274,6 +285,7 @@ int cbft_bls_sum_keys(cbft_ctx* c, uint32_t id, const uint8_t* signers256, uint8
 
 int cbft_bls_sum_keys_partial(cbft_ctx* c, uint32_t id, const uint8_t* signers256, uint32_t lo_id, uint32_t hi_id,
                               uint8_t* out_partial) {
+  c = cbft_dev0(c);
   if (!c || !signers256 || !out_partial || lo_id > hi_id) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   BlsKeySet* ks = find_set(c, id);
@@ -293,6 +305,7 @@ int cbft_bls_sum_keys_partial(cbft_ctx* c, uint32_t id, const uint8_t* signers25
 
 int cbft_bls_verify_multisig_partials(cbft_ctx* c, const uint8_t* msg, uint32_t len, const uint8_t* sig33,
                                       const uint8_t* key_partials, uint32_t count, int* out_ok) {
+  c = cbft_dev0(c);
   if (!c || !sig33 || !key_partials || !count || !out_ok || (len && !msg)) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
@@ -317,6 +330,7 @@ static void be32_scalar_words(uint32_t* w, const uint8_t* sk32) {
 }
 
 int cbft_bls_public_key(cbft_ctx* c, const uint8_t* sk32, uint8_t* out65) {
+  c = cbft_dev0(c);
   if (!c || !sk32 || !out65) return CBFT_EINVAL;
   uint32_t w[8];
   be32_scalar_words(w, sk32);
@@ -332,6 +346,7 @@ int cbft_bls_public_key(cbft_ctx* c, const uint8_t* sk32, uint8_t* out65) {
 }
 
 int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* msg, uint32_t len, uint8_t* out37) {
+  c = cbft_dev0(c);
   if (!c || !sk32 || !out37 || (len && !msg)) return CBFT_EINVAL;
   uint32_t w[8];
   be32_scalar_words(w, sk32);

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <new>
 #include <unordered_map>
@@ -68,6 +69,11 @@ static hipError_t build_comb(const uint8_t* d_pk, size_t nunits, int negate, con
   tmp.release();
   return e;
 }
+
+static int collect_locked(HostSlot& s);
+
+// A multi-GPU context runs BLS, RSA and profiling calls on its first device.
+cbft_ctx* cbft_dev0(cbft_ctx* c) { return (c && !c->kids.empty()) ? c->kids[0] : c; }
 
 #define CBFT_PROF_RING 256  // batches whose stage events profiling mode 2 keeps
 
@@ -137,7 +143,10 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
       rc = CBFT_ENODEV;
       break;
     }
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->compute[0], hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->compute[1], hipStreamNonBlocking) != hipSuccess) {
       rc = CBFT_EIO;
       break;
     }
@@ -180,10 +189,63 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   return CBFT_OK;
 }
 
+int cbft_open_devices(cbft_ctx** out, const int* devices, int ndevices, size_t max_batch) {
+  if (!out || !devices || ndevices < 1 || ndevices > 64) return CBFT_EINVAL;
+  *out = nullptr;
+  const int ndev = cbft_device_count();
+  if (ndev < 0) return ndev;
+  for (int i = 0; i < ndevices; i++)
+    if (devices[i] < 0 || devices[i] >= ndev) return CBFT_ENODEV;
+  if (ndevices == 1) return cbft_open(out, devices[0], max_batch);
+  const std::vector<int> devs(devices, devices + ndevices);
+  cbft_ctx* g = new (std::nothrow) cbft_ctx();
+  if (!g) return CBFT_ENOMEM;
+  g->device = devs[0];
+  const size_t per = max_batch ? (max_batch + devs.size() - 1) / devs.size() + 64 : 0;
+  for (int d : devs) {
+    cbft_ctx* k = nullptr;
+    const int rc = cbft_open(&k, d, per);
+    if (rc) {
+      cbft_close(g);
+      return rc;
+    }
+    g->kids.push_back(k);
+  }
+  *out = g;
+  return CBFT_OK;
+}
+
+int cbft_open_mask(cbft_ctx** out, uint32_t device_mask, size_t max_batch) {
+  if (!out || !device_mask) return CBFT_EINVAL;
+  int devs[32];
+  int nd = 0;
+  for (int d = 0; d < 32; d++)
+    if ((device_mask >> d) & 1u) devs[nd++] = d;
+  return cbft_open_devices(out, devs, nd, max_batch);
+}
+
+int cbft_device_of(cbft_ctx* c, int* out_devices, int max_out) {
+  if (!c) return CBFT_EINVAL;
+  const int n = c->kids.empty() ? 1 : (int)c->kids.size();
+  for (int i = 0; i < n && i < max_out && out_devices; i++)
+    out_devices[i] = c->kids.empty() ? c->device : c->kids[(size_t)i]->device;
+  return n;
+}
+
 void cbft_close(cbft_ctx* c) {
   if (!c) return;
+  if (!c->kids.empty()) {
+    for (cbft_ctx* k : c->kids) cbft_close(k);
+    delete c;
+    return;
+  }
   (void)hipSetDevice(c->device);
-  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (HostSlot& hs : c->hslots) {
+    std::lock_guard<std::mutex> g(hs.m);
+    (void)collect_locked(hs);
+  }
+  for (hipStream_t st : {c->stream, c->copy_stream, c->compute[0], c->compute[1]})
+    if (st) (void)hipStreamSynchronize(st);
   for (auto& kv : c->tables) {
     kv.second.pk.release();
     kv.second.comb.release();
@@ -218,11 +280,20 @@ void cbft_close(cbft_ctx* c) {
   for (DevBuf* b : {&c->rsa_scratch, &c->rsa_sig, &c->rsa_kidx}) b->release();
   for (hipEvent_t e : {c->rsa_done, c->rsa_ev[0], c->rsa_ev[1]})
     if (e) (void)hipEventDestroy(e);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  for (HostSlot& hs : c->hslots) {
+    for (DevBuf* b : {&hs.in, &hs.verd}) b->release();
+    hs.pack.release();
+    hs.hverd.release();
+    for (hipEvent_t e : {hs.copied, hs.done})
+      if (e) (void)hipEventDestroy(e);
+  }
+  for (hipStream_t st : {c->stream, c->copy_stream, c->compute[0], c->compute[1]})
+    if (st) (void)hipStreamDestroy(st);
   delete c;
 }
 
 int cbft_set_profiling(cbft_ctx* c, int enable) {
+  c = cbft_dev0(c);
   if (!c) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
@@ -241,6 +312,7 @@ int cbft_set_profiling(cbft_ctx* c, int enable) {
 }
 
 int cbft_stage_times_avg_ms(cbft_ctx* c, float* out, int nout, int* nbatches) {
+  c = cbft_dev0(c);
   if (!c || !out || nout < 3) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   if (c->prof_mode != 2 || c->ring_n == 0) return CBFT_EINVAL;
@@ -262,6 +334,7 @@ int cbft_stage_times_avg_ms(cbft_ctx* c, float* out, int nout, int* nbatches) {
 }
 
 int cbft_stage_times_ms(cbft_ctx* c, float* out, int nout) {
+  c = cbft_dev0(c);
   if (!c || !out || nout < 3) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->ev_valid) return CBFT_EINVAL;
@@ -273,14 +346,31 @@ int cbft_stage_times_ms(cbft_ctx* c, float* out, int nout) {
 
 int cbft_sync(cbft_ctx* c) {
   if (!c) return CBFT_EINVAL;
+  for (cbft_ctx* k : c->kids) {
+    const int rc = cbft_sync(k);
+    if (rc) return rc;
+  }
+  if (!c->kids.empty()) return CBFT_OK;
   (void)hipSetDevice(c->device);
-  CBFT_HIP(hipStreamSynchronize(c->stream));
+  for (hipStream_t st : {c->stream, c->copy_stream, c->compute[0], c->compute[1]}) CBFT_HIP(hipStreamSynchronize(st));
   return CBFT_OK;
 }
 
 int cbft_ed25519_load_keys_ex(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, int comb_radix, uint32_t* out_id) {
   if (!c || !out_id || (nkeys && !pk)) return CBFT_EINVAL;
   if (comb_radix && (comb_radix < 8 || comb_radix > 13)) return CBFT_EINVAL;
+  if (!c->kids.empty()) {  // replicate the table on every device (the children's ids stay in step)
+    uint32_t id0 = 0;
+    for (size_t k = 0; k < c->kids.size(); k++) {
+      uint32_t id = 0;
+      const int rc = cbft_ed25519_load_keys_ex(c->kids[k], pk, nkeys, comb_radix, &id);
+      if (rc) return rc;
+      if (k == 0) id0 = id;
+      if (id != id0) return CBFT_EIO;
+    }
+    *out_id = id0;
+    return CBFT_OK;
+  }
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
   KeyTable kt;
@@ -313,6 +403,14 @@ int cbft_ed25519_load_keys(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, uint3
 
 int cbft_ed25519_unload_keys(cbft_ctx* c, uint32_t id) {
   if (!c) return CBFT_EINVAL;
+  if (!c->kids.empty()) {
+    int rc = CBFT_OK;
+    for (cbft_ctx* k : c->kids) {
+      const int r = cbft_ed25519_unload_keys(k, id);
+      if (r && !rc) rc = r;
+    }
+    return rc;
+  }
   std::lock_guard<std::mutex> g(c->mu);
   auto it = c->tables.find(id);
   if (it == c->tables.end()) return CBFT_EINVAL;
@@ -328,7 +426,7 @@ int cbft_ed25519_unload_keys(cbft_ctx* c, uint32_t id) {
 // Launch the verify pipeline for a batch whose inputs are already on the device.
 static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, const uint32_t* d_kidx,
                          const uint8_t* d_sig, const uint8_t* d_msg, const uint64_t* d_off, const uint32_t* d_len,
-                         size_t n, uint64_t* d_verdicts, hipStream_t s) {
+                         uint32_t fixed_len, size_t n, uint64_t* d_verdicts, hipStream_t s) {
   int rc = reserve_work(c, n);
   if (rc) return rc;
   auto it = c->tables.end();
@@ -344,7 +442,8 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   // the slot's previous batch (maybe on another stream) must be done with its buffers
   if (slot.used) CBFT_HIP(hipStreamWaitEvent(s, slot.done, 0));
 
-  Ed25519Batch b{n, d_pk, d_kidx, d_sig, d_msg, d_off, d_len};
+  Ed25519Batch b{n, d_pk, d_kidx, d_sig, d_msg, d_off, d_len,
+                 table_id == CBFT_NO_KEY_TABLE ? (uint32_t)n : it->second.nkeys, fixed_len};
   Ed25519Work w{};
   // one inversion per K signatures per lane only where the batch keeps >= 64 finish waves; a
   // small (latency-bound) batch inverts per signature.  K = 16 at the 64K headline: the finish is
@@ -388,105 +487,319 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   return CBFT_OK;
 }
 
-// host-buffer batches up to this size go through the packed pinned staging image
-#define CBFT_STAGE_MAX_N 8192
+// ---------------------------------------------------------------- pinned host memory
+// Registry of cbft_host_alloc blocks (process-wide, so a multi-GPU context's children see the
+// blocks allocated through the group).  Host-buffer entry points DMA any input that lies inside
+// one of them straight to the device; other inputs are packed into a pinned image first.
+static std::mutex g_pin_mu;
+static std::map<uintptr_t, size_t> g_pinned;  // base -> bytes
 
-static int verify_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const uint32_t* key_idx,
-                       const uint8_t* sig, const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len,
-                       size_t n, uint8_t* bitmap) {
-  if (!c || (n && (!sig || !msg_off || !msg_len || !bitmap))) return CBFT_EINVAL;
-  if (n == 0) return CBFT_OK;
+static bool is_pinned(const void* p, size_t bytes) {
+  if (!p || !bytes) return false;
+  std::lock_guard<std::mutex> g(g_pin_mu);
+  auto it = g_pinned.upper_bound((uintptr_t)p);
+  if (it == g_pinned.begin()) return false;
+  --it;
+  return (uintptr_t)p + bytes <= it->first + it->second;
+}
+
+static inline size_t up256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+#define CBFT_PACK_MAX (4u << 20)  // pageable bytes of one batch packed into pinned staging
+
+// Device image of one host-buffer batch: [key idx | keys][sig][off][len][messages], 256-B aligned
+// parts (no off/len for fixed-length batches).
+struct BatchLayout {
+  size_t key, sig, off, len, msg;
+};
+static void batch_layout(size_t n, bool key_table, bool fixed, BatchLayout& l) {
+  l.key = 0;
+  l.sig = up256(l.key + (key_table ? n * 4 : n * 32));
+  l.off = up256(l.sig + n * 64);
+  l.len = up256(l.off + (fixed ? 0 : n * 8));
+  l.msg = up256(l.len + (fixed ? 0 : n * 4));
+}
+
+// Deliver a slot's verdicts to its batch's bitmap, waiting for the batch.  Caller holds s.m.
+static int collect_locked(HostSlot& s) {
+  if (!s.pending) return s.status;
+  s.pending = false;
+  hipError_t e = hipEventSynchronize(s.done);
+  if (e != hipSuccess) return s.status = cbft_fail(e, "hipEventSynchronize(batch done)", __FILE__, __LINE__);
+  const size_t nbytes = (s.n + 7) / 8;
+  std::memcpy(s.bitmap, s.hverd.p, nbytes);  // little-endian host: verdict words == bitmap bytes
+  if (s.n % 8) s.bitmap[nbytes - 1] &= (uint8_t)((1u << (s.n % 8)) - 1);
+  return s.status = CBFT_OK;
+}
+
+// Queue one host-buffer batch: H2D on the copy stream (pinned inputs DMA'd directly, pageable
+// ones packed into the slot's pinned image and moved with one DMA), the verify pipeline on one of
+// the two compute streams after the copy, the verdict words D2H into pinned memory.  Returns
+// once queued; cbft_wait (or a later submission that needs the slot) delivers the bitmap.
+// fixed_len: msg_off/msg_len are unused, message i = msg_blob[i * fixed_len, ...).
+static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const uint32_t* key_idx, const uint8_t* sig,
+                       const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len, bool fixed,
+                       uint32_t fixed_len, size_t n, uint8_t* bitmap, uint64_t* ticket) {
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
-  // message blob extent
-  uint64_t blob = 0;
-  for (size_t i = 0; i < n; i++) blob = std::max<uint64_t>(blob, msg_off[i] + msg_len[i]);
-  if (blob && !msg_blob) return CBFT_EINVAL;
-  if (table_id != CBFT_NO_KEY_TABLE) {
+  const bool kt = table_id != CBFT_NO_KEY_TABLE;
+  uint32_t nkeys = 0;
+  if (kt) {
     auto it = c->tables.find(table_id);
     if (it == c->tables.end() || !key_idx) return CBFT_EINVAL;
+    nkeys = it->second.nkeys;
     for (size_t i = 0; i < n; i++)
-      if (key_idx[i] >= it->second.nkeys) return CBFT_EINVAL;
+      if (key_idx[i] >= nkeys) return CBFT_EINVAL;
   } else if (!pk) {
     return CBFT_EINVAL;
   }
-  // size the work buffers first: the verdict buffer's address is taken below
-  int rc0 = reserve_work(c, n);
-  if (rc0) return rc0;
-  const size_t nw = (n + 63) / 64;
-  const bool kt = table_id != CBFT_NO_KEY_TABLE;
-  const uint64_t* hv = nullptr;
-  if (n <= CBFT_STAGE_MAX_N) {
-    // small (latency-bound) batch: one packed image [key idx | pk][sig][off][len][msg][verdict
-    // words], 256-B aligned parts, moved by one pinned H2D copy and one D2H for the verdicts
-    // (p50 at batch 1K 0.26 -> 0.24 ms).  Large batches keep the per-array pageable copies, which
-    // the runtime pipelines with its own staging (a serial host memcpy here would cost more).
-    auto up = [](size_t x) { return (x + 255) & ~(size_t)255; };
-    const size_t o_key = 0;
-    const size_t o_sig = up(o_key + (kt ? n * 4 : n * 32));
-    const size_t o_off = up(o_sig + n * 64);
-    const size_t o_len = up(o_off + n * 8);
-    const size_t o_msg = up(o_len + n * 4);
-    const size_t in_bytes = up(o_msg + blob + 16);
-    CBFT_HIP(c->hstage.reserve(in_bytes + nw * 8));
-    CBFT_HIP(c->dstage.reserve(in_bytes));
-    std::memcpy(c->hstage.as<uint8_t>(o_key), kt ? static_cast<const void*>(key_idx) : static_cast<const void*>(pk),
-                kt ? n * 4 : n * 32);
-    std::memcpy(c->hstage.as<uint8_t>(o_sig), sig, n * 64);
-    std::memcpy(c->hstage.as<uint8_t>(o_off), msg_off, n * 8);
-    std::memcpy(c->hstage.as<uint8_t>(o_len), msg_len, n * 4);
-    if (blob) std::memcpy(c->hstage.as<uint8_t>(o_msg), msg_blob, blob);
-    std::memset(c->hstage.as<uint8_t>(o_msg + blob), 0, 16);
-    CBFT_HIP(hipMemcpyAsync(c->dstage.p, c->hstage.p, o_msg + blob + 16, hipMemcpyHostToDevice, c->stream));
-    uint8_t* d = static_cast<uint8_t*>(c->dstage.p);
-    int rc = launch_locked(c, table_id, kt ? nullptr : d + o_key, kt ? reinterpret_cast<const uint32_t*>(d + o_key) : nullptr,
-                           d + o_sig, d + o_msg, reinterpret_cast<const uint64_t*>(d + o_off),
-                           reinterpret_cast<const uint32_t*>(d + o_len), n, c->verdicts.as<uint64_t>(), c->stream);
-    if (rc) return rc;
-    uint64_t* h = c->hstage.as<uint64_t>(in_bytes);
-    CBFT_HIP(hipMemcpyAsync(h, c->verdicts.p, nw * 8, hipMemcpyDeviceToHost, c->stream));
-    hv = h;
-  } else {
-    if (kt) {
-      CBFT_HIP(c->kidx.reserve(n * 4));
-      CBFT_HIP(hipMemcpyAsync(c->kidx.p, key_idx, n * 4, hipMemcpyHostToDevice, c->stream));
-    } else {
-      CBFT_HIP(c->pk.reserve(n * 32));
-      CBFT_HIP(hipMemcpyAsync(c->pk.p, pk, n * 32, hipMemcpyHostToDevice, c->stream));
+  // message bytes to move: [blo, bhi) of the blob (offsets need not start at 0)
+  uint64_t blo = 0, bhi = 0;
+  if (fixed) {
+    bhi = (uint64_t)fixed_len * n;
+  } else if (n) {
+    blo = UINT64_MAX;
+    for (size_t i = 0; i < n; i++) {
+      blo = std::min<uint64_t>(blo, msg_off[i]);
+      bhi = std::max<uint64_t>(bhi, msg_off[i] + msg_len[i]);
     }
-    CBFT_HIP(c->sig.reserve(n * 64));
-    CBFT_HIP(c->msg.reserve(blob + 16));
-    CBFT_HIP(c->off.reserve(n * 8));
-    CBFT_HIP(c->len.reserve(n * 4));
-    CBFT_HIP(hipMemcpyAsync(c->sig.p, sig, n * 64, hipMemcpyHostToDevice, c->stream));
-    if (blob) CBFT_HIP(hipMemcpyAsync(c->msg.p, msg_blob, blob, hipMemcpyHostToDevice, c->stream));
-    CBFT_HIP(hipMemcpyAsync(c->off.p, msg_off, n * 8, hipMemcpyHostToDevice, c->stream));
-    CBFT_HIP(hipMemcpyAsync(c->len.p, msg_len, n * 4, hipMemcpyHostToDevice, c->stream));
-    int rc = launch_locked(c, table_id, c->pk.as<uint8_t>(), c->kidx.as<uint32_t>(), c->sig.as<uint8_t>(),
-                           c->msg.as<uint8_t>(), c->off.as<uint64_t>(), c->len.as<uint32_t>(), n,
-                           c->verdicts.as<uint64_t>(), c->stream);
-    if (rc) return rc;
-    c->host_verdicts.resize(nw);
-    CBFT_HIP(hipMemcpyAsync(c->host_verdicts.data(), c->verdicts.p, nw * 8, hipMemcpyDeviceToHost, c->stream));
-    hv = c->host_verdicts.data();
   }
-  CBFT_HIP(hipStreamSynchronize(c->stream));
-  const size_t nbytes = (n + 7) / 8;
-  std::memcpy(bitmap, hv, nbytes);  // little-endian host: words == bytes
-  if (n % 8) bitmap[nbytes - 1] &= (uint8_t)((1u << (n % 8)) - 1);
+  const uint64_t blob = bhi - blo;
+  if (blob && !msg_blob) return CBFT_EINVAL;
+  int rc = reserve_work(c, n);
+  if (rc) return rc;
+  const uint64_t t = ++c->next_ticket;
+  HostSlot& s = c->hslots[t % CBFT_HOST_SLOTS];
+  std::lock_guard<std::mutex> sg(s.m);
+  rc = collect_locked(s);  // the slot's previous batch, if nobody has waited for it yet
+  if (rc) return rc;
+  const size_t nw = (n + 63) / 64;
+  BatchLayout lay;
+  batch_layout(n, kt, fixed, lay);
+  const size_t o_key = lay.key, o_sig = lay.sig, o_off = lay.off, o_len = lay.len, o_msg = lay.msg;
+  const size_t in_bytes = o_msg + blob + 16;
+  CBFT_HIP(s.in.reserve(in_bytes));
+  CBFT_HIP(s.verd.reserve(nw * 8));
+  CBFT_HIP(s.hverd.reserve(nw * 8));
+  if (!s.copied) CBFT_HIP(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
+  if (!s.done) CBFT_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  struct Part {
+    const void* src;
+    size_t bytes, off;
+  } parts[5] = {{kt ? static_cast<const void*>(key_idx) : static_cast<const void*>(pk), kt ? n * 4 : n * 32, o_key},
+                {sig, n * 64, o_sig},
+                {msg_off, fixed ? 0 : n * 8, o_off},
+                {msg_len, fixed ? 0 : n * 4, o_len},
+                {msg_blob ? msg_blob + blo : nullptr, (size_t)blob, o_msg}};
+  // pinned[k]: DMA straight from the caller's block.  Pageable parts of a small batch (total <=
+  // CBFT_PACK_MAX bytes: the latency path, p50 @ 1K) are packed into the slot's pinned image and
+  // moved by one DMA; larger pageable parts go through the runtime's own pipelined staging
+  // (hipMemcpyAsync from pageable memory), which beats a serial host memcpy into pinned memory.
+  bool pinned[5];
+  size_t pageable = 0;
+  for (int k = 0; k < 5; k++) {
+    pinned[k] = is_pinned(parts[k].src, parts[k].bytes);
+    if (parts[k].bytes && !pinned[k]) pageable += parts[k].bytes;
+  }
+  const bool pack = pageable <= CBFT_PACK_MAX;
+  size_t plo = SIZE_MAX, phi = 0;
+  for (int k = 0; k < 5; k++)
+    if (parts[k].bytes && !pinned[k] && pack) {
+      plo = std::min(plo, parts[k].off);
+      phi = std::max(phi, parts[k].off + parts[k].bytes);
+    }
+  uint8_t* din = s.in.as<uint8_t>();
+  // every part pinned and laid out in one host block exactly as in the device image
+  // (cbft_ed25519_batch_layout): the whole batch is one DMA
+  {
+    const uint8_t* base = nullptr;
+    size_t lo = SIZE_MAX, hi = 0;
+    bool same = true;
+    for (int k = 0; k < 5 && same; k++) {
+      if (!parts[k].bytes) continue;
+      const uint8_t* src = static_cast<const uint8_t*>(parts[k].src);
+      if (!pinned[k]) same = false;
+      else if (!base) base = src - parts[k].off;
+      else if (src - parts[k].off != base) same = false;
+      lo = std::min(lo, parts[k].off);
+      hi = std::max(hi, parts[k].off + parts[k].bytes);
+    }
+    if (same && base && is_pinned(base + lo, hi - lo)) {
+      CBFT_HIP(hipMemcpyAsync(din + lo, base + lo, hi - lo, hipMemcpyHostToDevice, c->copy_stream));
+      for (int k = 0; k < 5; k++) parts[k].bytes = 0;  // moved
+    }
+  }
+  if (!pack) {
+    for (int k = 0; k < 5; k++)
+      if (parts[k].bytes && !pinned[k])
+        CBFT_HIP(hipMemcpyAsync(din + parts[k].off, parts[k].src, parts[k].bytes, hipMemcpyHostToDevice, c->copy_stream));
+  }
+  if (phi) {
+    CBFT_HIP(s.pack.reserve(in_bytes));
+    for (int k = 0; k < 5; k++)
+      if (parts[k].bytes && !pinned[k]) std::memcpy(s.pack.as<uint8_t>(parts[k].off), parts[k].src, parts[k].bytes);
+    CBFT_HIP(hipMemcpyAsync(din + plo, s.pack.as<uint8_t>(plo), phi - plo, hipMemcpyHostToDevice, c->copy_stream));
+  }
+  // pinned parts after the packed run (stream order: they win where the run spans them)
+  for (int k = 0; k < 5; k++)
+    if (parts[k].bytes && pinned[k])
+      CBFT_HIP(hipMemcpyAsync(din + parts[k].off, parts[k].src, parts[k].bytes, hipMemcpyHostToDevice, c->copy_stream));
+  CBFT_HIP(hipEventRecord(s.copied, c->copy_stream));
+  hipStream_t cs = c->compute[t & 1];
+  CBFT_HIP(hipStreamWaitEvent(cs, s.copied, 0));
+  rc = launch_locked(c, table_id, kt ? nullptr : din + o_key, kt ? reinterpret_cast<const uint32_t*>(din + o_key) : nullptr,
+                     din + o_sig, din + o_msg - blo, fixed ? nullptr : reinterpret_cast<const uint64_t*>(din + o_off),
+                     fixed ? nullptr : reinterpret_cast<const uint32_t*>(din + o_len), fixed_len, n,
+                     s.verd.as<uint64_t>(), cs);
+  if (rc) return rc;
+  CBFT_HIP(hipMemcpyAsync(s.hverd.p, s.verd.p, nw * 8, hipMemcpyDeviceToHost, cs));
+  CBFT_HIP(hipEventRecord(s.done, cs));
+  s.ticket = t;
+  s.pending = true;
+  s.status = CBFT_OK;
+  s.n = n;
+  s.bitmap = bitmap;
+  *ticket = t;
   return CBFT_OK;
+}
+
+static int wait_one(cbft_ctx* c, uint64_t ticket) {
+  HostSlot& s = c->hslots[ticket % CBFT_HOST_SLOTS];
+  std::lock_guard<std::mutex> g(s.m);
+  if (s.ticket != ticket) return CBFT_OK;  // delivered when a later batch took the slot
+  (void)hipSetDevice(c->device);
+  return collect_locked(s);
+}
+
+// Multi-GPU context: static contiguous shards, boundaries on whole verdict words (64
+// signatures) so each device writes whole bytes of the caller's bitmap; one async batch per
+// device, all in flight together.
+static int group_submit(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const uint32_t* key_idx, const uint8_t* sig,
+                        const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len, bool fixed,
+                        uint32_t fixed_len, size_t n, uint8_t* bitmap, uint64_t* ticket) {
+  const size_t G = c->kids.size();
+  const size_t per = (((n + G - 1) / G) + 63) / 64 * 64;
+  std::vector<std::pair<size_t, uint64_t>> tk;
+  int rc = CBFT_OK;
+  for (size_t gi = 0; gi < G && rc == CBFT_OK; gi++) {
+    const size_t lo = gi * per;
+    if (lo >= n) break;
+    const size_t m = std::min(n, lo + per) - lo;
+    uint64_t kt = 0;
+    rc = submit_host(c->kids[gi], table_id, pk ? pk + lo * 32 : nullptr, key_idx ? key_idx + lo : nullptr, sig + lo * 64,
+                     fixed ? (msg_blob ? msg_blob + lo * (size_t)fixed_len : nullptr) : msg_blob,
+                     fixed ? nullptr : msg_off + lo, fixed ? nullptr : msg_len + lo, fixed, fixed_len, m, bitmap + lo / 8,
+                     &kt);
+    if (rc == CBFT_OK) tk.emplace_back(gi, kt);
+  }
+  if (rc != CBFT_OK) {
+    for (auto& p : tk) (void)wait_one(c->kids[p.first], p.second);
+    return rc;
+  }
+  std::lock_guard<std::mutex> g(c->group_mu);
+  const uint64_t t = ++c->next_ticket;
+  c->group_tickets[t] = std::move(tk);
+  *ticket = t;
+  return CBFT_OK;
+}
+
+static int submit_any(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const uint32_t* key_idx, const uint8_t* sig,
+                      const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len, bool fixed,
+                      uint32_t fixed_len, size_t n, uint8_t* bitmap, uint64_t* ticket) {
+  if (!c || !ticket || (n && (!sig || !bitmap || (!fixed && (!msg_off || !msg_len))))) return CBFT_EINVAL;
+  *ticket = 0;
+  if (n == 0) return CBFT_OK;
+  if (!c->kids.empty())
+    return group_submit(c, table_id, pk, key_idx, sig, msg_blob, msg_off, msg_len, fixed, fixed_len, n, bitmap, ticket);
+  return submit_host(c, table_id, pk, key_idx, sig, msg_blob, msg_off, msg_len, fixed, fixed_len, n, bitmap, ticket);
+}
+
+int cbft_wait(cbft_ctx* c, uint64_t ticket) {
+  if (!c) return CBFT_EINVAL;
+  if (ticket == 0) return CBFT_OK;  // an empty batch
+  if (c->kids.empty()) return wait_one(c, ticket);
+  std::vector<std::pair<size_t, uint64_t>> tk;
+  {
+    std::lock_guard<std::mutex> g(c->group_mu);
+    auto it = c->group_tickets.find(ticket);
+    if (it == c->group_tickets.end()) return CBFT_OK;  // already waited
+    tk = std::move(it->second);
+    c->group_tickets.erase(it);
+  }
+  int rc = CBFT_OK;
+  for (auto& p : tk) {
+    const int r = wait_one(c->kids[p.first], p.second);
+    if (r && !rc) rc = r;
+  }
+  return rc;
+}
+
+int cbft_ed25519_verify_batch_async(cbft_ctx* c, uint32_t table_id, const uint32_t* key_idx, const uint8_t* sig,
+                                    const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
+                                    uint8_t* bitmap, uint64_t* ticket) {
+  if (table_id == CBFT_NO_KEY_TABLE) return CBFT_EINVAL;
+  return submit_any(c, table_id, nullptr, key_idx, sig, msg_blob, msg_off, msg_len, false, 0, n, bitmap, ticket);
+}
+
+int cbft_ed25519_verify_fixed_async(cbft_ctx* c, uint32_t table_id, const uint32_t* key_idx, const uint8_t* sig,
+                                    const uint8_t* msg_blob, uint32_t msg_len, size_t n, uint8_t* bitmap,
+                                    uint64_t* ticket) {
+  if (table_id == CBFT_NO_KEY_TABLE) return CBFT_EINVAL;
+  return submit_any(c, table_id, nullptr, key_idx, sig, msg_blob, nullptr, nullptr, true, msg_len, n, bitmap, ticket);
 }
 
 int cbft_ed25519_verify_batch(cbft_ctx* c, uint32_t table_id, const uint32_t* key_idx, const uint8_t* sig,
                               const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
                               uint8_t* bitmap) {
-  if (table_id == CBFT_NO_KEY_TABLE) return CBFT_EINVAL;
-  return verify_host(c, table_id, nullptr, key_idx, sig, msg_blob, msg_off, msg_len, n, bitmap);
+  uint64_t t = 0;
+  int rc = cbft_ed25519_verify_batch_async(c, table_id, key_idx, sig, msg_blob, msg_off, msg_len, n, bitmap, &t);
+  return rc ? rc : cbft_wait(c, t);
 }
 
 int cbft_ed25519_verify_batch_pk(cbft_ctx* c, const uint8_t* pk, const uint8_t* sig, const uint8_t* msg_blob,
                                  const uint64_t* msg_off, const uint32_t* msg_len, size_t n, uint8_t* bitmap) {
-  return verify_host(c, CBFT_NO_KEY_TABLE, pk, nullptr, sig, msg_blob, msg_off, msg_len, n, bitmap);
+  if (n && !pk) return CBFT_EINVAL;
+  uint64_t t = 0;
+  int rc = submit_any(c, CBFT_NO_KEY_TABLE, pk, nullptr, sig, msg_blob, msg_off, msg_len, false, 0, n, bitmap, &t);
+  return rc ? rc : cbft_wait(c, t);
+}
+
+int cbft_ed25519_batch_layout(size_t n, uint32_t msg_len, size_t* off_key_idx, size_t* off_sig, size_t* off_msg,
+                              size_t* total_bytes) {
+  if (!off_key_idx || !off_sig || !off_msg || !total_bytes) return CBFT_EINVAL;
+  BatchLayout l;
+  batch_layout(n, true, true, l);
+  *off_key_idx = l.key;
+  *off_sig = l.sig;
+  *off_msg = l.msg;
+  *total_bytes = l.msg + (size_t)msg_len * n;
+  return CBFT_OK;
+}
+
+int cbft_host_alloc(cbft_ctx* c, size_t bytes, void** out) {
+  if (!c || !out || !bytes) return CBFT_EINVAL;
+  *out = nullptr;
+  CBFT_HIP(hipSetDevice(c->kids.empty() ? c->device : c->kids[0]->device));
+  void* p = nullptr;
+  CBFT_HIP(hipHostMalloc(&p, bytes, hipHostMallocPortable));  // DMA-able by every device
+  {
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    g_pinned[(uintptr_t)p] = bytes;
+  }
+  *out = p;
+  return CBFT_OK;
+}
+
+int cbft_host_free(cbft_ctx* c, void* p) {
+  if (!c || !p) return CBFT_EINVAL;
+  {
+    std::lock_guard<std::mutex> g(g_pin_mu);
+    auto it = g_pinned.find((uintptr_t)p);
+    if (it == g_pinned.end()) return CBFT_EINVAL;
+    g_pinned.erase(it);
+  }
+  CBFT_HIP(hipHostFree(p));
+  return CBFT_OK;
 }
 
 int cbft_ed25519_verify_batch_device(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, const uint32_t* d_key_idx,
@@ -494,11 +807,12 @@ int cbft_ed25519_verify_batch_device(cbft_ctx* c, uint32_t table_id, const uint8
                                      const uint32_t* d_len, size_t n, uint64_t* d_verdicts, void* stream) {
   if (!c || (n && (!d_sig || !d_off || !d_len || !d_verdicts))) return CBFT_EINVAL;
   if (table_id == CBFT_NO_KEY_TABLE && n && !d_pk) return CBFT_EINVAL;
+  if (!c->kids.empty()) return CBFT_EINVAL;  // device pointers belong to one GPU: use its own context
   if (n == 0) return CBFT_OK;
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
   hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
-  return launch_locked(c, table_id, d_pk, d_key_idx, d_sig, d_msg, d_off, d_len, n, d_verdicts, s);
+  return launch_locked(c, table_id, d_pk, d_key_idx, d_sig, d_msg, d_off, d_len, 0, n, d_verdicts, s);
 }
 
 }  // extern "C"

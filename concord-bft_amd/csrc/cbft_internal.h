@@ -99,6 +99,24 @@ struct WorkSlot {
   bool used = false;
 };
 
+// One in-flight host-buffer batch (cbft_ed25519_verify_batch_async and the blocking calls built on
+// it).  Inputs are DMA'd from the caller's pinned memory (cbft_host_alloc) straight into `in`,
+// or packed into `pack` first when they are pageable; the copy runs on the context's copy stream
+// while earlier batches' kernels run on the compute streams.  A slot is reused only after its
+// previous batch was collected (verdict words copied to that batch's bitmap).
+#define CBFT_HOST_SLOTS 4
+struct HostSlot {
+  DevBuf in, verd;      // packed device inputs, device verdict words
+  HostBuf pack, hverd;  // pinned packing image for pageable inputs, pinned verdict words
+  hipEvent_t copied = nullptr, done = nullptr;
+  std::mutex m;         // guards the fields below (collect vs. reuse)
+  uint64_t ticket = 0;  // batch currently owning the slot
+  bool pending = false; // submitted, verdicts not yet delivered
+  int status = 0;       // CBFT_* of the submission
+  uint8_t* bitmap = nullptr;
+  size_t n = 0;
+};
+
 // RSA verifier key table: per-key records (modulus, R^2 mod n, n0inv, e, validity) built on the
 // GPU at load time (one verifier per key, SigManager.cpp:139-150)
 struct RsaKeyTable {
@@ -110,6 +128,15 @@ struct cbft_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   std::mutex mu;
+  // multi-GPU context (cbft_open_mask): one child context per device, static contiguous shards
+  std::vector<cbft_ctx*> kids;
+  std::mutex group_mu;
+  std::unordered_map<uint64_t, std::vector<std::pair<size_t, uint64_t>>> group_tickets;  // ticket -> (kid, kid ticket)
+  // host-buffer pipeline
+  hipStream_t copy_stream = nullptr;
+  hipStream_t compute[2] = {nullptr, nullptr};
+  HostSlot hslots[CBFT_HOST_SLOTS];
+  uint64_t next_ticket = 0;
   DevBuf base_table, base_comb;
   std::unordered_map<uint32_t, KeyTable> tables;
   uint32_t next_table_id = 1;
@@ -154,6 +181,8 @@ struct cbft_ctx {
 };
 
 int cbft_fail(hipError_t e, const char* what, const char* file, int line);
+// the context BLS / RSA / profiling calls run on (a multi-GPU context's first device)
+cbft_ctx* cbft_dev0(cbft_ctx* c);
 
 #define CBFT_HIP(expr)                                                          \
   do {                                                                          \

@@ -41,6 +41,7 @@ extern "C" {
 
 int cbft_rsa_load_keys(cbft_ctx* c, const uint8_t* moduli, const uint32_t* exponents, uint32_t nkeys,
                        uint32_t* out_id) {
+  c = cbft_dev0(c);
   if (!c || !out_id || (nkeys && (!moduli || !exponents))) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
@@ -70,6 +71,7 @@ int cbft_rsa_load_keys(cbft_ctx* c, const uint8_t* moduli, const uint32_t* expon
 }
 
 int cbft_rsa_unload_keys(cbft_ctx* c, uint32_t id) {
+  c = cbft_dev0(c);
   if (!c) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   auto it = c->rsa_tables.find(id);
@@ -82,6 +84,7 @@ int cbft_rsa_unload_keys(cbft_ctx* c, uint32_t id) {
 }
 
 int cbft_rsa_key_status(cbft_ctx* c, uint32_t id, uint8_t* out_ok) {
+  c = cbft_dev0(c);
   if (!c || !out_ok) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   auto it = c->rsa_tables.find(id);
@@ -97,6 +100,7 @@ int cbft_rsa_key_status(cbft_ctx* c, uint32_t id, uint8_t* out_ok) {
 int cbft_rsa_verify_batch(cbft_ctx* c, uint32_t id, const uint32_t* key_idx, const uint8_t* sig,
                           const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
                           uint8_t* bitmap) {
+  c = cbft_dev0(c);
   if (!c || (n && (!key_idx || !sig || !msg_off || !msg_len || !bitmap))) return CBFT_EINVAL;
   if (n == 0) return CBFT_OK;
   std::lock_guard<std::mutex> g(c->mu);
@@ -136,6 +140,7 @@ int cbft_rsa_verify_batch(cbft_ctx* c, uint32_t id, const uint32_t* key_idx, con
 int cbft_rsa_verify_batch_device(cbft_ctx* c, uint32_t id, const uint32_t* d_key_idx, const uint8_t* d_sig,
                                  const uint8_t* d_msg, const uint64_t* d_off, const uint32_t* d_len, size_t n,
                                  uint64_t* d_verdicts, void* stream) {
+  c = cbft_dev0(c);
   if (!c || (n && (!d_key_idx || !d_sig || !d_off || !d_len || !d_verdicts))) return CBFT_EINVAL;
   if (reinterpret_cast<uintptr_t>(d_sig) & 3) return CBFT_EINVAL;  // signatures are read as words
   if (n == 0) return CBFT_OK;
@@ -148,6 +153,7 @@ int cbft_rsa_verify_batch_device(cbft_ctx* c, uint32_t id, const uint32_t* d_key
 }
 
 int cbft_rsa_kernel_ms(cbft_ctx* c, float* out_ms) {
+  c = cbft_dev0(c);
   if (!c || !out_ms) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   if (!c->rsa_ev_valid) return CBFT_EINVAL;

@@ -28,9 +28,13 @@ struct Ed25519Batch {
   const uint32_t* key_idx;  // nullable
   const uint8_t* sig;       // n x 64 B (R || S)
   const uint8_t* msg;       // message blob
-  const uint64_t* msg_off;  // n byte offsets into msg
-  const uint32_t* msg_len;  // n lengths
+  const uint64_t* msg_off;  // n byte offsets into msg; nullptr = fixed-length messages (below)
+  const uint32_t* msg_len;  // n lengths (unused when msg_off is nullptr)
+  uint32_t nkeys;           // entries of pk when key_idx is set: key_idx[i] >= nkeys verifies false
+  uint32_t fixed_len;       // msg_off == nullptr: message i = msg[i * fixed_len, (i + 1) * fixed_len)
 };
+// Messages longer than this verify false (SHA-512's 64 + len byte count must not wrap 32 bits).
+#define CBFT_MAX_MSG_LEN 0xFFFFFF00u
 
 // Geometry of a fixed-base comb table with signed radix-2^w digits (8 <= w <= 16):
 // npos positions of entries() = 2^(w-1) + 1 affine niels points (e * 2^(w j) * P, e = 0 ..

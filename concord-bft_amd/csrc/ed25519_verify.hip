@@ -196,17 +196,28 @@ __device__ __forceinline__ void load_msg_words(uint64_t* W, const uint8_t* m, ui
   }
 }
 
+// Key-table unit of signature i.  An index outside the table reads unit 0 instead (never past
+// the table) and K1 clears the signature's flag, so its verdict is false.
+__device__ __forceinline__ uint32_t batch_unit(const Ed25519Batch& b, size_t i) {
+  if (!b.key_idx) return (uint32_t)i;
+  const uint32_t k = b.key_idx[i];
+  return k < b.nkeys ? k : 0u;
+}
+
 __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const Ed25519Batch b, uint32_t* h_soa,
                                                                           uint8_t* flags) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= b.n) return;
-  const uint32_t key = b.key_idx ? b.key_idx[i] : (uint32_t)i;
+  const uint32_t key = batch_unit(b, i);
+  const bool key_ok = !b.key_idx || b.key_idx[i] < b.nkeys;
   uint32_t Aw[8], Rw[8], Sw[8];
   load_words8(Aw, b.pk + (size_t)key * 32);
   load_words8(Rw, b.sig + i * 64);
   load_words8(Sw, b.sig + i * 64 + 32);
-  const uint8_t* m = b.msg + b.msg_off[i];
-  const uint32_t len = b.msg_len[i];
+  const uint8_t* m = b.msg_off ? b.msg + b.msg_off[i] : b.msg + i * (size_t)b.fixed_len;
+  uint32_t len = b.msg_off ? b.msg_len[i] : b.fixed_len;
+  const bool len_ok = len <= CBFT_MAX_MSG_LEN;
+  if (!len_ok) len = 0;
   const uint32_t* safe = reinterpret_cast<const uint32_t*>(b.sig + i * 64);  // readable dword
 
   uint64_t H[8], W[16];
@@ -238,7 +249,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const E
   sc_reduce512(hw, dig);
 #pragma unroll
   for (int k = 0; k < 8; k++) h_soa[k * b.n + i] = hw[k];
-  flags[i] = sc_is_canonical(Sw) ? 1 : 0;
+  flags[i] = (sc_is_canonical(Sw) && key_ok && len_ok) ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -282,7 +293,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_LADDER_MIN_WAVES)
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= b.n) return;
 
-  const uint32_t unit = b.key_idx ? b.key_idx[i] : (uint32_t)i;
+  const uint32_t unit = batch_unit(b, i);
   const uint32_t* slab = tbl + (size_t)unit * (Shape::TA * CACHED_WORDS);
   uint32_t kA[9], kB[9];
   {
@@ -345,7 +356,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_finish_kernel(const
     uint32_t diff = 0;
 #pragma unroll
     for (int k = 0; k < 8; k++) diff |= Rp[k] ^ Rw[k];
-    const uint32_t unit = b.key_idx ? b.key_idx[i] : (uint32_t)i;
+    const uint32_t unit = batch_unit(b, i);
     verdict = (diff == 0) && flags[i] && aok[unit];
   }
   const uint64_t ballot = __ballot(verdict);
@@ -379,7 +390,7 @@ __global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519B
     bool ok = false;
     if (i < b.n) {
       fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
-      const uint32_t unit = b.key_idx ? b.key_idx[i] : (uint32_t)i;
+      const uint32_t unit = batch_unit(b, i);
       ok = flags[i] && aok[unit] && !fe_iszero(Z);
       if (!ok) fe_1(Z);
     }
@@ -648,7 +659,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
       sdig[jj][threadIdx.x] = (uint16_t)(d + 32768);
     }
   }
-  const uint32_t* akey = atbl + (size_t)b.key_idx[i] * cl.a.words_per_unit();
+  const uint32_t* akey = atbl + (size_t)batch_unit(b, i) * cl.a.words_per_unit();
   auto entry = [&](uint32_t jj, int d) {
     const uint32_t k = first + jj;
     const uint32_t ad = (uint32_t)(d < 0 ? -d : d);

@@ -15,9 +15,11 @@
  * Conventions:
  *   - every function returns 0 (CBFT_OK) or a negative errno-style code; no C++ exception ever
  *     crosses this boundary;
- *   - the caller owns every buffer; host-pointer entry points are blocking;
- *   - a context is bound to one GPU; calls on one context are serialised internally
- *     (thread-safe), distinct contexts run concurrently;
+ *   - the caller owns every buffer; host-pointer entry points are blocking unless named _async;
+ *   - a context is bound to one GPU (cbft_open) or to a set of GPUs (cbft_open_mask: Ed25519
+ *     batches shard statically across them); every entry point is thread-safe:
+ *     submissions are serialised briefly, waiting for results is not (batches of several
+ *     threads are in flight together);
  *   - a verdict never depends on batch composition (each signature is verified independently);
  *   - a bad signature is a 0 verdict bit, never an error code.
  * All integers are little-endian; keys are 32 raw bytes (RFC 8032 encoding), signatures are
@@ -57,7 +59,27 @@ const char* cbft_last_error(void);
 /* Open a context on GPU `device` for batches of up to `max_batch` signatures (the working
  * buffers grow on demand above that; max_batch only pre-sizes them). */
 int cbft_open(cbft_ctx** out, int device, size_t max_batch);
+/* Open one context over every GPU whose bit is set in device_mask (bit d = device d; SURVEY.md
+ * §8(b)).  Ed25519 key tables are replicated on each device; an Ed25519 host-buffer batch is cut
+ * into contiguous shards of whole 64-signature words, one per device, verified concurrently, and
+ * the verdicts land in the caller's one bitmap.  BLS, RSA and the profiling calls run on the
+ * lowest device of the mask; the _device entry points need a single-GPU context (CBFT_EINVAL).
+ * A one-bit mask is exactly cbft_open. */
+int cbft_open_mask(cbft_ctx** out, uint32_t device_mask, size_t max_batch);
+/* The same over an explicit device list, in shard order; a device may repeat (several shards,
+ * each with its own streams, on one GPU — how the multi-GPU geometry is tested on one GPU). */
+int cbft_open_devices(cbft_ctx** out, const int* devices, int ndevices, size_t max_batch);
+/* Devices of a context: returns their count and writes up to max_out device ordinals. */
+int cbft_device_of(cbft_ctx* ctx, int* out_devices, int max_out);
 void cbft_close(cbft_ctx* ctx);
+
+/* Page-locked host memory, DMA-able by every device.  A caller that builds its batches directly
+ * in such memory (signatures, key indices, the message blob) saves the host copy: the
+ * host-buffer entry points move any input lying inside a cbft_host_alloc block to the GPU with
+ * one DMA each, and pack other (pageable) inputs into internal pinned staging first.
+ * cbft_host_free only after every batch reading the block has been waited for. */
+int cbft_host_alloc(cbft_ctx* ctx, size_t bytes, void** out);
+int cbft_host_free(cbft_ctx* ctx, void* p);
 
 /* ---------------------------------------------------------------- Ed25519 ----------------
  * Verdict semantics are exactly OpenSSL 3.0.2 EVP_DigestVerify(ED25519) == 1:
@@ -79,8 +101,8 @@ int cbft_ed25519_load_keys_ex(cbft_ctx* ctx, const uint8_t* pk, uint32_t nkeys, 
                               uint32_t* out_key_table_id);
 int cbft_ed25519_unload_keys(cbft_ctx* ctx, uint32_t key_table_id);
 
-/* Verify n signatures against keys of a loaded table.
- *   key_idx[i]   : index of signature i's key in the table (< nkeys)
+/* Verify n signatures against keys of a loaded table (blocking: _async + cbft_wait).
+ *   key_idx[i]   : index of signature i's key in the table (< nkeys, else CBFT_EINVAL)
  *   sig          : n x 64 bytes
  *   msg_blob     : all messages; message i = msg_blob[msg_off[i] .. msg_off[i] + msg_len[i])
  *   verdict_bitmap: ceil(n/8) bytes, bit (i % 8) of byte i/8 = 1 iff signature i verifies
@@ -88,6 +110,30 @@ int cbft_ed25519_unload_keys(cbft_ctx* ctx, uint32_t key_table_id);
 int cbft_ed25519_verify_batch(cbft_ctx* ctx, uint32_t key_table_id, const uint32_t* key_idx, const uint8_t* sig,
                               const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
                               uint8_t* verdict_bitmap);
+
+/* Asynchronous form: queues the batch (host -> device copy on a copy stream, kernels on compute
+ * streams, so several batches overlap: batch i+1's copy runs under batch i's kernels) and returns
+ * a ticket.  Inputs in cbft_host_alloc memory are read by DMA after the call returns and must stay
+ * unchanged until cbft_wait(ticket); pageable inputs are copied before the call returns.
+ * verdict_bitmap is written no later than when cbft_wait(ticket) returns (possibly earlier, when
+ * a later submission needs the batch's slot).  n = 0 returns ticket 0. */
+int cbft_ed25519_verify_batch_async(cbft_ctx* ctx, uint32_t key_table_id, const uint32_t* key_idx,
+                                    const uint8_t* sig, const uint8_t* msg_blob, const uint64_t* msg_off,
+                                    const uint32_t* msg_len, size_t n, uint8_t* verdict_bitmap, uint64_t* out_ticket);
+/* Fixed-length messages (no offset/length arrays to move): message i = msg_blob[i * msg_len,
+ * (i + 1) * msg_len). */
+int cbft_ed25519_verify_fixed_async(cbft_ctx* ctx, uint32_t key_table_id, const uint32_t* key_idx,
+                                    const uint8_t* sig, const uint8_t* msg_blob, uint32_t msg_len, size_t n,
+                                    uint8_t* verdict_bitmap, uint64_t* out_ticket);
+/* Where to place a fixed-length batch's arrays inside one cbft_host_alloc block (key indices at
+ * +*off_key_idx, signatures at +*off_sig, messages at +*off_msg; *total_bytes in all) so that
+ * cbft_ed25519_verify_fixed_async moves the whole batch with ONE DMA: at the PCIe bound of the
+ * host path, one 21 MB copy per 64K batch instead of three. */
+int cbft_ed25519_batch_layout(size_t n, uint32_t msg_len, size_t* off_key_idx, size_t* off_sig, size_t* off_msg,
+                              size_t* total_bytes);
+/* Wait for a ticket's batch and deliver its verdicts (0 for ticket 0 or a ticket already waited
+ * for).  Any thread may wait; the context stays usable by other threads meanwhile. */
+int cbft_wait(cbft_ctx* ctx, uint64_t ticket);
 
 /* Same, with one raw 32-byte key per signature (pk = n x 32 bytes); the key is decoded per
  * signature inside the batch. */
@@ -98,7 +144,9 @@ int cbft_ed25519_verify_batch_pk(cbft_ctx* ctx, const uint8_t* pk, const uint8_t
 /* Device-resident variant: every pointer is device memory on the context's GPU, the call is
  * asynchronous on `stream` (a hipStream_t; NULL = the context's own stream) and writes
  * ceil(n/64) 64-bit verdict words (bit i % 64 of word i / 64).  key_table_id selects a loaded
- * table (then key_idx indexes it) or is CBFT_NO_KEY_TABLE (then d_pk holds n raw keys).
+ * table (then key_idx indexes it) or is CBFT_NO_KEY_TABLE (then d_pk holds n raw keys).  A
+ * key index >= the table's key count verifies false (the kernels never read past the table).
+ * Messages longer than 0xFFFFFF00 bytes verify false.
  * Use cbft_sync() (or the stream) before reading the verdicts. */
 #define CBFT_NO_KEY_TABLE 0xffffffffu
 int cbft_ed25519_verify_batch_device(cbft_ctx* ctx, uint32_t key_table_id, const uint8_t* d_pk,
