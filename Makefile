@@ -46,7 +46,7 @@ $(CPU_LIB): tools/cpu_baseline/openssl_ed25519.c
 	gcc -O2 -std=gnu11 -fPIC -shared -Wall -Wno-deprecated-declarations -o $@ $< -lcrypto -lpthread
 
 HOST_LIB := concord-bft_amd/libcbft_host.so
-HOST_SRC := concord-bft_amd/host/src/crypto_utils.cpp concord-bft_amd/host/src/rsa_host.cpp concord-bft_amd/host/src/sig_manager.cpp concord-bft_amd/host/src/bls_hip.cpp
+HOST_SRC := concord-bft_amd/host/src/crypto_utils.cpp concord-bft_amd/host/src/rsa_host.cpp concord-bft_amd/host/src/sig_manager.cpp concord-bft_amd/host/src/bls_hip.cpp concord-bft_amd/host/src/request_batch.cpp
 HOST_INC := -Iinclude -Iconcord-bft_amd/host/include
 host: $(HOST_LIB) tests/cpp/test_host tests/cpp/test_bls_host
 $(HOST_LIB): $(HOST_SRC) concord-bft_amd/host/include/*.hpp concord-bft_amd/host/include/threshsign/*.h* $(LIB)

@@ -52,6 +52,10 @@ ABI = [
     ("cbft_ed25519_load_keys_ex", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int, _u32p]),
     ("cbft_ed25519_unload_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
+    ("cbft_ed25519_append_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
+                                                _u32p]),
+    ("cbft_ed25519_table_size", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, _u32p,
+                                               ctypes.POINTER(ctypes.c_int)]),
     ("cbft_ed25519_verify_batch", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
       ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p]),
@@ -258,6 +262,20 @@ class Context:
         _check(self.lib.cbft_ed25519_load_keys_ex(self.handle, _ptr(arr), arr.shape[0], radix, ctypes.byref(tid)),
                "cbft_ed25519_load_keys_ex")
         return tid.value
+
+    def append_keys(self, tid: int, pks) -> int:
+        """Append keys to a loaded table; returns the first new key index."""
+        arr = _as_rows(pks, 32)
+        first = ctypes.c_uint32()
+        _check(self.lib.cbft_ed25519_append_keys(self.handle, tid, _ptr(arr), arr.shape[0], ctypes.byref(first)),
+               "cbft_ed25519_append_keys")
+        return first.value
+
+    def table_size(self, tid: int):
+        n, r = ctypes.c_uint32(), ctypes.c_int()
+        _check(self.lib.cbft_ed25519_table_size(self.handle, tid, ctypes.byref(n), ctypes.byref(r)),
+               "cbft_ed25519_table_size")
+        return n.value, r.value
 
     def unload_keys(self, tid: int):
         _check(self.lib.cbft_ed25519_unload_keys(self.handle, tid), "cbft_ed25519_unload_keys")

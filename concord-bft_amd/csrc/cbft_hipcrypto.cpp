@@ -146,7 +146,8 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->compute[0], hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->compute[1], hipStreamNonBlocking) != hipSuccess) {
+        hipStreamCreateWithFlags(&c->compute[1], hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->build_stream, hipStreamNonBlocking) != hipSuccess) {
       rc = CBFT_EIO;
       break;
     }
@@ -246,10 +247,11 @@ void cbft_close(cbft_ctx* c) {
   }
   for (hipStream_t st : {c->stream, c->copy_stream, c->compute[0], c->compute[1]})
     if (st) (void)hipStreamSynchronize(st);
+  if (c->build_stream) (void)hipStreamSynchronize(c->build_stream);
   for (auto& kv : c->tables) {
-    kv.second.pk.release();
-    kv.second.comb.release();
-    kv.second.aok.release();
+    std::lock_guard<std::mutex> ag(kv.second->append_mu);
+    for (DevBuf& b : kv.second->chunks) b.release();
+    kv.second->chunk_ptrs.release();
   }
   for (auto& kv : c->bls_sets) {
     kv.second.keys65.release();
@@ -287,7 +289,7 @@ void cbft_close(cbft_ctx* c) {
     for (hipEvent_t e : {hs.copied, hs.done})
       if (e) (void)hipEventDestroy(e);
   }
-  for (hipStream_t st : {c->stream, c->copy_stream, c->compute[0], c->compute[1]})
+  for (hipStream_t st : {c->stream, c->copy_stream, c->compute[0], c->compute[1], c->build_stream})
     if (st) (void)hipStreamDestroy(st);
   delete c;
 }
@@ -371,34 +373,103 @@ int cbft_ed25519_load_keys_ex(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, in
     *out_id = id0;
     return CBFT_OK;
   }
-  std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
-  KeyTable kt;
-  kt.nkeys = nkeys;
-  kt.geo = cbft_comb_geom(key_radix(comb_radix, nkeys));
-  const size_t n = std::max<uint32_t>(nkeys, 1);
-  CBFT_HIP(kt.pk.reserve(n * 32));
-  CBFT_HIP(kt.comb.reserve(n * kt.geo.words_per_unit() * sizeof(uint32_t)));
-  CBFT_HIP(kt.aok.reserve(n));
+  auto kt = std::make_shared<KeyTable>();
+  kt->geo = cbft_comb_geom(key_radix(comb_radix, nkeys));
+  CBFT_HIP(kt->chunk_ptrs.reserve(CBFT_MAX_KEY_CHUNKS * sizeof(void*)));
+  uint32_t id;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    id = c->next_table_id++;
+    if (id == CBFT_NO_KEY_TABLE) id = c->next_table_id++;
+    c->tables.emplace(id, kt);
+  }
   if (nkeys) {
-    hipError_t e = hipMemcpyAsync(kt.pk.p, pk, (size_t)nkeys * 32, hipMemcpyHostToDevice, c->stream);
-    if (e == hipSuccess) e = build_comb(kt.pk.as<uint8_t>(), nkeys, 1, kt.geo, kt.comb.as<uint32_t>(), kt.aok.as<uint8_t>(), c->stream);
-    if (e != hipSuccess) {
-      kt.pk.release();
-      kt.comb.release();
-      kt.aok.release();
-      return cbft_fail(e, "comb table build", __FILE__, __LINE__);
+    uint32_t first = 0;
+    const int rc = cbft_ed25519_append_keys(c, id, pk, nkeys, &first);
+    if (rc) {
+      (void)cbft_ed25519_unload_keys(c, id);
+      return rc;
     }
   }
-  uint32_t id = c->next_table_id++;
-  if (id == CBFT_NO_KEY_TABLE) id = c->next_table_id++;
-  c->tables.emplace(id, std::move(kt));
   *out_id = id;
   return CBFT_OK;
 }
 
 int cbft_ed25519_load_keys(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, uint32_t* out_id) {
   return cbft_ed25519_load_keys_ex(c, pk, nkeys, 0, out_id);
+}
+
+static std::shared_ptr<KeyTable> find_table(cbft_ctx* c, uint32_t id) {
+  std::lock_guard<std::mutex> g(c->mu);
+  auto it = c->tables.find(id);
+  return it == c->tables.end() ? nullptr : it->second;
+}
+
+// Append keys to a table: new chunks as needed (their pointers appended to the device chunk
+// array), the keys copied into their chunk slots and their comb tables built on the context's
+// build stream — all outside the context mutex, so verifies of the published keys continue —
+// then the key count is published.  Appends to one table are serialised by its append_mu.
+int cbft_ed25519_append_keys(cbft_ctx* c, uint32_t id, const uint8_t* pk, uint32_t nkeys, uint32_t* out_first) {
+  if (!c || !out_first || (nkeys && !pk)) return CBFT_EINVAL;
+  if (!c->kids.empty()) {
+    for (size_t k = 0; k < c->kids.size(); k++) {
+      uint32_t first = 0;
+      const int rc = cbft_ed25519_append_keys(c->kids[k], id, pk, nkeys, &first);
+      if (rc) return rc;
+      if (k == 0) *out_first = first;
+      if (first != *out_first) return CBFT_EIO;
+    }
+    return CBFT_OK;
+  }
+  auto kt = find_table(c, id);
+  if (!kt) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> ag(kt->append_mu);
+  CBFT_HIP(hipSetDevice(c->device));
+  uint32_t k0;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    k0 = kt->nkeys;
+  }
+  *out_first = k0;
+  if (!nkeys) return CBFT_OK;
+  if ((uint64_t)k0 + nkeys > (uint64_t)CBFT_MAX_KEY_CHUNKS * CBFT_KEY_CHUNK) return CBFT_E2BIG;
+  const size_t wpk = kt->geo.words_per_unit();
+  hipStream_t s = c->build_stream;
+  while (kt->chunks.size() * CBFT_KEY_CHUNK < (size_t)k0 + nkeys) {
+    DevBuf b;
+    CBFT_HIP(b.reserve(cbft_key_chunk_bytes(wpk)));
+    const size_t ci = kt->chunks.size();
+    kt->chunks.push_back(b);
+    CBFT_HIP(hipMemcpyAsync(kt->chunk_ptrs.as<void*>() + ci, &kt->chunks.back().p, sizeof(void*),
+                            hipMemcpyHostToDevice, s));
+    CBFT_HIP(hipStreamSynchronize(s));  // the source is a host variable
+  }
+  for (uint32_t a = k0; a < k0 + nkeys;) {
+    const uint32_t ci = a >> CBFT_KEY_CHUNK_SHIFT, slot = a & (CBFT_KEY_CHUNK - 1);
+    const uint32_t m = std::min<uint32_t>(k0 + nkeys - a, CBFT_KEY_CHUNK - slot);
+    uint8_t* base = kt->chunks[ci].as<uint8_t>();
+    uint8_t* dpk = base + (size_t)CBFT_KEY_CHUNK * wpk * 4 + (size_t)slot * 32;
+    uint8_t* daok = base + (size_t)CBFT_KEY_CHUNK * (wpk * 4 + 32) + slot;
+    uint32_t* dcomb = reinterpret_cast<uint32_t*>(base) + (size_t)slot * wpk;
+    hipError_t e = hipMemcpyAsync(dpk, pk + (size_t)(a - k0) * 32, (size_t)m * 32, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = build_comb(dpk, m, 1, kt->geo, dcomb, daok, s);
+    if (e != hipSuccess) return cbft_fail(e, "comb table build", __FILE__, __LINE__);
+    a += m;
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  kt->nkeys = k0 + nkeys;
+  return CBFT_OK;
+}
+
+int cbft_ed25519_table_size(cbft_ctx* c, uint32_t id, uint32_t* out_nkeys, int* out_radix) {
+  if (!c || !out_nkeys) return CBFT_EINVAL;
+  auto kt = find_table(cbft_dev0(c), id);
+  if (!kt) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(cbft_dev0(c)->mu);
+  *out_nkeys = kt->nkeys;
+  if (out_radix) *out_radix = kt->geo.w;
+  return CBFT_OK;
 }
 
 int cbft_ed25519_unload_keys(cbft_ctx* c, uint32_t id) {
@@ -411,15 +482,19 @@ int cbft_ed25519_unload_keys(cbft_ctx* c, uint32_t id) {
     }
     return rc;
   }
-  std::lock_guard<std::mutex> g(c->mu);
-  auto it = c->tables.find(id);
-  if (it == c->tables.end()) return CBFT_EINVAL;
+  std::shared_ptr<KeyTable> kt;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    auto it = c->tables.find(id);
+    if (it == c->tables.end()) return CBFT_EINVAL;
+    kt = it->second;
+    c->tables.erase(it);  // no new batch can name it
+  }
+  std::lock_guard<std::mutex> ag(kt->append_mu);  // an append in progress finishes first
   (void)hipSetDevice(c->device);
-  (void)hipDeviceSynchronize();  // in-flight device-path batches on caller streams read it
-  it->second.pk.release();
-  it->second.comb.release();
-  it->second.aok.release();
-  c->tables.erase(it);
+  (void)hipDeviceSynchronize();  // in-flight batches (any stream) read it
+  for (DevBuf& b : kt->chunks) b.release();
+  kt->chunk_ptrs.release();
   return CBFT_OK;
 }
 
@@ -429,10 +504,11 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
                          uint32_t fixed_len, size_t n, uint64_t* d_verdicts, hipStream_t s) {
   int rc = reserve_work(c, n);
   if (rc) return rc;
-  auto it = c->tables.end();
+  KeyTable* kt = nullptr;
   if (table_id != CBFT_NO_KEY_TABLE) {
-    it = c->tables.find(table_id);
+    auto it = c->tables.find(table_id);
     if (it == c->tables.end() || !d_kidx) return CBFT_EINVAL;
+    kt = it->second.get();
   }
   WorkSlot& slot = c->slots[c->next_slot++ % CBFT_WORK_SLOTS];
   if (table_id == CBFT_NO_KEY_TABLE) {
@@ -442,8 +518,8 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   // the slot's previous batch (maybe on another stream) must be done with its buffers
   if (slot.used) CBFT_HIP(hipStreamWaitEvent(s, slot.done, 0));
 
-  Ed25519Batch b{n, d_pk, d_kidx, d_sig, d_msg, d_off, d_len,
-                 table_id == CBFT_NO_KEY_TABLE ? (uint32_t)n : it->second.nkeys, fixed_len};
+  Ed25519Batch b{n, d_pk, d_kidx, KeyChunks{nullptr, 0}, d_sig, d_msg, d_off, d_len,
+                 kt ? kt->nkeys : (uint32_t)n, fixed_len};
   Ed25519Work w{};
   // one inversion per K signatures per lane only where the batch keeps >= 64 finish waves; a
   // small (latency-bound) batch inverts per signature.  K = 16 at the 64K headline: the finish is
@@ -462,11 +538,10 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     w.tbl = slot.ps_tbl.as<uint32_t>();
     w.aok = slot.ps_aok.as<uint8_t>();
   } else {
-    b.pk = it->second.pk.as<uint8_t>();
-    w.comb_tbl = it->second.comb.as<uint32_t>();
+    b.pk = nullptr;
+    b.keys = kt->view();
     w.base_comb = c->base_comb.as<uint32_t>();
-    w.comb = cbft_comb_ladder(it->second.geo.w, CBFT_COMB_B_RADIX);
-    w.aok = it->second.aok.as<uint8_t>();
+    w.comb = cbft_comb_ladder(kt->geo.w, CBFT_COMB_B_RADIX);
   }
   StageOrder order{};
   if (c->stage_order) {
@@ -547,7 +622,7 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
   if (kt) {
     auto it = c->tables.find(table_id);
     if (it == c->tables.end() || !key_idx) return CBFT_EINVAL;
-    nkeys = it->second.nkeys;
+    nkeys = it->second->nkeys;
     for (size_t i = 0; i < n; i++)
       if (key_idx[i] >= nkeys) return CBFT_EINVAL;
   } else if (!pk) {

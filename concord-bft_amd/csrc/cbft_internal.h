@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <unordered_map>
 #include <vector>
@@ -74,10 +75,17 @@ struct DevBuf {
   }
 };
 
+// An Ed25519 key table: chunks of CBFT_KEY_CHUNK keys (comb tables of -A, raw keys, decode
+// status; ed25519_verify.h KeyChunks).  Keys are appended into the last chunk / new chunks while
+// verifies against the already published keys keep running; `nkeys` (read and written under the
+// context's mutex) is raised only once the new keys' tables are built.
 struct KeyTable {
-  uint32_t nkeys = 0;
-  CombGeom geo{};        // radix of the per-key comb tables
-  DevBuf pk, comb, aok;  // raw keys, per-key comb tables of -A, decode status
+  uint32_t nkeys = 0;     // published keys
+  CombGeom geo{};         // radix of the per-key comb tables
+  std::vector<DevBuf> chunks;
+  DevBuf chunk_ptrs;      // CBFT_MAX_KEY_CHUNKS device pointers (only appended)
+  std::mutex append_mu;   // one append (or the unload) at a time
+  KeyChunks view() const { return KeyChunks{chunk_ptrs.as<const uint32_t* const>(), geo.words_per_unit()}; }
 };
 
 // BLS verifier key set: group public key + n share verification keys, decoded and with their
@@ -138,7 +146,8 @@ struct cbft_ctx {
   HostSlot hslots[CBFT_HOST_SLOTS];
   uint64_t next_ticket = 0;
   DevBuf base_table, base_comb;
-  std::unordered_map<uint32_t, KeyTable> tables;
+  std::unordered_map<uint32_t, std::shared_ptr<KeyTable>> tables;
+  hipStream_t build_stream = nullptr;  // key-table builds (appends), apart from the verify streams
   uint32_t next_table_id = 1;
   // per-batch work buffers
   WorkSlot slots[CBFT_WORK_SLOTS];

@@ -21,16 +21,43 @@
 #define CBFT_LADDER_MIN_WAVES 4  // waves/SIMD the ladder is register-allocated for
 #endif
 
+// A loaded key table lives in chunks of CBFT_KEY_CHUNK keys, so keys can be appended without
+// moving (or rebuilding) the ones already loaded: chunk c holds keys [c * CHUNK, (c + 1) * CHUNK)
+// as [comb tables: CHUNK x words_per_key words][raw keys: CHUNK x 32 B][decode status: CHUNK B].
+// `chunk` is a device array of chunk base pointers; entries are only ever appended.
+#define CBFT_KEY_CHUNK_SHIFT 8
+#define CBFT_KEY_CHUNK (1u << CBFT_KEY_CHUNK_SHIFT)
+#define CBFT_MAX_KEY_CHUNKS 4096  // 1,048,576 keys per table
+struct KeyChunks {
+  const uint32_t* const* chunk;
+  size_t wpk;  // comb words per key
+#ifdef __HIPCC__
+  __device__ __forceinline__ const uint32_t* base(uint32_t key) const { return chunk[key >> CBFT_KEY_CHUNK_SHIFT]; }
+  __device__ __forceinline__ const uint32_t* comb(uint32_t key) const {
+    return base(key) + (size_t)(key & (CBFT_KEY_CHUNK - 1)) * wpk;
+  }
+  __device__ __forceinline__ const uint8_t* pk(uint32_t key) const {
+    return reinterpret_cast<const uint8_t*>(base(key) + (size_t)CBFT_KEY_CHUNK * wpk) + (key & (CBFT_KEY_CHUNK - 1)) * 32u;
+  }
+  __device__ __forceinline__ bool aok(uint32_t key) const {
+    return reinterpret_cast<const uint8_t*>(base(key) + (size_t)CBFT_KEY_CHUNK * wpk)[CBFT_KEY_CHUNK * 32u +
+                                                                                       (key & (CBFT_KEY_CHUNK - 1))] != 0;
+  }
+#endif
+};
+inline size_t cbft_key_chunk_bytes(size_t wpk) { return (size_t)CBFT_KEY_CHUNK * (wpk * 4 + 32 + 1); }
+
 // One batch of signatures, all pointers in device memory.
 struct Ed25519Batch {
   size_t n;                 // signatures
-  const uint8_t* pk;        // public keys, 32 B each: key of sig i = pk[key_idx ? key_idx[i] : i]
-  const uint32_t* key_idx;  // nullable
+  const uint8_t* pk;        // per-signature keys (key_idx == nullptr): 32 B each, key of sig i = pk[i]
+  const uint32_t* key_idx;  // nullable: key of sig i = keys[key_idx[i]]
+  KeyChunks keys;           // the loaded key table (key_idx != nullptr)
   const uint8_t* sig;       // n x 64 B (R || S)
   const uint8_t* msg;       // message blob
   const uint64_t* msg_off;  // n byte offsets into msg; nullptr = fixed-length messages (below)
   const uint32_t* msg_len;  // n lengths (unused when msg_off is nullptr)
-  uint32_t nkeys;           // entries of pk when key_idx is set: key_idx[i] >= nkeys verifies false
+  uint32_t nkeys;           // keys of the table when key_idx is set: key_idx[i] >= nkeys verifies false
   uint32_t fixed_len;       // msg_off == nullptr: message i = msg[i * fixed_len, (i + 1) * fixed_len)
 };
 // Messages longer than this verify false (SHA-512's 64 + len byte count must not wrap 32 bits).
@@ -81,12 +108,11 @@ inline CombLadder cbft_comb_ladder(int wa, int wb) {
 // Device work buffers of one verify launch.
 struct Ed25519Work {
   const uint32_t* base_table;  // cbft_ed25519_base_table_words() words
-  const uint32_t* tbl;         // windowed -A tables, indexed like pk (per-signature key mode)
-  const uint32_t* comb_tbl;    // comb tables of -A per key (key-table mode; tbl unused)
-  const uint32_t* base_comb;   // comb table of B
+  const uint32_t* tbl;         // windowed -A tables per signature (per-signature key mode)
+  const uint32_t* base_comb;   // comb table of B (key-table mode; the -A combs are in Batch::keys)
   CombLadder comb;             // their geometry
   int finish_batch;            // signatures per lane sharing one inversion in K4 (2/4/8/16; else 1)
-  const uint8_t* aok;          // A decoded OK, indexed like pk
+  const uint8_t* aok;          // A decoded OK per signature (per-signature key mode)
   uint32_t* h_soa;             // 8 x n words
   uint8_t* flags;              // n bytes
   uint32_t* xyz_soa;           // 27 x n words

@@ -204,6 +204,11 @@ __device__ __forceinline__ uint32_t batch_unit(const Ed25519Batch& b, size_t i) 
   return k < b.nkeys ? k : 0u;
 }
 
+// A decoded (the key's or the signature's own)
+__device__ __forceinline__ bool unit_aok(const Ed25519Batch& b, const uint8_t* aok, uint32_t unit) {
+  return b.key_idx ? b.keys.aok(unit) : aok[unit] != 0;
+}
+
 __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const Ed25519Batch b, uint32_t* h_soa,
                                                                           uint8_t* flags) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -211,7 +216,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const E
   const uint32_t key = batch_unit(b, i);
   const bool key_ok = !b.key_idx || b.key_idx[i] < b.nkeys;
   uint32_t Aw[8], Rw[8], Sw[8];
-  load_words8(Aw, b.pk + (size_t)key * 32);
+  load_words8(Aw, b.key_idx ? b.keys.pk(key) : b.pk + (size_t)key * 32);
   load_words8(Rw, b.sig + i * 64);
   load_words8(Sw, b.sig + i * 64 + 32);
   const uint8_t* m = b.msg_off ? b.msg + b.msg_off[i] : b.msg + i * (size_t)b.fixed_len;
@@ -357,7 +362,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_finish_kernel(const
 #pragma unroll
     for (int k = 0; k < 8; k++) diff |= Rp[k] ^ Rw[k];
     const uint32_t unit = batch_unit(b, i);
-    verdict = (diff == 0) && flags[i] && aok[unit];
+    verdict = (diff == 0) && flags[i] && unit_aok(b, aok, unit);
   }
   const uint64_t ballot = __ballot(verdict);
   if ((threadIdx.x & 63) == 0 && i < b.n) verdict_words[i >> 6] = ballot;
@@ -391,7 +396,7 @@ __global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519B
     if (i < b.n) {
       fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
       const uint32_t unit = batch_unit(b, i);
-      ok = flags[i] && aok[unit] && !fe_iszero(Z);
+      ok = flags[i] && unit_aok(b, aok, unit) && !fe_iszero(Z);
       if (!ok) fe_1(Z);
     }
     okmask |= (ok ? 1u : 0u) << j;
@@ -621,8 +626,8 @@ __device__ __forceinline__ void add256(uint32_t* s, const uint32_t* off) {
 #endif
 
 __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
-    ed25519_comb_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* atbl,
-                               const uint32_t* btbl, const CombLadder cl, uint32_t* xyz_soa) {
+    ed25519_comb_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* btbl,
+                               const CombLadder cl, uint32_t* xyz_soa) {
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t q = threadIdx.x & 3u;
   size_t i = g >> 2;
@@ -659,7 +664,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
       sdig[jj][threadIdx.x] = (uint16_t)(d + 32768);
     }
   }
-  const uint32_t* akey = atbl + (size_t)batch_unit(b, i) * cl.a.words_per_unit();
+  const uint32_t* akey = b.keys.comb(batch_unit(b, i));
   auto entry = [&](uint32_t jj, int d) {
     const uint32_t k = first + jj;
     const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
@@ -780,7 +785,7 @@ hipError_t cbft_ed25519_launch_prep(const uint8_t* d_pk, size_t nunits, uint32_t
 hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& w, hipStream_t stream,
                                       hipEvent_t* ev, const StageOrder* order) {
   if (b.n == 0) return hipSuccess;
-  const bool comb = w.comb_tbl && w.base_comb && b.key_idx;
+  const bool comb = b.keys.chunk && w.base_comb && b.key_idx;
   if (comb && (w.comb.nper < 1 || w.comb.nper > COMB_MAX_STEPS || 4 * w.comb.nper < w.comb.a.npos + w.comb.b.npos))
     return hipErrorInvalidValue;
   const dim3 grid(grid_for(b.n)), block(CBFT_VERIFY_BLOCK);
@@ -794,7 +799,7 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   if (ev) (void)hipEventRecord(ev[1], stream);
   if (comb) {
     hipLaunchKernelGGL(ed25519_comb_ladder_kernel, dim3((unsigned)((4 * b.n + CBFT_VERIFY_BLOCK - 1) / CBFT_VERIFY_BLOCK)),
-                       block, 0, stream, b, w.h_soa, w.comb_tbl, w.base_comb, w.comb, w.xyz_soa);
+                       block, 0, stream, b, w.h_soa, w.base_comb, w.comb, w.xyz_soa);
   } else {
     hipLaunchKernelGGL(ed25519_ladder_kernel, grid, block, 0, stream, b, w.h_soa, w.tbl, w.base_table, w.xyz_soa);
   }

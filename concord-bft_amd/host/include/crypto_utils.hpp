@@ -160,6 +160,10 @@ bool fromHex(const std::string& hex, std::vector<uint8_t>& out);
 bool parseEd25519PublicKey(const std::string& s, KeyFormat fmt, uint8_t out[32]);
 std::string ed25519PublicKeyToPem(const uint8_t raw[32]);
 
+// Number of GPU batches the Ed25519 engine has run for coalesced single verify() calls
+// (instrumentation: N concurrent verify() calls complete in fewer than N batches).
+uint64_t ed25519EngineBatches();
+
 // Selects the GPU the engine opens (default 0; CBFT_DEVICE env var overrides).  Must be called
 // before the first verifier is constructed.
 void setEd25519Device(int device);

@@ -1,0 +1,157 @@
+// Batch extraction from the reference's wire formats: the
+// serial per-request signature loops of bftengine, each replaced by a walk over the message
+// bytes that applies the reference's non-cryptographic checks per request and then verifies every
+// signature with ONE SigManager::verifySigBatch call.
+//
+//   ClientRequestMsg::validateImp        ClientRequestMsg.cpp:99-214   (per request: size, ids,
+//                                        expected signature length, HAS_PRE_PROCESSED_FLAG skip,
+//                                        expectedMsgSize; signed region = the request payload,
+//                                        ClientRequestMsg.hpp:65, signature after the cid,
+//                                        ClientRequestMsg.cpp:242-248)
+//   PrePrepareMsg::validate's loop       PrePrepareMsg.cpp:116-125 over RequestsIterator
+//                                        (PrePrepareMsg.cpp:258-350); the loop throws at the first
+//                                        invalid request
+//   ClientBatchRequestMsg                ClientBatchRequestMsg.cpp (checkElements, then one
+//                                        ClientRequestMsg per element) validated by
+//                                        PreProcessor::checkClientBatchMsgCorrectness
+//                                        (PreProcessor.cpp:557-590): every element is validated,
+//                                        the loop does not stop at an invalid one
+//   PreProcessResultMsg::validatePreProcessResultSignatures  PreProcessResultMsg.cpp:57-99: f+1
+//                                        replica signatures over SHA3-256(result || result code ||
+//                                        client id || seq num) (PreProcessResultHashCreator.hpp:19-35)
+//
+// Wire structs are packed little-endian mirrors of the reference's (ClientMsgs.hpp:23-50,
+// PrePrepareMsg.hpp:33-53, MessageBase.hpp:30-33).  Outcomes equal the serial reference loop's:
+// the same request fails first with the same kind of error, and SigManager's counters move for
+// exactly the signatures the serial loop would have verified.
+#pragma once
+
+#include <cstdint>
+#include <optional>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "sig_manager.hpp"
+
+namespace bftEngine::impl {
+
+#pragma pack(push, 1)
+struct MessageBaseHeader {  // MessageBase.hpp:30-33
+  uint16_t msgType;
+  uint32_t spanContextSize;
+};
+
+struct ClientRequestMsgHeader {  // ClientMsgs.hpp:33-50
+  uint16_t msgType;              // REQUEST_MSG_TYPE (700)
+  uint32_t spanContextSize;
+  uint16_t idOfClientProxy;
+  uint64_t flags;
+  uint32_t result;
+  uint64_t reqSeqNum;
+  uint32_t requestLength;
+  uint64_t timeoutMilli;
+  uint32_t cidLength;
+  uint16_t reqSignatureLength;
+  uint32_t extraDataLength;
+};
+
+struct ClientBatchRequestMsgHeader {  // ClientMsgs.hpp:25-31
+  uint16_t msgType;                   // BATCH_REQUEST_MSG_TYPE (750)
+  uint32_t cidSize;
+  uint16_t clientId;
+  uint32_t numOfMessagesInBatch;
+  uint32_t dataSize;
+};
+
+struct PrePrepareMsgHeader {  // PrePrepareMsg.hpp:34-46
+  MessageBaseHeader header;
+  int64_t viewNum;
+  int64_t seqNum;
+  int64_t epochNum;
+  uint16_t flags;
+  uint64_t batchCidLength;
+  int64_t time;
+  uint8_t digestOfRequests[32];
+  uint16_t numberOfRequests;
+  uint32_t endLocationOfLastRequest;
+};
+#pragma pack(pop)
+static_assert(sizeof(ClientRequestMsgHeader) == 50, "ClientRequestMsgHeader is 50 B");
+static_assert(sizeof(ClientBatchRequestMsgHeader) == 16, "ClientBatchRequestMsgHeader is 16 B");
+static_assert(sizeof(PrePrepareMsgHeader) == 86, "PrePrepareMsg::Header is 86 B");
+
+// Flag bits (Replica.hpp:44-51, SimpleClient.hpp:43-51)
+enum : uint64_t {
+  READ_ONLY_REQ = 0x1,
+  PRE_PROCESS_REQ = 0x2,
+  HAS_PRE_PROCESSED_FLAG = 0x4,
+  KEY_EXCHANGE_FLAG = 0x8,
+  EMPTY_CLIENT_REQ = 0x10,
+  RECONFIG_FLAG = 0x20,
+};
+constexpr uint32_t kMaxClientBatchSize = 1024;  // MAX_BATCH_SIZE of ClientBatchRequestMsg::checkElements
+
+// Total size of a packed ClientRequestMsg as the reference computes it (compRequestMsgSize,
+// ClientRequestMsg.cpp:26-29), from its header.
+uint64_t clientRequestMsgSize(const ClientRequestMsgHeader& h);
+
+// One ClientRequestMsg to validate: its bytes [body, body + size) (size = the message's size(),
+// for an embedded request = clientRequestMsgSize) and its sender (the node the message came from;
+// for a request embedded in a PrePrepare the reference uses idOfClientProxy, ClientRequestMsg.cpp:24).
+struct ClientRequestView {
+  const char* body;
+  uint64_t size;
+  PrincipalId senderId;
+};
+
+// Outcome of validating a list of requests: ok[i] = validate() of request i would not throw;
+// error[i] = the message it would throw with (empty when ok).  firstFailure = index of the first
+// request that fails (or size when all pass).
+struct RequestValidation {
+  std::vector<bool> ok;
+  std::vector<std::string> error;
+  size_t firstFailure = 0;
+};
+
+// ClientRequestMsg::validateImp over many requests with one signature batch.  stopAtFirstFailure
+// = the caller's loop throws at the first invalid request (PrePrepareMsg::validate): requests after
+// it are not validated and their signatures not counted.  Otherwise (PreProcessor's client batch
+// loop) every request is validated and counted.
+RequestValidation validateClientRequests(const std::vector<ClientRequestView>& reqs, const ReplicasInfo& repInfo,
+                                         const SigManager& sigManager, bool stopAtFirstFailure);
+
+// PrePrepareMsg::validate's request loop (PrePrepareMsg.cpp:116-125) for the PrePrepare message
+// bytes [body, body + size): the requests between payloadShift() and endLocationOfLastRequest,
+// numberOfRequests of them (checkRequests, PrePrepareMsg.cpp:258-306, must hold: else
+// std::runtime_error("... advanced")).  With client transaction signing enabled, every embedded
+// request is validated as ClientRequestMsg::validate; throws std::runtime_error with the first
+// failing request's error, exactly where the serial loop would.  Returns the number of requests.
+size_t validatePrePrepareRequests(const char* body, uint64_t size, const ReplicasInfo& repInfo,
+                                  const SigManager& sigManager);
+
+// The requests of a ClientBatchRequestMsg [body, body + size) (ClientBatchRequestMsg.cpp:
+// checkElements, then getClientPreProcessRequestMsgs): throws std::runtime_error if the batch
+// itself is malformed (ClientBatchRequestMsg::validate); else validates every element like
+// PreProcessor::checkClientBatchMsgCorrectness does (all of them, in one signature batch) and
+// returns the per-element outcome.
+RequestValidation validateClientBatchRequestMsg(const char* body, uint64_t size, const ReplicasInfo& repInfo,
+                                                const SigManager& sigManager);
+
+// PreProcessResultMsg::validatePreProcessResultSignatures (PreProcessResultMsg.cpp:57-99) for the
+// ClientRequestMsg-format message [body, body + size) whose extra data holds the serialized result
+// signatures (sender u16 BE, result u32 BE, length u32 BE, signature; PreProcessResultMsg.cpp:
+// 101-160).  Returns the reference's error text, or nullopt when all f+1 signatures verify (own
+// signature: recomputed and compared, as there).  Throws std::runtime_error on a malformed
+// signature buffer (deserializeResultSignatures).
+std::optional<std::string> validatePreProcessResultSignatures(const char* body, uint64_t size, ReplicaId myReplicaId,
+                                                              int16_t fVal, const SigManager& sigManager);
+
+// SHA3-256(result bytes (only when resultCode == SUCCESS = 0) || resultCode u32 || clientId u16
+// || reqSeqNum u64), host byte order as the reference's update(&x, sizeof x)
+// (PreProcessResultHashCreator.hpp:21-34).
+std::string preProcessResultHash(const char* result, uint32_t len, uint32_t resultCode, uint16_t clientId,
+                                 uint64_t reqSeqNum);
+
+}  // namespace bftEngine::impl

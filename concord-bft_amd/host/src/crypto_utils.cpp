@@ -3,8 +3,12 @@
 
 #include <openssl/evp.h>
 
+#include <algorithm>
+#include <atomic>
+#include <condition_variable>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <map>
 #include <mutex>
 #include <shared_mutex>
@@ -114,12 +118,38 @@ std::string ed25519PublicKeyToPem(const uint8_t raw[32]) {
 static int g_device = -1;
 void setEd25519Device(int device) { g_device = device; }
 
-// Per-process owner of the GPU context and of the device key table.  Keys are registered when a
-// verifier is constructed (deduplicated: equal keys share an index, as SigManager shares one
-// verifier object between principals with the same key, SigManager.cpp:139-150); the device
-// table is rebuilt lazily before the first batch that needs a newly registered key.
+// Comb radix of the engine's key table, chosen once for the expected number of keys
+// ($CBFT_EXPECTED_KEYS, default 4,096) against a 64 GB budget of the 288 GB HBM (the library's
+// own rule for a table loaded in one go, cbft_hipcrypto.cpp key_radix): radix 13 (10.5 MB per
+// key) up to ~6,100 keys, 11 (3.0 MB) up to ~21,000, then 8 (0.53 MB).
+static int engineRadix() {
+  if (const char* e = std::getenv("CBFT_COMB_RADIX")) return std::atoi(e);
+  double keys = 4096;
+  if (const char* e = std::getenv("CBFT_EXPECTED_KEYS")) keys = std::atof(e);
+  auto bytes_per_key = [](int w, int npos) { return (double)npos * ((1 << (w - 1)) + 1) * 128.0; };
+  if (keys * bytes_per_key(13, 20) <= 64e9) return 13;
+  if (keys * bytes_per_key(11, 23) <= 64e9) return 11;
+  return 8;
+}
+
+// Per-process owner of the GPU context and of the device key table.
+//
+// Keys are registered when a verifier is constructed (deduplicated: equal keys share an index,
+// as SigManager shares one verifier object between principals with the same key,
+// SigManager.cpp:139-150).  A registered key is appended to the device table (its comb table
+// built alone; the keys already loaded are untouched) before the first batch that needs it;
+// batches that only name loaded keys never wait for an append.
+//
+// verifyOne() coalesces concurrent single verifies (the reference calls IVerifier::verify from
+// 40 + 24 pool threads, ReplicaConfig.hpp:202-212): callers queue their request; one of them
+// leads a batch as soon as fewer than kMaxInflight batches are on the GPU, taking everything
+// queued by then.  A lone caller goes straight to the GPU; under load, requests that arrive
+// while batches run are verified together in the next one.
 class Ed25519Engine {
  public:
+  static constexpr int kMaxInflight = 2;
+  static constexpr size_t kMaxBatch = 65536;
+
   static std::shared_ptr<Ed25519Engine> get() {
     static std::mutex m;
     static std::weak_ptr<Ed25519Engine> inst;
@@ -136,7 +166,7 @@ class Ed25519Engine {
   }
 
   uint32_t registerKey(const uint8_t raw[32]) {
-    std::lock_guard<std::mutex> g(mu_);
+    std::lock_guard<std::mutex> g(keys_mu_);
     std::string k(reinterpret_cast<const char*>(raw), 32);
     auto it = index_.find(k);
     if (it != index_.end()) return it->second;
@@ -146,18 +176,22 @@ class Ed25519Engine {
     return idx;
   }
 
+  // One GPU batch; out[i] = verdict of reqs[i] (false for non-Ed25519 verifiers).
   void verify(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out) {
     out.assign(reqs.size(), false);
-    // signatures of the wrong length are rejected without a GPU round trip (EVP returns 0)
+    // wrong-length signatures (EVP returns 0) and messages the kernel's 32-bit SHA-512 length
+    // cannot hold (> CBFT's 0xFFFFFF00 bytes) are rejected without a GPU round trip
     std::vector<size_t> pos;
     pos.reserve(reqs.size());
     size_t blob = 0;
+    uint32_t maxKey = 0;
     std::vector<const EdDSAVerifier*> ver(reqs.size(), nullptr);
     for (size_t i = 0; i < reqs.size(); i++) {
       ver[i] = dynamic_cast<const EdDSAVerifier*>(reqs[i].verifier);
-      if (reqs[i].sigLength == 64 && ver[i]) {
+      if (reqs[i].sigLength == 64 && ver[i] && reqs[i].dataLength <= kMaxMsg) {
         pos.push_back(i);
         blob += reqs[i].dataLength;
+        maxKey = std::max(maxKey, ver[i]->engineKeyIndex());
       }
     }
     if (pos.empty()) return;
@@ -175,22 +209,7 @@ class Ed25519Engine {
       if (r.dataLength) std::memcpy(&msg[o], r.data, r.dataLength);
       o += r.dataLength;
     }
-    // the device table must cover every registered key; a rebuild (new key) takes the table
-    // lock exclusively, verifies hold it shared for the duration of the GPU call
-    std::shared_lock<std::shared_mutex> rd(tbl_mu_);
-    while (true) {
-      {
-        std::lock_guard<std::mutex> g(mu_);
-        if (loaded_ == keys_.size() / 32 && table_ != CBFT_NO_KEY_TABLE) break;
-      }
-      rd.unlock();
-      {
-        std::unique_lock<std::shared_mutex> wr(tbl_mu_);
-        std::lock_guard<std::mutex> g(mu_);
-        ensureTableLocked();
-      }
-      rd.lock();
-    }
+    ensureLoaded(maxKey);
     int rc = cbft_ed25519_verify_batch(ctx_, table_, kidx.data(), sig.data(), msg.data(), off.data(), len.data(), n,
                                        bitmap.data());
     if (rc != CBFT_OK)
@@ -199,7 +218,65 @@ class Ed25519Engine {
     for (size_t j = 0; j < n; j++) out[pos[j]] = (bitmap[j >> 3] >> (j & 7)) & 1;
   }
 
+  bool verifyOne(const EdDSAVerifier* v, const char* data, size_t len, const char* sig, size_t sigLen) {
+    if (sigLen != 64 || len > kMaxMsg) return false;
+    Pending p{v, data, len, sig, sigLen};
+    std::unique_lock<std::mutex> lk(q_mu_);
+    queue_.push_back(&p);
+    while (!p.done) {
+      if (!leader_ && !queue_.empty()) {
+        leader_ = true;
+        q_cv_.wait(lk, [&] { return inflight_ < kMaxInflight || queue_.size() >= kMaxBatch; });
+        std::vector<Pending*> batch;
+        batch.swap(queue_);
+        leader_ = false;
+        inflight_++;
+        q_cv_.notify_all();  // the next arrival (or a waiter) may lead the next batch
+        lk.unlock();
+        runBatch(batch);
+        lk.lock();
+        inflight_--;
+        for (Pending* q : batch) q->done = true;
+        q_cv_.notify_all();
+      } else {
+        q_cv_.wait(lk);
+      }
+    }
+    lk.unlock();
+    if (p.err) std::rethrow_exception(p.err);
+    return p.verdict;
+  }
+
+  uint64_t batchesRun() const { return batches_.load(); }
+
  private:
+  static constexpr size_t kMaxMsg = 0xFFFFFF00u;
+  struct Pending {
+    const EdDSAVerifier* v;
+    const char* data;
+    size_t len;
+    const char* sig;
+    size_t sigLen;
+    bool done = false;
+    bool verdict = false;
+    std::exception_ptr err;
+  };
+
+  void runBatch(std::vector<Pending*>& batch) {
+    std::vector<VerifyRequest> reqs(batch.size());
+    for (size_t i = 0; i < batch.size(); i++)
+      reqs[i] = {batch[i]->v, batch[i]->data, batch[i]->len, batch[i]->sig, batch[i]->sigLen};
+    std::vector<bool> out;
+    try {
+      verify(reqs, out);
+      for (size_t i = 0; i < batch.size(); i++) batch[i]->verdict = out[i];
+    } catch (...) {
+      auto e = std::current_exception();
+      for (Pending* q : batch) q->err = e;
+    }
+    batches_++;
+  }
+
   Ed25519Engine() {
     int dev = g_device;
     if (dev < 0) {
@@ -207,31 +284,47 @@ class Ed25519Engine {
       dev = e ? std::atoi(e) : 0;
     }
     int rc = cbft_open(&ctx_, dev, 0);
+    if (rc == CBFT_OK) rc = cbft_ed25519_load_keys_ex(ctx_, nullptr, 0, engineRadix(), &table_);
     if (rc != CBFT_OK)
-      throw std::runtime_error(std::string("cbft_open: ") + cbft_strerror(rc) + " " + cbft_last_error());
+      throw std::runtime_error(std::string("Ed25519 engine: ") + cbft_strerror(rc) + " " + cbft_last_error());
   }
 
-  void ensureTableLocked() {
-    const uint32_t nkeys = (uint32_t)keys_.size() / 32;
-    if (nkeys == loaded_ && table_ != CBFT_NO_KEY_TABLE) return;
-    uint32_t id;
-    int rc = cbft_ed25519_load_keys(ctx_, keys_.data(), nkeys, &id);
-    if (rc != CBFT_OK)
-      throw std::runtime_error(std::string("cbft_ed25519_load_keys: ") + cbft_strerror(rc) + " " +
+  // Append every registered key not yet on the device, if key `need` is among them.
+  void ensureLoaded(uint32_t need) {
+    if (need < loaded_.load(std::memory_order_acquire)) return;
+    std::lock_guard<std::mutex> ag(append_mu_);
+    const uint32_t have = loaded_.load();
+    if (need < have) return;  // another thread appended it meanwhile
+    std::vector<uint8_t> fresh;
+    {
+      std::lock_guard<std::mutex> g(keys_mu_);
+      fresh.assign(keys_.begin() + (size_t)have * 32, keys_.end());
+    }
+    uint32_t first = 0;
+    const uint32_t m = (uint32_t)(fresh.size() / 32);
+    int rc = cbft_ed25519_append_keys(ctx_, table_, fresh.data(), m, &first);
+    if (rc != CBFT_OK || first != have)
+      throw std::runtime_error(std::string("cbft_ed25519_append_keys: ") + cbft_strerror(rc) + " " +
                                cbft_last_error());
-    if (table_ != CBFT_NO_KEY_TABLE) cbft_ed25519_unload_keys(ctx_, table_);
-    table_ = id;
-    loaded_ = nkeys;
+    loaded_.store(have + m, std::memory_order_release);
   }
 
   cbft_ctx* ctx_ = nullptr;
-  std::mutex mu_;                // guards keys_, index_, table_, loaded_
-  std::shared_mutex tbl_mu_;     // device table lifetime vs in-flight verifies
+  uint32_t table_ = CBFT_NO_KEY_TABLE;
+  std::mutex keys_mu_;  // guards keys_, index_
   std::vector<uint8_t> keys_;
   std::map<std::string, uint32_t> index_;
-  uint32_t table_ = CBFT_NO_KEY_TABLE;
-  uint32_t loaded_ = 0;
+  std::mutex append_mu_;  // one append at a time
+  std::atomic<uint32_t> loaded_{0};
+  std::mutex q_mu_;  // coalescing queue
+  std::condition_variable q_cv_;
+  std::vector<Pending*> queue_;
+  bool leader_ = false;
+  int inflight_ = 0;
+  std::atomic<uint64_t> batches_{0};
 };
+
+uint64_t ed25519EngineBatches() { return Ed25519Engine::get()->batchesRun(); }
 
 // ---------------------------------------------------------------------------------- verifier
 EdDSAVerifier::EdDSAVerifier(const std::string& str_pub_key, KeyFormat fmt) : key_str_(str_pub_key) {
@@ -243,10 +336,7 @@ EdDSAVerifier::EdDSAVerifier(const std::string& str_pub_key, KeyFormat fmt) : ke
 EdDSAVerifier::~EdDSAVerifier() = default;
 
 bool EdDSAVerifier::verify(const std::string& data, const std::string& sig) const {
-  std::vector<VerifyRequest> r{{this, data.data(), data.size(), sig.data(), sig.size()}};
-  std::vector<bool> out;
-  engine_->verify(r, out);
-  return out[0];
+  return engine_->verifyOne(this, data.data(), data.size(), sig.data(), sig.size());
 }
 
 void EdDSAVerifier::verifyBatch(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out) {

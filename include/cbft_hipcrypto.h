@@ -100,6 +100,16 @@ int cbft_ed25519_load_keys(cbft_ctx* ctx, const uint8_t* pk /* nkeys x 32 */, ui
 int cbft_ed25519_load_keys_ex(cbft_ctx* ctx, const uint8_t* pk, uint32_t nkeys, int comb_radix,
                               uint32_t* out_key_table_id);
 int cbft_ed25519_unload_keys(cbft_ctx* ctx, uint32_t key_table_id);
+/* Append nkeys keys to a loaded table (new client keys, key rotation: SigManager::
+ * setClientPublicKey, SigManager.cpp:250-264; KeyExchangeManager.cpp:310-320).  The keys get
+ * indices *out_first_index .. + nkeys - 1; the keys already loaded are neither moved nor rebuilt,
+ * and batches against them keep running while the new keys' tables are built (only the new
+ * indices are unusable until this call returns).  Up to 1,048,576 keys per table (CBFT_E2BIG);
+ * the table keeps the comb radix it was loaded with.  A table loaded with nkeys = 0 starts empty. */
+int cbft_ed25519_append_keys(cbft_ctx* ctx, uint32_t key_table_id, const uint8_t* pk, uint32_t nkeys,
+                             uint32_t* out_first_index);
+/* Published key count and comb radix of a table. */
+int cbft_ed25519_table_size(cbft_ctx* ctx, uint32_t key_table_id, uint32_t* out_nkeys, int* out_radix);
 
 /* Verify n signatures against keys of a loaded table (blocking: _async + cbft_wait).
  *   key_idx[i]   : index of signature i's key in the table (< nkeys, else CBFT_EINVAL)

@@ -8,14 +8,20 @@
 #include <openssl/pem.h>
 #include <openssl/rsa.h>
 
+#include <atomic>
 #include <cassert>
+#include <chrono>
 #include <cstdio>
+#include <memory>
+#include <thread>
+#include <tuple>
 #include <cstring>
 #include <random>
 #include <string>
 #include <vector>
 
 #include "crypto_utils.hpp"
+#include "request_batch.hpp"
 #include "sig_manager.hpp"
 
 using namespace concord::util::crypto;
@@ -99,26 +105,34 @@ static int testRsa() {
   CHECK(threw);
 
   // --- SigManager with RSA replicas (e = 17, as bftengine/tests/messages/helper.cpp) and RSA +
-  // Ed25519 clients in one batch: verdicts and counters as with single verifies
+  // Ed25519 clients in one batch: verdicts and counters as with single verifies.  Id space
+  // (ReplicasInfo.cpp:71-140): replicas 0..3, external clients 4..7, internal clients 8..11.
   EdDSASigner ed(seedHex(50), KeyFormat::HexaDecimalStrippedFormat);
-  ReplicasInfo ri;
-  ri.numReplicas = 4;
-  ri.externalClients = {200, 201};
-  std::vector<std::pair<std::set<PrincipalId>, std::string>> keys = {
-      {{0, 1, 2, 3}, kr.pubHex}, {{200}, kc.pubHex}, {{201}, ed.getPubKeyHex()}};
-  SigManager sm(1, {kr.privHex, KeyFormat::HexaDecimalStrippedFormat}, keys, KeyFormat::HexaDecimalStrippedFormat,
-                ri);
-  CHECK(sm.getSigLength(0) == 256 && sm.getSigLength(201) == 64 && sm.getMySigLength() == 256);
+  ReplicaIdsConfig cfg;
+  cfg.replicaId = 1;
+  cfg.numOfExternalClients = 4;
+  ReplicasInfo ri(cfg);
+  std::set<std::pair<PrincipalId, const std::string>> replicaKeys;
+  for (PrincipalId r = 0; r < 4; r++) replicaKeys.insert({r, kr.pubHex});
+  std::set<std::pair<const std::string, std::set<uint16_t>>> clientKeys = {{kc.pubHex, {4}}, {ed.getPubKeyHex(), {5}}};
+  std::unique_ptr<SigManager> smp(SigManager::initInTesting(1, kr.privHex, replicaKeys,
+                                                            KeyFormat::HexaDecimalStrippedFormat, &clientKeys,
+                                                            KeyFormat::HexaDecimalStrippedFormat, ri));
+  SigManager& sm = *smp;
+  const PrincipalId C_RSA = 4, C_ED = 5;
+  CHECK(sm.getSigLength(0) == 256 && sm.getSigLength(C_ED) == 64 && sm.getMySigLength() == 256);
+  CHECK(sm.getSigLength(1) == 256);  // own id: this replica's signer (SigManager.cpp:183-186)
+  CHECK(sm.isClientTransactionSigningEnabled());
   RSASigner sr(kr.privHex, KeyFormat::HexaDecimalStrippedFormat);
   std::vector<std::string> datas, sigs;
   std::vector<PrincipalId> who;
   std::vector<bool> expect;
   std::mt19937 g(17);
   for (int i = 0; i < 120; i++) {
-    const PrincipalId p = (i % 3 == 0) ? (PrincipalId)(i % 4) : (i % 3 == 1 ? 200 : 201);
+    const PrincipalId p = (i % 3 == 0) ? (PrincipalId)(i % 4) : (i % 3 == 1 ? C_RSA : C_ED);
     std::string d(1 + g() % 400, '\0');
     for (auto& ch : d) ch = (char)g();
-    std::string s = p < 4 ? sr.sign(d) : (p == 200 ? sc.sign(d) : ed.sign(d));
+    std::string s = p < 4 ? sr.sign(d) : (p == C_RSA ? sc.sign(d) : ed.sign(d));
     bool ok = true;
     if (i % 5 == 0) {
       d[0]++;
@@ -154,6 +168,258 @@ static int testRsa() {
   return 0;
 }
 
+// ------------------------------------------------------------------ reference wire formats
+// A packed ClientRequestMsg: header (ClientMsgs.hpp:33-50) | span | request | cid | sig | extra
+static std::string clientRequest(uint16_t client, uint64_t flags, uint64_t seq, const std::string& req,
+                                 const std::string& cid, const std::string& sig, const std::string& extra = "") {
+  ClientRequestMsgHeader h{};
+  h.msgType = 700;
+  h.idOfClientProxy = client;
+  h.flags = flags;
+  h.result = 1;
+  h.reqSeqNum = seq;
+  h.requestLength = (uint32_t)req.size();
+  h.cidLength = (uint32_t)cid.size();
+  h.reqSignatureLength = (uint16_t)sig.size();
+  h.extraDataLength = (uint32_t)extra.size();
+  return std::string(reinterpret_cast<const char*>(&h), sizeof h) + req + cid + sig + extra;
+}
+
+// A PrePrepareMsg (PrePrepareMsg.hpp:33-53) carrying the given packed requests
+static std::string prePrepare(const std::vector<std::string>& reqs) {
+  PrePrepareMsgHeader h{};
+  h.header.msgType = 3;
+  h.seqNum = 1;
+  h.flags = 0x3;
+  const std::string cid = "batch-cid";
+  h.batchCidLength = cid.size();
+  h.numberOfRequests = (uint16_t)reqs.size();
+  std::string body;
+  for (auto& r : reqs) body += r;
+  h.endLocationOfLastRequest = (uint32_t)(sizeof h + cid.size() + body.size());
+  return std::string(reinterpret_cast<const char*>(&h), sizeof h) + cid + body;
+}
+
+static std::string clientBatch(uint16_t sender, const std::vector<std::string>& reqs) {
+  ClientBatchRequestMsgHeader h{};
+  h.msgType = 750;
+  const std::string cid = "cb";
+  h.cidSize = (uint32_t)cid.size();
+  h.clientId = sender;
+  h.numOfMessagesInBatch = (uint32_t)reqs.size();
+  std::string body;
+  for (auto& r : reqs) body += r;
+  h.dataSize = (uint32_t)body.size();
+  return std::string(reinterpret_cast<const char*>(&h), sizeof h) + cid + body;
+}
+
+static uint64_t verifiedTotal(const SigManager& sm) {
+  const auto& m = sm.metrics();
+  return m.external_client_request_signatures_verified + m.external_client_request_signature_verification_failed +
+         m.peer_replicas_signatures_verified + m.peer_replicas_signature_verification_failed;
+}
+
+// Message-level batch checks (request_batch.hpp) against what the reference's serial loops do.
+template <class SignerOf>
+static int testMessages(SigManager& sm, const ReplicasInfo& ri, std::vector<EdDSASigner>& signers, SignerOf signerOf) {
+  (void)signers;
+  std::mt19937 g(99);
+  auto payload = [&](size_t n) {
+    std::string p(n, '\0');
+    for (auto& ch : p) ch = (char)g();
+    return p;
+  };
+  // 60 requests from clients 4..11 (client 8's key was rotated above: it signs with seed 99)
+  EdDSASigner rotated(seedHex(99), KeyFormat::HexaDecimalStrippedFormat);
+  std::vector<std::string> reqs;
+  std::vector<std::string> payloads;
+  for (int i = 0; i < 60; i++) {
+    const uint16_t c = (uint16_t)(4 + i % 8);
+    std::string p = payload(32 + (size_t)(g() % 900));
+    EdDSASigner& s = c == 8 ? rotated : signerOf(c);
+    reqs.push_back(clientRequest(c, 0, 1000 + i, p, "cid-" + std::to_string(i), s.sign(p)));
+    payloads.push_back(p);
+  }
+  // (1) a valid PrePrepare: every signature verified in one batch
+  uint64_t before = verifiedTotal(sm);
+  std::string pp = prePrepare(reqs);
+  CHECK(validatePrePrepareRequests(pp.data(), pp.size(), ri, sm) == 60);
+  CHECK(verifiedTotal(sm) - before == 60);
+  // (2) a bad signature at request 23: throws there; the serial loop verified 0..23 only
+  {
+    std::vector<std::string> r2 = reqs;
+    r2[23][sizeof(ClientRequestMsgHeader) + 5] ^= 1;  // a payload byte: the signature no longer matches
+    std::string pp2 = prePrepare(r2);
+    before = verifiedTotal(sm);
+    const uint64_t failBefore = sm.metrics().external_client_request_signature_verification_failed;
+    bool threw = false;
+    try {
+      validatePrePrepareRequests(pp2.data(), pp2.size(), ri, sm);
+    } catch (const std::runtime_error& e) {
+      threw = std::string(e.what()).find("Signature verification failed") != std::string::npos;
+    }
+    CHECK(threw);
+    CHECK(verifiedTotal(sm) - before == 24);
+    CHECK(sm.metrics().external_client_request_signature_verification_failed - failBefore == 1);
+  }
+  // (3) a wrong signature length at request 10 and a bad signature at 40: the length error wins
+  // and no signature after request 9 is counted
+  {
+    std::vector<std::string> r3 = reqs;
+    r3[10] = clientRequest(5, 0, 7, payloads[10], "x", std::string(63, 'a'));
+    r3[40][sizeof(ClientRequestMsgHeader) + 2] ^= 1;
+    std::string pp3 = prePrepare(r3);
+    before = verifiedTotal(sm);
+    std::string what;
+    try {
+      validatePrePrepareRequests(pp3.data(), pp3.size(), ri, sm);
+    } catch (const std::runtime_error& e) {
+      what = e.what();
+    }
+    CHECK(what.find("Unexpected request signature length") != std::string::npos);
+    CHECK(verifiedTotal(sm) - before == 10);
+  }
+  // (4) HAS_PRE_PROCESSED_FLAG: the signature length is still checked, the signature is not
+  // verified (ClientRequestMsg.cpp:172-174); an empty request carries no signature
+  {
+    std::vector<std::string> r4 = {reqs[0], clientRequest(6, HAS_PRE_PROCESSED_FLAG, 5, "payload", "c",
+                                                          std::string(64, '\x01')),
+                                   clientRequest(7, 0, 6, "", "c", "")};
+    std::string pp4 = prePrepare(r4);
+    before = verifiedTotal(sm);
+    CHECK(validatePrePrepareRequests(pp4.data(), pp4.size(), ri, sm) == 3);
+    CHECK(verifiedTotal(sm) - before == 1);
+  }
+  // (5) structural errors: a request count that does not match the bytes
+  {
+    std::string pp5 = prePrepare(reqs);
+    PrePrepareMsgHeader h;
+    std::memcpy(&h, pp5.data(), sizeof h);
+    h.numberOfRequests = 61;
+    std::memcpy(&pp5[0], &h, sizeof h);
+    bool threw = false;
+    try {
+      validatePrePrepareRequests(pp5.data(), pp5.size(), ri, sm);
+    } catch (const std::runtime_error& e) {
+      threw = std::string(e.what()).find("advanced") != std::string::npos;
+    }
+    CHECK(threw);
+  }
+  // (6) a client batch (PreProcessor::checkClientBatchMsgCorrectness): every element validated,
+  // the bad ones reported individually, every signature counted
+  {
+    std::vector<std::string> r6(reqs.begin(), reqs.begin() + 10);
+    r6[3][sizeof(ClientRequestMsgHeader) + 1] ^= 1;
+    r6[8][sizeof(ClientRequestMsgHeader) + 1] ^= 1;
+    std::string cb = clientBatch(4, r6);
+    before = verifiedTotal(sm);
+    RequestValidation v = validateClientBatchRequestMsg(cb.data(), cb.size(), ri, sm);
+    CHECK(v.ok.size() == 10 && v.firstFailure == 3);
+    for (int i = 0; i < 10; i++) CHECK(v.ok[i] == (i != 3 && i != 8));
+    CHECK(verifiedTotal(sm) - before == 10);
+    std::string bad = clientBatch(4, {clientRequest(5, 0, 1, "p", "c", std::string(10, 'x'))});
+    bool threw = false;
+    try {
+      validateClientBatchRequestMsg(bad.data(), bad.size(), ri, sm);
+    } catch (const std::runtime_error&) {
+      threw = true;
+    }
+    CHECK(threw);  // checkElements: signature length != getSigLength(client)
+  }
+  return 0;
+}
+
+// PreProcessResultMsg::validatePreProcessResultSignatures with f + 1 = 2 replica signatures.
+static int testPreProcessResult(const SigManager& sm, std::vector<EdDSASigner>& signers) {
+  const std::string result = "pre-execution result bytes";
+  const uint16_t client = 5;
+  const uint64_t seq = 77;
+  const std::string hash = preProcessResultHash(result.data(), (uint32_t)result.size(), 0, client, seq);
+  auto ser = [](const std::vector<std::tuple<uint16_t, uint32_t, std::string>>& sigs) {
+    std::string o;
+    for (auto& [sender, res, sig] : sigs) {
+      o += (char)(sender >> 8);
+      o += (char)sender;
+      for (int k = 3; k >= 0; k--) o += (char)(res >> (8 * k));
+      const uint32_t l = (uint32_t)sig.size();
+      for (int k = 3; k >= 0; k--) o += (char)(l >> (8 * k));
+      o += sig;
+    }
+    return o;
+  };
+  auto msg = [&](const std::string& extra) { return clientRequest(client, 0, seq, result, "cid", "", extra); };
+  std::string good = msg(ser({{2, 0, signers[2].sign(hash)}, {1, 0, signers[1].sign(hash)}}));
+  CHECK(!validatePreProcessResultSignatures(good.data(), good.size(), 3, 1, sm).has_value());
+  // own signature (replica 0 = this SigManager's signer) is recomputed and compared
+  std::string own = msg(ser({{0, 0, signers[0].sign(hash)}, {3, 0, signers[3].sign(hash)}}));
+  CHECK(!validatePreProcessResultSignatures(own.data(), own.size(), 0, 1, sm).has_value());
+  std::string badsig = signers[1].sign(hash);
+  badsig[7] ^= 1;
+  std::string bad = msg(ser({{2, 0, signers[2].sign(hash)}, {1, 0, badsig}}));
+  auto r = validatePreProcessResultSignatures(bad.data(), bad.size(), 3, 1, sm);
+  CHECK(r.has_value() && r->find("invalid signature") != std::string::npos);
+  std::string three = msg(ser({{1, 0, signers[1].sign(hash)}, {2, 0, signers[2].sign(hash)},
+                               {3, 0, signers[3].sign(hash)}}));
+  r = validatePreProcessResultSignatures(three.data(), three.size(), 0, 1, sm);
+  CHECK(r.has_value() && r->find("unexpected number") != std::string::npos);
+  std::string dup = msg(ser({{2, 0, signers[2].sign(hash)}, {2, 0, signers[2].sign(hash)}}));  // a set: one sender
+  r = validatePreProcessResultSignatures(dup.data(), dup.size(), 0, 1, sm);
+  CHECK(r.has_value());
+  return 0;
+}
+
+// 64 threads call EdDSAVerifier::verify concurrently (the reference's pool threads) while new
+// client keys are registered: verdicts exact, calls coalesced into fewer GPU batches.
+static int testConcurrent() {
+  const int T = 64, K = 24;
+  std::vector<std::unique_ptr<EdDSASigner>> sg;
+  std::vector<std::unique_ptr<EdDSAVerifier>> vf;
+  for (int k = 0; k < 8; k++) {
+    sg.emplace_back(new EdDSASigner(seedHex(300 + k), KeyFormat::HexaDecimalStrippedFormat));
+    vf.emplace_back(new EdDSAVerifier(sg.back()->getPubKeyHex(), KeyFormat::HexaDecimalStrippedFormat));
+  }
+  std::vector<std::vector<std::string>> msgs(T), sigs(T);
+  std::vector<std::vector<bool>> expect(T);
+  for (int t = 0; t < T; t++) {
+    std::mt19937 g(5000 + t);
+    for (int k = 0; k < K; k++) {
+      std::string m(16 + g() % 500, '\0');
+      for (auto& ch : m) ch = (char)g();
+      std::string s = sg[(t + k) % 8]->sign(m);
+      const bool ok = (t * K + k) % 9 != 0;
+      if (!ok) s[3] ^= 0x20;
+      msgs[t].push_back(m);
+      sigs[t].push_back(s);
+      expect[t].push_back(ok);
+    }
+  }
+  std::atomic<int> bad{0};
+  const uint64_t b0 = ed25519EngineBatches();
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<std::thread> th;
+  for (int t = 0; t < T; t++)
+    th.emplace_back([&, t] {
+      for (int k = 0; k < K; k++)
+        if (vf[(t + k) % 8]->verify(msgs[t][k], sigs[t][k]) != expect[t][k]) bad++;
+    });
+  // meanwhile: new clients join (keys appended to the live device table)
+  std::vector<std::unique_ptr<EdDSAVerifier>> late;
+  for (int k = 0; k < 6; k++) {
+    EdDSASigner s(seedHex(400 + k), KeyFormat::HexaDecimalStrippedFormat);
+    late.emplace_back(new EdDSAVerifier(s.getPubKeyHex(), KeyFormat::HexaDecimalStrippedFormat));
+    std::string m = "late client " + std::to_string(k);
+    if (!late.back()->verify(m, s.sign(m))) bad++;
+  }
+  for (auto& x : th) x.join();
+  const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  const uint64_t batches = ed25519EngineBatches() - b0;
+  CHECK(bad == 0);
+  CHECK(batches < (uint64_t)(T * K + 6));
+  std::printf("test_host: %d concurrent verify() calls in %llu GPU batches, %.0f verifies/s\n", T * K + 6,
+              (unsigned long long)batches, (T * K + 6) / secs);
+  return 0;
+}
+
 int main() {
   if (testRsa() != 0) return 1;
   // --- IVerifier/ISigner round trip, hex and PEM key formats
@@ -181,32 +447,48 @@ int main() {
   }
   CHECK(threw);
 
-  // --- SigManager: 4 replicas + 8 clients, clients 100..103 share one key
-  ReplicasInfo ri;
-  ri.numReplicas = 4;
-  std::vector<std::pair<std::set<PrincipalId>, std::string>> keys;
+  // --- SigManager: 4 replicas + 8 external clients 4..11 (ReplicasInfo layout), clients 4..7
+  // share one key (SigManager.cpp:66-85: one key, many principals)
+  ReplicaIdsConfig cfg;
+  cfg.replicaId = 0;
+  cfg.numOfExternalClients = 8;
+  ReplicasInfo ri(cfg);
+  std::set<std::pair<PrincipalId, const std::string>> replicaKeys;
+  std::set<std::pair<const std::string, std::set<uint16_t>>> clientKeys;
   std::vector<EdDSASigner> signers;
   signers.reserve(16);
   for (int r = 0; r < 4; r++) {
     signers.emplace_back(seedHex(10 + r), KeyFormat::HexaDecimalStrippedFormat);
-    keys.push_back({{(PrincipalId)r}, signers.back().getPubKeyHex()});
+    replicaKeys.insert({(PrincipalId)r, signers.back().getPubKeyHex()});
   }
   for (int c = 0; c < 5; c++) {
     signers.emplace_back(seedHex(20 + c), KeyFormat::HexaDecimalStrippedFormat);
-    std::set<PrincipalId> ids;
+    std::set<uint16_t> ids;
     if (c == 0)
-      ids = {100, 101, 102, 103};
+      ids = {4, 5, 6, 7};
     else
-      ids = {(PrincipalId)(103 + c)};
-    for (auto id : ids) ri.externalClients.insert(id);
-    keys.push_back({ids, signers.back().getPubKeyHex()});
+      ids = {(uint16_t)(7 + c)};
+    clientKeys.insert({signers.back().getPubKeyHex(), ids});
   }
-  SigManager sm(0, {seedHex(10), KeyFormat::HexaDecimalStrippedFormat}, keys, KeyFormat::HexaDecimalStrippedFormat,
-                ri);
-  CHECK(sm.getSigLength(0) == 64 && sm.getSigLength(999) == 0);
-  auto signerOf = [&](PrincipalId p) -> EdDSASigner& { return p < 4 ? signers[p] : (p <= 103 ? signers[4] : signers[4 + (p - 103)]); };
+  std::unique_ptr<SigManager> smp(SigManager::initInTesting(0, seedHex(10), replicaKeys,
+                                                            KeyFormat::HexaDecimalStrippedFormat, &clientKeys,
+                                                            KeyFormat::HexaDecimalStrippedFormat, ri));
+  SigManager& sm = *smp;
+  CHECK(sm.getSigLength(0) == 64 && sm.getSigLength(999) == 0 && sm.getSigLength(4) == 64);
+  {  // ids outside their ranges are refused (the reference asserts, SigManager.cpp:58,76-79)
+    bool threw = false;
+    std::set<std::pair<const std::string, std::set<uint16_t>>> badClients = {{signers[4].getPubKeyHex(), {2}}};
+    try {
+      delete SigManager::initInTesting(0, "", replicaKeys, KeyFormat::HexaDecimalStrippedFormat, &badClients,
+                                       KeyFormat::HexaDecimalStrippedFormat, ri);
+    } catch (const std::invalid_argument&) {
+      threw = true;
+    }
+    CHECK(threw);
+  }
+  auto signerOf = [&](PrincipalId p) -> EdDSASigner& { return p < 4 ? signers[p] : (p <= 7 ? signers[4] : signers[4 + (p - 7)]); };
 
-  std::vector<PrincipalId> pids = {0, 1, 2, 3, 100, 101, 102, 103, 104, 105, 106, 107};
+  std::vector<PrincipalId> pids = {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11};
   std::vector<std::string> datas, sigs;
   std::mt19937 g(7);
   for (int i = 0; i < 300; i++) {
@@ -240,6 +522,7 @@ int main() {
   uint64_t okC = 0, okR = 0, badC = 0, badR = 0;
   for (size_t i = 0; i < 300; i++) {
     bool client = ri.isIdOfExternalClient(items[i].pid);
+    CHECK(client == (items[i].pid >= 4));
     (expect[i] ? (client ? okC : okR) : (client ? badC : badR))++;
   }
   const auto& m = sm.metrics();
@@ -254,17 +537,25 @@ int main() {
     CHECK(sm.verifySig(items[i].pid, items[i].data, items[i].dataLength, items[i].sig, items[i].sigLength) ==
           expect[i]);
 
-  // key rotation: client 104 gets a new key; old signatures fail, new ones pass
+  // key rotation: client 8 gets a new key; old signatures fail, new ones pass
   EdDSASigner rotated(seedHex(99), KeyFormat::HexaDecimalStrippedFormat);
-  sm.setClientPublicKey(rotated.getPubKeyHex(), 104, KeyFormat::HexaDecimalStrippedFormat);
+  sm.setClientPublicKey(rotated.getPubKeyHex(), 8, KeyFormat::HexaDecimalStrippedFormat);
   std::string d = "after rotation";
-  CHECK(sm.verifySig(104, d.data(), d.size(), rotated.sign(d).data(), 64));
-  CHECK(!sm.verifySig(104, d.data(), d.size(), signerOf(104).sign(d).data(), 64));
+  CHECK(sm.verifySig(8, d.data(), d.size(), rotated.sign(d).data(), 64));
+  CHECK(!sm.verifySig(8, d.data(), d.size(), signerOf(8).sign(d).data(), 64));
+  // only external clients / client services may be rotated (SigManager.cpp:252): a replica id
+  // is ignored
+  sm.setClientPublicKey(rotated.getPubKeyHex(), 2, KeyFormat::HexaDecimalStrippedFormat);
+  CHECK(sm.verifySig(2, d.data(), d.size(), signers[2].sign(d).data(), 64));
+  CHECK(sm.getPublicKeyOfVerifier(8) == rotated.getPubKeyHex());
 
   // own signature
   char os[64];
   sm.sign(d.data(), d.size(), os, 64);
   CHECK(sm.verifySig(0, d.data(), d.size(), os, 64));
+  if (testMessages(sm, ri, signers, signerOf) != 0) return 1;
+  if (testPreProcessResult(sm, signers) != 0) return 1;
+  if (testConcurrent() != 0) return 1;
   std::printf("test_host: all checks passed (%zu batch items)\n", items.size());
   return 0;
 }

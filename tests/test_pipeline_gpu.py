@@ -205,3 +205,51 @@ def test_single_dma_batch_layout(ctx, base):
         assert np.array_equal(cb.bitmap_to_bools(out.tobytes(), n), exp)
     finally:
         ctx.host_free(blk)
+
+
+def test_append_keys_incremental_and_concurrent(ctx):
+    """Keys appended to a live table (chunk boundaries at 256 keys) get the next indices; the
+    loaded keys are not rebuilt and batches against them run while appends build new tables."""
+    ss = sigsets.make_sigset(6000, nkeys=1100, msg_len=(32, 300), seed=77, invalid_frac=0.1)
+    tid = ctx.load_keys(ss.pk[:300], radix=8)
+    assert ctx.table_size(tid) == (300, 8)
+    old = ss.key_idx < 300
+    msgs = ss.msgs()
+    errors, stop = [], threading.Event()
+
+    def hammer():  # verifies against the first 300 keys while appends run
+        idx = np.nonzero(old)[0][:800]
+        try:
+            while not stop.is_set():
+                bm = ctx.verify(tid, ss.key_idx[idx], ss.sig[idx], [msgs[i] for i in idx])
+                if not np.array_equal(cb.bitmap_to_bools(bm, idx.size), ss.expected[idx]):
+                    errors.append("mismatch during append")
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = threading.Thread(target=hammer)
+    th.start()
+    try:
+        firsts = [ctx.append_keys(tid, ss.pk[a:b]) for a, b in ((300, 301), (301, 700), (700, 1100))]
+    finally:
+        stop.set()
+        th.join(timeout=60)
+    assert firsts == [300, 301, 700] and not errors, errors[:3]
+    assert ctx.table_size(tid)[0] == 1100
+    got = cb.bitmap_to_bools(ctx.verify(tid, ss.key_idx, ss.sig, msgs), ss.n)
+    ctx.unload_keys(tid)
+    assert np.array_equal(got, ss.expected)
+
+
+def test_append_to_empty_table_and_index_bounds(ctx):
+    ss = sigsets.make_sigset(500, nkeys=40, msg_len=64, seed=78)
+    tid = ctx.load_keys(np.zeros((0, 32), dtype=np.uint8), radix=8)
+    try:
+        assert ctx.table_size(tid)[0] == 0
+        with pytest.raises(cb.CbftError):  # index 0 is not loaded yet
+            ctx.verify(tid, ss.key_idx[:1], ss.sig[:1], ss.msgs()[:1])
+        assert ctx.append_keys(tid, ss.pk) == 0
+        got = cb.bitmap_to_bools(ctx.verify(tid, ss.key_idx, ss.sig, ss.msgs()), ss.n)
+        assert np.array_equal(got, ss.expected)
+    finally:
+        ctx.unload_keys(tid)
