@@ -9,8 +9,10 @@
 #define BLS_G2A_WORDS 37     // affine G2 (x.a, x.b, y.a, y.b, inf flag) of a decoded key
 
 size_t cbft_bls_lines_words_per_key();
+// d_scratch: cbft_bls_keys_scratch_words(nkeys) words (line normalisation, freed after the call)
+size_t cbft_bls_keys_scratch_words(uint32_t nkeys);
 hipError_t cbft_bls_launch_keys(const uint8_t* d_keys65, uint32_t nkeys, uint32_t* d_lines, uint8_t* d_ok,
-                                uint32_t* d_aff, hipStream_t s);
+                                uint32_t* d_aff, uint32_t* d_scratch, hipStream_t s);
 hipError_t cbft_bls_launch_gen_lines(uint32_t* d_lines, hipStream_t s);
 hipError_t cbft_bls_launch_hash(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, hipStream_t s);
 hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uint32_t n, const uint32_t* d_H,
@@ -19,9 +21,13 @@ hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uin
                                         uint32_t* d_sig, uint32_t* d_ids, hipStream_t s);
 // lambda over all k shares; the MSM over shares [lo, hi); d_out_jac (nullable): write the sum as
 // one Jacobian partial (BLS_JAC_WORDS) instead of compressing it into d_out33
+// d_inv: the table of inverses 1..BLS_INV_TABLE mod r (cbft_bls_launch_inv_table; unused with multisig)
 hipError_t cbft_bls_launch_combine(const uint32_t* d_sig, const uint32_t* d_ids, const uint8_t* d_use, uint32_t k,
-                                   uint32_t lo, uint32_t hi, int multisig, uint32_t* d_lambda, uint32_t* d_partial,
-                                   uint8_t* d_out33, uint32_t* d_sig_aff, uint32_t* d_out_jac, hipStream_t s);
+                                   uint32_t lo, uint32_t hi, int multisig, const uint32_t* d_inv, uint32_t* d_lambda,
+                                   uint32_t* d_partial, uint8_t* d_out33, uint32_t* d_sig_aff, uint32_t* d_out_jac,
+                                   hipStream_t s);
+#define BLS_INV_TABLE 2048  // d^-1 mod r for d = 1 .. 2048 (share ids are <= 2048, IThresholdVerifier.h:36)
+hipError_t cbft_bls_launch_inv_table(uint32_t* d_inv, hipStream_t s);
 hipError_t cbft_bls_launch_g1_parts(const uint32_t* d_parts, uint32_t count, uint8_t* d_out33, hipStream_t s);
 #define BLS_G2_PART_WORDS 55  // Jacobian G2 partial key sum + bad-key flag
 hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok, uint32_t n, const uint8_t* d_bitmap,

@@ -1,81 +1,14 @@
-// BLS BN-P254 threshold-signature kernels for gfx950 (threshsign path).
+// BLS BN-P254 G1 / scalar kernels for gfx950 (threshsign path).
 //
-//   bls_keys_kernel          per G2 key: decompress + subgroup check + 70 Miller-loop lines
-//                            (BlsThresholdVerifier ctor; lines make per-share work G2-free)
 //   bls_hash_kernel          H = g1_map(digest)            (BlsAccumulatorBase.cpp:55-60)
-//   bls_share_verify_kernel  lane per share: parse, e(H, vk_id) e(-sigma, g2) == 1
-//                            (BlsAccumulatorBase::verifyShare, BlsAccumulatorBase.cpp:62-84)
-//   bls_lagrange_kernel      lane per share: lambda_i = prod_{j!=i} j/(j-i) mod r
+//   bls_inv_table_kernel     inverses of 1..2048 mod r (once per context)
+//   bls_lagrange_kernel      one wave per share: lambda_i = prod_{j!=i} j/(j-i) mod r
 //                            (lagrangeCoeffAccumReduced, LagrangeInterpolation.cpp:202-292)
 //   bls_msm_kernel           lane per share: lambda_i sigma_i, LDS tree sum per block
 //                            (fastMultExp, FastMultExp.cpp:26-59; multisig: lambda = 1)
 //   bls_msm_finish_kernel    sum of block partials -> 33-byte compressed G1
-//   bls_g2_sum_kernel        multisig PK = sum vk_i over the signer bitmap, + its lines
-//   bls_verify_kernel        e(H, PK) e(-sigma, g2) == 1   (BlsThresholdVerifier.cpp:69-96)
-// One lane per pairing check: the per-lane state (an Fp12 accumulator + temporaries) lives in
-// VGPRs/scratch; the G2 side is entirely precomputed.
-#include <hip/hip_runtime.h>
-
-#include "bls_kernels.h"
-#include "bls_ops.h"
-#include "bn254_pair6.h"
-
-#define LINES_PER_KEY (BN_ATE_LINES * BN_LINE_WORDS)
-
-__device__ __forceinline__ void g1a_store(uint32_t* o, const g1a& a) {
-  for (int i = 0; i < 9; i++) {
-    o[i] = a.x.v[i];
-    o[9 + i] = a.y.v[i];
-  }
-  o[18] = a.inf ? 1u : 0u;
-}
-__device__ __forceinline__ void g1a_load(g1a& a, const uint32_t* o) {
-  for (int i = 0; i < 9; i++) {
-    a.x.v[i] = o[i];
-    a.y.v[i] = o[9 + i];
-  }
-  a.inf = o[18] != 0;
-}
-
-__device__ __forceinline__ void g2a_store(uint32_t* o, const g2a& a) {
-  for (int i = 0; i < 9; i++) {
-    o[i] = a.x.a.v[i];
-    o[9 + i] = a.x.b.v[i];
-    o[18 + i] = a.y.a.v[i];
-    o[27 + i] = a.y.b.v[i];
-  }
-  o[36] = a.inf ? 1u : 0u;
-}
-__device__ __forceinline__ void g2a_load(g2a& a, const uint32_t* o) {
-  for (int i = 0; i < 9; i++) {
-    a.x.a.v[i] = o[i];
-    a.x.b.v[i] = o[9 + i];
-    a.y.a.v[i] = o[18 + i];
-    a.y.b.v[i] = o[27 + i];
-  }
-  a.inf = o[36] != 0;
-}
-
-__global__ void __launch_bounds__(64) bls_keys_kernel(const uint8_t* keys65, uint32_t nkeys, uint32_t* lines,
-                                                      uint8_t* ok, uint32_t* aff) {
-  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= nkeys) return;
-  g2a q;
-  bool good = g2_decompress(q, keys65 + 65 * (size_t)k) && !q.inf;
-  ok[k] = good ? 1 : 0;
-  if (!good) q.inf = true;
-  g2a_store(aff + (size_t)k * BLS_G2A_WORDS, q);
-  if (good) g2_precompute_lines(lines + (size_t)k * LINES_PER_KEY, q);
-}
-
-__global__ void bls_gen_lines_kernel(uint32_t* lines) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  g2a q;
-  fp2_load(q.x, Bn254Consts::G2X);
-  fp2_load(q.y, Bn254Consts::G2Y);
-  q.inf = false;
-  g2_precompute_lines(lines, q);
-}
+//   bls_sign_kernel          sigma = sk * g1_map(msg)     (BlsThresholdSigner.cpp:32-47)
+#include "bls_common.h"
 
 __global__ void bls_hash_kernel(const uint8_t* msg, uint32_t len, uint32_t* H) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
@@ -84,94 +17,271 @@ __global__ void bls_hash_kernel(const uint8_t* msg, uint32_t len, uint32_t* H) {
   g1a_store(H, h);
 }
 
-// shares: k x 37 bytes.  out: valid[k] (1 = verified), sig[k] (parsed affine point, 19 words),
-// ids[k].  A share whose id is outside [1, n] or whose point does not decode is invalid.
-// One 8-lane group per share: the pairing check runs on six lanes (bn254_pair6.h); parsing is
-// done by every lane of the group (same latency as one) and lane 0 writes the results.
-__global__ void __launch_bounds__(64) bls_share_verify_kernel(const uint8_t* shares, uint32_t k, uint32_t n,
-                                                              const uint32_t* H, const uint32_t* vk_lines,
-                                                              const uint8_t* vk_ok, const uint32_t* gen_lines,
-                                                              int do_verify, uint8_t* valid, uint32_t* sig,
-                                                              uint32_t* ids) {
-  const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) >> 3;
-  if (j >= k) return;  // whole groups exit together
-  const P6 g = p6_lane();
-  const bool lead = (threadIdx.x & 7) == 0;
-  uint32_t id;
-  g1a s;
-  bool good = bls_parse_share(id, s, shares + 37 * (size_t)j);
-  good = good && id >= 1 && id <= n;
-  if (lead) {
-    ids[j] = id;
-    g1a_store(sig + 19 * (size_t)j, s);
-  }
-  if (good && do_verify) {
-    good = vk_ok[id - 1] != 0;
-    if (good) {
-      g1a P[2];
-      g1a_load(P[0], H);
-      P[1] = s;
-      if (!s.inf) f_neg(P[1].y, s.y);
-      const uint32_t* l[2] = {vk_lines + (size_t)(id - 1) * LINES_PER_KEY, gen_lines};
-      // e(O, Q) = 1: an infinite sigma checks against e(H, vk) alone
-      if (P[1].inf)
-        good = p6_pairing_check<1>(P, l, g);
-      else
-        good = p6_pairing_check<2>(P, l, g);
-    }
-  }
-  if (lead) valid[j] = good ? 1 : 0;
+// inv[d] = d^-1 mod r (Montgomery form), d = 1 .. BLS_INV_TABLE (the reference keeps the same
+// table of small inverses, Library.cpp:22-41); built once per context.
+__global__ void __launch_bounds__(64) bls_inv_table_kernel(uint32_t* inv) {
+  const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x + 1;
+  if (d > BLS_INV_TABLE) return;
+  uint32_t w[8] = {d, 0, 0, 0, 0, 0, 0, 0};
+  fr x;
+  f_from_words(x, w);
+  fr_inv(x, x);
+  for (int q = 0; q < 9; q++) inv[9 * (size_t)(d - 1) + q] = x.v[q];
 }
 
-// lambda_i = prod_{j != i} j / (j - i) mod r over the shares with use[j] != 0; words out (LE)
+__device__ __forceinline__ void fr_shfl_xor(fr& r, const fr& x, int m) {
+#pragma unroll
+  for (int q = 0; q < 9; q++) r.v[q] = (uint32_t)__shfl_xor((int)x.v[q], m);
+}
+
+// lambda_i = prod_{j != i} id_j / (id_j - id_i) mod r over the shares with use[j] != 0
+// (lagrangeCoeffAccumReduced, LagrangeInterpolation.cpp:202-292; the coefficients are unique, so
+// any evaluation order gives the reference's values).  One wave per coefficient: lane l takes
+// j = l, l + 64, ..., multiplying id_j into the numerator and inv[|id_j - id_i|] into the
+// inverted denominator and counting the j with id_j < id_i (each flips the sign); a butterfly
+// over the wave combines the lanes.  No inversion at run time: O(k / 64 + 6) multiplications of
+// latency per coefficient, k waves in flight.  Words out (LE).
 __global__ void __launch_bounds__(64) bls_lagrange_kernel(const uint32_t* ids, const uint8_t* use, uint32_t k,
-                                                          uint32_t* lambda) {
-  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+                                                          const uint32_t* inv, uint32_t* lambda) {
+  const uint32_t i = blockIdx.x;
+  const int ln = threadIdx.x;
   if (i >= k) return;
+  const uint32_t me = ids[i];
+  fr num, den;
+  f_one(num);
+  f_one(den);
+  uint32_t below = 0;
+  const bool on = use[i] != 0;
+  for (uint32_t j = ln; on && j < k; j += 64) {
+    if (j == i || !use[j]) continue;
+    const uint32_t o = ids[j];
+    uint32_t v[8] = {o, 0, 0, 0, 0, 0, 0, 0};
+    fr t;
+    f_from_words(t, v);
+    f_mul(num, num, t);
+    const uint32_t d = o > me ? o - me : me - o;  // 1 <= d < BLS_INV_TABLE (distinct ids <= 2048)
+    fr iv;
+#pragma unroll
+    for (int q = 0; q < 9; q++) iv.v[q] = inv[9 * (size_t)(d - 1) + q];
+    f_mul(den, den, iv);
+    below += o < me ? 1u : 0u;
+  }
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) {
+    fr a, b;
+    fr_shfl_xor(a, num, m);
+    fr_shfl_xor(b, den, m);
+    f_mul(num, num, a);
+    f_mul(den, den, b);
+    below += (uint32_t)__shfl_xor((int)below, m);
+  }
+  if (ln != 0) return;
   uint32_t w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  if (use[i]) {
-    fr num, den, t, d;
-    f_one(num);
-    f_one(den);
-    const uint32_t me = ids[i];
-    for (uint32_t j = 0; j < k; j++) {
-      if (j == i || !use[j]) continue;
-      const uint32_t o = ids[j];
-      uint32_t v[8] = {o, 0, 0, 0, 0, 0, 0, 0};
-      f_from_words(t, v);
-      f_mul(num, num, t);
-      uint32_t dv[8] = {o > me ? o - me : me - o, 0, 0, 0, 0, 0, 0, 0};
-      f_from_words(d, dv);
-      if (o < me) f_neg(d, d);
-      f_mul(den, den, d);
-    }
-    fr_inv(den, den);
+  if (on) {
     f_mul(num, num, den);
+    if (below & 1u) f_neg(num, num);  // each id_j < id_i contributes 1 / (negative)
     f_to_words(w, num);
   }
   for (int q = 0; q < 8; q++) lambda[8 * (size_t)i + q] = w[q];
 }
 
 #define MSM_BLOCK 64
-// partial[b] = sum over this block's lanes of lambda_j * sig_j (Jacobian, 27 words)
+
+// ---- GLV (Gallant-Lambert-Vanstone) on BN-P254 G1: phi(x, y) = (beta x, y) = [lam] P with
+// beta^3 = 1 in Fp, lam^2 + lam + 1 = 0 mod r.  k = k1 + k2 lam (mod r) with |k1|, |k2| < 2^128
+// from the short lattice basis v1 = (a1, b1), v2 = (a2, b2) of {(x, y): x + y lam = 0 mod r}
+// (extended Euclid on (r, lam)): c1 = floor(k g1 / 2^256), c2 = floor(k g2 / 2^256) with
+// g1 = floor(b2 2^256 / r), g2 = floor(-b1 2^256 / r); k1 = k - c1 a1 - c2 a2, k2 = -c1 b1 - c2 b2.
+// (Constants derived with the Python oracle; any decomposition with k1 + k2 lam = k mod r gives
+// the same point, the bound only sizes the ladder.)
+__constant__ const uint32_t kGlvG1[3] = {0x8a6b4904u, 0x7937ca68u, 0x00000003u};
+__constant__ const uint32_t kGlvG2[5] = {0x36bf3357u, 0xc0eb31ffu, 0x04a017b9u, 0xa01fab7eu, 0x00000002u};
+__constant__ const uint32_t kGlvA1[2] = {0x00000001u, 0x81000000u};
+__constant__ const uint32_t kGlvA2[4] = {0x00000004u, 0x85000000u, 0x00000002u, 0x61818000u};
+__constant__ const uint32_t kGlvB1[4] = {0x00000003u, 0x04000000u, 0x00000002u, 0x61818000u};  // |b1|, b1 < 0
+__constant__ const uint32_t kGlvB2[2] = {0x00000001u, 0x81000000u};
+__constant__ const uint32_t kGlvBeta[8] = {0x00000007u, 0xcd800000u, 0x00000006u, 0x49090000u,
+                                           0x00000002u, 0x49b36240u, 0x00000000u, 0x00000000u};
+
+// out[0..no) = (a[0..na) * b[0..nb)) words [shift, shift + no) (schoolbook, 32-bit words)
+template <int NA, int NB, int NO>
+__device__ __forceinline__ void mp_mul(uint32_t* out, const uint32_t* a, const uint32_t* b, int shift) {
+  uint32_t t[NA + NB];
+#pragma unroll
+  for (int i = 0; i < NA + NB; i++) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < NA; i++) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < NB; j++) {
+      c += (uint64_t)a[i] * b[j] + t[i + j];
+      t[i + j] = (uint32_t)c;
+      c >>= 32;
+    }
+    t[i + NB] = (uint32_t)c;
+  }
+#pragma unroll
+  for (int i = 0; i < NO; i++) out[i] = (shift + i < NA + NB) ? t[shift + i] : 0u;
+}
+
+// a -= b (mod 2^256), 8 words
+__device__ __forceinline__ void mp_sub8(uint32_t* a, const uint32_t* b) {
+  int64_t br = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const int64_t d = (int64_t)a[i] - b[i] + br;
+    a[i] = (uint32_t)d;
+    br = d >> 32;
+  }
+}
+// |a| and its sign (a as two's complement mod 2^256)
+__device__ __forceinline__ bool mp_abs8(uint32_t* a) {
+  const bool neg = (a[7] >> 31) != 0;
+  if (neg) {
+    uint64_t c = 1;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      c += (uint32_t)~a[i];
+      a[i] = (uint32_t)c;
+      c >>= 32;
+    }
+  }
+  return neg;
+}
+
+// k (8 LE words, < r) -> |k1|, |k2| (5 words each, < 2^129 with the window offset headroom) and
+// their signs
+__device__ __forceinline__ void glv_split(const uint32_t* k, uint32_t* k1, uint32_t* k2, bool& n1, bool& n2) {
+  uint32_t c1[3], c2[5], g1[3], g2[5], a1[2], a2[4], b1[4], b2[2];
+#pragma unroll
+  for (int i = 0; i < 3; i++) g1[i] = kGlvG1[i];
+#pragma unroll
+  for (int i = 0; i < 5; i++) g2[i] = kGlvG2[i];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    a1[i] = kGlvA1[i];
+    b2[i] = kGlvB2[i];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    a2[i] = kGlvA2[i];
+    b1[i] = kGlvB1[i];
+  }
+  mp_mul<8, 3, 3>(c1, k, g1, 8);
+  mp_mul<8, 5, 5>(c2, k, g2, 8);
+  uint32_t t[8], p[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) t[i] = k[i];
+  mp_mul<3, 2, 8>(p, c1, a1, 0);
+  mp_sub8(t, p);
+  mp_mul<5, 4, 8>(p, c2, a2, 0);
+  mp_sub8(t, p);  // k1 = k - c1 a1 - c2 a2
+  n1 = mp_abs8(t);
+#pragma unroll
+  for (int i = 0; i < 5; i++) k1[i] = t[i];
+  mp_mul<3, 4, 8>(t, c1, b1, 0);  // -c1 b1 = c1 |b1|
+  mp_mul<5, 2, 8>(p, c2, b2, 0);
+  mp_sub8(t, p);  // k2 = c1 |b1| - c2 b2
+  n2 = mp_abs8(t);
+#pragma unroll
+  for (int i = 0; i < 5; i++) k2[i] = t[i];
+}
+
+// signed radix-16 digits of a < 2^128 scalar: s + 8 (16^0 + ... + 16^31), nibble i minus 8 for
+// i < 32, the carry into bit 128 as digit 32 (0 or 1)
+__device__ __forceinline__ int glv_digit(const uint32_t* so, int i) {
+  const int nib = (int)((so[i >> 3] >> (4 * (i & 7))) & 15u);
+  return i < 32 ? nib - 8 : nib;
+}
+__device__ __forceinline__ void glv_offset(uint32_t* s) {
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 5; i++) {
+    c += (uint64_t)s[i] + (i < 4 ? 0x88888888u : 0u);
+    s[i] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+
+__device__ __forceinline__ void g1j_neg_if(g1j& p, bool neg) {
+  fp n;
+  f_neg(n, p.Y);
+#pragma unroll
+  for (int q = 0; q < 9; q++) p.Y.v[q] = neg ? n.v[q] : p.Y.v[q];
+}
+
+// partial[b] = sum over this block's lanes of lambda_j sigma_j (Jacobian, 27 words).
+// lambda_j sigma_j = k1 sigma_j + k2 phi(sigma_j) (GLV): 33 signed radix-16 windows, each 4
+// doublings + one addition from a per-lane LDS table {1..8} sigma (+ one from the same table
+// mapped by phi: X -> beta X) -- 132 doublings and 66 additions instead of 256 and ~128 for
+// fastMultExp's double-and-add (FastMultExp.cpp:26-59).  Multisig (unit scalars): sum sigma_j.
 __global__ void __launch_bounds__(MSM_BLOCK) bls_msm_kernel(const uint32_t* sig, const uint32_t* lambda,
                                                             const uint8_t* use, uint32_t k, int unit_scalars,
                                                             uint32_t* partial) {
   __shared__ uint32_t sp[MSM_BLOCK][27];
+  __shared__ uint32_t tbl[8][27][MSM_BLOCK];  // [multiple - 1][word][lane]: conflict-free
   const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  const int ln = threadIdx.x;
   g1j acc;
   g1_set_inf(acc);
-  if (j < k && use[j]) {
+  const bool live = j < k && use[j];
+  if (live && unit_scalars) {
     g1a s;
     g1a_load(s, sig + 19 * (size_t)j);
-    g1j p;
-    g1_from_affine(p, s);
-    if (unit_scalars) {
-      acc = p;
-    } else {
-      uint32_t lw[8];
+    g1_from_affine(acc, s);
+  }
+  if (!unit_scalars) {  // block-uniform
+    g1a s;
+    uint32_t lw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (live) {
+      g1a_load(s, sig + 19 * (size_t)j);
       for (int q = 0; q < 8; q++) lw[q] = lambda[8 * (size_t)j + q];
-      g1_mul(acc, p, lw);
+    } else {
+      s.inf = true;
+    }
+    g1j P;
+    g1_from_affine(P, s);
+    // table m * sigma, m = 1..8
+    g1j T = P;
+    for (int m = 1; m <= 8; m++) {
+      if (m == 2) g1_dbl(T, P);
+      else if (m > 2) g1_add(T, T, P);
+      for (int q = 0; q < 9; q++) {
+        tbl[m - 1][q][ln] = T.X.v[q];
+        tbl[m - 1][9 + q][ln] = T.Y.v[q];
+        tbl[m - 1][18 + q][ln] = T.Z.v[q];
+      }
+    }
+    uint32_t k1[5], k2[5];
+    bool n1, n2;
+    glv_split(lw, k1, k2, n1, n2);
+    glv_offset(k1);
+    glv_offset(k2);
+    fp beta;
+    {
+      uint32_t bw[8];
+      for (int q = 0; q < 8; q++) bw[q] = kGlvBeta[q];
+      f_from_words(beta, bw);
+    }
+#pragma nounroll
+    for (int w = 32; w >= 0; w--) {
+      if (w != 32)
+        for (int d = 0; d < 4; d++) g1_dbl(acc, acc);
+#pragma unroll
+      for (int half = 0; half < 2; half++) {
+        const int dg = glv_digit(half ? k2 : k1, w);
+        if (dg == 0) continue;
+        const int m = (dg < 0 ? -dg : dg) - 1;
+        g1j E;
+        for (int q = 0; q < 9; q++) {
+          E.X.v[q] = tbl[m][q][ln];
+          E.Y.v[q] = tbl[m][9 + q][ln];
+          E.Z.v[q] = tbl[m][18 + q][ln];
+        }
+        if (half) f_mul(E.X, E.X, beta);  // phi(m sigma)
+        g1j_neg_if(E, (dg < 0) != (half ? n2 : n1));
+        g1_add(acc, acc, E);
+      }
     }
   }
   for (int stride = MSM_BLOCK / 2; stride >= 1; stride >>= 1) {
@@ -235,137 +345,6 @@ __global__ void bls_msm_finish_kernel(const uint32_t* partial, uint32_t nparts, 
   if (sig_aff) g1a_store(sig_aff, a);
 }
 
-// multisig public key = sum of vk_i for set bits (bit id-1, LSB first) of the 256-byte bitmap,
-// then its Miller-loop lines (BlsMultisigVerifier.cpp:33-38, 89-95).  One block: each of the
-// SUM_THREADS lanes adds its strided share of the (already decoded, at load) keys in Jacobian
-// form, then an LDS tree halves the partial sums; lane 0 normalises, compresses and computes
-// the lines.  A selected key that did not decode makes the result invalid (ok = 0).
-#define SUM_THREADS 256
-// normalise, compress (out65) and compute the Miller lines of a summed key; bad = a selected
-// key did not decode
-__device__ void g2_sum_tail(const g2j& acc, bool bad, uint32_t* lines, uint8_t* ok, uint8_t* out65) {
-  g2a s;
-  g2_to_affine(s, acc);
-  const bool good = !bad;
-  if (out65) {
-    if (good) {
-      g2_compress(out65, s);
-    } else {
-      for (int q = 0; q < 65; q++) out65[q] = 0;
-    }
-  }
-  const bool usable = good && !s.inf;
-  ok[0] = usable ? 1 : 0;
-  if (usable && lines) g2_precompute_lines(lines, s);
-}
-
-__device__ __forceinline__ void g2j_store(uint32_t* o, const g2j& a) {
-  const fp2* src[3] = {&a.X, &a.Y, &a.Z};
-  for (int c = 0; c < 3; c++)
-    for (int q = 0; q < 9; q++) {
-      o[18 * c + q] = src[c]->a.v[q];
-      o[18 * c + 9 + q] = src[c]->b.v[q];
-    }
-}
-__device__ __forceinline__ void g2j_load(g2j& a, const uint32_t* o) {
-  fp2* dst[3] = {&a.X, &a.Y, &a.Z};
-  for (int c = 0; c < 3; c++)
-    for (int q = 0; q < 9; q++) {
-      dst[c]->a.v[q] = o[18 * c + q];
-      dst[c]->b.v[q] = o[18 * c + 9 + q];
-    }
-}
-
-// Signer ids [lo_id, hi_id) only (a rank's slice of a sharded multisig key sum).  With out_part
-// the block writes its Jacobian sum (54 words) + the bad-key flag (1 word) and stops there.
-__global__ void __launch_bounds__(SUM_THREADS) bls_g2_sum_kernel(const uint32_t* aff, const uint8_t* key_ok,
-                                                                 uint32_t n, const uint8_t* bitmap, uint32_t lo_id,
-                                                                 uint32_t hi_id, uint32_t* lines, uint8_t* ok,
-                                                                 uint8_t* out65, uint32_t* out_part) {
-  __shared__ uint32_t sp[SUM_THREADS / 2][54];
-  __shared__ int bad;
-  const int t = threadIdx.x;
-  if (t == 0) bad = 0;
-  __syncthreads();
-  g2j acc;
-  fp2_one(acc.X);
-  fp2_one(acc.Y);
-  fp2_zero(acc.Z);
-  bool mine_bad = false;
-  const uint32_t lo = lo_id < 1 ? 1 : lo_id, hi = hi_id > n + 1 ? n + 1 : hi_id;
-  for (uint32_t id = lo + t; id < hi; id += SUM_THREADS) {
-    if (!((bitmap[(id - 1) >> 3] >> ((id - 1) & 7)) & 1)) continue;
-    if (!key_ok[id - 1]) {
-      mine_bad = true;
-      continue;
-    }
-    g2a q;
-    g2a_load(q, aff + (size_t)(id - 1) * BLS_G2A_WORDS);
-    g2j p;
-    p.X = q.x;
-    p.Y = q.y;
-    fp2_one(p.Z);
-    g2_add_j(acc, acc, p);
-  }
-  if (mine_bad) atomicOr(&bad, 1);
-  for (int stride = SUM_THREADS / 2; stride >= 1; stride >>= 1) {
-    if (t >= stride && t < 2 * stride) g2j_store(sp[t - stride], acc);
-    __syncthreads();
-    if (t < stride) {
-      g2j o;
-      g2j_load(o, sp[t]);
-      g2_add_j(acc, acc, o);
-    }
-    __syncthreads();
-  }
-  if (t != 0) return;
-  if (out_part) {
-    g2j_store(out_part, acc);
-    out_part[54] = bad ? 1u : 0u;
-    return;
-  }
-  g2_sum_tail(acc, bad != 0, lines, ok, out65);
-}
-
-// Sum of count G2 partials (55 words each, from bls_g2_sum_kernel's out_part) + the tail.
-__global__ void bls_g2_parts_kernel(const uint32_t* parts, uint32_t count, uint32_t* lines, uint8_t* ok,
-                                    uint8_t* out65) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  g2j acc;
-  fp2_one(acc.X);
-  fp2_one(acc.Y);
-  fp2_zero(acc.Z);
-  bool bad = false;
-  for (uint32_t b = 0; b < count; b++) {
-    g2j o;
-    g2j_load(o, parts + 55 * (size_t)b);
-    bad |= parts[55 * (size_t)b + 54] != 0;
-    g2_add_j(acc, acc, o);
-  }
-  g2_sum_tail(acc, bad, lines, ok, out65);
-}
-
-// e(H, PK) * e(-sigma, g2) == 1 for a combined signature (33 bytes); one 8-lane group
-__global__ void __launch_bounds__(64) bls_verify_kernel(const uint32_t* H, const uint8_t* sig33,
-                                                        const uint32_t* pk_lines, const uint8_t* pk_ok,
-                                                        const uint32_t* gen_lines, uint8_t* result) {
-  if (threadIdx.x >= 8 || blockIdx.x != 0) return;
-  const P6 g = p6_lane();
-  g1a P[2];
-  g1a_load(P[0], H);
-  bool good = pk_ok[0] && g1_decompress(P[1], sig33);
-  if (good) {
-    const uint32_t* l[2] = {pk_lines, gen_lines};
-    if (P[1].inf) {
-      good = p6_pairing_check<1>(P, l, g);
-    } else {
-      f_neg(P[1].y, P[1].y);
-      good = p6_pairing_check<2>(P, l, g);
-    }
-  }
-  if (threadIdx.x == 0) result[0] = good ? 1 : 0;
-}
-
 // sigma_i = sk_i * g1_map(msg) as a 37-byte share (BlsThresholdSigner::signData,
 // BlsThresholdSigner.cpp:32-47): 4-byte big-endian id || 33-byte compressed G1.  sk: 8 LE words.
 __global__ void bls_sign_kernel(const uint8_t* msg, uint32_t len, const uint32_t* sk, uint32_t id, uint8_t* out37) {
@@ -386,59 +365,21 @@ __global__ void bls_sign_kernel(const uint8_t* msg, uint32_t len, const uint32_t
   g1_compress(out37 + 4, a);
 }
 
-// vk = sk * g2 as 65 compressed bytes: the signer's public key (BlsThresholdSigner's
-// publicKey_(secretKey) -> g2_mul_gen, BlsThresholdSigner.cpp:25; IThresholdSigner::
-// getShareVerificationKey).  sk: 8 LE words (< r).  One lane, double-and-add (a one-off per key).
-__global__ void bls_pubkey_kernel(const uint32_t* sk, uint8_t* out65) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
-  g2j G, acc;
-  fp2_load(G.X, Bn254Consts::G2X);
-  fp2_load(G.Y, Bn254Consts::G2Y);
-  fp2_one(G.Z);
-  fp2_one(acc.X);
-  fp2_one(acc.Y);
-  fp2_zero(acc.Z);
-  for (int i = 255; i >= 0; i--) {
-    g2_dbl_j(acc, acc);
-    if ((sk[i >> 5] >> (i & 31)) & 1) g2_add_j(acc, acc, G);
-  }
-  g2a a;
-  g2_to_affine(a, acc);
-  g2_compress(out65, a);
-}
-
 // ------------------------------------------------------------------------------ launchers
-size_t cbft_bls_lines_words_per_key() { return (size_t)LINES_PER_KEY; }
-
-hipError_t cbft_bls_launch_keys(const uint8_t* d_keys65, uint32_t nkeys, uint32_t* d_lines, uint8_t* d_ok,
-                                uint32_t* d_aff, hipStream_t s) {
-  if (!nkeys) return hipSuccess;
-  hipLaunchKernelGGL(bls_keys_kernel, dim3((nkeys + 63) / 64), dim3(64), 0, s, d_keys65, nkeys, d_lines, d_ok,
-                     d_aff);
-  return hipGetLastError();
-}
-hipError_t cbft_bls_launch_gen_lines(uint32_t* d_lines, hipStream_t s) {
-  hipLaunchKernelGGL(bls_gen_lines_kernel, dim3(1), dim3(64), 0, s, d_lines);
-  return hipGetLastError();
-}
 hipError_t cbft_bls_launch_hash(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, hipStream_t s) {
   hipLaunchKernelGGL(bls_hash_kernel, dim3(1), dim3(64), 0, s, d_msg, len, d_H);
   return hipGetLastError();
 }
-hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uint32_t n, const uint32_t* d_H,
-                                        const uint32_t* d_vk_lines, const uint8_t* d_vk_ok,
-                                        const uint32_t* d_gen_lines, int do_verify, uint8_t* d_valid,
-                                        uint32_t* d_sig, uint32_t* d_ids, hipStream_t s) {
-  if (!k) return hipSuccess;
-  hipLaunchKernelGGL(bls_share_verify_kernel, dim3((8 * k + 63) / 64), dim3(64), 0, s, d_shares, k, n, d_H, d_vk_lines,
-                     d_vk_ok, d_gen_lines, do_verify, d_valid, d_sig, d_ids);
+hipError_t cbft_bls_launch_inv_table(uint32_t* d_inv, hipStream_t s) {
+  hipLaunchKernelGGL(bls_inv_table_kernel, dim3((BLS_INV_TABLE + 63) / 64), dim3(64), 0, s, d_inv);
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_combine(const uint32_t* d_sig, const uint32_t* d_ids, const uint8_t* d_use, uint32_t k,
-                                   uint32_t lo, uint32_t hi, int multisig, uint32_t* d_lambda, uint32_t* d_partial,
-                                   uint8_t* d_out33, uint32_t* d_sig_aff, uint32_t* d_out_jac, hipStream_t s) {
+                                   uint32_t lo, uint32_t hi, int multisig, const uint32_t* d_inv, uint32_t* d_lambda,
+                                   uint32_t* d_partial, uint8_t* d_out33, uint32_t* d_sig_aff, uint32_t* d_out_jac,
+                                   hipStream_t s) {
   if (!multisig && k)
-    hipLaunchKernelGGL(bls_lagrange_kernel, dim3((k + 63) / 64), dim3(64), 0, s, d_ids, d_use, k, d_lambda);
+    hipLaunchKernelGGL(bls_lagrange_kernel, dim3(k), dim3(64), 0, s, d_ids, d_use, k, d_inv, d_lambda);
   hi = hi < k ? hi : k;
   lo = lo < hi ? lo : hi;
   const uint32_t m = hi - lo;  // the MSM runs over shares [lo, hi) only
@@ -454,31 +395,8 @@ hipError_t cbft_bls_launch_g1_parts(const uint32_t* d_parts, uint32_t count, uin
   hipLaunchKernelGGL(bls_msm_finish_kernel, dim3(1), dim3(64), 0, s, d_parts, count, d_out33, nullptr, nullptr);
   return hipGetLastError();
 }
-hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok, uint32_t n, const uint8_t* d_bitmap,
-                                  uint32_t lo_id, uint32_t hi_id, uint32_t* d_lines, uint8_t* d_ok, uint8_t* d_out65,
-                                  uint32_t* d_out_part, hipStream_t s) {
-  hipLaunchKernelGGL(bls_g2_sum_kernel, dim3(1), dim3(SUM_THREADS), 0, s, d_aff, d_key_ok, n, d_bitmap, lo_id, hi_id,
-                     d_lines, d_ok, d_out65, d_out_part);
-  return hipGetLastError();
-}
-hipError_t cbft_bls_launch_g2_parts(const uint32_t* d_parts, uint32_t count, uint32_t* d_lines, uint8_t* d_ok,
-                                    uint8_t* d_out65, hipStream_t s) {
-  hipLaunchKernelGGL(bls_g2_parts_kernel, dim3(1), dim3(64), 0, s, d_parts, count, d_lines, d_ok, d_out65);
-  return hipGetLastError();
-}
-hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, const uint32_t* d_pk_lines,
-                                  const uint8_t* d_pk_ok, const uint32_t* d_gen_lines, uint8_t* d_result,
-                                  hipStream_t s) {
-  hipLaunchKernelGGL(bls_verify_kernel, dim3(1), dim3(64), 0, s, d_H, d_sig33, d_pk_lines, d_pk_ok, d_gen_lines,
-                     d_result);
-  return hipGetLastError();
-}
 hipError_t cbft_bls_launch_sign(const uint8_t* d_msg, uint32_t len, const uint32_t* d_sk, uint32_t id,
                                 uint8_t* d_out37, hipStream_t s) {
   hipLaunchKernelGGL(bls_sign_kernel, dim3(1), dim3(64), 0, s, d_msg, len, d_sk, id, d_out37);
-  return hipGetLastError();
-}
-hipError_t cbft_bls_launch_pubkey(const uint32_t* d_sk, uint8_t* d_out65, hipStream_t s) {
-  hipLaunchKernelGGL(bls_pubkey_kernel, dim3(1), dim3(64), 0, s, d_sk, d_out65);
   return hipGetLastError();
 }

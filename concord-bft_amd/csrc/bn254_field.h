@@ -17,7 +17,7 @@
 // Heavy tower/curve/pairing routines are compiled once and called (objects pass through
 // scratch): fully inlining the pairing into its kernels makes the code object explode
 // (a > 40 min compile measured); field-level ops stay inlined inside each routine.
-#define BN_HDN __host__ __device__ __noinline__
+#define BN_HDN static __host__ __device__ __noinline__
 #else
 #define BN_HD inline
 #define BN_HDN inline

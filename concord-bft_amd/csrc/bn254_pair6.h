@@ -212,12 +212,48 @@ __device__ __noinline__ void p6_inv(fp2& r, const fp2& x, const P6& g) {
   p6_pick(r, t, g);
 }
 
+// x^2 for x in the cyclotomic subgroup of Fp12 (every value of the final exponentiation after
+// its easy part), Granger-Scott: view f = A + B w + C w^2 over Fp4 = Fp2[t]/(t^2 - xi), t = w^3
+// (A = e0 + e3 t, B = e1 + e4 t, C = e2 + e5 t); then
+//   f^2 = (3A^2 - 2 conj A) + (3 t C^2 + 2 conj B) w + (3B^2 - 2 conj C) w^2
+// (checked against the oracle's F12).  Each lane needs one half of one Fp4 square of a pair
+// (x, y): P = x^2 + xi y^2 (even k) or Q = 2xy (odd k), formed uniformly from three Fp2 squares
+// (x^2, y^2, (x + y)^2): 6 Fp multiplications and 2 gathers per lane instead of p6_sqr's 12 and 8.
+__device__ __forceinline__ void p6_cyc_sqr(fp2& r, const fp2& a, const P6& g) {
+  // sources of (x, y) per k: A for k = 0, 3; C for k = 4, 1; B for k = 2, 5
+  const int sx = (g.k == 0 || g.k == 3) ? 0 : ((g.k == 1 || g.k == 4) ? 2 : 1);
+  fp2 x, y, x2, y2, s, p, q;
+  fp2_shfl(x, a, g.base + sx);
+  fp2_shfl(y, a, g.base + sx + 3);
+  fp2_sqr(x2, x);
+  fp2_sqr(y2, y);
+  fp2_add(s, x, y);
+  fp2_sqr(s, s);
+  fp2_mul_xi(p, y2);
+  fp2_add(p, p, x2);  // P = x^2 + xi y^2
+  fp2_sub(q, s, x2);
+  fp2_sub(q, q, y2);  // Q = 2xy
+  const bool odd = (g.k & 1) != 0;
+  fp2_select(p, q, odd);
+  fp2_mul_xi(q, p);
+  fp2_select(p, q, g.k == 1);  // the t C^2 term: t (cx + cy t) = xi cy + cx t
+  fp2 three, two;
+  fp2_add(three, p, p);
+  fp2_add(three, three, p);
+  fp2_add(two, a, a);
+  fp2 plus, minus;
+  fp2_add(plus, three, two);
+  fp2_sub(minus, three, two);
+  r = minus;
+  fp2_select(r, plus, odd);
+}
+
 // x^u for x in the cyclotomic subgroup: u = -(2^62 + 2^55 + 1)
 __device__ __forceinline__ void p6_pow_u(fp2& r, const fp2& x, const P6& g) {
   fp2 acc = x;
 #pragma nounroll
   for (int i = 61; i >= 0; i--) {
-    p6_sqr(acc, acc, g);
+    p6_cyc_sqr(acc, acc, g);
     if (i == 55 || i == 0) p6_mul(acc, acc, x, g);
   }
   p6_conj(r, acc, g);
@@ -229,7 +265,7 @@ __device__ __forceinline__ void p6_pow_small(fp2& r, const fp2& x, uint32_t e, c
   while (!((e >> top) & 1)) top--;
 #pragma nounroll
   for (int i = top - 1; i >= 0; i--) {
-    p6_sqr(acc, acc, g);
+    p6_cyc_sqr(acc, acc, g);
     if ((e >> i) & 1) p6_mul(acc, acc, x, g);
   }
   r = acc;
@@ -254,7 +290,7 @@ __device__ __forceinline__ void p6_final_exp(fp2& r, const fp2& f, const P6& g) 
   p6_mul(b30, b30, b6, g);
   p6_pow_small(a12, a, 12, g);
   p6_pow_small(a18, a, 18, g);
-  p6_sqr(g2, gg, g);
+  p6_cyc_sqr(g2, gg, g);
   fp2 t0, t1, t2, t3;
   p6_mul(t0, c36, b30, g);
   p6_mul(t0, t0, a18, g);

@@ -56,9 +56,13 @@ int cbft_bls_load_keys(cbft_ctx* c, const uint8_t* pk65, const uint8_t* vks65, u
   CBFT_HIP(hipMemcpyAsync(ks.keys65.p, pk65, 65, hipMemcpyHostToDevice, c->stream));
   if (n)
     CBFT_HIP(hipMemcpyAsync(ks.keys65.as<uint8_t>() + 65, vks65, (size_t)n * 65, hipMemcpyHostToDevice, c->stream));
-  CBFT_HIP(cbft_bls_launch_keys(ks.keys65.as<uint8_t>(), (uint32_t)nk, ks.lines.as<uint32_t>(), ks.ok.as<uint8_t>(),
-                                ks.aff.as<uint32_t>(), c->stream));
-  CBFT_HIP(hipStreamSynchronize(c->stream));
+  DevBuf scratch;
+  CBFT_HIP(scratch.reserve(cbft_bls_keys_scratch_words((uint32_t)nk) * 4));
+  hipError_t e = cbft_bls_launch_keys(ks.keys65.as<uint8_t>(), (uint32_t)nk, ks.lines.as<uint32_t>(),
+                                      ks.ok.as<uint8_t>(), ks.aff.as<uint32_t>(), scratch.as<uint32_t>(), c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  scratch.release();
+  CBFT_HIP(e);
   uint32_t id = c->next_bls_id++;
   c->bls_sets.emplace(id, std::move(ks));
   *out_id = id;
@@ -107,7 +111,7 @@ int cbft_bls_hash_to_g1(cbft_ctx* c, const uint8_t* msg, uint32_t len, uint8_t* 
   uint8_t one = 1;
   CBFT_HIP(hipMemcpyAsync(c->bls_use.p, &one, 1, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(cbft_bls_launch_combine(c->bls_H.as<uint32_t>(), nullptr, c->bls_use.as<uint8_t>(), 1, 0, 1, 1, nullptr,
-                                   c->bls_partial.as<uint32_t>(), c->bls_out.as<uint8_t>(), nullptr, nullptr,
+                                   nullptr, c->bls_partial.as<uint32_t>(), c->bls_out.as<uint8_t>(), nullptr, nullptr,
                                    c->stream));
   CBFT_HIP(hipMemcpyAsync(out33, c->bls_out.p, 33, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipStreamSynchronize(c->stream));
@@ -176,8 +180,13 @@ static int bls_combine_range(cbft_ctx* c, const uint8_t* shares37, uint32_t k, u
   CBFT_HIP(hipStreamSynchronize(c->stream));
   for (uint32_t j = 0; j < k; j++)
     if (!v[j]) return CBFT_EINVAL;
+  if (!multisig && !c->bls_inv.p) {  // inverses of 1..2048 mod r, once per context
+    CBFT_HIP(c->bls_inv.reserve((size_t)BLS_INV_TABLE * 9 * 4));
+    CBFT_HIP(cbft_bls_launch_inv_table(c->bls_inv.as<uint32_t>(), c->stream));
+  }
   CBFT_HIP(cbft_bls_launch_combine(c->bls_sig.as<uint32_t>(), c->bls_ids.as<uint32_t>(), c->bls_valid.as<uint8_t>(),
-                                   k, lo, hi, multisig, c->bls_lambda.as<uint32_t>(), c->bls_partial.as<uint32_t>(),
+                                   k, lo, hi, multisig, c->bls_inv.as<uint32_t>(), c->bls_lambda.as<uint32_t>(),
+                                   c->bls_partial.as<uint32_t>(),
                                    c->bls_out.as<uint8_t>(), nullptr,
                                    out_part ? c->bls_out.as<uint32_t>() : nullptr, c->stream));
   if (out_part)

@@ -53,6 +53,30 @@ int shim_g2_decompress(const uint8_t* in65, uint8_t* out65) {
   return 1;
 }
 
+// 1 iff the inversion-free, batch-normalised line precomputation equals the affine one word for
+// word (both kernels' formats), 0 if they differ, -1 if the key does not decode
+int shim_lines_match(const uint8_t* in65) {
+  g2a q;
+  if (!g2_decompress(q, in65) || q.inf) return -1;
+  std::vector<uint32_t> a(BN_ATE_LINES * BN_LINE_WORDS), b(a.size()), scr(BN_ATE_LINES * 36);
+  g2_precompute_lines(a.data(), q);
+  g2_precompute_lines_batch(b.data(), q, scr.data());
+  // compare the field elements canonically (limbs hold a value < 2p: either representative)
+  for (size_t e = 0; e < a.size(); e += 9) {
+    fp x, y;
+    for (int i = 0; i < 9; i++) {
+      x.v[i] = a[e + i];
+      y.v[i] = b[e + i];
+    }
+    uint32_t wx[8], wy[8];
+    f_to_words(wx, x);
+    f_to_words(wy, y);
+    for (int i = 0; i < 8; i++)
+      if (wx[i] != wy[i]) return 0;
+  }
+  return 1;
+}
+
 void shim_g1_map(const uint8_t* msg, uint32_t len, uint8_t* out33) {
   g1a h;
   g1_map(h, msg, len);

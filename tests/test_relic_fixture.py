@@ -86,3 +86,12 @@ def test_host_build_g1_codec_matches_oracle(s):
         lib.shim_sign_share(sk.to_bytes(32, "big"), i, msg, len(msg), out)
         assert out.raw == B.sign_share(sk, i, msg)
         assert B.parse_share(out.raw) == (i, B.ec_mul(sk, H))
+
+
+def test_batched_line_precompute_equals_affine():
+    """The inversion-free Miller-line precomputation (Jacobian steps + one batched inversion,
+    bn254_pairing.h g2_precompute_lines_batch) gives the affine per-step lines word for word, on
+    every RELIC key of the fixture."""
+    lib = blsgen.shim()
+    keys = [b for s in SYSTEMS for b in s.vks + [s.pk]]
+    assert [lib.shim_lines_match(b) for b in keys] == [1] * len(keys)
