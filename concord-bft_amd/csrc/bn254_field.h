@@ -93,20 +93,20 @@ BN_HD void f_redc(Fe<F>& r, uint64_t* c) {
 // first (17 independent mad chains), then f_redc: bit-identical to the interleaved FIPS form
 // (the same m_k), but with a dependency chain ~4x shorter, which is what a pairing running on
 // few lanes waits on.
+//
+// Accumulation order is row-wise (a_i against every b_j): consecutive mads update different
+// columns, so a lone wave (a pairing check runs one wave per SIMD) issues them back to back
+// instead of waiting out the v_mad_u64_u32 latency of a column chain.
 template <class F>
 BN_HD void f_mul(Fe<F>& r, const Fe<F>& a, const Fe<F>& b) {
   uint64_t c[2 * BN_LIMBS];
 #pragma unroll
-  for (int k = 0; k < 2 * BN_LIMBS - 1; k++) {
-    uint64_t acc = 0;
+  for (int k = 0; k < 2 * BN_LIMBS; k++) c[k] = 0;
 #pragma unroll
-    for (int i = 0; i < BN_LIMBS; i++) {
-      const int j = k - i;
-      if (j >= 0 && j < BN_LIMBS) acc = bn_mad(a.v[i], b.v[j], acc);
-    }
-    c[k] = acc;
+  for (int i = 0; i < BN_LIMBS; i++) {
+#pragma unroll
+    for (int j = 0; j < BN_LIMBS; j++) c[i + j] = bn_mad(a.v[i], b.v[j], c[i + j]);
   }
-  c[2 * BN_LIMBS - 1] = 0;
   f_redc(r, c);
 }
 
@@ -117,17 +117,13 @@ BN_HD void f_sqr(Fe<F>& r, const Fe<F>& a) {
   for (int i = 0; i < BN_LIMBS; i++) a2[i] = a.v[i] << 1;
   uint64_t c[2 * BN_LIMBS];
 #pragma unroll
-  for (int k = 0; k < 2 * BN_LIMBS - 1; k++) {
-    uint64_t acc = 0;
+  for (int k = 0; k < 2 * BN_LIMBS; k++) c[k] = 0;
 #pragma unroll
-    for (int i = 0; i < BN_LIMBS; i++) {
-      const int j = k - i;
-      if (j > i && j < BN_LIMBS) acc = bn_mad(a2[i], a.v[j], acc);
-    }
-    if ((k & 1) == 0 && (k >> 1) < BN_LIMBS) acc = bn_mad(a.v[k >> 1], a.v[k >> 1], acc);
-    c[k] = acc;
+  for (int i = 0; i < BN_LIMBS; i++) {  // row-wise, as f_mul
+    c[2 * i] = bn_mad(a.v[i], a.v[i], c[2 * i]);
+#pragma unroll
+    for (int j = i + 1; j < BN_LIMBS; j++) c[i + j] = bn_mad(a2[i], a.v[j], c[i + j]);
   }
-  c[2 * BN_LIMBS - 1] = 0;
   f_redc(r, c);
 }
 

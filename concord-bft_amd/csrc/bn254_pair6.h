@@ -82,7 +82,7 @@ __constant__ const uint8_t kP6Sq[6][4][3] = {
 __device__ __forceinline__ void p6_sqr(fp2& r, const fp2& a, const P6& g) {
   fp2 acc;
   fp2_zero(acc);
-#pragma nounroll
+#pragma nounroll  // unrolling measured no faster (share verify 4.06 vs 4.01 ms) and compiles slower
   for (int t = 0; t < 4; t++) {
     const int i = kP6Sq[g.k][t][0], j = kP6Sq[g.k][t][1], fl = kP6Sq[g.k][t][2];
     fp2 ai, aj, p, q;

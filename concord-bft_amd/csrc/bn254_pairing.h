@@ -550,7 +550,7 @@ BN_HD void fp2_fetch(fp2& x, const uint32_t* o) {
 }
 
 // doubling step: records (A, B, C) of the tangent at T, T <- 2T
-BN_HDN void line_dbl_j(uint32_t* ln, uint32_t* sa, g2j& T) {
+BN_HD void line_dbl_j(uint32_t* ln, uint32_t* sa, g2j& T) {
   fp2 XX, YY, ZZ, YYYY, t, A, B, C, D, E, F;
   fp2_sqr(XX, T.X);
   fp2_sqr(YY, T.Y);
@@ -588,7 +588,7 @@ BN_HDN void line_dbl_j(uint32_t* ln, uint32_t* sa, g2j& T) {
 }
 
 // addition step with affine (qx, qy): records (A, B, C) of the line through T and Q, T <- T + Q
-BN_HDN void line_add_j(uint32_t* ln, uint32_t* sa, g2j& T, const fp2& qx, const fp2& qy) {
+BN_HD void line_add_j(uint32_t* ln, uint32_t* sa, g2j& T, const fp2& qx, const fp2& qy) {
   fp2 ZZ, U2, S2, H, R, A, C, t, HH, I, J, V, r;
   fp2_sqr(ZZ, T.Z);
   fp2_mul(U2, qx, ZZ);
