@@ -1,0 +1,392 @@
+// Pairing check with one Fp12 spread over a whole wave (gfx950 device code only).
+//
+// Latency of one pairing check is the instruction stream of one lane.  bn254_pair12.h gives
+// each of the 12 Fp components of f = sum_k e_k w^k (e_k in Fp2) its own lane; here every
+// component gets THREE lanes (sub-lanes s = 0, 1, 2; lane 12 s + 2 k + h holds component h of
+// e_k, lanes 36..63 shadow lanes 0..27) and the products an Fp12 operation needs are dealt out
+// to the sub-lanes, then summed with two ds_bpermute gathers:
+//   op          Fp mults per lane   (bn254_pair12.h)
+//   mul         4                   12    6 split products per component, 2 per sub-lane
+//   sqr         2                    8    even k: two diagonal squares on s = 0, one cross
+//                                         term on s = 1, 2; odd k: one cross term per sub-lane
+//   cyc_sqr     1                    3    x^2, y^2, (x + y)^2 on s = 0, 1, 2 (Granger-Scott)
+//   line        3                    6    f_k yP | xP (f_{k-1} lambda) | f_{k-3} mu
+// All three sub-lanes of a component end every operation with the same bits (the sub-lane
+// partials are summed in the order s = 0, 1, 2 on every lane), so the state is replicated and
+// any sub-lane can serve a gather.  Results equal the 12-lane and one-lane pairing checks
+// exactly (same GT element; tests/test_bls_gpu.py and tests/test_relic_gpu.py against the
+// Python oracle).
+#pragma once
+#include "bn254_pair12.h"
+
+struct P36 {
+  int k;     // coefficient 0..5
+  int h;     // component: 0 = real, 1 = imaginary
+  int s;     // sub-lane 0..2
+  int lane;  // lane within the wave
+};
+
+__device__ __forceinline__ P36 p36_lane() {
+  P36 g;
+  g.lane = threadIdx.x & 63;
+  const int e = g.lane < 36 ? g.lane : g.lane - 36;
+  const int c = e % 12;
+  g.s = e / 12;
+  g.k = c >> 1;
+  g.h = c & 1;
+  return g;
+}
+
+__device__ __forceinline__ int p36_src(int k2, int h2, int s2) { return 12 * s2 + 2 * k2 + h2; }
+
+// (my component, the other component) of coefficient k2 of x
+__device__ __forceinline__ void p36_fetch(fp& m, fp& o, const fp& x, int k2, const P36& g) {
+  fp_shfl(m, x, p36_src(k2, g.h, g.s));
+  fp_shfl(o, x, p36_src(k2, 1 - g.h, g.s));
+}
+
+// r = sum over the three sub-lanes of component (k, h) of part, in the order 0, 1, 2
+__device__ __forceinline__ void p36_sum3(fp& r, const fp& part, const P36& g) {
+  fp q0, q1, q2;
+  fp_shfl(q0, part, p36_src(g.k, g.h, 0));
+  fp_shfl(q1, part, p36_src(g.k, g.h, 1));
+  fp_shfl(q2, part, p36_src(g.k, g.h, 2));
+  f_add(r, q0, q1);
+  f_add(r, r, q2);
+}
+
+// my component of xi * z, z held componentwise by this lane and its partner (same k, s)
+__device__ __forceinline__ void p36_xi(fp& r, const fp& z, const P36& g) {
+  fp zo;
+  fp_shfl(zo, z, p36_src(g.k, 1 - g.h, g.s));
+  p12_cxi(r, z, zo, g.h);
+}
+
+// r = a * b: sub-lane s forms the terms i = 2s, 2s + 1 of c_k = sum_i a_i b_{k-i} (xi on wrap)
+__device__ __forceinline__ void p36_mul(fp& r, const fp& a, const fp& b, const P36& g) {
+  fp acc, accw;
+  f_zero(acc);
+  f_zero(accw);
+#pragma unroll
+  for (int t = 0; t < 2; t++) {
+    const int i = 2 * g.s + t;
+    int j = g.k - i;
+    const bool wrap = j < 0;
+    if (wrap) j += 6;
+    fp am, ao, bm, bo, p, q;
+    p36_fetch(am, ao, a, i, g);
+    p36_fetch(bm, bo, b, j, g);
+    p12_cmul(p, am, ao, bm, bo, g.h);
+    f_add(q, wrap ? accw : acc, p);
+    fp_sel(acc, q, !wrap);
+    fp_sel(accw, q, wrap);
+  }
+  fp w;
+  p36_xi(w, accw, g);
+  f_add(acc, acc, w);
+  p36_sum3(r, acc, g);
+}
+
+// r = a^2 (the term table kP12Sq of bn254_pair12.h).  Even k: s = 0 squares the two diagonal
+// terms (a_i^2, one component each: (x0 + x1)(x0 - x1) or 2 x0 x1), s = 1, 2 the cross terms
+// 2 a_i a_j; odd k: one cross term per sub-lane.  Two multiplications per lane.
+__device__ __forceinline__ void p36_sqr(fp& r, const fp& a, const P36& g) {
+  const bool even = (g.k & 1) == 0;
+  const bool diag = even && g.s == 0;
+  const int tt = even ? g.s + 1 : g.s;  // cross term index
+  const int f1 = diag ? kP12Sq[g.k][0][0] : kP12Sq[g.k][tt][0];
+  const int f2 = diag ? kP12Sq[g.k][1][0] : kP12Sq[g.k][tt][1];
+  const bool cwrap = (kP12Sq[g.k][tt][2] & 2) != 0;
+  fp xm, xo, zm, zo;
+  p36_fetch(xm, xo, a, f1, g);
+  p36_fetch(zm, zo, a, f2, g);
+  fp s1, d1, s2, d2;
+  f_add(s1, xm, xo);
+  f_sub(d1, xm, xo);
+  f_add(s2, zm, zo);
+  f_sub(d2, zm, zo);
+  // diag: (h ? x1 x0 : (x0 + x1)(x0 - x1)), same for z;  cross: split product (x * z)_h
+  fp X1 = diag ? (g.h ? xm : s1) : (g.h ? xo : xm);
+  fp Y1 = diag ? (g.h ? xo : d1) : zm;
+  fp X2 = diag ? (g.h ? zm : s2) : (g.h ? xm : xo);
+  fp Y2 = diag ? (g.h ? zo : d2) : zo;
+  fp P1, P2;
+  f_mul(P1, X1, Y1);
+  f_mul(P2, X2, Y2);
+  fp acc, accw, t, t2;
+  // diag: acc = (h ? 2 P1 : P1), accw = (h ? 2 P2 : P2) (the second diagonal term wraps)
+  // cross: T = 2 (h ? P1 + P2 : P1 - P2), into accw if it wraps
+  f_add(s1, P1, P1);
+  f_add(s2, P2, P2);
+  fp dA = g.h ? s1 : P1, dB = g.h ? s2 : P2;
+  f_add(t, P1, P2);
+  f_sub(t2, P1, P2);
+  fp c = g.h ? t : t2;
+  f_add(c, c, c);
+  fp zero;
+  f_zero(zero);
+  acc = diag ? dA : (cwrap ? zero : c);
+  accw = diag ? dB : (cwrap ? c : zero);
+  fp w;
+  p36_xi(w, accw, g);
+  f_add(acc, acc, w);
+  p36_sum3(r, acc, g);
+}
+
+// Granger-Scott cyclotomic squaring (p6_cyc_sqr's formulas): s = 0, 1, 2 square x, y, x + y
+// (one component each), then P = x^2 + xi y^2 (even k) or Q = (x + y)^2 - x^2 - y^2 (odd k)
+__device__ __forceinline__ void p36_cyc_sqr(fp& r, const fp& a, const P36& g) {
+  const int sx = (g.k == 0 || g.k == 3) ? 0 : ((g.k == 1 || g.k == 4) ? 2 : 1);
+  fp fm, fo, ym, yo;
+  p36_fetch(fm, fo, a, g.s == 1 ? sx + 3 : sx, g);
+  p36_fetch(ym, yo, a, sx + 3, g);
+  fp wm, wo, sm, so;
+  f_add(sm, fm, ym);
+  f_add(so, fo, yo);
+  wm = g.s == 2 ? sm : fm;
+  wo = g.s == 2 ? so : fo;
+  fp prod;
+  p12_csqr(prod, wm, wo, g.h);
+  const bool odd = (g.k & 1) != 0;
+  fp X2, Y2, G3;
+  fp_shfl(X2, prod, p36_src(g.k, g.h, 0));
+  fp_shfl(Y2, prod, p36_src(g.k, g.h, 1));
+  fp_shfl(G3, prod, odd ? p36_src(g.k, g.h, 2) : p36_src(g.k, 1 - g.h, 1));  // (x+y)^2_h | y^2_h'
+  fp p, q;
+  p12_cxi(p, Y2, G3, g.h);
+  f_add(p, X2, p);  // P = x^2 + xi y^2
+  f_sub(q, G3, X2);
+  f_sub(q, q, Y2);  // Q = 2xy
+  fp v = odd ? q : p;
+  fp vx;
+  p36_xi(vx, v, g);  // t C^2 term for k = 1
+  fp_sel(v, vx, g.k == 1);
+  fp three, two, plus, minus;
+  f_add(three, v, v);
+  f_add(three, three, v);
+  f_add(two, a, a);
+  f_add(plus, three, two);
+  f_sub(minus, three, two);
+  r = odd ? plus : minus;
+}
+
+__device__ __forceinline__ void p36_coef(fp& m, fp& o, const uint32_t* c, int h) {
+#pragma unroll
+  for (int i = 0; i < 9; i++) {
+    const uint32_t x0 = c[i], x1 = c[9 + i];
+    m.v[i] = h ? x1 : x0;
+    o.v[i] = h ? x0 : x1;
+  }
+}
+
+// f <- f * (yP + s w + mu w^3), s = -lambda xP, for one precomputed line:
+//   s = 0: f_k yP;  s = 1: -xP (f_{k-1} lambda) (xi for k = 0);  s = 2: f_{k-3} mu (xi for k < 3)
+__device__ __forceinline__ void p36_line1(fp& f, const uint32_t* ln, const g1a& P, const P36& g) {
+  fp om, oo, cm, co;
+  p36_fetch(om, oo, f, g.s == 1 ? (g.k + 5) % 6 : (g.k + 3) % 6, g);
+  p36_coef(cm, co, ln + (g.s == 2 ? 18 : 0), g.h);
+  const fp u = g.h ? oo : om, v = g.h ? om : oo;
+  fp X1 = g.s == 0 ? f : u;
+  fp Y1 = g.s == 0 ? P.y : cm;
+  fp P1, P2, P3, C, t;
+  f_mul(P1, X1, Y1);
+  f_mul(P2, v, co);
+  f_add(C, P1, P2);
+  f_sub(t, P1, P2);
+  C = g.h ? C : t;
+  f_mul(P3, C, P.x);
+  f_neg(P3, P3);
+  fp T = g.s == 0 ? P1 : (g.s == 1 ? P3 : C);
+  const bool wrap = (g.s == 1 && g.k == 0) || (g.s == 2 && g.k < 3);
+  fp w;
+  p36_xi(w, T, g);
+  fp_sel(T, w, wrap);
+  p36_sum3(f, T, g);
+}
+
+__device__ __forceinline__ void p36_one(fp& r, const P36& g) {
+  f_zero(r);
+  fp one;
+  f_one(one);
+  fp_sel(r, one, g.k == 0 && g.h == 0);
+}
+
+__device__ __forceinline__ void p36_conj(fp& r, const fp& x, const P36& g) {
+  fp n;
+  f_neg(n, x);
+  r = x;
+  fp_sel(r, n, (g.k & 1) != 0);
+}
+
+// x -> x^(p^J) (see p12_frob)
+template <int J>
+__device__ __forceinline__ void p36_frob(fp& r, const fp& x, const P36& g) {
+  fp c = x;
+  if (J & 1) {
+    fp n;
+    f_neg(n, x);
+    fp_sel(c, n, g.h == 1);
+  }
+  if (J == 2) {
+    fp q, gm;
+    f_one(gm);
+    fp_load(q, Bn254Consts::G2_1, 0);
+    fp_sel(gm, q, g.k == 1);
+    fp_load(q, Bn254Consts::G2_2, 0);
+    fp_sel(gm, q, g.k == 2);
+    fp_load(q, Bn254Consts::G2_3, 0);
+    fp_sel(gm, q, g.k == 3);
+    fp_load(q, Bn254Consts::G2_4, 0);
+    fp_sel(gm, q, g.k == 4);
+    fp_load(q, Bn254Consts::G2_5, 0);
+    fp_sel(gm, q, g.k == 5);
+    f_mul(r, c, gm);
+    return;
+  }
+  fp2 gm, t;
+  fp2_one(gm);
+  if (J == 1) {
+    fp2_load(t, Bn254Consts::G1_1);
+    p12_sel2(gm, t, g.k == 1);
+    fp2_load(t, Bn254Consts::G1_2);
+    p12_sel2(gm, t, g.k == 2);
+    fp2_load(t, Bn254Consts::G1_3);
+    p12_sel2(gm, t, g.k == 3);
+    fp2_load(t, Bn254Consts::G1_4);
+    p12_sel2(gm, t, g.k == 4);
+    fp2_load(t, Bn254Consts::G1_5);
+    p12_sel2(gm, t, g.k == 5);
+  } else {
+    fp2_load(t, Bn254Consts::G3_1);
+    p12_sel2(gm, t, g.k == 1);
+    fp2_load(t, Bn254Consts::G3_2);
+    p12_sel2(gm, t, g.k == 2);
+    fp2_load(t, Bn254Consts::G3_3);
+    p12_sel2(gm, t, g.k == 3);
+    fp2_load(t, Bn254Consts::G3_4);
+    p12_sel2(gm, t, g.k == 4);
+    fp2_load(t, Bn254Consts::G3_5);
+    p12_sel2(gm, t, g.k == 5);
+  }
+  fp co;
+  fp_shfl(co, c, p36_src(g.k, 1 - g.h, g.s));
+  const fp gmm = g.h ? gm.b : gm.a, gmo = g.h ? gm.a : gm.b;
+  p12_cmul(r, c, co, gmm, gmo, g.h);
+}
+
+__device__ __noinline__ void p36_inv(fp& r, const fp& x, const P36& g) {
+  fp12 f, t;
+  fp_shfl(f.c0.c0.a, x, p36_src(0, 0, 0));
+  fp_shfl(f.c0.c0.b, x, p36_src(0, 1, 0));
+  fp_shfl(f.c1.c0.a, x, p36_src(1, 0, 0));
+  fp_shfl(f.c1.c0.b, x, p36_src(1, 1, 0));
+  fp_shfl(f.c0.c1.a, x, p36_src(2, 0, 0));
+  fp_shfl(f.c0.c1.b, x, p36_src(2, 1, 0));
+  fp_shfl(f.c1.c1.a, x, p36_src(3, 0, 0));
+  fp_shfl(f.c1.c1.b, x, p36_src(3, 1, 0));
+  fp_shfl(f.c0.c2.a, x, p36_src(4, 0, 0));
+  fp_shfl(f.c0.c2.b, x, p36_src(4, 1, 0));
+  fp_shfl(f.c1.c2.a, x, p36_src(5, 0, 0));
+  fp_shfl(f.c1.c2.b, x, p36_src(5, 1, 0));
+  fp12_inv(t, f);
+  const fp2* e[6] = {&t.c0.c0, &t.c1.c0, &t.c0.c1, &t.c1.c1, &t.c0.c2, &t.c1.c2};
+  fp2 pick = t.c0.c0;
+#pragma unroll
+  for (int k = 1; k < 6; k++) p12_sel2(pick, *e[k], g.k == k);
+  r = g.h ? pick.b : pick.a;
+}
+
+__device__ __forceinline__ void p36_pow_u(fp& r, const fp& x, const P36& g) {
+  fp acc = x;
+#pragma nounroll
+  for (int i = 61; i >= 0; i--) {
+    p36_cyc_sqr(acc, acc, g);
+    if (i == 55 || i == 0) p36_mul(acc, acc, x, g);
+  }
+  p36_conj(r, acc, g);
+}
+
+__device__ __forceinline__ void p36_pow_small(fp& r, const fp& x, uint32_t e, const P36& g) {
+  fp acc = x;
+  int top = 31;
+  while (!((e >> top) & 1)) top--;
+#pragma nounroll
+  for (int i = top - 1; i >= 0; i--) {
+    p36_cyc_sqr(acc, acc, g);
+    if ((e >> i) & 1) p36_mul(acc, acc, x, g);
+  }
+  r = acc;
+}
+
+__device__ __forceinline__ void p36_final_exp(fp& r, const fp& f, const P36& g) {
+  fp t, gg;
+  p36_inv(t, f, g);
+  p36_conj(gg, f, g);
+  p36_mul(gg, gg, t, g);
+  p36_frob<2>(t, gg, g);
+  p36_mul(gg, t, gg, g);
+  fp a, b, c, c36, b6, b18, b30, a12, a18, g2;
+  p36_pow_u(a, gg, g);
+  p36_pow_u(b, a, g);
+  p36_pow_u(c, b, g);
+  p36_pow_small(c36, c, 36, g);
+  p36_pow_small(b6, b, 6, g);
+  p36_pow_small(b18, b6, 3, g);
+  p36_mul(b30, b18, b6, g);
+  p36_mul(b30, b30, b6, g);
+  p36_pow_small(a12, a, 12, g);
+  p36_pow_small(a18, a, 18, g);
+  p36_cyc_sqr(g2, gg, g);
+  fp t0, t1, t2, t3;
+  p36_mul(t0, c36, b30, g);
+  p36_mul(t0, t0, a18, g);
+  p36_mul(t0, t0, g2, g);
+  p36_conj(t0, t0, g);
+  p36_mul(t1, c36, b18, g);
+  p36_mul(t1, t1, a12, g);
+  p36_conj(t1, t1, g);
+  p36_mul(t1, t1, gg, g);
+  p36_mul(t2, b6, gg, g);
+  p36_frob<1>(t1, t1, g);
+  p36_frob<2>(t2, t2, g);
+  p36_frob<3>(t3, gg, g);
+  p36_mul(t0, t0, t1, g);
+  p36_mul(t0, t0, t2, g);
+  p36_mul(r, t0, t3, g);
+}
+
+// prod_{j < NP} e(P_j, Q_j) == 1 ?  (lines of Q_j precomputed; P_j not infinity).
+// Called by all 64 lanes of a wave together; every lane returns the verdict.
+template <int NP>
+__device__ __forceinline__ bool p36_pairing_check(const g1a* P, const uint32_t* const* lines, const P36& g) {
+  fp f;
+  p36_one(f, g);
+  int k = 0;
+#pragma nounroll
+  for (int i = BN_ATE_DBL - 1; i >= 0; i--) {
+    p36_sqr(f, f, g);
+#pragma unroll
+    for (int j = 0; j < NP; j++) p36_line1(f, lines[j] + k * BN_LINE_WORDS, P[j], g);
+    k++;
+    if (bn_ate_bit(i)) {
+#pragma unroll
+      for (int j = 0; j < NP; j++) p36_line1(f, lines[j] + k * BN_LINE_WORDS, P[j], g);
+      k++;
+    }
+  }
+  p36_conj(f, f, g);
+  for (int t = 0; t < 2; t++) {
+#pragma unroll
+    for (int j = 0; j < NP; j++) p36_line1(f, lines[j] + k * BN_LINE_WORDS, P[j], g);
+    k++;
+  }
+  fp e;
+  p36_final_exp(e, f, g);
+  fp want;
+  p36_one(want, g);
+  const bool mine = f_eq(e, want);
+  bool all = true;
+#pragma unroll
+  for (int q = 0; q < 12; q++) all = all && (__shfl((int)mine, q) != 0);
+  return all;
+}
