@@ -41,3 +41,41 @@ __device__ __forceinline__ void g2a_load(g2a& a, const uint32_t* o) {
   a.inf = o[36] != 0;
 }
 
+
+// g1_map (bls_ops.h) with the try-and-increment candidates x, x + 1, ..., x + 63 tried on the
+// 64 lanes of a wave at once: the lowest lane whose x^3 + 2 is a square wins, which is the point
+// the sequential loop returns; every lane gets it.  One sqrt latency instead of two on average
+// (half of all x are abscissas).  All 64 lanes must call it together.
+__device__ __forceinline__ void g1_map_wave(g1a& r, const uint8_t* msg, uint32_t len) {
+  uint8_t d[32];
+  sha256(d, msg, len);
+  uint32_t w[8];
+  be32_to_words(w, d);
+  fp x, two, rhs, y, off, step;
+  f_from_words(x, w);
+  const uint32_t lane = threadIdx.x & 63;
+  uint32_t t[8] = {2, 0, 0, 0, 0, 0, 0, 0};
+  f_from_words(two, t);
+  t[0] = lane;
+  f_from_words(off, t);
+  t[0] = 64;
+  f_from_words(step, t);
+  f_add(x, x, off);
+  for (;;) {
+    f_sqr(rhs, x);
+    f_mul(rhs, rhs, x);
+    f_add(rhs, rhs, two);
+    const bool ok = fp_sqrt(y, rhs);
+    const unsigned long long m = __ballot(ok);
+    if (m) {
+      const int src = __ffsll(m) - 1;
+      for (int i = 0; i < BN_LIMBS; i++) {
+        r.x.v[i] = (uint32_t)__shfl((int)x.v[i], src);
+        r.y.v[i] = (uint32_t)__shfl((int)y.v[i], src);
+      }
+      break;
+    }
+    f_add(x, x, step);
+  }
+  r.inf = false;
+}

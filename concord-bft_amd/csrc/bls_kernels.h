@@ -35,9 +35,10 @@ hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok
                                   uint32_t* d_out_part, hipStream_t s);
 hipError_t cbft_bls_launch_g2_parts(const uint32_t* d_parts, uint32_t count, uint32_t* d_lines, uint8_t* d_ok,
                                     uint8_t* d_out65, hipStream_t s);
-hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, const uint32_t* d_pk_lines,
-                                  const uint8_t* d_pk_ok, const uint32_t* d_gen_lines, uint8_t* d_result,
-                                  hipStream_t s);
+// H = g1_map(msg) (-> d_H when non-null) and e(H, PK) e(-sigma, g2) == 1 in one launch
+hipError_t cbft_bls_launch_verify(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, const uint8_t* d_sig33,
+                                  const uint32_t* d_pk_lines, const uint8_t* d_pk_ok, const uint32_t* d_gen_lines,
+                                  uint8_t* d_result, hipStream_t s);
 hipError_t cbft_bls_launch_sign(const uint8_t* d_msg, uint32_t len, const uint32_t* d_sk, uint32_t id,
                                 uint8_t* d_out37, hipStream_t s);
 hipError_t cbft_bls_launch_pubkey(const uint32_t* d_sk, uint8_t* d_out65, hipStream_t s);

@@ -10,11 +10,12 @@
 //   bls_sign_kernel          sigma = sk * g1_map(msg)     (BlsThresholdSigner.cpp:32-47)
 #include "bls_common.h"
 
-__global__ void bls_hash_kernel(const uint8_t* msg, uint32_t len, uint32_t* H) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// one wave: the candidates are tried 64 at a time (g1_map_wave)
+__global__ void __launch_bounds__(64) bls_hash_kernel(const uint8_t* msg, uint32_t len, uint32_t* H) {
+  if (blockIdx.x != 0) return;
   g1a h;
-  g1_map(h, msg, len);
-  g1a_store(H, h);
+  g1_map_wave(h, msg, len);
+  if (threadIdx.x == 0) g1a_store(H, h);
 }
 
 // inv[d] = d^-1 mod r (Montgomery form), d = 1 .. BLS_INV_TABLE (the reference keeps the same

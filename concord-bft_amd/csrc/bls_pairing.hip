@@ -1,71 +1,164 @@
 // BLS BN-P254 pairing-check kernels for gfx950 (threshsign path).
 //
-//   bls_share_verify_kernel  one wave per share: parse, e(H, vk_id) e(-sigma, g2) == 1
+//   bls_share_verify_kernel  one (2-wave) block per share: parse, e(H, vk_id) e(-sigma, g2) == 1
 //                            (BlsAccumulatorBase::verifyShare, BlsAccumulatorBase.cpp:62-84)
-//   bls_verify_kernel        e(H, PK) e(-sigma, g2) == 1   (BlsThresholdVerifier.cpp:69-96)
-// The G2 side is precomputed (bls_keys.hip); the Fp12 accumulator is spread over a whole wave,
-// three lanes per Fp component (bn254_pair36.h).
+//   bls_verify_kernel        H = g1_map(msg), e(H, PK) e(-sigma, g2) == 1
+//                            (BlsThresholdVerifier.cpp:69-96)
+// The G2 side is precomputed (bls_keys.hip); each Fp12 accumulator is spread over a whole wave,
+// three lanes per Fp component (bn254_pair36.h).  The two Miller loops of a check run on two
+// waves of one block (two SIMDs): wave 0 the (H, key) pair, wave 1 decodes sigma and runs the
+// (-sigma, g2) pair; wave 1 hands its Miller value over through LDS, wave 0 multiplies and
+// runs the final exponentiation.  A pairing check is one instruction stream per wave (a lone
+// wave per SIMD, issue-bound), so splitting the pairs takes one Miller loop's line evaluations
+// off the critical path, and with them the sqrt of sigma's decompression (and, in
+// bls_verify_kernel, the hash to G1, which wave 0 computes while wave 1 decodes sigma).
 #include "bls_common.h"
 #include "bn254_pair36.h"
 
-// shares: k x 37 bytes.  out: valid[k] (1 = verified), sig[k] (parsed affine point, 19 words),
-// ids[k].  A share whose id is outside [1, n] or whose point does not decode is invalid.
-// One wave per share: the pairing check runs on 36 lanes (bn254_pair36.h); parsing is
-// done by every lane of the group (same latency as one) and lane 0 writes the results.
-__global__ void __launch_bounds__(64) bls_share_verify_kernel(const uint8_t* shares, uint32_t k, uint32_t n,
-                                                              const uint32_t* H, const uint32_t* vk_lines,
-                                                              const uint8_t* vk_ok, const uint32_t* gen_lines,
-                                                              int do_verify, uint8_t* valid, uint32_t* sig,
-                                                              uint32_t* ids) {
-  const uint32_t j = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (j >= k) return;  // whole waves exit together
-  const P36 g = p36_lane();
-  const bool lead = (threadIdx.x & 63) == 0;
-  uint32_t id;
-  g1a s;
-  bool good = bls_parse_share(id, s, shares + 37 * (size_t)j);
-  good = good && id >= 1 && id <= n;
-  if (lead) {
-    ids[j] = id;
-    g1a_store(sig + 19 * (size_t)j, s);
-  }
-  if (good && do_verify) {
-    good = vk_ok[id - 1] != 0;
-    if (good) {
-      g1a P[2];
-      g1a_load(P[0], H);
-      P[1] = s;
-      if (!s.inf) f_neg(P[1].y, s.y);
-      const uint32_t* l[2] = {vk_lines + (size_t)(id - 1) * LINES_PER_KEY, gen_lines};
-      // e(O, Q) = 1: an infinite sigma checks against e(H, vk) alone
-      if (P[1].inf)
-        good = p36_pairing_check<1>(P, l, g);
-      else
-        good = p36_pairing_check<2>(P, l, g);
-    }
-  }
-  if (lead) valid[j] = good ? 1 : 0;
+#define PAIR_BLOCK 128  // two waves
+#define SIMDS 1024       // 256 CUs x 4 SIMDs (MI355X)
+
+// wave 1 -> wave 0: its Miller value (36 lanes x 9 limbs) and a flag
+struct PairXchg {
+  uint32_t f[36][BN_LIMBS];
+  int ok;
+};
+
+__device__ __forceinline__ void xchg_put(PairXchg& x, const fp& f, const P36& g) {
+  if (g.lane < 36)
+    for (int i = 0; i < BN_LIMBS; i++) x.f[g.lane][i] = f.v[i];
+}
+__device__ __forceinline__ void xchg_get(fp& f, const PairXchg& x, const P36& g) {
+  const int l = g.lane < 36 ? g.lane : g.lane - 36;  // shadows read the lane they mirror
+  for (int i = 0; i < BN_LIMBS; i++) f.v[i] = x.f[l][i];
 }
 
-// e(H, PK) * e(-sigma, g2) == 1 for a combined signature (33 bytes); one wave
-__global__ void __launch_bounds__(64) bls_verify_kernel(const uint32_t* H, const uint8_t* sig33,
-                                                        const uint32_t* pk_lines, const uint8_t* pk_ok,
-                                                        const uint32_t* gen_lines, uint8_t* result) {
-  if (blockIdx.x != 0) return;
+// shares: k x 37 bytes.  out: valid[k] (1 = verified), sig[k] (parsed affine point, 19 words),
+// ids[k].  A share whose id is outside [1, n] or whose point does not decode is invalid.
+// do_verify = 0: parse only, valid = decodable && id in range.
+//   WAVES = 2: one 2-wave block per share (the two Miller loops in parallel): the latency form,
+//              used while 2k waves fit the chip's 1,024 SIMDs;
+//   WAVES = 1: one wave per share, both pairs on it: the throughput form for larger k and for
+//              parse-only launches (two waves of a share would share SIMDs with other shares).
+template <int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint8_t* shares, uint32_t k, uint32_t n,
+                                                                      const uint32_t* H, const uint32_t* vk_lines,
+                                                                      const uint8_t* vk_ok, const uint32_t* gen_lines,
+                                                                      int do_verify, uint8_t* valid, uint32_t* sig,
+                                                                      uint32_t* ids) {
+  __shared__ PairXchg xc;
+  const uint32_t j = blockIdx.x;
+  if (j >= k) return;  // whole blocks exit together
+  const int wave = threadIdx.x >> 6;
   const P36 g = p36_lane();
-  g1a P[2];
-  g1a_load(P[0], H);
-  bool good = pk_ok[0] && g1_decompress(P[1], sig33);
-  if (good) {
-    const uint32_t* l[2] = {pk_lines, gen_lines};
-    if (P[1].inf) {
-      good = p36_pairing_check<1>(P, l, g);
+  const uint8_t* sh = shares + 37 * (size_t)j;
+  const uint32_t id = ((uint32_t)sh[0] << 24) | ((uint32_t)sh[1] << 16) | ((uint32_t)sh[2] << 8) | sh[3];
+  const bool id_ok = id >= 1 && id <= n;
+  const bool key_ok = do_verify && id_ok && vk_ok[id - 1] != 0;
+  const uint32_t* vkl = key_ok ? vk_lines + (size_t)(id - 1) * LINES_PER_KEY : nullptr;
+  if (WAVES == 1) {
+    uint32_t pid;
+    g1a s;
+    bool good = bls_parse_share(pid, s, sh) && id_ok;
+    if (g.lane == 0) {
+      ids[j] = id;
+      g1a_store(sig + 19 * (size_t)j, s);
+    }
+    if (do_verify) {
+      good = good && key_ok;
+      if (good) {
+        g1a P[2];
+        g1a_load(P[0], H);
+        P[1] = s;
+        if (!s.inf) f_neg(P[1].y, s.y);
+        const uint32_t* l[2] = {vkl, gen_lines};
+        good = P[1].inf ? p36_pairing_check<1>(P, l, g) : p36_pairing_check<2>(P, l, g);
+      }
+    }
+    if (g.lane == 0) valid[j] = good ? 1 : 0;
+    return;
+  }
+  fp f;
+  if (wave == 1) {
+    uint32_t pid;
+    g1a s;
+    const bool parsed = bls_parse_share(pid, s, sh) && id_ok;
+    if (g.lane == 0) {
+      ids[j] = id;
+      g1a_store(sig + 19 * (size_t)j, s);
+    }
+    if (parsed && key_ok && !s.inf) {
+      g1a P = s;
+      f_neg(P.y, s.y);
+      const uint32_t* l[1] = {gen_lines};
+      p36_miller<1>(f, &P, l, g);
     } else {
-      f_neg(P[1].y, P[1].y);
-      good = p36_pairing_check<2>(P, l, g);
+      p36_one(f, g);  // e(O, g2) = 1: an infinite sigma checks against e(H, vk) alone
+    }
+    xchg_put(xc, f, g);
+    if (g.lane == 0) xc.ok = parsed ? 1 : 0;
+  } else if (key_ok) {
+    g1a P;
+    g1a_load(P, H);
+    const uint32_t* l[1] = {vkl};
+    p36_miller<1>(f, &P, l, g);
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  bool good = xc.ok != 0;
+  if (do_verify) {
+    good = good && key_ok;
+    if (good) {
+      fp f1;
+      xchg_get(f1, xc, g);
+      p36_mul(f, f, f1, g);
+      good = p36_is_one_after_final_exp(f, g);
     }
   }
-  if (threadIdx.x == 0) result[0] = good ? 1 : 0;
+  if (g.lane == 0) valid[j] = good ? 1 : 0;
+}
+
+// H = g1_map(msg) on wave 0 (also stored to H_out when non-null), sigma from 33 bytes on wave 1:
+// e(H, PK) * e(-sigma, g2) == 1 for a combined signature.  One block of two waves.
+__global__ void __launch_bounds__(PAIR_BLOCK) bls_verify_kernel(const uint8_t* msg, uint32_t len, uint32_t* H_out,
+                                                                const uint8_t* sig33, const uint32_t* pk_lines,
+                                                                const uint8_t* pk_ok, const uint32_t* gen_lines,
+                                                                uint8_t* result) {
+  __shared__ PairXchg xc;
+  if (blockIdx.x != 0) return;
+  const int wave = threadIdx.x >> 6;
+  const P36 g = p36_lane();
+  fp f;
+  if (wave == 1) {
+    g1a s;
+    const bool ok = g1_decompress(s, sig33);
+    if (ok && !s.inf) {
+      g1a P = s;
+      f_neg(P.y, s.y);
+      const uint32_t* l[1] = {gen_lines};
+      p36_miller<1>(f, &P, l, g);
+    } else {
+      p36_one(f, g);
+    }
+    xchg_put(xc, f, g);
+    if (g.lane == 0) xc.ok = ok ? 1 : 0;
+  } else {
+    g1a P;
+    g1_map_wave(P, msg, len);
+    if (g.lane == 0 && H_out) g1a_store(H_out, P);
+    const uint32_t* l[1] = {pk_lines};
+    p36_miller<1>(f, &P, l, g);
+  }
+  __syncthreads();
+  if (wave != 0) return;
+  bool good = xc.ok != 0 && pk_ok[0] != 0;
+  if (good) {
+    fp f1;
+    xchg_get(f1, xc, g);
+    p36_mul(f, f, f1, g);
+    good = p36_is_one_after_final_exp(f, g);
+  }
+  if (g.lane == 0) result[0] = good ? 1 : 0;
 }
 
 // ------------------------------------------------------------------------------ launchers
@@ -74,14 +167,18 @@ hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uin
                                         const uint32_t* d_gen_lines, int do_verify, uint8_t* d_valid,
                                         uint32_t* d_sig, uint32_t* d_ids, hipStream_t s) {
   if (!k) return hipSuccess;
-  hipLaunchKernelGGL(bls_share_verify_kernel, dim3(k), dim3(64), 0, s, d_shares, k, n, d_H, d_vk_lines,
-                     d_vk_ok, d_gen_lines, do_verify, d_valid, d_sig, d_ids);
+  if (do_verify && 2 * (size_t)k <= SIMDS)
+    hipLaunchKernelGGL(bls_share_verify_kernel<2>, dim3(k), dim3(128), 0, s, d_shares, k, n, d_H, d_vk_lines,
+                       d_vk_ok, d_gen_lines, do_verify, d_valid, d_sig, d_ids);
+  else
+    hipLaunchKernelGGL(bls_share_verify_kernel<1>, dim3(k), dim3(64), 0, s, d_shares, k, n, d_H, d_vk_lines,
+                       d_vk_ok, d_gen_lines, do_verify, d_valid, d_sig, d_ids);
   return hipGetLastError();
 }
-hipError_t cbft_bls_launch_verify(const uint32_t* d_H, const uint8_t* d_sig33, const uint32_t* d_pk_lines,
-                                  const uint8_t* d_pk_ok, const uint32_t* d_gen_lines, uint8_t* d_result,
-                                  hipStream_t s) {
-  hipLaunchKernelGGL(bls_verify_kernel, dim3(1), dim3(64), 0, s, d_H, d_sig33, d_pk_lines, d_pk_ok, d_gen_lines,
-                     d_result);
+hipError_t cbft_bls_launch_verify(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, const uint8_t* d_sig33,
+                                  const uint32_t* d_pk_lines, const uint8_t* d_pk_ok, const uint32_t* d_gen_lines,
+                                  uint8_t* d_result, hipStream_t s) {
+  hipLaunchKernelGGL(bls_verify_kernel, dim3(1), dim3(PAIR_BLOCK), 0, s, d_msg, len, d_H, d_sig33, d_pk_lines,
+                     d_pk_ok, d_gen_lines, d_result);
   return hipGetLastError();
 }

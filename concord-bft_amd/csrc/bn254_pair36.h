@@ -355,11 +355,12 @@ __device__ __forceinline__ void p36_final_exp(fp& r, const fp& f, const P36& g) 
   p36_mul(r, t0, t3, g);
 }
 
-// prod_{j < NP} e(P_j, Q_j) == 1 ?  (lines of Q_j precomputed; P_j not infinity).
-// Called by all 64 lanes of a wave together; every lane returns the verdict.
+// f = prod_{j < NP} of the Miller values of (P_j, Q_j) (lines of Q_j precomputed; P_j not
+// infinity), conjugation and the two Frobenius lines included: the value final_exp takes.
+// Miller values of disjoint pair sets multiply (the loop squares and conjugates a product), so
+// two waves may run one pair each and multiply their f.  All 64 lanes of the wave call it.
 template <int NP>
-__device__ __forceinline__ bool p36_pairing_check(const g1a* P, const uint32_t* const* lines, const P36& g) {
-  fp f;
+__device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* const* lines, const P36& g) {
   p36_one(f, g);
   int k = 0;
 #pragma nounroll
@@ -380,6 +381,10 @@ __device__ __forceinline__ bool p36_pairing_check(const g1a* P, const uint32_t* 
     for (int j = 0; j < NP; j++) p36_line1(f, lines[j] + k * BN_LINE_WORDS, P[j], g);
     k++;
   }
+}
+
+// final_exp(f) == 1 ?  Every lane returns the verdict.
+__device__ __forceinline__ bool p36_is_one_after_final_exp(const fp& f, const P36& g) {
   fp e;
   p36_final_exp(e, f, g);
   fp want;
@@ -389,4 +394,12 @@ __device__ __forceinline__ bool p36_pairing_check(const g1a* P, const uint32_t* 
 #pragma unroll
   for (int q = 0; q < 12; q++) all = all && (__shfl((int)mine, q) != 0);
   return all;
+}
+
+// prod_{j < NP} e(P_j, Q_j) == 1 on one wave
+template <int NP>
+__device__ __forceinline__ bool p36_pairing_check(const g1a* P, const uint32_t* const* lines, const P36& g) {
+  fp f;
+  p36_miller<NP>(f, P, lines, g);
+  return p36_is_one_after_final_exp(f, g);
 }

@@ -24,10 +24,16 @@ static int bls_gen_lines(cbft_ctx* c) {
   return CBFT_OK;
 }
 
-static int bls_upload_msg_hash(cbft_ctx* c, const uint8_t* msg, uint32_t len) {
+static int bls_upload_msg(cbft_ctx* c, const uint8_t* msg, uint32_t len) {
   CBFT_HIP(c->bls_msg.reserve(len + 1));
   CBFT_HIP(c->bls_H.reserve(19 * 4));
   if (len) CBFT_HIP(hipMemcpyAsync(c->bls_msg.p, msg, len, hipMemcpyHostToDevice, c->stream));
+  return CBFT_OK;
+}
+
+static int bls_upload_msg_hash(cbft_ctx* c, const uint8_t* msg, uint32_t len) {
+  int rc = bls_upload_msg(c, msg, len);
+  if (rc) return rc;
   CBFT_HIP(cbft_bls_launch_hash(c->bls_msg.as<uint8_t>(), len, c->bls_H.as<uint32_t>(), c->stream));
   return CBFT_OK;
 }
@@ -225,13 +231,15 @@ int cbft_bls_combine_finish(cbft_ctx* c, const uint8_t* partials, uint32_t count
   return CBFT_OK;
 }
 
-static int bls_verify_with_lines(cbft_ctx* c, const uint8_t* sig33, const uint32_t* d_lines, const uint8_t* d_ok,
-                                 int* out_ok) {
+// the message is on the device (bls_upload_msg): the verify kernel hashes it itself
+static int bls_verify_with_lines(cbft_ctx* c, uint32_t len, const uint8_t* sig33, const uint32_t* d_lines,
+                                 const uint8_t* d_ok, int* out_ok) {
   CBFT_HIP(c->bls_shares.reserve(33));
   CBFT_HIP(c->bls_out.reserve(33));
   CBFT_HIP(hipMemcpyAsync(c->bls_shares.p, sig33, 33, hipMemcpyHostToDevice, c->stream));
-  CBFT_HIP(cbft_bls_launch_verify(c->bls_H.as<uint32_t>(), c->bls_shares.as<uint8_t>(), d_lines, d_ok,
-                                  c->bls_gen_lines.as<uint32_t>(), c->bls_out.as<uint8_t>(), c->stream));
+  CBFT_HIP(cbft_bls_launch_verify(c->bls_msg.as<uint8_t>(), len, c->bls_H.as<uint32_t>(), c->bls_shares.as<uint8_t>(),
+                                  d_lines, d_ok, c->bls_gen_lines.as<uint32_t>(), c->bls_out.as<uint8_t>(),
+                                  c->stream));
   uint8_t r = 0;
   CBFT_HIP(hipMemcpyAsync(&r, c->bls_out.p, 1, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipStreamSynchronize(c->stream));
@@ -247,9 +255,9 @@ int cbft_bls_verify(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, 
   if (!ks) return CBFT_EINVAL;
   CBFT_HIP(hipSetDevice(c->device));
   int rc = bls_gen_lines(c);
-  if (!rc) rc = bls_upload_msg_hash(c, msg, len);
+  if (!rc) rc = bls_upload_msg(c, msg, len);
   if (rc) return rc;
-  return bls_verify_with_lines(c, sig33, ks->lines.as<uint32_t>(), ks->ok.as<uint8_t>(), out_ok);
+  return bls_verify_with_lines(c, len, sig33, ks->lines.as<uint32_t>(), ks->ok.as<uint8_t>(), out_ok);
 }
 
 int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, const uint8_t* sig33,
@@ -261,7 +269,7 @@ int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint3
   if (!ks) return CBFT_EINVAL;
   CBFT_HIP(hipSetDevice(c->device));
   int rc = bls_gen_lines(c);
-  if (!rc) rc = bls_upload_msg_hash(c, msg, len);
+  if (!rc) rc = bls_upload_msg(c, msg, len);
   if (rc) return rc;
   CBFT_HIP(c->bls_bitmap.reserve(256));
   CBFT_HIP(c->bls_ms_lines.reserve(cbft_bls_lines_words_per_key() * 4));
@@ -270,7 +278,7 @@ int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint3
   CBFT_HIP(cbft_bls_launch_g2_sum(ks->aff.as<uint32_t>() + BLS_G2A_WORDS, ks->ok.as<uint8_t>() + 1, ks->n,
                                   c->bls_bitmap.as<uint8_t>(), 1, ks->n + 1, c->bls_ms_lines.as<uint32_t>(),
                                   c->bls_ms_ok.as<uint8_t>(), nullptr, nullptr, c->stream));
-  return bls_verify_with_lines(c, sig33, c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), out_ok);
+  return bls_verify_with_lines(c, len, sig33, c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), out_ok);
 }
 
 int cbft_bls_sum_keys(cbft_ctx* c, uint32_t id, const uint8_t* signers256, uint8_t* out65) {
@@ -319,7 +327,7 @@ int cbft_bls_verify_multisig_partials(cbft_ctx* c, const uint8_t* msg, uint32_t 
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
   int rc = bls_gen_lines(c);
-  if (!rc) rc = bls_upload_msg_hash(c, msg, len);
+  if (!rc) rc = bls_upload_msg(c, msg, len);
   if (rc) return rc;
   CBFT_HIP(c->bls_partial.reserve((size_t)count * CBFT_BLS_G2_PARTIAL_BYTES));
   CBFT_HIP(c->bls_ms_lines.reserve(cbft_bls_lines_words_per_key() * 4));
@@ -328,7 +336,7 @@ int cbft_bls_verify_multisig_partials(cbft_ctx* c, const uint8_t* msg, uint32_t 
                           hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(cbft_bls_launch_g2_parts(c->bls_partial.as<uint32_t>(), count, c->bls_ms_lines.as<uint32_t>(),
                                     c->bls_ms_ok.as<uint8_t>(), nullptr, c->stream));
-  return bls_verify_with_lines(c, sig33, c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), out_ok);
+  return bls_verify_with_lines(c, len, sig33, c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), out_ok);
 }
 
 // 32-byte big-endian scalar -> 8 little-endian words
