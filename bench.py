@@ -557,6 +557,7 @@ def bench_bls(ctx, args, cpu_threads):
            "pairings_per_s": 2 * nsh / (t_share * 1e-3),
            "combine_ms": t_comb, "verify_ms": t_ver, "optimistic_ms": t_opt, "multisig_ms": t_ms,
            "verdicts": "share verdicts == planted bad set; combined sig == sk*H(m) byte-exact"}
+    out["roofline"] = _bls_roofline()
     if not args.no_cpu:
         workload.cpu_bls_verify_shares(cert, h33, threads=cpu_threads)  # warm-up
         c0 = time.perf_counter()
@@ -569,6 +570,29 @@ def bench_bls(ctx, args, cpu_threads):
                                          f"(absent) and not an optimized CPU pairing; no speed-up is claimed "
                                          f"against it"}
     return out
+
+
+def _bls_roofline():
+    """BLS kernels are latency-bound, not throughput-bound: a pairing check is one dependent
+    instruction stream per wave (36 of 64 lanes carry the Fp12 state, bn254_pair36.h), 760
+    checks fill 760 of 1,024 SIMDs once, and a certificate is a chain of such kernels.  Their
+    roofline is therefore the per-wave issue rate, with the MAD64 fraction alongside to show how
+    far from the throughput peak the latency form sits.  Numbers from one rocprofv3 --pmc pass
+    (tools/bls_prof.sh -> tools/pmc_bls.py -> profiles/pmc_bls.json)."""
+    path = os.path.join(ROOT, "profiles", "pmc_bls.json")
+    if not os.path.exists(path):
+        return None
+    rec = json.load(open(path))
+    ks = {}
+    for name, k in rec["kernels"].items():
+        ks[name] = {key: k.get(key) for key in ("duration_ms", "waves", "mad_frac_of_peak", "wave_cycles_per_valu",
+                                                "valu_insts_per_wave")}
+    return {"bound": "latency: one wave per pairing check / point chain (per-wave VALU issue)",
+            "peak_mad64_lane_ops_per_s": rec.get("mad64_peak_lane_ops_per_s"),
+            "per_wave_issue_floor_cycles_per_valu": 4.8,
+            "per_wave_issue_floor_basis": "v_mad_u64_u32 at saturation, 13.3 lanes/clk/SIMD "
+                                          "(profiles/r01_intrate_microbench.txt): a wave64 mad every 4.8 cycles",
+            "kernels": ks, "source": "profiles/pmc_bls.json"}
 
 
 def _openssl_version():

@@ -3,9 +3,13 @@
 //
 //   bls_keys_kernel          per G2 key: decompress + subgroup check + 70 Miller-loop lines
 //                            (BlsThresholdVerifier ctor; lines make per-share work G2-free)
-//   bls_g2_sum_kernel        multisig PK = sum vk_i over the signer bitmap, + its lines
+//   bls_g2_sum_kernel        multisig PK = sum vk_i over the signer bitmap (Jacobian partial, or
+//                            compressed for cbft_bls_sum_keys)
+//   bls_g2_lines_kernel      sum of partials -> affine PK -> its unnormalised Miller lines, the
+//                            products of each line step spread over one wave (bn254_g2wave.h)
 //   bls_pubkey_kernel        vk = sk * g2
 #include "bls_common.h"
+#include "bn254_g2wave.h"
 
 #define LINE_SCRATCH_WORDS (BN_ATE_LINES * 36)  // g2_precompute_lines_batch scratch per key
 
@@ -32,28 +36,22 @@ __global__ void bls_gen_lines_kernel(uint32_t* lines) {
   g2_precompute_lines_batch(lines, q, scr);
 }
 
-// multisig public key = sum of vk_i for set bits (bit id-1, LSB first) of the 256-byte bitmap,
-// then its Miller-loop lines (BlsMultisigVerifier.cpp:33-38, 89-95).  One block: each of the
-// SUM_THREADS lanes adds its strided share of the (already decoded, at load) keys in Jacobian
-// form, then an LDS tree halves the partial sums; lane 0 normalises, compresses and computes
-// the lines.  A selected key that did not decode makes the result invalid (ok = 0).
+// multisig public key = sum of vk_i for set bits (bit id-1, LSB first) of the 256-byte bitmap
+// (BlsMultisigVerifier.cpp:33-38, 89-95).  One block: each of the SUM_THREADS lanes adds its
+// strided share of the (already decoded, at load) keys in Jacobian form, then an LDS tree halves
+// the partial sums.  A selected key that did not decode makes the result invalid (ok = 0).
 #define SUM_THREADS 256
-// normalise, compress (out65) and compute the Miller lines of a summed key; bad = a selected
-// key did not decode
-__device__ void g2_sum_tail(const g2j& acc, bool bad, uint32_t* lines, uint8_t* ok, uint8_t* out65, uint32_t* scr) {
+// normalise and compress (out65) a summed key; bad = a selected key did not decode
+__device__ void g2_sum_tail(const g2j& acc, bool bad, uint8_t* ok, uint8_t* out65) {
   g2a s;
   g2_to_affine(s, acc);
   const bool good = !bad;
-  if (out65) {
-    if (good) {
-      g2_compress(out65, s);
-    } else {
-      for (int q = 0; q < 65; q++) out65[q] = 0;
-    }
+  if (good) {
+    g2_compress(out65, s);
+  } else {
+    for (int q = 0; q < 65; q++) out65[q] = 0;
   }
-  const bool usable = good && !s.inf;
-  ok[0] = usable ? 1 : 0;
-  if (usable && lines) g2_precompute_lines_batch(lines, s, scr);
+  ok[0] = good && !s.inf ? 1 : 0;
 }
 
 __device__ __forceinline__ void g2j_store(uint32_t* o, const g2j& a) {
@@ -74,11 +72,12 @@ __device__ __forceinline__ void g2j_load(g2j& a, const uint32_t* o) {
 }
 
 // Signer ids [lo_id, hi_id) only (a rank's slice of a sharded multisig key sum).  With out_part
-// the block writes its Jacobian sum (54 words) + the bad-key flag (1 word) and stops there.
+// the block writes its Jacobian sum (54 words) + the bad-key flag (1 word) (-> bls_g2_lines_kernel),
+// else the compressed sum into out65.
 __global__ void __launch_bounds__(SUM_THREADS) bls_g2_sum_kernel(const uint32_t* aff, const uint8_t* key_ok,
                                                                  uint32_t n, const uint8_t* bitmap, uint32_t lo_id,
-                                                                 uint32_t hi_id, uint32_t* lines, uint8_t* ok,
-                                                                 uint8_t* out65, uint32_t* out_part) {
+                                                                 uint32_t hi_id, uint8_t* ok, uint8_t* out65,
+                                                                 uint32_t* out_part) {
   __shared__ uint32_t sp[SUM_THREADS / 2][54];
   __shared__ int bad;
   const int t = threadIdx.x;
@@ -121,13 +120,15 @@ __global__ void __launch_bounds__(SUM_THREADS) bls_g2_sum_kernel(const uint32_t*
     out_part[54] = bad ? 1u : 0u;
     return;
   }
-  g2_sum_tail(acc, bad != 0, lines, ok, out65, &sp[0][0]);  // the tree is done with sp: reuse it
+  g2_sum_tail(acc, bad != 0, ok, out65);
 }
 
-// Sum of count G2 partials (55 words each, from bls_g2_sum_kernel's out_part) + the tail.
-__global__ void bls_g2_parts_kernel(const uint32_t* parts, uint32_t count, uint32_t* lines, uint8_t* ok,
-                                    uint8_t* out65) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// PK = sum of count G2 partials (55 words each, bls_g2_sum_kernel's out_part), then its
+// BN_ATE_LINES unnormalised (A, B, C) lines (BN_ABC_WORDS each) computed by the whole wave.
+// ok = 0 when a selected key did not decode or PK is infinity.
+__global__ void __launch_bounds__(64) bls_g2_lines_kernel(const uint32_t* parts, uint32_t count, uint32_t* lines,
+                                                          uint8_t* ok) {
+  if (blockIdx.x != 0) return;
   g2j acc;
   fp2_one(acc.X);
   fp2_one(acc.Y);
@@ -139,8 +140,11 @@ __global__ void bls_g2_parts_kernel(const uint32_t* parts, uint32_t count, uint3
     bad |= parts[55 * (size_t)b + 54] != 0;
     g2_add_j(acc, acc, o);
   }
-  __shared__ uint32_t scr[LINE_SCRATCH_WORDS];
-  g2_sum_tail(acc, bad, lines, ok, out65, scr);
+  g2a s;
+  g2_to_affine(s, acc);
+  const bool usable = !bad && !s.inf;
+  if (threadIdx.x == 0) ok[0] = usable ? 1 : 0;
+  if (usable) g2w_lines_abc(lines, s);
 }
 
 // vk = sk * g2 as 65 compressed bytes: the signer's public key (BlsThresholdSigner's
@@ -179,15 +183,16 @@ hipError_t cbft_bls_launch_gen_lines(uint32_t* d_lines, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok, uint32_t n, const uint8_t* d_bitmap,
-                                  uint32_t lo_id, uint32_t hi_id, uint32_t* d_lines, uint8_t* d_ok, uint8_t* d_out65,
-                                  uint32_t* d_out_part, hipStream_t s) {
+                                  uint32_t lo_id, uint32_t hi_id, uint8_t* d_ok, uint8_t* d_out65, uint32_t* d_out_part,
+                                  hipStream_t s) {
   hipLaunchKernelGGL(bls_g2_sum_kernel, dim3(1), dim3(SUM_THREADS), 0, s, d_aff, d_key_ok, n, d_bitmap, lo_id, hi_id,
-                     d_lines, d_ok, d_out65, d_out_part);
+                     d_ok, d_out65, d_out_part);
   return hipGetLastError();
 }
-hipError_t cbft_bls_launch_g2_parts(const uint32_t* d_parts, uint32_t count, uint32_t* d_lines, uint8_t* d_ok,
-                                    uint8_t* d_out65, hipStream_t s) {
-  hipLaunchKernelGGL(bls_g2_parts_kernel, dim3(1), dim3(64), 0, s, d_parts, count, d_lines, d_ok, d_out65);
+size_t cbft_bls_abc_lines_words() { return (size_t)BN_ATE_LINES * BN_ABC_WORDS; }
+hipError_t cbft_bls_launch_g2_lines(const uint32_t* d_parts, uint32_t count, uint32_t* d_lines, uint8_t* d_ok,
+                                    hipStream_t s) {
+  hipLaunchKernelGGL(bls_g2_lines_kernel, dim3(1), dim3(64), 0, s, d_parts, count, d_lines, d_ok);
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_pubkey(const uint32_t* d_sk, uint8_t* d_out65, hipStream_t s) {

@@ -204,6 +204,29 @@ __device__ __forceinline__ void p36_line1(fp& f, const uint32_t* ln, const g1a& 
   p36_sum3(f, T, g);
 }
 
+// f <- f * (A yP + B xP w + C w^3) for an unnormalised line (bn254_g2wave.h, 54 words):
+//   s = 0: yP (f_k A);  s = 1: xP (f_{k-1} B) (xi for k = 0);  s = 2: f_{k-3} C (xi for k < 3)
+// Three multiplications per lane, as p36_line1.
+__device__ __forceinline__ void p36_line_abc(fp& f, const uint32_t* ln, const g1a& P, const P36& g) {
+  fp om, oo, cm, co;
+  p36_fetch(om, oo, f, g.s == 0 ? g.k : (g.s == 1 ? (g.k + 5) % 6 : (g.k + 3) % 6), g);
+  p36_coef(cm, co, ln + 18 * g.s, g.h);
+  const fp u = g.h ? oo : om, v = g.h ? om : oo;
+  fp P1, P2, P3, C, t;
+  f_mul(P1, u, cm);
+  f_mul(P2, v, co);
+  f_add(C, P1, P2);
+  f_sub(t, P1, P2);
+  C = g.h ? C : t;
+  f_mul(P3, C, g.s == 0 ? P.y : P.x);
+  fp T = g.s == 2 ? C : P3;
+  const bool wrap = (g.s == 1 && g.k == 0) || (g.s == 2 && g.k < 3);
+  fp w;
+  p36_xi(w, T, g);
+  fp_sel(T, w, wrap);
+  p36_sum3(f, T, g);
+}
+
 __device__ __forceinline__ void p36_one(fp& r, const P36& g) {
   f_zero(r);
   fp one;
@@ -355,30 +378,37 @@ __device__ __forceinline__ void p36_final_exp(fp& r, const fp& f, const P36& g) 
   p36_mul(r, t0, t3, g);
 }
 
-// f = prod_{j < NP} of the Miller values of (P_j, Q_j) (lines of Q_j precomputed; P_j not
-// infinity), conjugation and the two Frobenius lines included: the value final_exp takes.
+// f = prod_{j < NP} of the Miller values of (P_j, Q_j) (lines of Q_j precomputed, normalised or
+// ABC; P_j not infinity), conjugation and the two Frobenius lines included: the value final_exp takes.
 // Miller values of disjoint pair sets multiply (the loop squares and conjugates a product), so
 // two waves may run one pair each and multiply their f.  All 64 lanes of the wave call it.
-template <int NP>
+template <int NP, bool ABC = false>
 __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* const* lines, const P36& g) {
+  constexpr int W = ABC ? 54 : BN_LINE_WORDS;  // ABC: unnormalised lines (bn254_g2wave.h)
   p36_one(f, g);
   int k = 0;
+  auto line = [&](int j) {
+    if (ABC)
+      p36_line_abc(f, lines[j] + k * W, P[j], g);
+    else
+      p36_line1(f, lines[j] + k * W, P[j], g);
+  };
 #pragma nounroll
   for (int i = BN_ATE_DBL - 1; i >= 0; i--) {
     p36_sqr(f, f, g);
 #pragma unroll
-    for (int j = 0; j < NP; j++) p36_line1(f, lines[j] + k * BN_LINE_WORDS, P[j], g);
+    for (int j = 0; j < NP; j++) line(j);
     k++;
     if (bn_ate_bit(i)) {
 #pragma unroll
-      for (int j = 0; j < NP; j++) p36_line1(f, lines[j] + k * BN_LINE_WORDS, P[j], g);
+      for (int j = 0; j < NP; j++) line(j);
       k++;
     }
   }
   p36_conj(f, f, g);
   for (int t = 0; t < 2; t++) {
 #pragma unroll
-    for (int j = 0; j < NP; j++) p36_line1(f, lines[j] + k * BN_LINE_WORDS, P[j], g);
+    for (int j = 0; j < NP; j++) line(j);
     k++;
   }
 }

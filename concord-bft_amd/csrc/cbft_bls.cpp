@@ -232,13 +232,13 @@ int cbft_bls_combine_finish(cbft_ctx* c, const uint8_t* partials, uint32_t count
 }
 
 // the message is on the device (bls_upload_msg): the verify kernel hashes it itself
-static int bls_verify_with_lines(cbft_ctx* c, uint32_t len, const uint8_t* sig33, const uint32_t* d_lines,
+static int bls_verify_with_lines(cbft_ctx* c, uint32_t len, const uint8_t* sig33, const uint32_t* d_lines, int abc,
                                  const uint8_t* d_ok, int* out_ok) {
   CBFT_HIP(c->bls_shares.reserve(33));
   CBFT_HIP(c->bls_out.reserve(33));
   CBFT_HIP(hipMemcpyAsync(c->bls_shares.p, sig33, 33, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(cbft_bls_launch_verify(c->bls_msg.as<uint8_t>(), len, c->bls_H.as<uint32_t>(), c->bls_shares.as<uint8_t>(),
-                                  d_lines, d_ok, c->bls_gen_lines.as<uint32_t>(), c->bls_out.as<uint8_t>(),
+                                  d_lines, abc, d_ok, c->bls_gen_lines.as<uint32_t>(), c->bls_out.as<uint8_t>(),
                                   c->stream));
   uint8_t r = 0;
   CBFT_HIP(hipMemcpyAsync(&r, c->bls_out.p, 1, hipMemcpyDeviceToHost, c->stream));
@@ -257,7 +257,7 @@ int cbft_bls_verify(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, 
   int rc = bls_gen_lines(c);
   if (!rc) rc = bls_upload_msg(c, msg, len);
   if (rc) return rc;
-  return bls_verify_with_lines(c, len, sig33, ks->lines.as<uint32_t>(), ks->ok.as<uint8_t>(), out_ok);
+  return bls_verify_with_lines(c, len, sig33, ks->lines.as<uint32_t>(), 0, ks->ok.as<uint8_t>(), out_ok);
 }
 
 int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, const uint8_t* sig33,
@@ -272,13 +272,17 @@ int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint3
   if (!rc) rc = bls_upload_msg(c, msg, len);
   if (rc) return rc;
   CBFT_HIP(c->bls_bitmap.reserve(256));
-  CBFT_HIP(c->bls_ms_lines.reserve(cbft_bls_lines_words_per_key() * 4));
+  CBFT_HIP(c->bls_ms_lines.reserve(cbft_bls_abc_lines_words() * 4));
   CBFT_HIP(c->bls_ms_ok.reserve(1));
+  CBFT_HIP(c->bls_partial.reserve(CBFT_BLS_G2_PARTIAL_BYTES));
   CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
+  // PK = sum vk_i (one Jacobian partial), then its lines on one wave, then the 2-wave verify
   CBFT_HIP(cbft_bls_launch_g2_sum(ks->aff.as<uint32_t>() + BLS_G2A_WORDS, ks->ok.as<uint8_t>() + 1, ks->n,
-                                  c->bls_bitmap.as<uint8_t>(), 1, ks->n + 1, c->bls_ms_lines.as<uint32_t>(),
-                                  c->bls_ms_ok.as<uint8_t>(), nullptr, nullptr, c->stream));
-  return bls_verify_with_lines(c, len, sig33, c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), out_ok);
+                                  c->bls_bitmap.as<uint8_t>(), 1, ks->n + 1, c->bls_ms_ok.as<uint8_t>(), nullptr,
+                                  c->bls_partial.as<uint32_t>(), c->stream));
+  CBFT_HIP(cbft_bls_launch_g2_lines(c->bls_partial.as<uint32_t>(), 1, c->bls_ms_lines.as<uint32_t>(),
+                                    c->bls_ms_ok.as<uint8_t>(), c->stream));
+  return bls_verify_with_lines(c, len, sig33, c->bls_ms_lines.as<uint32_t>(), 1, c->bls_ms_ok.as<uint8_t>(), out_ok);
 }
 
 int cbft_bls_sum_keys(cbft_ctx* c, uint32_t id, const uint8_t* signers256, uint8_t* out65) {
@@ -293,7 +297,7 @@ int cbft_bls_sum_keys(cbft_ctx* c, uint32_t id, const uint8_t* signers256, uint8
   CBFT_HIP(c->bls_out.reserve(65));
   CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(cbft_bls_launch_g2_sum(ks->aff.as<uint32_t>() + BLS_G2A_WORDS, ks->ok.as<uint8_t>() + 1, ks->n,
-                                  c->bls_bitmap.as<uint8_t>(), 1, ks->n + 1, nullptr, c->bls_ms_ok.as<uint8_t>(),
+                                  c->bls_bitmap.as<uint8_t>(), 1, ks->n + 1, c->bls_ms_ok.as<uint8_t>(),
                                   c->bls_out.as<uint8_t>(), nullptr, c->stream));
   CBFT_HIP(hipMemcpyAsync(out65, c->bls_out.p, 65, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipStreamSynchronize(c->stream));
@@ -313,8 +317,8 @@ int cbft_bls_sum_keys_partial(cbft_ctx* c, uint32_t id, const uint8_t* signers25
   CBFT_HIP(c->bls_partial.reserve(CBFT_BLS_G2_PARTIAL_BYTES));
   CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(cbft_bls_launch_g2_sum(ks->aff.as<uint32_t>() + BLS_G2A_WORDS, ks->ok.as<uint8_t>() + 1, ks->n,
-                                  c->bls_bitmap.as<uint8_t>(), lo_id, hi_id, nullptr, c->bls_ms_ok.as<uint8_t>(),
-                                  nullptr, c->bls_partial.as<uint32_t>(), c->stream));
+                                  c->bls_bitmap.as<uint8_t>(), lo_id, hi_id, c->bls_ms_ok.as<uint8_t>(), nullptr,
+                                  c->bls_partial.as<uint32_t>(), c->stream));
   CBFT_HIP(hipMemcpyAsync(out_partial, c->bls_partial.p, CBFT_BLS_G2_PARTIAL_BYTES, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipStreamSynchronize(c->stream));
   return CBFT_OK;
@@ -330,13 +334,13 @@ int cbft_bls_verify_multisig_partials(cbft_ctx* c, const uint8_t* msg, uint32_t 
   if (!rc) rc = bls_upload_msg(c, msg, len);
   if (rc) return rc;
   CBFT_HIP(c->bls_partial.reserve((size_t)count * CBFT_BLS_G2_PARTIAL_BYTES));
-  CBFT_HIP(c->bls_ms_lines.reserve(cbft_bls_lines_words_per_key() * 4));
+  CBFT_HIP(c->bls_ms_lines.reserve(cbft_bls_abc_lines_words() * 4));
   CBFT_HIP(c->bls_ms_ok.reserve(1));
   CBFT_HIP(hipMemcpyAsync(c->bls_partial.p, key_partials, (size_t)count * CBFT_BLS_G2_PARTIAL_BYTES,
                           hipMemcpyHostToDevice, c->stream));
-  CBFT_HIP(cbft_bls_launch_g2_parts(c->bls_partial.as<uint32_t>(), count, c->bls_ms_lines.as<uint32_t>(),
-                                    c->bls_ms_ok.as<uint8_t>(), nullptr, c->stream));
-  return bls_verify_with_lines(c, len, sig33, c->bls_ms_lines.as<uint32_t>(), c->bls_ms_ok.as<uint8_t>(), out_ok);
+  CBFT_HIP(cbft_bls_launch_g2_lines(c->bls_partial.as<uint32_t>(), count, c->bls_ms_lines.as<uint32_t>(),
+                                    c->bls_ms_ok.as<uint8_t>(), c->stream));
+  return bls_verify_with_lines(c, len, sig33, c->bls_ms_lines.as<uint32_t>(), 1, c->bls_ms_ok.as<uint8_t>(), out_ok);
 }
 
 // 32-byte big-endian scalar -> 8 little-endian words
