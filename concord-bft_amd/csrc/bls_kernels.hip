@@ -4,11 +4,12 @@
 //   bls_inv_table_kernel     inverses of 1..2048 mod r (once per context)
 //   bls_lagrange_kernel      one wave per share: lambda_i = prod_{j!=i} j/(j-i) mod r
 //                            (lagrangeCoeffAccumReduced, LagrangeInterpolation.cpp:202-292)
-//   bls_msm_kernel           lane per share: lambda_i sigma_i, LDS tree sum per block
+//   bls_msm_kernel           lane quad per share: lambda_i sigma_i, LDS tree sum per block
 //                            (fastMultExp, FastMultExp.cpp:26-59; multisig: lambda = 1)
 //   bls_msm_finish_kernel    sum of block partials -> 33-byte compressed G1
 //   bls_sign_kernel          sigma = sk * g1_map(msg)     (BlsThresholdSigner.cpp:32-47)
 #include "bls_common.h"
+#include "bn254_g1quad.h"
 
 // one wave: the candidates are tried 64 at a time (g1_map_wave)
 __global__ void __launch_bounds__(64) bls_hash_kernel(const uint8_t* msg, uint32_t len, uint32_t* H) {
@@ -86,7 +87,7 @@ __global__ void __launch_bounds__(64) bls_lagrange_kernel(const uint32_t* ids, c
   for (int q = 0; q < 8; q++) lambda[8 * (size_t)i + q] = w[q];
 }
 
-#define MSM_BLOCK 64
+#define MSM_QUADS 16  // shares (lane quads) per 64-lane MSM block
 
 // ---- GLV (Gallant-Lambert-Vanstone) on BN-P254 G1: phi(x, y) = (beta x, y) = [lam] P with
 // beta^3 = 1 in Fp, lam^2 + lam + 1 = 0 mod r.  k = k1 + k2 lam (mod r) with |k1|, |k2| < 2^128
@@ -211,18 +212,52 @@ __device__ __forceinline__ void g1j_neg_if(g1j& p, bool neg) {
   for (int q = 0; q < 9; q++) p.Y.v[q] = neg ? n.v[q] : p.Y.v[q];
 }
 
-// partial[b] = sum over this block's lanes of lambda_j sigma_j (Jacobian, 27 words).
-// lambda_j sigma_j = k1 sigma_j + k2 phi(sigma_j) (GLV): 33 signed radix-16 windows, each 4
-// doublings + one addition from a per-lane LDS table {1..8} sigma (+ one from the same table
-// mapped by phi: X -> beta X) -- 132 doublings and 66 additions instead of 256 and ~128 for
-// fastMultExp's double-and-add (FastMultExp.cpp:26-59).  Multisig (unit scalars): sum sigma_j.
-__global__ void __launch_bounds__(MSM_BLOCK) bls_msm_kernel(const uint32_t* sig, const uint32_t* lambda,
-                                                            const uint8_t* use, uint32_t k, int unit_scalars,
-                                                            uint32_t* partial) {
-  __shared__ uint32_t sp[MSM_BLOCK][27];
-  __shared__ uint32_t tbl[8][27][MSM_BLOCK];  // [multiple - 1][word][lane]: conflict-free
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-  const int ln = threadIdx.x;
+// Jacobian point <-> 27 LDS / global words, the quad's lane q moving words q, q + 4, ...
+__device__ __forceinline__ void g1j_put(uint32_t* o, int stride, const g1j& a, int q) {
+#pragma unroll
+  for (int w = 0; w < 27; w++) {
+    const uint32_t v = w < 9 ? a.X.v[w] : (w < 18 ? a.Y.v[w - 9] : a.Z.v[w - 18]);
+    if ((w & 3) == q) o[w * stride] = v;
+  }
+}
+__device__ __forceinline__ void g1j_get(g1j& a, const uint32_t* o, int stride) {
+#pragma unroll
+  for (int w = 0; w < 9; w++) {
+    a.X.v[w] = o[w * stride];
+    a.Y.v[w] = o[(9 + w) * stride];
+    a.Z.v[w] = o[(18 + w) * stride];
+  }
+}
+
+// sum of the MSM_QUADS quads' points of a 64-lane block (LDS tree, quad adds); quad 0 ends
+// with it
+__device__ __forceinline__ void g1q_block_sum(g1j& acc, uint32_t (*sp)[27], int qd, int q) {
+#pragma unroll 1
+  for (int stride = MSM_QUADS / 2; stride >= 1; stride >>= 1) {
+    if (qd >= stride && qd < 2 * stride) g1j_put(sp[qd - stride], 1, acc, q);
+    __syncthreads();
+    if (qd < stride) {
+      g1j o;
+      g1j_get(o, sp[qd], 1);
+      g1q_add(acc, acc, o, q);
+    }
+    __syncthreads();
+  }
+}
+
+// partial[b] = sum over this block's 16 shares of lambda_j sigma_j (Jacobian, 27 words).  One lane
+// QUAD per share (bn254_g1quad.h: the independent products of each doubling / addition on
+// separate lanes).  lambda_j sigma_j = k1 sigma_j + k2 phi(sigma_j) (GLV): 33 signed radix-16
+// windows, each 4 doublings + one addition from the share's LDS table {1..8} sigma (+ one from
+// the phi table {1..8} phi(sigma), phi: X -> beta X) -- 132 doublings and 66 additions instead
+// of 256 and ~128 for fastMultExp's double-and-add (FastMultExp.cpp:26-59).  Multisig (unit
+// scalars): sum sigma_j.
+__global__ void __launch_bounds__(64) bls_msm_kernel(const uint32_t* sig, const uint32_t* lambda, const uint8_t* use,
+                                                     uint32_t k, int unit_scalars, uint32_t* partial) {
+  __shared__ uint32_t sp[MSM_QUADS / 2][27];
+  __shared__ uint32_t tbl[2][8][27][MSM_QUADS];  // [phi][multiple - 1][word][quad]
+  const int qd = threadIdx.x >> 2, q = threadIdx.x & 3;
+  const uint32_t j = blockIdx.x * MSM_QUADS + qd;
   g1j acc;
   g1_set_inf(acc);
   const bool live = j < k && use[j];
@@ -236,114 +271,86 @@ __global__ void __launch_bounds__(MSM_BLOCK) bls_msm_kernel(const uint32_t* sig,
     uint32_t lw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (live) {
       g1a_load(s, sig + 19 * (size_t)j);
-      for (int q = 0; q < 8; q++) lw[q] = lambda[8 * (size_t)j + q];
+      for (int w = 0; w < 8; w++) lw[w] = lambda[8 * (size_t)j + w];
     } else {
       s.inf = true;
     }
     g1j P;
     g1_from_affine(P, s);
-    // table m * sigma, m = 1..8
+    fp beta;
+    {
+      uint32_t bw[8];
+      for (int w = 0; w < 8; w++) bw[w] = kGlvBeta[w];
+      f_from_words(beta, bw);
+    }
+    // tables m * sigma and phi(m * sigma), m = 1..8
     g1j T = P;
+#pragma unroll 1
     for (int m = 1; m <= 8; m++) {
-      if (m == 2) g1_dbl(T, P);
-      else if (m > 2) g1_add(T, T, P);
-      for (int q = 0; q < 9; q++) {
-        tbl[m - 1][q][ln] = T.X.v[q];
-        tbl[m - 1][9 + q][ln] = T.Y.v[q];
-        tbl[m - 1][18 + q][ln] = T.Z.v[q];
-      }
+      if (m == 2)
+        g1q_dbl(T, P, q);
+      else if (m > 2)
+        g1q_add(T, T, P, q);
+      g1j_put(&tbl[0][m - 1][0][qd], MSM_QUADS, T, q);
+      g1j F = T;
+      f_mul(F.X, T.X, beta);
+      g1j_put(&tbl[1][m - 1][0][qd], MSM_QUADS, F, q);
     }
     uint32_t k1[5], k2[5];
     bool n1, n2;
     glv_split(lw, k1, k2, n1, n2);
     glv_offset(k1);
     glv_offset(k2);
-    fp beta;
-    {
-      uint32_t bw[8];
-      for (int q = 0; q < 8; q++) bw[q] = kGlvBeta[q];
-      f_from_words(beta, bw);
-    }
 #pragma nounroll
     for (int w = 32; w >= 0; w--) {
       if (w != 32)
-        for (int d = 0; d < 4; d++) g1_dbl(acc, acc);
+#pragma unroll 1
+        for (int d = 0; d < 4; d++) g1q_dbl(acc, acc, q);
 #pragma unroll
       for (int half = 0; half < 2; half++) {
         const int dg = glv_digit(half ? k2 : k1, w);
-        if (dg == 0) continue;
+        if (dg == 0) continue;  // quad-uniform
         const int m = (dg < 0 ? -dg : dg) - 1;
         g1j E;
-        for (int q = 0; q < 9; q++) {
-          E.X.v[q] = tbl[m][q][ln];
-          E.Y.v[q] = tbl[m][9 + q][ln];
-          E.Z.v[q] = tbl[m][18 + q][ln];
-        }
-        if (half) f_mul(E.X, E.X, beta);  // phi(m sigma)
+        g1j_get(E, &tbl[half][m][0][qd], MSM_QUADS);
         g1j_neg_if(E, (dg < 0) != (half ? n2 : n1));
-        g1_add(acc, acc, E);
+        g1q_add(acc, acc, E, q);
       }
     }
   }
-  for (int stride = MSM_BLOCK / 2; stride >= 1; stride >>= 1) {
-    const int t = threadIdx.x;
-    if (t >= stride && t < 2 * stride) {
-      for (int q = 0; q < 9; q++) {
-        sp[t - stride][q] = acc.X.v[q];
-        sp[t - stride][9 + q] = acc.Y.v[q];
-        sp[t - stride][18 + q] = acc.Z.v[q];
-      }
-    }
-    __syncthreads();
-    if (t < stride) {
-      g1j o;
-      for (int q = 0; q < 9; q++) {
-        o.X.v[q] = sp[t][q];
-        o.Y.v[q] = sp[t][9 + q];
-        o.Z.v[q] = sp[t][18 + q];
-      }
-      g1_add(acc, acc, o);
-    }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    uint32_t* o = partial + 27 * (size_t)blockIdx.x;
-    for (int q = 0; q < 9; q++) {
-      o[q] = acc.X.v[q];
-      o[9 + q] = acc.Y.v[q];
-      o[18 + q] = acc.Z.v[q];
-    }
-  }
+  __syncthreads();
+  g1q_block_sum(acc, sp, qd, q);
+  if (qd == 0) g1j_put(partial + 27 * (size_t)blockIdx.x, 1, acc, q);
 }
 
 // Sum of nparts Jacobian partials (27 words each): compressed into out33, or (out_jac) left as
-// one Jacobian partial -- the form ranks exchange when a combine is sharded across GPUs.
-__global__ void bls_msm_finish_kernel(const uint32_t* partial, uint32_t nparts, uint8_t* out33, uint32_t* sig_aff,
-                                      uint32_t* out_jac) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+// one Jacobian partial -- the form ranks exchange when a combine is sharded across GPUs.  One
+// block of 16 quads: quad qd sums partials qd, qd + 16, ..., then the LDS tree.
+__global__ void __launch_bounds__(64) bls_msm_finish_kernel(const uint32_t* partial, uint32_t nparts, uint8_t* out33,
+                                                            uint32_t* sig_aff, uint32_t* out_jac) {
+  __shared__ uint32_t sp[MSM_QUADS / 2][27];
+  if (blockIdx.x != 0) return;
+  const int qd = threadIdx.x >> 2, q = threadIdx.x & 3;
   g1j acc;
   g1_set_inf(acc);
-  for (uint32_t b = 0; b < nparts; b++) {
+#pragma unroll 1
+  for (uint32_t b = qd; b < nparts; b += MSM_QUADS) {
     g1j o;
-    for (int q = 0; q < 9; q++) {
-      o.X.v[q] = partial[27 * b + q];
-      o.Y.v[q] = partial[27 * b + 9 + q];
-      o.Z.v[q] = partial[27 * b + 18 + q];
-    }
-    g1_add(acc, acc, o);
+    g1j_get(o, partial + 27 * (size_t)b, 1);
+    g1q_add(acc, acc, o, q);
   }
+  g1q_block_sum(acc, sp, qd, q);
+  if (qd != 0) return;
   if (out_jac) {
-    for (int q = 0; q < 9; q++) {
-      out_jac[q] = acc.X.v[q];
-      out_jac[9 + q] = acc.Y.v[q];
-      out_jac[18 + q] = acc.Z.v[q];
-    }
+    g1j_put(out_jac, 1, acc, q);
     return;
   }
   g1a a;
   g1_to_affine(a, acc);
-  g1_compress(out33, a);
-  if (sig_aff) g1a_store(sig_aff, a);
+  if (q == 0) {
+    g1_compress(out33, a);
+    if (sig_aff) g1a_store(sig_aff, a);
+  }
 }
 
 // sigma_i = sk_i * g1_map(msg) as a 37-byte share (BlsThresholdSigner::signData,
@@ -384,9 +391,9 @@ hipError_t cbft_bls_launch_combine(const uint32_t* d_sig, const uint32_t* d_ids,
   hi = hi < k ? hi : k;
   lo = lo < hi ? lo : hi;
   const uint32_t m = hi - lo;  // the MSM runs over shares [lo, hi) only
-  const uint32_t nparts = (m + MSM_BLOCK - 1) / MSM_BLOCK;
+  const uint32_t nparts = (m + MSM_QUADS - 1) / MSM_QUADS;
   if (m)
-    hipLaunchKernelGGL(bls_msm_kernel, dim3(nparts), dim3(MSM_BLOCK), 0, s, d_sig + 19 * (size_t)lo,
+    hipLaunchKernelGGL(bls_msm_kernel, dim3(nparts), dim3(64), 0, s, d_sig + 19 * (size_t)lo,
                        d_lambda + 8 * (size_t)lo, d_use + lo, m, multisig, d_partial);
   hipLaunchKernelGGL(bls_msm_finish_kernel, dim3(1), dim3(64), 0, s, d_partial, nparts, d_out33, d_sig_aff,
                      d_out_jac);

@@ -178,7 +178,7 @@ static int bls_combine_range(cbft_ctx* c, const uint8_t* shares37, uint32_t k, u
   int rc = bls_shares(c, nullptr, shares37, k, 0);
   if (rc) return rc;
   CBFT_HIP(c->bls_lambda.reserve((size_t)k * 8 * 4));
-  CBFT_HIP(c->bls_partial.reserve((size_t)((k + 63) / 64 + 1) * BLS_JAC_WORDS * 4));
+  CBFT_HIP(c->bls_partial.reserve((size_t)((k + 15) / 16 + 1) * BLS_JAC_WORDS * 4));
   CBFT_HIP(c->bls_out.reserve(BLS_JAC_WORDS * 4));
   // every share decoded? (the parse kernel wrote valid = decodable && id in range)
   std::vector<uint8_t> v(k);
