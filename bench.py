@@ -545,7 +545,17 @@ def bench_bls(ctx, args, cpu_threads):
             c = ctx.bls_combine(use, multisig=True)
             assert ctx.bls_verify_multisig(kid, cert.msg, c, bytes(bitmap))
 
+        def fused():  # cbft_bls_combine_threshold, fallback form: verify shares, combine valid, verify
+            sig, ok, badv = ctx.bls_combine_threshold(kid, cert.msg, cert.shares, optimistic=False)
+            assert ok and sig == cert.expected_sig
+
+        def policy():  # reference policy: optimistic combine of all 760 (fails: 10 % bad) -> fallback
+            sig, ok, badv = ctx.bls_combine_threshold(kid, cert.msg, cert.shares, optimistic=True)
+            assert ok and sig == cert.expected_sig
+
         t_cert = _median_ms(certificate, runs)
+        t_fused = _median_ms(fused, runs)
+        t_policy = _median_ms(policy, runs)
         t_opt = _median_ms(optimistic, runs)
         t_ms = _median_ms(multisig, runs)
     finally:
@@ -555,6 +565,13 @@ def bench_bls(ctx, args, cpu_threads):
            "certificate_ms": t_cert, "certificates_per_s": 1e3 / t_cert,
            "share_verify_ms": t_share, "shares_per_s": nsh / (t_share * 1e-3),
            "pairings_per_s": 2 * nsh / (t_share * 1e-3),
+           "certificate_fused_ms": t_fused,
+           "certificate_fused_basis": "one cbft_bls_combine_threshold(optimistic=0) call: 760 share verifies, "
+                                      "Lagrange + MSM over the valid ones, final verify, all on the device",
+           "certificate_policy_ms": t_policy,
+           "certificate_policy_basis": "cbft_bls_combine_threshold(optimistic=1): the reference's "
+                                       "SignaturesProcessingJob order -- optimistic combine of all shares + verify "
+                                       "(fails with 10 % bad), then the fallback",
            "combine_ms": t_comb, "verify_ms": t_ver, "optimistic_ms": t_opt, "multisig_ms": t_ms,
            "verdicts": "share verdicts == planted bad set; combined sig == sk*H(m) byte-exact"}
     out["roofline"] = _bls_roofline()

@@ -91,6 +91,9 @@ ABI = [
                                         ctypes.c_void_p]),
     ("cbft_bls_verify", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
                                        ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
+    ("cbft_bls_combine_threshold", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32,
+      ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]),
     ("cbft_bls_verify_multisig", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_char_p,
       ctypes.POINTER(ctypes.c_int)]),
@@ -397,6 +400,18 @@ class Context:
         _check(self.lib.cbft_bls_combine(self.handle, b"".join(shares), len(shares), 1 if multisig else 0, out),
                "cbft_bls_combine")
         return out.raw
+
+    def bls_combine_threshold(self, kid: int, msg: bytes, shares: Sequence[bytes], optimistic: bool = True):
+        """The certificate policy in one call (cbft_bls_combine_threshold): returns (sig33, ok,
+        bad) with bad[j] = share j failed share verification."""
+        k = len(shares)
+        sig = ctypes.create_string_buffer(33)
+        bad = ctypes.create_string_buffer(max(1, (k + 7) // 8))
+        ok = ctypes.c_int()
+        _check(self.lib.cbft_bls_combine_threshold(self.handle, kid, msg, len(msg), b"".join(shares), k,
+                                                    1 if optimistic else 0, sig, bad, ctypes.byref(ok)),
+               "cbft_bls_combine_threshold")
+        return sig.raw, bool(ok.value), bitmap_to_bools(bad.raw, k)
 
     def bls_verify(self, kid: int, msg: bytes, sig33: bytes) -> bool:
         ok = ctypes.c_int()

@@ -28,6 +28,7 @@ hipError_t cbft_bls_launch_combine(const uint32_t* d_sig, const uint32_t* d_ids,
                                    hipStream_t s);
 #define BLS_INV_TABLE 2048  // d^-1 mod r for d = 1 .. 2048 (share ids are <= 2048, IThresholdVerifier.h:36)
 hipError_t cbft_bls_launch_inv_table(uint32_t* d_inv, hipStream_t s);
+hipError_t cbft_bls_launch_and(const uint8_t* d_a, const uint8_t* d_b, uint8_t* d_use, uint32_t k, hipStream_t s);
 hipError_t cbft_bls_launch_g1_parts(const uint32_t* d_parts, uint32_t count, uint8_t* d_out33, hipStream_t s);
 #define BLS_G2_PART_WORDS 55  // Jacobian G2 partial key sum + bad-key flag
 // multisig key sum over the bitmap's ids in [lo_id, hi_id): Jacobian partial (d_out_part,

@@ -373,7 +373,18 @@ __global__ void bls_sign_kernel(const uint8_t* msg, uint32_t len, const uint32_t
   g1_compress(out37 + 4, a);
 }
 
+// use[j] = a[j] && b[j] (first occurrence of an id && share verified), k bytes
+__global__ void __launch_bounds__(256) bls_and_kernel(const uint8_t* a, const uint8_t* b, uint8_t* use, uint32_t k) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < k) use[j] = (a[j] && b[j]) ? 1 : 0;
+}
+
 // ------------------------------------------------------------------------------ launchers
+hipError_t cbft_bls_launch_and(const uint8_t* d_a, const uint8_t* d_b, uint8_t* d_use, uint32_t k, hipStream_t s) {
+  if (!k) return hipSuccess;
+  hipLaunchKernelGGL(bls_and_kernel, dim3((k + 255) / 256), dim3(256), 0, s, d_a, d_b, d_use, k);
+  return hipGetLastError();
+}
 hipError_t cbft_bls_launch_hash(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, hipStream_t s) {
   hipLaunchKernelGGL(bls_hash_kernel, dim3(1), dim3(64), 0, s, d_msg, len, d_H);
   return hipGetLastError();

@@ -260,6 +260,99 @@ int cbft_bls_verify(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, 
   return bls_verify_with_lines(c, len, sig33, ks->lines.as<uint32_t>(), 0, ks->ok.as<uint8_t>(), out_ok);
 }
 
+// The SignaturesProcessingJob policy (CollectorOfThresholdSignatures.hpp:363-406) as one call,
+// every step on the device with the shares staged and parsed once:
+//   optimistic: combine all shares (first share per id), verify the combined signature;
+//   otherwise (or optimistic = 0): verify every share, combine the valid ones, verify.
+int cbft_bls_combine_threshold(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, const uint8_t* shares37,
+                               uint32_t k, int optimistic, uint8_t* out_sig33, uint8_t* bad_bitmap, int* out_ok) {
+  c = cbft_dev0(c);
+  if (!c || !out_sig33 || !out_ok || (k && (!shares37 || !bad_bitmap)) || (len && !msg) || k > BLS_MAX_SHARES)
+    return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);
+  BlsKeySet* ks = find_set(c, id);
+  if (!ks) return CBFT_EINVAL;
+  CBFT_HIP(hipSetDevice(c->device));
+  // the accumulators keep the first share of an id (ThresholdAccumulatorBase::add); later ones
+  // are ignored, neither combined nor reported
+  std::vector<uint8_t> first(k ? k : 1, 0);
+  {
+    std::vector<uint8_t> seen(BLS_MAX_SHARES + 1, 0);
+    for (uint32_t j = 0; j < k; j++) {
+      const uint8_t* sh = shares37 + 37 * (size_t)j;
+      const uint32_t sid = ((uint32_t)sh[0] << 24) | ((uint32_t)sh[1] << 16) | ((uint32_t)sh[2] << 8) | sh[3];
+      if (sid >= 1 && sid <= BLS_MAX_SHARES) {
+        first[j] = seen[sid] ? 0 : 1;
+        seen[sid] = 1;
+      } else {
+        first[j] = 1;  // out of range: fails parse (id check), reported bad
+      }
+    }
+  }
+  int rc = bls_gen_lines(c);
+  if (!rc) rc = bls_upload_msg_hash(c, msg, len);
+  if (rc) return rc;
+  CBFT_HIP(c->bls_first.reserve(k ? k : 1));
+  CBFT_HIP(c->bls_use.reserve(k ? k : 1));
+  CBFT_HIP(c->bls_lambda.reserve((size_t)(k ? k : 1) * 8 * 4));
+  CBFT_HIP(c->bls_partial.reserve((size_t)((k + 15) / 16 + 1) * BLS_JAC_WORDS * 4));
+  CBFT_HIP(c->bls_out.reserve(BLS_JAC_WORDS * 4));
+  CBFT_HIP(c->bls_flag.reserve(1));
+  if (!c->bls_inv.p) {
+    CBFT_HIP(c->bls_inv.reserve((size_t)BLS_INV_TABLE * 9 * 4));
+    CBFT_HIP(cbft_bls_launch_inv_table(c->bls_inv.as<uint32_t>(), c->stream));
+  }
+  if (k) CBFT_HIP(hipMemcpyAsync(c->bls_first.p, first.data(), k, hipMemcpyHostToDevice, c->stream));
+  // combine over d_use, then verify the device-resident result: result byte -> bls_flag
+  auto combine_verify = [&]() -> int {
+    CBFT_HIP(cbft_bls_launch_combine(c->bls_sig.as<uint32_t>(), c->bls_ids.as<uint32_t>(), c->bls_use.as<uint8_t>(),
+                                     k, 0, k, 0, c->bls_inv.as<uint32_t>(), c->bls_lambda.as<uint32_t>(),
+                                     c->bls_partial.as<uint32_t>(), c->bls_out.as<uint8_t>(), nullptr, nullptr,
+                                     c->stream));
+    CBFT_HIP(cbft_bls_launch_verify(c->bls_msg.as<uint8_t>(), len, nullptr, c->bls_out.as<uint8_t>(),
+                                    ks->lines.as<uint32_t>(), 0, ks->ok.as<uint8_t>(),
+                                    c->bls_gen_lines.as<uint32_t>(), c->bls_flag.as<uint8_t>(), c->stream));
+    return CBFT_OK;
+  };
+  std::vector<uint8_t> v(k ? k : 1, 0);
+  uint8_t ok = 0;
+  bool done = false;
+  if (optimistic && k) {
+    rc = bls_shares(c, ks, shares37, k, 0);  // parse only
+    if (rc) return rc;
+    CBFT_HIP(cbft_bls_launch_and(c->bls_first.as<uint8_t>(), c->bls_valid.as<uint8_t>(), c->bls_use.as<uint8_t>(), k,
+                                 c->stream));
+    rc = combine_verify();
+    if (rc) return rc;
+    CBFT_HIP(hipMemcpyAsync(v.data(), c->bls_valid.p, k, hipMemcpyDeviceToHost, c->stream));
+    CBFT_HIP(hipMemcpyAsync(&ok, c->bls_flag.p, 1, hipMemcpyDeviceToHost, c->stream));
+    CBFT_HIP(hipStreamSynchronize(c->stream));
+    bool all_parsed = true;
+    for (uint32_t j = 0; j < k; j++) all_parsed = all_parsed && (v[j] || !first[j]);
+    done = ok && all_parsed;
+    if (done) std::memset(bad_bitmap, 0, (k + 7) / 8);
+  }
+  if (!done) {
+    if (k) {
+      rc = bls_shares(c, ks, shares37, k, 1);  // parse + verify every share
+      if (rc) return rc;
+      CBFT_HIP(cbft_bls_launch_and(c->bls_first.as<uint8_t>(), c->bls_valid.as<uint8_t>(), c->bls_use.as<uint8_t>(),
+                                   k, c->stream));
+    }
+    rc = combine_verify();
+    if (rc) return rc;
+    if (k) CBFT_HIP(hipMemcpyAsync(v.data(), c->bls_valid.p, k, hipMemcpyDeviceToHost, c->stream));
+    CBFT_HIP(hipMemcpyAsync(&ok, c->bls_flag.p, 1, hipMemcpyDeviceToHost, c->stream));
+    CBFT_HIP(hipStreamSynchronize(c->stream));
+    if (k) std::memset(bad_bitmap, 0, (k + 7) / 8);
+    for (uint32_t j = 0; j < k; j++)
+      if (first[j] && !v[j]) bad_bitmap[j >> 3] |= (uint8_t)(1u << (j & 7));
+  }
+  CBFT_HIP(hipMemcpy(out_sig33, c->bls_out.p, 33, hipMemcpyDeviceToHost));
+  *out_ok = ok ? 1 : 0;
+  return CBFT_OK;
+}
+
 int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, const uint8_t* sig33,
                              const uint8_t* signers256, int* out_ok) {
   c = cbft_dev0(c);

@@ -252,6 +252,18 @@ int cbft_bls_verify_shares(cbft_ctx* ctx, uint32_t keyset, const uint8_t* msg, u
  * repeats or a share does not decode. */
 int cbft_bls_combine(cbft_ctx* ctx, const uint8_t* shares37, uint32_t k, int multisig, uint8_t* out33);
 
+/* The threshold certificate in one call: the SignaturesProcessingJob policy
+ * (CollectorOfThresholdSignatures.hpp:363-406; SURVEY.md §8(b) cbft_bls_combine_threshold).
+ * The first share of each id is used (later duplicates are ignored, as the accumulators do).
+ * optimistic = 1: combine all shares without verifying them, verify the combined signature; if
+ * that fails (or a share does not decode), or optimistic = 0: verify every share, combine the
+ * valid ones (Lagrange over their ids), verify.  out_sig33 = the combined signature, *out_ok = it
+ * verifies under the key set's PK; bad_bitmap (ceil(k/8) bytes): bit j = share j failed share
+ * verification (all zero when the optimistic combine verified). */
+int cbft_bls_combine_threshold(cbft_ctx* ctx, uint32_t keyset, const uint8_t* msg, uint32_t len,
+                               const uint8_t* shares37, uint32_t k, int optimistic, uint8_t* out_sig33,
+                               uint8_t* bad_bitmap, int* out_ok);
+
 /* e(H(msg), PK) == e(sig, g2) with the key set's group PK (BlsThresholdVerifier.cpp:69-96). */
 int cbft_bls_verify(cbft_ctx* ctx, uint32_t keyset, const uint8_t* msg, uint32_t len, const uint8_t* sig33,
                     int* out_ok);

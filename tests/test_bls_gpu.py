@@ -125,6 +125,37 @@ def test_full_size_commit_certificate(ctx):
         ctx.bls_unload_keys(kid)
 
 
+@pytest.mark.parametrize("optimistic", [True, False])
+def test_combine_threshold_policy(ctx, optimistic):
+    """cbft_bls_combine_threshold = SignaturesProcessingJob (CollectorOfThresholdSignatures.hpp:
+    363-406): all-good shares combine optimistically with an empty bad set; with doubled shares
+    the call falls back to per-share verification, reports exactly the bad ones and combines the
+    valid ones; later duplicates of an id are ignored; too few valid shares -> not ok."""
+    n, t = 16, 11
+    sk, sks, pk, vks = blsgen.keyset(n, t, seed=33)
+    msg = b"combine_threshold digest 0123456"
+    rng = random.Random(3)
+    ids = sorted(rng.sample(range(1, n + 1), 14))
+    sh = blsgen.shares(sks, ids, msg)
+    want = blsgen.sign_point(sk, msg)
+    kid = ctx.bls_load_keys(pk, vks)
+    try:
+        sig, ok, bad = ctx.bls_combine_threshold(kid, msg, sh, optimistic)
+        assert ok and sig == want and not bad.any()
+        badset = {1, 5, 9}
+        mixed = [blsgen.doubled(s) if j in badset else s for j, s in enumerate(sh)]
+        mixed.append(sh[0])  # a later duplicate of an id: ignored, not reported
+        sig, ok, bad = ctx.bls_combine_threshold(kid, msg, mixed, optimistic)
+        assert ok and sig == want
+        assert bad.tolist() == [j in badset for j in range(len(mixed))]
+        few = [blsgen.doubled(s) if j >= 9 else s for j, s in enumerate(sh)]  # 9 valid < t = 11
+        sig, ok, bad = ctx.bls_combine_threshold(kid, msg, few, optimistic)
+        assert not ok and bad.tolist() == [j >= 9 for j in range(len(few))]
+        assert not ctx.bls_combine_threshold(kid, msg + b"x", sh, optimistic)[1]
+    finally:
+        ctx.bls_unload_keys(kid)
+
+
 def test_sign_matches_oracle(ctx):
     # IThresholdSigner::signData: id (4 B big-endian) || sk * g1_map(msg) (BlsThresholdSigner.cpp:32-47)
     rng = random.Random(5)
