@@ -146,11 +146,7 @@ class RsaEngine {
         if (loaded_ == exps_.size() && table_ != kNoTable) break;
       }
       rd.unlock();
-      {
-        std::unique_lock<std::shared_mutex> wr(tbl_mu_);
-        std::lock_guard<std::mutex> g(mu_);
-        ensureTableLocked();
-      }
+      refreshTable();  // builds beside the old table; verifies keep using it meanwhile
       rd.lock();
     }
     const int rc = cbft_rsa_verify_batch(ctx_, table_, kidx.data(), sig.data(), msg.data(), off.data(), len.data(),
@@ -167,20 +163,39 @@ class RsaEngine {
     if (rc != CBFT_OK) fail("cbft_open", rc);
   }
 
-  void ensureTableLocked() {
-    const uint32_t nkeys = (uint32_t)exps_.size();
-    if (nkeys == loaded_ && table_ != kNoTable) return;
+  // Rebuild the device key table for the keys registered so far WITHOUT blocking verifies: the
+  // new table is built while readers keep the old one (tbl_mu_ shared), then swapped in under a
+  // short exclusive lock; the old one is unloaded once no reader can hold it.  RSA key records are
+  // 1.5 KB each, so a rebuild is cheap (one rsa_keys_kernel launch) and the two tables together
+  // stay small; builds are serialised by build_mu_.
+  void refreshTable() {
+    std::lock_guard<std::mutex> b(build_mu_);
+    std::vector<uint8_t> mods;
+    std::vector<uint32_t> exps;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (loaded_ == exps_.size() && table_ != kNoTable) return;
+      mods = mods_;
+      exps = exps_;
+    }
     uint32_t id;
-    const int rc = cbft_rsa_load_keys(ctx_, mods_.data(), exps_.data(), nkeys, &id);
+    const int rc = cbft_rsa_load_keys(ctx_, mods.data(), exps.data(), (uint32_t)exps.size(), &id);
     if (rc != CBFT_OK) fail("cbft_rsa_load_keys", rc);
-    if (table_ != kNoTable) cbft_rsa_unload_keys(ctx_, table_);
-    table_ = id;
-    loaded_ = nkeys;
+    uint32_t old;
+    {
+      std::unique_lock<std::shared_mutex> wr(tbl_mu_);
+      std::lock_guard<std::mutex> g(mu_);
+      old = table_;
+      table_ = id;
+      loaded_ = (uint32_t)exps.size();
+    }
+    if (old != kNoTable) cbft_rsa_unload_keys(ctx_, old);  // readers now see table_ = id
   }
 
   cbft_ctx* ctx_ = nullptr;
   std::mutex mu_;             // guards mods_, exps_, index_, table_, loaded_
   std::shared_mutex tbl_mu_;  // device table lifetime vs in-flight verifies
+  std::mutex build_mu_;       // one table rebuild at a time
   std::vector<uint8_t> mods_;
   std::vector<uint32_t> exps_;
   std::map<std::string, uint32_t> index_;
