@@ -6,7 +6,7 @@ LIB     := concord-bft_amd/libcbft_hipcrypto.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall -Wno-unused-function
 ORACLE_LIB := oracle/libcbft_oracle.so
 
-.PHONY: all lib oracle clean shim
+.PHONY: all lib oracle clean shim sanitize
 all: lib oracle cpu host shim
 
 lib: $(LIB)
@@ -69,3 +69,16 @@ SHIM := tests/cpp/libbn254_shim.so
 shim: $(SHIM)
 $(SHIM): tests/cpp/bn254_shim.cpp $(CSRC)/bn254_*.h $(CSRC)/bls_ops.h $(CSRC)/sha256.h
 	g++ -O3 -funroll-loops -std=c++17 -fPIC -shared -Wall -Wno-unknown-pragmas -I$(CSRC) -o $@ $< -lpthread
+
+# Host-layer sanitizer builds (host code only: the HIP library itself is not instrumented).
+# ASan+UBSan and TSan variants of the C++ host library and its tests; run on a GPU box with
+# tools/sanitize.sh.
+SAN_DIR := tests/cpp/san
+sanitize: $(LIB)
+	mkdir -p $(SAN_DIR)
+	for s in address,undefined thread; do \
+	  t=$$(echo $$s | cut -d, -f1); \
+	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 -fPIC -shared $(HOST_INC) -o $(SAN_DIR)/libcbft_host_$$t.so $(HOST_SRC) -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' && \
+	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 $(HOST_INC) -o $(SAN_DIR)/test_host_$$t tests/cpp/test_host.cpp -L$(SAN_DIR) -lcbft_host_$$t -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' && \
+	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 $(HOST_INC) -o $(SAN_DIR)/test_bls_host_$$t tests/cpp/test_bls_host.cpp -L$(SAN_DIR) -lcbft_host_$$t -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' || exit 1; \
+	done
