@@ -53,18 +53,16 @@ static int key_radix(int requested, uint32_t nkeys) {
 }
 
 // Build comb tables for nunits encoded points (d_pk, 32 B each) into d_tbl, in launches of at
-// most kCombBuildLanes lanes; synchronous.
+// most kCombBuildLanes lanes (B's radix-2^22 table alone is 196,608 lanes); synchronous.
 static hipError_t build_comb(const uint8_t* d_pk, size_t nunits, int negate, const CombGeom& g, uint32_t* d_tbl,
                              uint8_t* d_aok, hipStream_t s) {
-  const size_t lanes_per_unit = (size_t)g.npos * g.chunks();
-  const size_t chunk = std::max<size_t>(1, std::min(nunits, kCombBuildLanes / lanes_per_unit));
+  const size_t lanes = nunits * (size_t)g.npos * g.chunks();
+  const size_t step = std::min(lanes, kCombBuildLanes);
   DevBuf tmp;
-  hipError_t e = tmp.reserve(cbft_ed25519_comb_tmp_words(g, chunk) * sizeof(uint32_t));
-  for (size_t k0 = 0; e == hipSuccess && k0 < nunits; k0 += chunk) {
-    const size_t m = std::min(chunk, nunits - k0);
-    e = cbft_ed25519_launch_comb_tables(d_pk + k0 * 32, m, negate, g, d_tbl + k0 * g.words_per_unit(),
-                                        tmp.as<uint32_t>(), d_aok ? d_aok + k0 : nullptr, s);
-  }
+  hipError_t e = tmp.reserve(cbft_ed25519_comb_tmp_words(step) * sizeof(uint32_t));
+  for (size_t l0 = 0; e == hipSuccess && l0 < lanes; l0 += step)
+    e = cbft_ed25519_launch_comb_tables(d_pk, nunits, negate, g, d_tbl, tmp.as<uint32_t>(), d_aok, l0,
+                                        std::min(step, lanes - l0), s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   tmp.release();
   return e;
@@ -137,6 +135,14 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   c->device = device;
   if (const char* e = getenv("CBFT_FINISH_BATCH")) c->finish_batch = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e);
+  if (const char* e = getenv("CBFT_LADDER_LANES")) {
+    const int l = atoi(e);
+    if (l == 2 || l == 4) c->ladder_lanes = l;
+  }
+  if (const char* e = getenv("CBFT_B_RADIX")) {
+    const int r = atoi(e);
+    if (r >= 16 && r <= CBFT_COMB_MAX_RADIX) c->b_radix = r;
+  }
   int rc = CBFT_OK;
   do {
     if (hipSetDevice(device) != hipSuccess) {
@@ -164,7 +170,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
       static const uint8_t kB[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
                                      0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
                                      0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
-      const CombGeom gb = cbft_comb_geom(CBFT_COMB_B_RADIX);
+      const CombGeom gb = cbft_comb_geom(c->b_radix);
       DevBuf enc;
       if (c->base_comb.reserve(gb.words_per_unit() * 4) != hipSuccess || enc.reserve(32) != hipSuccess) {
         enc.release();
@@ -541,7 +547,8 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     b.pk = nullptr;
     b.keys = kt->view();
     w.base_comb = c->base_comb.as<uint32_t>();
-    w.comb = cbft_comb_ladder(kt->geo.w, CBFT_COMB_B_RADIX);
+    w.comb = cbft_comb_ladder(kt->geo.w, c->b_radix);
+    w.comb_lanes = c->ladder_lanes ? c->ladder_lanes : 4;
   }
   StageOrder order{};
   if (c->stage_order) {

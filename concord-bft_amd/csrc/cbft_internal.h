@@ -158,6 +158,8 @@ struct cbft_ctx {
   // ladder-to-ladder instead of two streams marching in phase (both finishes together, 7/8 of
   // the SIMDs idle).  $CBFT_STAGE_ORDER: 0 off, 1 hash + ladder, 2 ladder only.
   int stage_order = 1;
+  int b_radix = CBFT_COMB_B_RADIX;  // radix of B's comb table ($CBFT_B_RADIX, 16..22)
+  int ladder_lanes = 0;             // comb ladder lanes per signature ($CBFT_LADDER_LANES 2 | 4; 0 = by batch)
   hipEvent_t stage_done[2] = {nullptr, nullptr};  // last hash, last ladder
   bool stage_used = false;
   DevBuf verdicts;

@@ -63,7 +63,7 @@ struct Ed25519Batch {
 // Messages longer than this verify false (SHA-512's 64 + len byte count must not wrap 32 bits).
 #define CBFT_MAX_MSG_LEN 0xFFFFFF00u
 
-// Geometry of a fixed-base comb table with signed radix-2^w digits (8 <= w <= 16):
+// Geometry of a fixed-base comb table with signed radix-2^w digits (8 <= w <= 22):
 // npos positions of entries() = 2^(w-1) + 1 affine niels points (e * 2^(w j) * P, e = 0 ..
 // 2^(w-1)), 32 words each.  npos is the least count whose top digit stays <= 2^(w-1) for every
 // scalar < L (tests/test_comb_recode.py).
@@ -75,8 +75,8 @@ struct CombGeom {
   __host__ __device__ size_t words_per_unit() const { return (size_t)npos * entries() * 32; }
 };
 inline int cbft_comb_npos(int w) {
-  static const int kPos[17] = {0, 0, 0, 0, 0, 0, 0, 0, 32, 29, 26, 23, 22, 20, 19, 17, 16};
-  return (w >= 8 && w <= 16) ? kPos[w] : 0;
+  static const int kPos[23] = {0, 0, 0, 0, 0, 0, 0, 0, 32, 29, 26, 23, 22, 20, 19, 17, 16, 15, 15, 14, 13, 13, 12};
+  return (w >= 8 && w <= 22) ? kPos[w] : 0;
 }
 inline CombGeom cbft_comb_geom(int w) { return CombGeom{w, cbft_comb_npos(w)}; }
 
@@ -103,7 +103,11 @@ inline CombLadder cbft_comb_ladder(int wa, int wb) {
   c.nper = (c.a.npos + c.b.npos + 3) / 4;
   return c;
 }
-#define CBFT_COMB_B_RADIX 16     // B's table: 16 positions x 32,769 entries (67 MB per context)
+// B's table: radix 2^16 by default (16 positions x 32,769 entries, 67 MB per context: a verify
+// against a radix-2^13 key table is 20 + 16 = 36 additions, 9 per lane of a quad).  Radix 2^22
+// (12 positions, 3.2 GB) makes it 32 additions, 8 per lane; $CBFT_B_RADIX selects 16..22.
+#define CBFT_COMB_B_RADIX 16
+#define CBFT_COMB_MAX_RADIX 22
 
 // Device work buffers of one verify launch.
 struct Ed25519Work {
@@ -111,6 +115,7 @@ struct Ed25519Work {
   const uint32_t* tbl;         // windowed -A tables per signature (per-signature key mode)
   const uint32_t* base_comb;   // comb table of B (key-table mode; the -A combs are in Batch::keys)
   CombLadder comb;             // their geometry
+  int comb_lanes;              // lanes per signature of the comb ladder: 4 (quad) or 2 (pair)
   int finish_batch;            // signatures per lane sharing one inversion in K4 (2/4/8/16; else 1)
   const uint8_t* aok;          // A decoded OK per signature (per-signature key mode)
   uint32_t* h_soa;             // 8 x n words
@@ -120,9 +125,14 @@ struct Ed25519Work {
 };
 
 size_t cbft_ed25519_table_words_per_unit();
-size_t cbft_ed25519_comb_tmp_words(const CombGeom& g, size_t nunits);
+// staging words for `lanes` table-build lanes (18 KB each)
+size_t cbft_ed25519_comb_tmp_words(size_t lanes);
+// Comb tables of nunits encoded points (32 B each at d_pk): build lanes [lane0, lane0 + nlanes) of
+// the nunits * npos * chunks() lanes (lane = (unit, position, chunk of 128 multiples)); d_tmp holds
+// cbft_ed25519_comb_tmp_words(nlanes) words.
 hipError_t cbft_ed25519_launch_comb_tables(const uint8_t* d_pk, size_t nunits, int negate, const CombGeom& g,
-                                           uint32_t* d_tbl, uint32_t* d_tmp, uint8_t* d_aok, hipStream_t stream);
+                                           uint32_t* d_tbl, uint32_t* d_tmp, uint8_t* d_aok, size_t lane0,
+                                           size_t nlanes, hipStream_t stream);
 size_t cbft_ed25519_base_table_words();
 hipError_t cbft_ed25519_build_base_table(uint32_t* d_tbl, hipStream_t stream);
 hipError_t cbft_ed25519_launch_prep(const uint8_t* d_pk, size_t nunits, uint32_t* d_tbl, uint8_t* d_aok,

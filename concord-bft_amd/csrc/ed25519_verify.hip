@@ -473,8 +473,11 @@ __global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519B
 // tbl[unit][j][128c+1 .. 128c+128]; the c = 0 lane also writes the identity entry 0.
 __global__ void __launch_bounds__(COMB_TABLE_BLOCK) ed25519_comb_table_kernel(const uint8_t* pk, size_t nunits,
                                                                              int negate, CombGeom geo, uint32_t* tbl,
-                                                                             uint32_t* tmp, uint8_t* aok) {
-  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+                                                                             uint32_t* tmp, uint8_t* aok, size_t lane0,
+                                                                             size_t nlanes) {
+  const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // lane of this launch (tmp slot)
+  if (gl >= nlanes) return;
+  const size_t g = lane0 + gl;
   const int chunks = geo.chunks();
   const size_t u = g / ((size_t)geo.npos * chunks);
   const int j = (int)((g / chunks) % geo.npos);
@@ -497,12 +500,12 @@ __global__ void __launch_bounds__(COMB_TABLE_BLOCK) ed25519_comb_table_kernel(co
   }
   ge_cached cj;
   ge_p3_to_cached(cj, Pj);
-  // Q = (128c + 1) P_j, MSB first over the 15 bits a chunk index can have (w <= 16)
+  // Q = (128c + 1) P_j, MSB first over the w - 1 bits a multiple index can have
   ge_p3 Q;
   ge_p3_0(Q);
   const uint32_t k0 = (uint32_t)c * COMB_CHUNK + 1u;
 #pragma nounroll
-  for (int bit = 14; bit >= 0; bit--) {
+  for (int bit = geo.w - 2; bit >= 0; bit--) {
     ge_p1p1 r;
     ge_dbl(r, Q.X, Q.Y, Q.Z);
     ge_p1p1_to_p3(Q, r);
@@ -511,7 +514,7 @@ __global__ void __launch_bounds__(COMB_TABLE_BLOCK) ed25519_comb_table_kernel(co
       ge_p1p1_to_p3(Q, r);
     }
   }
-  uint32_t* t = tmp + g * (size_t)COMB_TMP_WORDS_PER_LANE;
+  uint32_t* t = tmp + gl * (size_t)COMB_TMP_WORDS_PER_LANE;
   uint32_t* out = tbl + (u * geo.npos + j) * (size_t)geo.entries() * COMB_STRIDE;
   fe acc;
   fe_1(acc);
@@ -621,6 +624,10 @@ __device__ __forceinline__ void add256(uint32_t* s, const uint32_t* off) {
   }
 }
 
+#ifndef CBFT_LADDER_NOFETCH
+#define CBFT_LADDER_NOFETCH 0
+#endif
+
 #ifndef CBFT_COMB_MIN_WAVES
 #define CBFT_COMB_MIN_WAVES 4
 #endif
@@ -635,9 +642,9 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
   if (!live) i = b.n - 1;  // tail quads compute a copy (all lanes stay active for the DPP)
   const uint32_t ntot = cl.a.npos + cl.b.npos;
   const uint32_t first = q * cl.nper;
-  // Digits of this lane's additions, 16-bit offset binary (d + 2^15), kept in LDS
-  // ([step][thread]: conflict-free) so the addition loop holds no digit registers.
-  __shared__ uint16_t sdig[COMB_MAX_STEPS][CBFT_VERIFY_BLOCK];
+  // Digits of this lane's additions (signed, up to +-2^21), kept in LDS ([step][thread]:
+  // conflict-free) so the addition loop holds no digit registers.
+  __shared__ int32_t sdig[COMB_MAX_STEPS][CBFT_VERIFY_BLOCK];
   {
     uint32_t hs[8], ss[8];
 #pragma unroll
@@ -658,10 +665,9 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
       const uint32_t ch = chunk_at(s, pos * w, w);
       const uint32_t half = 1u << (w - 1);
       // top digit in [0, 2^(w-1)]; only S >= L (flagged, rejected in K4) can exceed it
-      const uint32_t tmax = half - (w == 16 ? 1u : 0u);
-      int d = pos == top ? (int)(ch < tmax ? ch : tmax) : (int)ch - (int)half;
+      int d = pos == top ? (int)(ch < half ? ch : half) : (int)ch - (int)half;
       if (jj >= cl.nper || k >= ntot) d = 0;
-      sdig[jj][threadIdx.x] = (uint16_t)(d + 32768);
+      sdig[jj][threadIdx.x] = d;
     }
   }
   const uint32_t* akey = b.keys.comb(batch_unit(b, i));
@@ -672,7 +678,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
     const uint32_t pos = k < ntot ? k - cl.a.npos : 0u;  // past the last position: identity
     return btbl + ((size_t)pos * cl.b.entries() + ad) * COMB_STRIDE;
   };
-  auto digit = [&](int jj) { return (int)sdig[jj][threadIdx.x] - 32768; };
+  auto digit = [&](int jj) { return sdig[jj][threadIdx.x]; };
   ge_p3 P;
   ge_p3_0(P);
   // Table entries are staged through LDS with global_load_lds (no VGPR destination): entry
@@ -705,7 +711,9 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
     const bool neg = d < 0;
     if (jj + 1 < cl.nper) {
       d = digit(jj + 1);
+#if !CBFT_LADDER_NOFETCH  // (probe builds only: compute without the table traffic, wrong verdicts)
       request(entry(jj + 1, d));
+#endif
     }
     ge_p1p1 t;
     {
@@ -749,19 +757,161 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
 }
 
 // ---------------------------------------------------------------------------------------
-// host-side launch helpers (used by cbft_hipcrypto.cpp)
+// The same comb sum on TWO lanes per signature (lane q of a pair takes additions q*nper ..
+// q*nper + nper - 1, nper = ceil(positions / 2)), one DPP combine.  Per signature that is
+// 2 x (16 x 7M + 8M) = 240 lane-M at the default geometry against 4 x (8 x 7M + 17M) = 292 for
+// the quad form (whose two combine levels are a quarter of a lane's work), at 2 waves per SIMD
+// for a 64K batch instead of 4 (256 VGPRs per lane; gfx950 issues the mad / 64-bit mix ~9 %
+// slower per instruction at 2 waves than at 4: tools/microbench/intrate2.hip).  The lower
+// occupancy buys LDS for a second entry stage: entries jj+1 and jj+2 are in flight while
+// addition jj runs, so the key-table / B-table reads (random over tens of GB) stay hidden.
+// The two recoded scalars sit in LDS ([word][lane]) and each digit is extracted right before
+// its entry is requested.
 // ---------------------------------------------------------------------------------------
-size_t cbft_ed25519_comb_tmp_words(const CombGeom& g, size_t nunits) {
-  return nunits * (size_t)g.npos * g.chunks() * COMB_TMP_WORDS_PER_LANE;
+#define COMB2_BLOCK 128
+#define COMB2_MAX_STEPS 24  // additions per lane: radix-2^8 keys + radix-2^16 B = 48 positions
+#ifndef CBFT_COMB2_MIN_WAVES
+#define CBFT_COMB2_MIN_WAVES 2
+#endif
+
+__global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
+    ed25519_comb2_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* btbl,
+                                const CombLadder cl, uint32_t* xyz_soa) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t q = threadIdx.x & 1u;
+  size_t i = g >> 1;
+  const bool live = i < b.n;
+  if (!live) i = b.n - 1;  // tail pairs compute a copy (both lanes stay active for the DPP)
+  const uint32_t na = (uint32_t)cl.a.npos, ntot = na + (uint32_t)cl.b.npos;
+  const uint32_t nper = (ntot + 1u) >> 1;
+  const uint32_t first = q * nper;
+  __shared__ uint4 stage[COMB2_BLOCK / 64][2][7][64];  // per wave: two lane-linear 7 KB entry images
+  __shared__ uint32_t sc[16][COMB2_BLOCK];              // h + offA (words 0..7), S + offB (8..15)
+  {
+    uint32_t hs[8], ss[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) hs[k] = h_soa[k * b.n + i];
+    load_words8(ss, b.sig + i * 64 + 32);
+    add256(hs, cl.offA);
+    add256(ss, cl.offB);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      sc[k][threadIdx.x] = hs[k];
+      sc[8 + k][threadIdx.x] = ss[k];
+    }
+  }
+  // signed digit of this lane's step jj (0 = the identity entry past the last position)
+  auto digit = [&](uint32_t jj) -> int {
+    const uint32_t k = first + jj;
+    if (jj >= nper || k >= ntot) return 0;
+    const bool isA = k < na;
+    const uint32_t pos = isA ? k : k - na;
+    const uint32_t w = isA ? (uint32_t)cl.a.w : (uint32_t)cl.b.w;
+    const uint32_t top = (isA ? (uint32_t)cl.a.npos : (uint32_t)cl.b.npos) - 1u;
+    const uint32_t off = pos * w, wi = off >> 5, base = isA ? 0u : 8u;
+    const uint32_t lo = sc[base + wi][threadIdx.x];
+    const uint32_t hi = wi < 7u ? sc[base + wi + 1u][threadIdx.x] : 0u;  // bits >= 256 read as 0
+    const uint32_t ch = (uint32_t)((((uint64_t)hi << 32) | lo) >> (off & 31u)) & ((1u << w) - 1u);
+    const uint32_t half = 1u << (w - 1u);
+    // top digit in [0, 2^(w-1)]; only S >= L (flagged, rejected in K4) can exceed it
+    return pos == top ? (int)(ch < half ? ch : half) : (int)ch - (int)half;
+  };
+  const uint32_t* akey = b.keys.comb(batch_unit(b, i));
+  auto entry = [&](uint32_t jj, int d) {
+    const uint32_t k = first + jj;
+    const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+    if (k < na) return akey + ((size_t)k * cl.a.entries() + ad) * COMB_STRIDE;
+    const uint32_t pos = k < ntot ? k - na : 0u;
+    return btbl + ((size_t)pos * cl.b.entries() + ad) * COMB_STRIDE;
+  };
+  const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
+  auto request = [&](uint32_t slot, const uint32_t* e) {
+#pragma unroll
+    for (int c = 0; c < 7; c++)
+      __builtin_amdgcn_global_load_lds(e + 4 * c, (__attribute__((address_space(3))) void*)&stage[wv][slot][c][0], 16,
+                                       0, 0);
+  };
+  ge_p3 P;
+  ge_p3_0(P);
+  int dcur = digit(0), dnext = digit(1);
+  request(0, entry(0, dcur));
+  if (nper > 1u) request(1, entry(1, dnext));
+#pragma nounroll
+  for (uint32_t jj = 0; jj < nper; jj++) {
+    const uint32_t slot = jj & 1u;
+    if (jj + 1u < nper)
+      asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // entry jj landed; jj + 1 may still fly
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t ew[28];
+#pragma unroll
+    for (int c = 0; c < 7; c++) {
+      const uint4 v = stage[wv][slot][c][ln];
+      ew[4 * c] = v.x;
+      ew[4 * c + 1] = v.y;
+      ew[4 * c + 2] = v.z;
+      ew[4 * c + 3] = v.w;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry jj is in VGPRs: its stage is free
+    const bool neg = dcur < 0;
+    dcur = dnext;
+    if (jj + 2u < nper) {
+      dnext = digit(jj + 2u);
+      request(slot, entry(jj + 2u, dnext));
+    }
+    ge_p1p1 t;
+    {
+      // niels (y+x, y-x, 2dxy), negated by swapping y+x <-> y-x and C <-> -C (ge_add_mem)
+      fe A, B, C, D, s, e;
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) e.v[k] = neg ? ew[9 + k] : ew[k];
+      fe_add(s, P.Y, P.X);
+      fe_mul(A, s, e);
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) e.v[k] = neg ? ew[k] : ew[9 + k];
+      fe_sub(s, P.Y, P.X);
+      fe_mul(B, s, e);
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) e.v[k] = ew[18 + k];
+      fe_mul(C, e, P.T);
+      fe_add(D, P.Z, P.Z);
+      fe_sub(t.X, A, B);
+      fe_add(t.Y, A, B);
+      fe_add(s, D, C);
+      fe_carry(s);
+      fe_sub(e, D, C);
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        t.Z.v[k] = neg ? e.v[k] : s.v[k];
+        t.T.v[k] = neg ? s.v[k] : e.v[k];
+      }
+    }
+    fe_mul(P.T, t.X, t.Y);
+    fe_mul(P.X, t.X, t.T);
+    fe_mul(P.Y, t.Y, t.Z);
+    fe_mul(P.Z, t.Z, t.T);
+  }
+  quad_combine<0xB1>(P, false);  // P += partner lane's P
+  if (live && q == 0) {
+    fe_store_soa(xyz_soa, b.n, i, P.X);
+    fe_store_soa(xyz_soa + 9 * b.n, b.n, i, P.Y);
+    fe_store_soa(xyz_soa + 18 * b.n, b.n, i, P.Z);
+  }
 }
 
+// ---------------------------------------------------------------------------------------
+// host-side launch helpers (used by cbft_hipcrypto.cpp)
+// ---------------------------------------------------------------------------------------
+size_t cbft_ed25519_comb_tmp_words(size_t lanes) { return lanes * COMB_TMP_WORDS_PER_LANE; }
+
 hipError_t cbft_ed25519_launch_comb_tables(const uint8_t* d_pk, size_t nunits, int negate, const CombGeom& g,
-                                           uint32_t* d_tbl, uint32_t* d_tmp, uint8_t* d_aok, hipStream_t stream) {
-  if (nunits == 0) return hipSuccess;
-  if (g.w < 8 || g.w > 16) return hipErrorInvalidValue;
-  const size_t lanes = nunits * g.npos * g.chunks();
-  hipLaunchKernelGGL(ed25519_comb_table_kernel, dim3((unsigned)((lanes + COMB_TABLE_BLOCK - 1) / COMB_TABLE_BLOCK)),
-                     dim3(COMB_TABLE_BLOCK), 0, stream, d_pk, nunits, negate, g, d_tbl, d_tmp, d_aok);
+                                           uint32_t* d_tbl, uint32_t* d_tmp, uint8_t* d_aok, size_t lane0,
+                                           size_t nlanes, hipStream_t stream) {
+  if (nunits == 0 || nlanes == 0) return hipSuccess;
+  if (g.w < 8 || g.w > CBFT_COMB_MAX_RADIX || g.npos < 1) return hipErrorInvalidValue;
+  if (lane0 + nlanes > nunits * g.npos * g.chunks()) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ed25519_comb_table_kernel, dim3((unsigned)((nlanes + COMB_TABLE_BLOCK - 1) / COMB_TABLE_BLOCK)),
+                     dim3(COMB_TABLE_BLOCK), 0, stream, d_pk, nunits, negate, g, d_tbl, d_tmp, d_aok, lane0, nlanes);
   return hipGetLastError();
 }
 size_t cbft_ed25519_table_words_per_unit() { return (size_t)Shape::TA * CACHED_WORDS; }
@@ -788,6 +938,7 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   const bool comb = b.keys.chunk && w.base_comb && b.key_idx;
   if (comb && (w.comb.nper < 1 || w.comb.nper > COMB_MAX_STEPS || 4 * w.comb.nper < w.comb.a.npos + w.comb.b.npos))
     return hipErrorInvalidValue;
+  if (comb && w.comb_lanes == 2 && w.comb.a.npos + w.comb.b.npos > 2 * COMB2_MAX_STEPS) return hipErrorInvalidValue;
   const dim3 grid(grid_for(b.n)), block(CBFT_VERIFY_BLOCK);
   hipError_t e;
   if (order && order->wait && order->hash && (e = hipStreamWaitEvent(stream, order->done[0], 0)) != hipSuccess)
@@ -797,7 +948,10 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   if (order && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;
   if (order && order->wait && (e = hipStreamWaitEvent(stream, order->done[1], 0)) != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[1], stream);
-  if (comb) {
+  if (comb && w.comb_lanes == 2) {
+    hipLaunchKernelGGL(ed25519_comb2_ladder_kernel, dim3((unsigned)((2 * b.n + COMB2_BLOCK - 1) / COMB2_BLOCK)),
+                       dim3(COMB2_BLOCK), 0, stream, b, w.h_soa, w.base_comb, w.comb, w.xyz_soa);
+  } else if (comb) {
     hipLaunchKernelGGL(ed25519_comb_ladder_kernel, dim3((unsigned)((4 * b.n + CBFT_VERIFY_BLOCK - 1) / CBFT_VERIFY_BLOCK)),
                        block, 0, stream, b, w.h_soa, w.base_comb, w.comb, w.xyz_soa);
   } else {

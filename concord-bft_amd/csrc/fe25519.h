@@ -88,11 +88,41 @@ FE_INLINE void fe_neg(fe& r, const fe& a) {
 //   unbounded top h8 (weight 2^261 * 2^(29(k-9)) == 1216 * 2^(29(k-9))); then the low
 //   columns start their mad chains from (carry + 1216 h_k); the final carry (weight 2^261)
 //   wraps with *1216 into limb 0.  Live state: operands + h[9] + one accumulator.
+//
+// The whole product is ONE dependent chain of v_mad_u64_u32 (each column's chain starts from the
+// previous column's carry).  The mads are written as (non-volatile) inline asm so that LLVM cannot
+// reassociate the chain into per-column partial sums: that costs a v_lshl_add_u64 per column to
+// merge the carry back in (4.7 cycles per wave-instruction at 4 waves/SIMD), while the chain's
+// latency is free -- on gfx950 a dependent mad chain issues at the same rate as eight independent
+// ones from 1 to 16 waves per SIMD (tools/microbench/intrate2.hip, profiles/r02_intrate2.txt).
 #define FE_COLUMN(acc, k, TERM)                                  \
   _Pragma("unroll") for (int i = 0; i < FE_LIMBS; i++) {         \
     int j = (k) - i;                                             \
     if (j >= 0 && j < FE_LIMBS) { TERM }                         \
   }
+
+#ifndef CBFT_FE_CHAIN
+#define CBFT_FE_CHAIN 1
+#endif
+
+// acc += a * b (one v_mad_u64_u32, not reassociable)
+FE_INLINE void mac(uint64_t& acc, uint32_t a, uint32_t b) {
+#if CBFT_FE_CHAIN
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
+#else
+  acc = mad64(a, b, acc);
+#endif
+}
+// acc += a * 1216 (the 2^261 fold; the constant rides in an SGPR)
+FE_INLINE void mac1216(uint64_t& acc, uint32_t a) {
+#if CBFT_FE_CHAIN
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "s"(1216u));
+#else
+  acc = mad64(a, 1216u, acc);
+#endif
+}
 
 FE_INLINE void fe_mul(fe& r, const fe& a, const fe& b) {
   fe o;  // r may alias a or b
@@ -100,17 +130,16 @@ FE_INLINE void fe_mul(fe& r, const fe& a, const fe& b) {
   uint64_t t = 0;
 #pragma unroll
   for (int k = 9; k < 17; k++) {
-    uint64_t acc = t;
-    FE_COLUMN(acc, k, acc = mad64(a.v[i], b.v[j], acc);)
-    h[k - 9] = (uint32_t)acc & FE_MASK;
-    t = acc >> 29;
+    FE_COLUMN(t, k, mac(t, a.v[i], b.v[j]);)
+    h[k - 9] = (uint32_t)t & FE_MASK;
+    t >>= 29;
   }
   h[8] = (uint32_t)t;  // < 2^32 (c16 <= 2^60.003 + carry)
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 9; k++) {
-    acc = mad64(h[k], 1216u, acc);
-    FE_COLUMN(acc, k, acc = mad64(a.v[i], b.v[j], acc);)
+    mac1216(acc, h[k]);
+    FE_COLUMN(acc, k, mac(acc, a.v[i], b.v[j]);)
     o.v[k] = (uint32_t)acc & FE_MASK;
     acc >>= 29;
   }
@@ -130,19 +159,18 @@ FE_INLINE void fe_sq(fe& r, const fe& a) {
   uint64_t t = 0;
 #pragma unroll
   for (int k = 9; k < 17; k++) {
-    uint64_t acc = t;
-    FE_COLUMN(acc, k, if (j > i) acc = mad64(a2[i], a.v[j], acc);)
-    if ((k & 1) == 0) acc = mad64(a.v[k >> 1], a.v[k >> 1], acc);
-    h[k - 9] = (uint32_t)acc & FE_MASK;
-    t = acc >> 29;
+    FE_COLUMN(t, k, if (j > i) mac(t, a2[i], a.v[j]);)
+    if ((k & 1) == 0) mac(t, a.v[k >> 1], a.v[k >> 1]);
+    h[k - 9] = (uint32_t)t & FE_MASK;
+    t >>= 29;
   }
   h[8] = (uint32_t)t;
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 9; k++) {
-    acc = mad64(h[k], 1216u, acc);
-    FE_COLUMN(acc, k, if (j > i) acc = mad64(a2[i], a.v[j], acc);)
-    if ((k & 1) == 0) acc = mad64(a.v[k >> 1], a.v[k >> 1], acc);
+    mac1216(acc, h[k]);
+    FE_COLUMN(acc, k, if (j > i) mac(acc, a2[i], a.v[j]);)
+    if ((k & 1) == 0) mac(acc, a.v[k >> 1], a.v[k >> 1]);
     o.v[k] = (uint32_t)acc & FE_MASK;
     acc >>= 29;
   }

@@ -10,7 +10,9 @@ import random
 import pytest
 
 L = 2**252 + 27742317777372353535851937790883648493
-NPOS = {8: 32, 9: 29, 10: 26, 11: 23, 12: 22, 13: 20, 14: 19, 15: 17, 16: 16}
+NPOS = {8: 32, 9: 29, 10: 26, 11: 23, 12: 22, 13: 20, 14: 19, 15: 17, 16: 16, 17: 15, 18: 15, 19: 14, 20: 13,
+        21: 13, 22: 12}
+B_RADICES = (16, 22)  # B's table: CBFT_COMB_B_RADIX (22) and the $CBFT_B_RADIX=16 alternative
 
 
 def offset(w, npos):
@@ -47,8 +49,7 @@ def test_recode_sums_and_ranges(w):
         assert sum(d << (w * j) for j, d in enumerate(ds)) == s
         assert all(-half <= d <= half - 1 for d in ds[:-1])
         assert 0 <= ds[-1] <= half
-        if w == 16:  # 16-bit offset-binary digit storage: the top digit must stay <= 2^15 - 1
-            assert ds[-1] <= half - 1
+        assert -(1 << 21) <= min(ds) and max(ds) <= 1 << 21  # the ladder's digit storage (int32 LDS)
 
 
 @pytest.mark.parametrize("w", sorted(NPOS))
@@ -62,8 +63,11 @@ def test_npos_is_minimal(w):
 def test_lane_split_covers_all_positions():
     # additions dealt to the 4 lanes of a quad: lane q takes q*nper .. q*nper+nper-1
     for wa in range(8, 14):
-        total = NPOS[wa] + NPOS[16]
-        nper = (total + 3) // 4
-        assert nper <= 12  # COMB_MAX_STEPS
-        seen = [q * nper + jj for q in range(4) for jj in range(nper) if q * nper + jj < total]
-        assert seen == list(range(total))
+        for wb in B_RADICES:
+            total = NPOS[wa] + NPOS[wb]
+            nper = (total + 3) // 4
+            assert nper <= 12  # COMB_MAX_STEPS
+            seen = [q * nper + jj for q in range(4) for jj in range(nper) if q * nper + jj < total]
+            assert seen == list(range(total))
+    # the default geometry: radix-2^13 keys + radix-2^22 B = 32 additions, 8 per lane
+    assert (NPOS[13] + NPOS[22] + 3) // 4 == 8

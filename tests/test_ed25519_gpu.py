@@ -69,6 +69,23 @@ def test_golden_key_table_radix(ctx, golden, radix):
         ctx.unload_keys(tid)
 
 
+@pytest.mark.parametrize("b_radix", [16, 17, 20])
+@pytest.mark.parametrize("radix", [8, 13])
+def test_golden_base_table_radix(golden, monkeypatch, b_radix, radix):
+    """B's comb radix ($CBFT_B_RADIX; the default 22 is covered above): the ladder's lane split
+    changes with it (radix-2^13 keys: 9 additions per lane at B radix 16, 9 at 17, 9 at 20, 8 at 22)."""
+    monkeypatch.setenv("CBFT_B_RADIX", str(b_radix))
+    keys = sorted({v.pk for v in golden})
+    index = {k: i for i, k in enumerate(keys)}
+    with cb.Context(device=0) as c:
+        tid = c.load_keys(keys, radix=radix)
+        n = len(golden)
+        got = _bools(c.verify(tid, [index[v.pk] for v in golden], [v.sig for v in golden],
+                              [v.msg for v in golden]), n)
+    exp = np.array([bool(v.verdict) for v in golden])
+    assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
+
+
 def test_load_keys_bad_radix(ctx):
     lib = ctx.lib
     tid = ctypes.c_uint32()

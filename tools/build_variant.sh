@@ -1,0 +1,15 @@
+#!/bin/bash
+# Build a variant of libcbft_hipcrypto with extra compile flags, for A/B runs on the GPU box
+# (select it there with CBFT_LIB=<path>).  Usage: tools/build_variant.sh <out.so> <flags...>
+set -e
+cd "$(dirname "$0")/.."
+out=$1; shift
+tmp=$(mktemp -d)
+for src in ed25519_verify.hip cbft_hipcrypto.cpp bls_kernels.hip bls_pairing.hip bls_keys.hip cbft_bls.cpp rsa_verify.hip cbft_rsa.cpp; do
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Iconcord-bft_amd/csrc -Wno-unused-function "$@" \
+    -c concord-bft_amd/csrc/$src -o "$tmp/${src%.*}.o" &
+done
+wait
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out" "$tmp"/*.o
+rm -rf "$tmp"
+echo "built $out ($*)"
