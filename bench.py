@@ -252,13 +252,17 @@ def main():
     del src, dst
 
     # ---- roofline: the dominant kernel (INT32 VALU) + the PCIe bound of the whole step
-    kname = "ed25519_comb_ladder_kernel"
+    # the ladder layout the library picks (cbft_hipcrypto.cpp): two lanes per signature from 32K
+    lanes = int(os.environ.get("CBFT_LADDER_LANES", "0")) or (2 if n >= 32768 else 4)
+    b_radix = int(os.environ.get("CBFT_B_RADIX", "22"))
+    kname = "ed25519_comb2_ladder_kernel" if lanes == 2 else "ed25519_comb_ladder_kernel"
     traffic = slot_ops = None
     pmc = os.path.join(ROOT, "profiles", "pmc_ladder.json")
     if os.path.exists(pmc):
         try:
             rec = json.load(open(pmc))
-            if rec.get("kernel") == kname and rec.get("batch") == n and rec.get("comb_radix") == args.comb_radix:
+            if rec.get("kernel") == kname and rec.get("batch") == n and rec.get("comb_radix") == args.comb_radix \
+                    and rec.get("b_radix", 16) == b_radix:
                 traffic = rec.get("hbm_bytes_per_launch")
                 k = rec["counters"][kname]
                 slot_ops = (k["SQ_INSTS_VALU"] + k["SQ_INSTS_VALU_INT64"]) * 64
@@ -342,6 +346,7 @@ def main():
             "config": {"workload": "ed25519_verify_64k_256B_4096keys (BASELINE config #2: host batch, H2D of "
                                    "sig+msg timed, key table resident)",
                        "batch_per_gpu": n, "msg_len": L, "nkeys": args.nkeys, "comb_radix": args.comb_radix,
+                       "b_comb_radix": b_radix, "ladder_lanes_per_signature": lanes,
                        "inputs": "pinned host memory (cbft_host_alloc) -> GPU each step; bitmap -> host",
                        "inflight_batches": depth,
                        "parallelism": f"static shard x{world}" + (", RCCL all-gather of verdict bitmaps"

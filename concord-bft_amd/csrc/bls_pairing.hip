@@ -121,6 +121,10 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
 // H = g1_map(msg) on wave 0 (also stored to H_out when non-null), sigma from 33 bytes on wave 1:
 // e(H, PK) * e(-sigma, g2) == 1 for a combined signature.  One block of two waves.
 // pk_abc: the key's lines are unnormalised (a fresh multisig key, bn254_g2wave.h).
+// CBFT_BLS_PHASES (probe builds only): phase timestamps (bn254_pair36.h: BLS_STAMP), printed
+// by lane 0 of wave 0 at the end in 10 ns wall-clock ticks.
+#define BLS_PHASE(slot) BLS_STAMP(slot)
+
 __global__ void __launch_bounds__(PAIR_BLOCK) bls_verify_kernel(const uint8_t* msg, uint32_t len, uint32_t* H_out,
                                                                 const uint8_t* sig33, const uint32_t* pk_lines,
                                                                 int pk_abc, const uint8_t* pk_ok,
@@ -129,10 +133,12 @@ __global__ void __launch_bounds__(PAIR_BLOCK) bls_verify_kernel(const uint8_t* m
   if (blockIdx.x != 0) return;
   const int wave = threadIdx.x >> 6;
   const P36 g = p36_lane();
+  BLS_PHASE(wave);
   fp f;
   if (wave == 1) {
     g1a s;
     const bool ok = g1_decompress(s, sig33);
+    BLS_PHASE(2);
     if (ok && !s.inf) {
       g1a P = s;
       f_neg(P.y, s.y);
@@ -141,17 +147,20 @@ __global__ void __launch_bounds__(PAIR_BLOCK) bls_verify_kernel(const uint8_t* m
     } else {
       p36_one(f, g);
     }
+    BLS_PHASE(3);
     xchg_put(xc, f, g);
     if (g.lane == 0) xc.ok = ok ? 1 : 0;
   } else {
     g1a P;
     g1_map_wave(P, msg, len);
+    BLS_PHASE(4);
     if (g.lane == 0 && H_out) g1a_store(H_out, P);
     const uint32_t* l[1] = {pk_lines};
     if (pk_abc)
       p36_miller<1, true>(f, &P, l, g);
     else
       p36_miller<1>(f, &P, l, g);
+    BLS_PHASE(5);
   }
   __syncthreads();
   if (wave != 0) return;
@@ -160,9 +169,21 @@ __global__ void __launch_bounds__(PAIR_BLOCK) bls_verify_kernel(const uint8_t* m
     fp f1;
     xchg_get(f1, xc, g);
     p36_mul(f, f, f1, g);
+    BLS_PHASE(6);
     good = p36_is_one_after_final_exp(f, g);
+    BLS_PHASE(11);
   }
   if (g.lane == 0) result[0] = good ? 1 : 0;
+#if CBFT_BLS_PHASES
+  if (g.lane == 0) {
+    const uint64_t t0 = g_bls_phase[0];
+    printf("bls_verify phases (us from start): w1 decompressed %.1f w1 miller %.1f | w0 hashed %.1f miller %.1f "
+           "joined %.1f fe_inv %.1f fe_easy %.1f fe_pow_u %.1f fe_done %.1f\n",
+           (g_bls_phase[2] - t0) * 0.01, (g_bls_phase[3] - t0) * 0.01, (g_bls_phase[4] - t0) * 0.01,
+           (g_bls_phase[5] - t0) * 0.01, (g_bls_phase[6] - t0) * 0.01, (g_bls_phase[8] - t0) * 0.01,
+           (g_bls_phase[9] - t0) * 0.01, (g_bls_phase[10] - t0) * 0.01, (g_bls_phase[11] - t0) * 0.01);
+  }
+#endif
 }
 
 // ------------------------------------------------------------------------------ launchers

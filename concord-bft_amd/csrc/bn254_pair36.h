@@ -341,17 +341,37 @@ __device__ __forceinline__ void p36_pow_small(fp& r, const fp& x, uint32_t e, co
   r = acc;
 }
 
+#ifndef CBFT_BLS_PHASES
+#define CBFT_BLS_PHASES 0
+#endif
+// phase timestamps (probe builds): slot -> 10 ns wall-clock tick, printed once by the kernel
+#if CBFT_BLS_PHASES
+__device__ uint64_t g_bls_phase[16];
+#define BLS_STAMP(slot)                                                 \
+  do {                                                                  \
+    if ((threadIdx.x & 63) == 0) g_bls_phase[(slot)] = wall_clock64(); \
+  } while (0)
+#else
+#define BLS_STAMP(slot) \
+  do {                  \
+  } while (0)
+#endif
+#define P36_PHASE(name) BLS_STAMP(name)
+
 __device__ __forceinline__ void p36_final_exp(fp& r, const fp& f, const P36& g) {
   fp t, gg;
   p36_inv(t, f, g);
+  P36_PHASE(8);
   p36_conj(gg, f, g);
   p36_mul(gg, gg, t, g);
   p36_frob<2>(t, gg, g);
   p36_mul(gg, t, gg, g);
+  P36_PHASE(9);
   fp a, b, c, c36, b6, b18, b30, a12, a18, g2;
   p36_pow_u(a, gg, g);
   p36_pow_u(b, a, g);
   p36_pow_u(c, b, g);
+  P36_PHASE(10);
   p36_pow_small(c36, c, 36, g);
   p36_pow_small(b6, b, 6, g);
   p36_pow_small(b18, b6, 3, g);

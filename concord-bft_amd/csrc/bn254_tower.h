@@ -84,12 +84,17 @@ BN_HD void fp2_mul_xi(fp2& r, const fp2& x) {  // (a + b i)(1 + i) = (a - b) + (
   f_add(r.b, x.a, x.b);
   r.a = t;
 }
+// VAR: variable-time inversion (fp_inv_var) -- public values only (final exponentiations)
+template <bool VAR = false>
 BN_HDN void fp2_inv(fp2& r, const fp2& x) {
   fp n, t;
   f_sqr(n, x.a);
   f_sqr(t, x.b);
   f_add(n, n, t);
-  fp_inv(n, n);
+  if (VAR)
+    fp_inv_var(n, n);
+  else
+    fp_inv(n, n);
   f_mul(r.a, x.a, n);
   f_mul(t, x.b, n);
   f_neg(r.b, t);
@@ -194,6 +199,7 @@ BN_HDN void fp6_mul_01(fp6& r, const fp6& x, const fp2& s0, const fp2& s1) {
   r.c1 = c1;
   r.c2 = c2;
 }
+template <bool VAR = false>
 BN_HDN void fp6_inv(fp6& r, const fp6& x) {
   fp2 t0, t1, t2, u, v, n;
   // t0 = c0^2 - xi c1 c2, t1 = xi c2^2 - c0 c1, t2 = c1^2 - c0 c2
@@ -215,7 +221,7 @@ BN_HDN void fp6_inv(fp6& r, const fp6& x) {
   fp2_mul_xi(u, u);
   fp2_mul(n, x.c0, t0);
   fp2_add(n, n, u);
-  fp2_inv(n, n);
+  fp2_inv<VAR>(n, n);
   fp2_mul(r.c0, t0, n);
   fp2_mul(r.c1, t1, n);
   fp2_mul(r.c2, t2, n);
@@ -254,13 +260,15 @@ BN_HD void fp12_conj(fp12& r, const fp12& x) {
   r.c0 = x.c0;
   fp6_neg(r.c1, x.c1);
 }
+// Only the final exponentiations invert in Fp12, always of a Miller value computed from public
+// inputs (signatures, hashes, keys), so the variable-time Fp inversion is used.
 BN_HDN void fp12_inv(fp12& r, const fp12& x) {  // (c0 - c1 w) / (c0^2 - v c1^2)
   fp6 t0, t1;
   fp6_mul(t0, x.c0, x.c0);
   fp6_mul(t1, x.c1, x.c1);
   fp6_mul_v(t1, t1);
   fp6_sub(t0, t0, t1);
-  fp6_inv(t0, t0);
+  fp6_inv<true>(t0, t0);
   fp6_mul(r.c0, x.c0, t0);
   fp6_mul(t1, x.c1, t0);
   fp6_neg(r.c1, t1);

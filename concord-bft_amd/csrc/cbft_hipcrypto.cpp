@@ -548,7 +548,9 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     b.keys = kt->view();
     w.base_comb = c->base_comb.as<uint32_t>();
     w.comb = cbft_comb_ladder(kt->geo.w, c->b_radix);
-    w.comb_lanes = c->ladder_lanes ? c->ladder_lanes : 4;
+    // pair ladder (fewer additions in total, 2 waves/SIMD) once a batch fills the chip with it;
+    // the quad ladder (half the additions per lane) for the latency of small batches
+    w.comb_lanes = c->ladder_lanes ? c->ladder_lanes : (n >= 32768 ? 2 : 4);
   }
   StageOrder order{};
   if (c->stage_order) {

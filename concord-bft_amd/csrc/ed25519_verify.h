@@ -103,10 +103,11 @@ inline CombLadder cbft_comb_ladder(int wa, int wb) {
   c.nper = (c.a.npos + c.b.npos + 3) / 4;
   return c;
 }
-// B's table: radix 2^16 by default (16 positions x 32,769 entries, 67 MB per context: a verify
-// against a radix-2^13 key table is 20 + 16 = 36 additions, 9 per lane of a quad).  Radix 2^22
-// (12 positions, 3.2 GB) makes it 32 additions, 8 per lane; $CBFT_B_RADIX selects 16..22.
-#define CBFT_COMB_B_RADIX 16
+// B's table: radix 2^22 by default (12 positions x 2,097,153 entries, 3.2 GB per context of the
+// 288 GB HBM), so a verify against a radix-2^13 key table is 20 + 12 = 32 additions: 16 per lane
+// of a pair, 8 per lane of a quad (radix 2^16: 16 positions, 67 MB, 36 additions; measured on
+// MI355X at 64K: pair ladder 104 us at 2^22 vs 112 us at 2^16).  $CBFT_B_RADIX selects 16..22.
+#define CBFT_COMB_B_RADIX 22
 #define CBFT_COMB_MAX_RADIX 22
 
 // Device work buffers of one verify launch.

@@ -356,7 +356,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_finish_kernel(const
     fe_load_soa(Y, xyz_soa + 9 * b.n, b.n, i);
     fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
     uint32_t Rp[8], Rw[8];
-    ge_tobytes(Rp, X, Y, Z);
+    ge_tobytes<false>(Rp, X, Y, Z);
     load_words8(Rw, b.sig + i * 64);
     uint32_t diff = 0;
 #pragma unroll
@@ -400,12 +400,12 @@ __global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519B
       if (!ok) fe_1(Z);
     }
     okmask |= (ok ? 1u : 0u) << j;
-    fe_mul(acc, acc, Z);
+    fe_mul<false>(acc, acc, Z);
 #pragma unroll
     for (int k = 0; k < FE_LIMBS; k++) pre[j][k][ln] = acc.v[k];
   }
   fe inv;
-  fe_invert(inv, acc);
+  fe_invert<false>(inv, acc);
 #pragma nounroll
   for (int j = K - 1; j >= 0; j--) {
     const size_t i = base + (size_t)j * 64 + ln;
@@ -415,19 +415,19 @@ __global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519B
       fe p;
 #pragma unroll
       for (int k = 0; k < FE_LIMBS; k++) p.v[k] = pre[j - 1][k][ln];
-      fe_mul(zi, inv, p);
+      fe_mul<false>(zi, inv, p);
     } else {
       fe_copy(zi, inv);
     }
     bool verdict = false;
     if (ok) {
       fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
-      fe_mul(inv, inv, Z);
+      fe_mul<false>(inv, inv, Z);
       fe X, Y, x, y;
       fe_load_soa(X, xyz_soa, b.n, i);
       fe_load_soa(Y, xyz_soa + 9 * b.n, b.n, i);
-      fe_mul(x, X, zi);
-      fe_mul(y, Y, zi);
+      fe_mul<false>(x, X, zi);
+      fe_mul<false>(y, Y, zi);
       uint32_t Rp[8], Rw[8];
       fe_to_words(Rp, y);
       Rp[7] ^= fe_isnegative(x) << 31;
@@ -843,16 +843,31 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
       asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // entry jj landed; jj + 1 may still fly
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // The stage is read with asm ds_reads: the compiler would otherwise see LDS reads after
+    // global_load_lds writes and wait for ALL of them (vmcnt(0)), serialising the two stages.
     uint32_t ew[28];
+    {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const uint32_t addr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint4*)&stage[wv][slot][0][ln]);
+      u32x4 v[7];
+#define COMB2_DS_READ(c) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v[c]) : "v"(addr), "i"((c) * 1024))
+      COMB2_DS_READ(0);
+      COMB2_DS_READ(1);
+      COMB2_DS_READ(2);
+      COMB2_DS_READ(3);
+      COMB2_DS_READ(4);
+      COMB2_DS_READ(5);
+      COMB2_DS_READ(6);
+#undef COMB2_DS_READ
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry jj is in VGPRs: its stage is free
 #pragma unroll
-    for (int c = 0; c < 7; c++) {
-      const uint4 v = stage[wv][slot][c][ln];
-      ew[4 * c] = v.x;
-      ew[4 * c + 1] = v.y;
-      ew[4 * c + 2] = v.z;
-      ew[4 * c + 3] = v.w;
+      for (int c = 0; c < 7; c++) {
+        ew[4 * c] = v[c].x;
+        ew[4 * c + 1] = v[c].y;
+        ew[4 * c + 2] = v[c].z;
+        ew[4 * c + 3] = v[c].w;
+      }
     }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry jj is in VGPRs: its stage is free
     const bool neg = dcur < 0;
     dcur = dnext;
     if (jj + 2u < nper) {

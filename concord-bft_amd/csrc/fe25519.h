@@ -101,36 +101,42 @@ FE_INLINE void fe_neg(fe& r, const fe& a) {
     if (j >= 0 && j < FE_LIMBS) { TERM }                         \
   }
 
+// CBFT_FE_CHAIN: default for the template argument C of the multiply family; kernels whose
+// waves run alone on a SIMD (the inversion chains of K4) pass C = false: there the hazard nops
+// between dependent asm mads cost issue slots no other wave can use.
 #ifndef CBFT_FE_CHAIN
 #define CBFT_FE_CHAIN 1
 #endif
 
-// acc += a * b (one v_mad_u64_u32, not reassociable)
+// acc += a * b (CHAIN: one v_mad_u64_u32, not reassociable)
+template <bool CHAIN>
 FE_INLINE void mac(uint64_t& acc, uint32_t a, uint32_t b) {
-#if CBFT_FE_CHAIN
-  uint64_t cc;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
-#else
-  acc = mad64(a, b, acc);
-#endif
+  if (CHAIN) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
+  } else {
+    acc = mad64(a, b, acc);
+  }
 }
 // acc += a * 1216 (the 2^261 fold; the constant rides in an SGPR)
+template <bool CHAIN>
 FE_INLINE void mac1216(uint64_t& acc, uint32_t a) {
-#if CBFT_FE_CHAIN
-  uint64_t cc;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "s"(1216u));
-#else
-  acc = mad64(a, 1216u, acc);
-#endif
+  if (CHAIN) {
+    uint64_t cc;
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "s"(1216u));
+  } else {
+    acc = mad64(a, 1216u, acc);
+  }
 }
 
+template <bool C = CBFT_FE_CHAIN>
 FE_INLINE void fe_mul(fe& r, const fe& a, const fe& b) {
   fe o;  // r may alias a or b
   uint32_t h[9];
   uint64_t t = 0;
 #pragma unroll
   for (int k = 9; k < 17; k++) {
-    FE_COLUMN(t, k, mac(t, a.v[i], b.v[j]);)
+    FE_COLUMN(t, k, mac<C>(t, a.v[i], b.v[j]);)
     h[k - 9] = (uint32_t)t & FE_MASK;
     t >>= 29;
   }
@@ -138,8 +144,8 @@ FE_INLINE void fe_mul(fe& r, const fe& a, const fe& b) {
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 9; k++) {
-    mac1216(acc, h[k]);
-    FE_COLUMN(acc, k, mac(acc, a.v[i], b.v[j]);)
+    mac1216<C>(acc, h[k]);
+    FE_COLUMN(acc, k, mac<C>(acc, a.v[i], b.v[j]);)
     o.v[k] = (uint32_t)acc & FE_MASK;
     acc >>= 29;
   }
@@ -150,6 +156,7 @@ FE_INLINE void fe_mul(fe& r, const fe& a, const fe& b) {
   r = o;
 }
 
+template <bool C = CBFT_FE_CHAIN>
 FE_INLINE void fe_sq(fe& r, const fe& a) {
   fe o;  // r may alias a or b
   uint32_t a2[FE_LIMBS];
@@ -159,8 +166,8 @@ FE_INLINE void fe_sq(fe& r, const fe& a) {
   uint64_t t = 0;
 #pragma unroll
   for (int k = 9; k < 17; k++) {
-    FE_COLUMN(t, k, if (j > i) mac(t, a2[i], a.v[j]);)
-    if ((k & 1) == 0) mac(t, a.v[k >> 1], a.v[k >> 1]);
+    FE_COLUMN(t, k, if (j > i) mac<C>(t, a2[i], a.v[j]);)
+    if ((k & 1) == 0) mac<C>(t, a.v[k >> 1], a.v[k >> 1]);
     h[k - 9] = (uint32_t)t & FE_MASK;
     t >>= 29;
   }
@@ -168,9 +175,9 @@ FE_INLINE void fe_sq(fe& r, const fe& a) {
   uint64_t acc = 0;
 #pragma unroll
   for (int k = 0; k < 9; k++) {
-    mac1216(acc, h[k]);
-    FE_COLUMN(acc, k, if (j > i) mac(acc, a2[i], a.v[j]);)
-    if ((k & 1) == 0) mac(acc, a.v[k >> 1], a.v[k >> 1]);
+    mac1216<C>(acc, h[k]);
+    FE_COLUMN(acc, k, if (j > i) mac<C>(acc, a2[i], a.v[j]);)
+    if ((k & 1) == 0) mac<C>(acc, a.v[k >> 1], a.v[k >> 1]);
     o.v[k] = (uint32_t)acc & FE_MASK;
     acc >>= 29;
   }
@@ -198,10 +205,11 @@ FE_INLINE void fe_mul_small(fe& r, const fe& a, uint32_t s) {
 }
 
 // r = a^(2^n) (n >= 1); a runtime (not unrolled) loop keeps code size to one square body
+template <bool C = CBFT_FE_CHAIN>
 FE_INLINE void fe_sqn(fe& r, const fe& a, int n) {
-  fe_sq(r, a);
+  fe_sq<C>(r, a);
 #pragma nounroll
-  for (int i = 1; i < n; i++) fe_sq(r, r);
+  for (int i = 1; i < n; i++) fe_sq<C>(r, r);
 }
 
 // Canonical 8x32-bit little-endian words of a (fully reduced into [0, p)).
@@ -283,42 +291,45 @@ FE_INLINE void fe_cmov(fe& r, const fe& a, bool c) {
 
 // z^(2^250 - 1) and z^11: the shared prefix of inversion (p-2 = 2^255 - 21) and of the
 // square-root power (p-5)/8 = 2^252 - 3.  Chain: 11 multiplies + 254 squarings in total.
+template <bool C = CBFT_FE_CHAIN>
 FE_INLINE void fe_pow_2_250_1(fe& z250, fe& z11, const fe& z) {
   fe z2, z9, t0, t1, t2;
-  fe_sq(z2, z);             // 2
-  fe_sqn(t0, z2, 2);        // 8
-  fe_mul(z9, t0, z);        // 9
-  fe_mul(z11, z9, z2);      // 11
-  fe_sq(t0, z11);           // 22
-  fe_mul(t0, t0, z9);       // 31 = 2^5 - 1
-  fe_sqn(t1, t0, 5);
-  fe_mul(t0, t1, t0);       // 2^10 - 1
-  fe_sqn(t1, t0, 10);
-  fe_mul(t1, t1, t0);       // 2^20 - 1
-  fe_sqn(t2, t1, 20);
-  fe_mul(t1, t2, t1);       // 2^40 - 1
-  fe_sqn(t1, t1, 10);
-  fe_mul(t0, t1, t0);       // 2^50 - 1
-  fe_sqn(t1, t0, 50);
-  fe_mul(t1, t1, t0);       // 2^100 - 1
-  fe_sqn(t2, t1, 100);
-  fe_mul(t1, t2, t1);       // 2^200 - 1
-  fe_sqn(t1, t1, 50);
-  fe_mul(z250, t1, t0);     // 2^250 - 1
+  fe_sq<C>(z2, z);             // 2
+  fe_sqn<C>(t0, z2, 2);        // 8
+  fe_mul<C>(z9, t0, z);        // 9
+  fe_mul<C>(z11, z9, z2);      // 11
+  fe_sq<C>(t0, z11);           // 22
+  fe_mul<C>(t0, t0, z9);       // 31 = 2^5 - 1
+  fe_sqn<C>(t1, t0, 5);
+  fe_mul<C>(t0, t1, t0);       // 2^10 - 1
+  fe_sqn<C>(t1, t0, 10);
+  fe_mul<C>(t1, t1, t0);       // 2^20 - 1
+  fe_sqn<C>(t2, t1, 20);
+  fe_mul<C>(t1, t2, t1);       // 2^40 - 1
+  fe_sqn<C>(t1, t1, 10);
+  fe_mul<C>(t0, t1, t0);       // 2^50 - 1
+  fe_sqn<C>(t1, t0, 50);
+  fe_mul<C>(t1, t1, t0);       // 2^100 - 1
+  fe_sqn<C>(t2, t1, 100);
+  fe_mul<C>(t1, t2, t1);       // 2^200 - 1
+  fe_sqn<C>(t1, t1, 50);
+  fe_mul<C>(z250, t1, t0);     // 2^250 - 1
 }
 
 // r = z^(p-2) = z^(2^255 - 21)
+template <bool C = CBFT_FE_CHAIN>
 FE_INLINE void fe_invert(fe& r, const fe& z) {
   fe z250, z11;
-  fe_pow_2_250_1(z250, z11, z);
-  fe_sqn(z250, z250, 5);    // 2^255 - 32
-  fe_mul(r, z250, z11);     // 2^255 - 21
+  fe_pow_2_250_1<C>(z250, z11, z);
+  fe_sqn<C>(z250, z250, 5);    // 2^255 - 32
+  fe_mul<C>(r, z250, z11);     // 2^255 - 21
 }
 
 // r = z^((p-5)/8) = z^(2^252 - 3)
+template <bool C = CBFT_FE_CHAIN>
 FE_INLINE void fe_pow22523(fe& r, const fe& z) {
   fe z250, z11;
-  fe_pow_2_250_1(z250, z11, z);
-  fe_sqn(z250, z250, 2);    // 2^252 - 4
-  fe_mul(r, z250, z);       // 2^252 - 3
+  fe_pow_2_250_1<C>(z250, z11, z);
+  fe_sqn<C>(z250, z250, 2);    // 2^252 - 4
+  fe_mul<C>(r, z250, z);       // 2^252 - 3
 }

@@ -164,11 +164,12 @@ FE_INLINE bool ge_frombytes(ge_p3& h, const uint32_t* w) {
 }
 
 // Canonical encoding of (X:Y:Z) into 8 little-endian words.
+template <bool C = CBFT_FE_CHAIN>
 FE_INLINE void ge_tobytes(uint32_t* out, const fe& X, const fe& Y, const fe& Z) {
   fe zi, x, y;
-  fe_invert(zi, Z);
-  fe_mul(x, X, zi);
-  fe_mul(y, Y, zi);
+  fe_invert<C>(zi, Z);
+  fe_mul<C>(x, X, zi);
+  fe_mul<C>(y, Y, zi);
   fe_to_words(out, y);
   out[7] ^= fe_isnegative(x) << 31;
 }

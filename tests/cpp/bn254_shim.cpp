@@ -22,6 +22,23 @@ static void fp12_flat(uint8_t* out, const fp12& x) {  // 12 x 32-byte big-endian
 
 extern "C" {
 
+// fp_inv_var and fp_inv of the canonical integer x (32-byte big-endian, < p): out_var, out_fermat
+// (big-endian canonical).  Returns 1 if both agree.
+int shim_fp_inv(const uint8_t* x32, uint8_t* out_var, uint8_t* out_fermat) {
+  uint32_t w[8];
+  be32_to_words(w, x32);
+  fp a, r1, r2;
+  f_from_words(a, w);
+  fp_inv_var(r1, a);
+  fp_inv(r2, a);
+  f_to_words(w, r1);
+  words_to_be32(out_var, w);
+  uint32_t w2[8];
+  f_to_words(w2, r2);
+  words_to_be32(out_fermat, w2);
+  return std::memcmp(w, w2, sizeof w) == 0 ? 1 : 0;
+}
+
 int shim_g1_decompress(const uint8_t* in33, uint8_t* out64) {
   g1a a;
   if (!g1_decompress(a, in33)) return 0;

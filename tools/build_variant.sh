@@ -5,11 +5,13 @@ set -e
 cd "$(dirname "$0")/.."
 out=$1; shift
 tmp=$(mktemp -d)
+pids=()
 for src in ed25519_verify.hip cbft_hipcrypto.cpp bls_kernels.hip bls_pairing.hip bls_keys.hip cbft_bls.cpp rsa_verify.hip cbft_rsa.cpp; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Iconcord-bft_amd/csrc -Wno-unused-function "$@" \
     -c concord-bft_amd/csrc/$src -o "$tmp/${src%.*}.o" &
+  pids+=($!)
 done
-wait
+for p in "${pids[@]}"; do wait "$p" || { echo "compile failed"; rm -rf "$tmp"; exit 1; }; done
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out" "$tmp"/*.o
 rm -rf "$tmp"
 echo "built $out ($*)"
