@@ -79,3 +79,21 @@ __device__ __forceinline__ void g1_map_wave(g1a& r, const uint8_t* msg, uint32_t
   }
   r.inf = false;
 }
+
+// Jacobian G2 point <-> 54 words (X | Y | Z, Fp2 = a | b, 9 limbs each): key-sum partials
+__device__ __forceinline__ void g2j_store(uint32_t* o, const g2j& a) {
+  const fp2* src[3] = {&a.X, &a.Y, &a.Z};
+  for (int c = 0; c < 3; c++)
+    for (int q = 0; q < 9; q++) {
+      o[18 * c + q] = src[c]->a.v[q];
+      o[18 * c + 9 + q] = src[c]->b.v[q];
+    }
+}
+__device__ __forceinline__ void g2j_load(g2j& a, const uint32_t* o) {
+  fp2* dst[3] = {&a.X, &a.Y, &a.Z};
+  for (int c = 0; c < 3; c++)
+    for (int q = 0; q < 9; q++) {
+      dst[c]->a.v[q] = o[18 * c + q];
+      dst[c]->b.v[q] = o[18 * c + 9 + q];
+    }
+}

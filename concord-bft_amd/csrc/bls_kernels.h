@@ -41,6 +41,11 @@ size_t cbft_bls_abc_lines_words();
 hipError_t cbft_bls_launch_g2_lines(const uint32_t* d_parts, uint32_t count, uint32_t* d_lines, uint8_t* d_ok,
                                     hipStream_t s);
 // H = g1_map(msg) (-> d_H when non-null) and e(H, PK) e(-sigma, g2) == 1 in one launch
+// multisig verify in one launch: PK = sum of count key-sum partials, its lines streamed from one
+// wave to the Miller loop of another, sigma's pair on a third (d_pk_ok = PK usable)
+hipError_t cbft_bls_launch_verify_multisig(const uint32_t* d_parts, uint32_t count, const uint8_t* d_msg, uint32_t len,
+                                           const uint8_t* d_sig33, const uint32_t* d_gen_lines, uint8_t* d_pk_ok,
+                                           uint8_t* d_result, hipStream_t s);
 // pk_abc: d_pk_lines are unnormalised (A, B, C) lines (cbft_bls_launch_g2_lines)
 hipError_t cbft_bls_launch_verify(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, const uint8_t* d_sig33,
                                   const uint32_t* d_pk_lines, int pk_abc, const uint8_t* d_pk_ok,

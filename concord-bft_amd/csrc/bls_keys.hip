@@ -54,23 +54,6 @@ __device__ void g2_sum_tail(const g2j& acc, bool bad, uint8_t* ok, uint8_t* out6
   ok[0] = good && !s.inf ? 1 : 0;
 }
 
-__device__ __forceinline__ void g2j_store(uint32_t* o, const g2j& a) {
-  const fp2* src[3] = {&a.X, &a.Y, &a.Z};
-  for (int c = 0; c < 3; c++)
-    for (int q = 0; q < 9; q++) {
-      o[18 * c + q] = src[c]->a.v[q];
-      o[18 * c + 9 + q] = src[c]->b.v[q];
-    }
-}
-__device__ __forceinline__ void g2j_load(g2j& a, const uint32_t* o) {
-  fp2* dst[3] = {&a.X, &a.Y, &a.Z};
-  for (int c = 0; c < 3; c++)
-    for (int q = 0; q < 9; q++) {
-      dst[c]->a.v[q] = o[18 * c + q];
-      dst[c]->b.v[q] = o[18 * c + 9 + q];
-    }
-}
-
 // Signer ids [lo_id, hi_id) only (a rank's slice of a sharded multisig key sum).  With out_part
 // the block writes its Jacobian sum (54 words) + the bad-key flag (1 word) (-> bls_g2_lines_kernel),
 // else the compressed sum into out65.

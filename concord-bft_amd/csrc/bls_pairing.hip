@@ -13,6 +13,7 @@
 // off the critical path, and with them the sqrt of sigma's decompression (and, in
 // bls_verify_kernel, the hash to G1, which wave 0 computes while wave 1 decodes sigma).
 #include "bls_common.h"
+#include "bn254_g2wave.h"
 #include "bn254_pair36.h"
 
 #define PAIR_BLOCK 128  // two waves
@@ -186,6 +187,86 @@ __global__ void __launch_bounds__(PAIR_BLOCK) bls_verify_kernel(const uint8_t* m
 #endif
 }
 
+// Multisig verify in one 3-wave block (BlsMultisigVerifier: e(H, sum vk_i) e(-sigma, g2) == 1):
+//   wave 0  PK = sum of the key-sum partials (bls_g2_sum_kernel), to affine, then its 70
+//           unnormalised lines (bn254_g2wave.h) into LDS, publishing each as it lands;
+//   wave 1  H = g1_map(msg), then the (H, PK) Miller loop, reading each line as soon as wave 0
+//           has published it (the loop trails the line computation instead of following it);
+//   wave 2  decompress sigma, the (-sigma, g2) Miller loop over the precomputed generator lines.
+// Wave 1 joins the two Miller values and runs the final exponentiation.  Every wave reaches the
+// end: wave 0 publishes "all lines" even when PK is unusable (bad key, infinity).
+#define MS_BLOCK 192
+__global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uint32_t* parts, uint32_t count,
+                                                                       const uint8_t* msg, uint32_t len,
+                                                                       const uint8_t* sig33, const uint32_t* gen_lines,
+                                                                       uint8_t* pk_ok, uint8_t* result) {
+  __shared__ PairXchg xc;
+  __shared__ uint32_t lines[BN_ATE_LINES * BN_ABC_WORDS];
+  __shared__ int progress;
+  __shared__ int usable;
+  if (blockIdx.x != 0) return;
+  const int wave = threadIdx.x >> 6;
+  const P36 g = p36_lane();
+  if (threadIdx.x == 0) {
+    progress = 0;
+    usable = 0;
+    xc.ok = 0;
+  }
+  __syncthreads();
+  fp f;
+  if (wave == 0) {
+    g2j acc;
+    fp2_one(acc.X);
+    fp2_one(acc.Y);
+    fp2_zero(acc.Z);
+    bool bad = false;
+    for (uint32_t b = 0; b < count; b++) {
+      g2j o;
+      g2j_load(o, parts + 55 * (size_t)b);
+      bad |= parts[55 * (size_t)b + 54] != 0;
+      g2_add_j(acc, acc, o);
+    }
+    g2a s;
+    g2_to_affine<true>(s, acc);  // public point: variable-time inversion
+    const bool ok = !bad && !s.inf;
+    if (g.lane == 0) {
+      pk_ok[0] = ok ? 1 : 0;
+      usable = ok ? 1 : 0;
+    }
+    if (ok) g2w_lines_abc(lines, s, &progress);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    if (g.lane == 0) progress = BN_ATE_LINES + 1;  // release the consumer whatever happened
+  } else if (wave == 1) {
+    g1a P;
+    g1_map_wave(P, msg, len);
+    const uint32_t* l[1] = {lines};
+    p36_miller<1, true>(f, &P, l, g, &progress);
+  } else {
+    g1a s;
+    const bool ok = g1_decompress(s, sig33);
+    if (ok && !s.inf) {
+      g1a P = s;
+      f_neg(P.y, s.y);
+      const uint32_t* l[1] = {gen_lines};
+      p36_miller<1>(f, &P, l, g);
+    } else {
+      p36_one(f, g);
+    }
+    xchg_put(xc, f, g);
+    if (g.lane == 0) xc.ok = ok ? 1 : 0;
+  }
+  __syncthreads();
+  if (wave != 1) return;
+  bool good = xc.ok != 0 && usable != 0;
+  if (good) {
+    fp f1;
+    xchg_get(f1, xc, g);
+    p36_mul(f, f, f1, g);
+    good = p36_is_one_after_final_exp(f, g);
+  }
+  if (g.lane == 0) result[0] = good ? 1 : 0;
+}
+
 // ------------------------------------------------------------------------------ launchers
 hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uint32_t n, const uint32_t* d_H,
                                         const uint32_t* d_vk_lines, const uint8_t* d_vk_ok,
@@ -205,5 +286,12 @@ hipError_t cbft_bls_launch_verify(const uint8_t* d_msg, uint32_t len, uint32_t* 
                                   const uint32_t* d_gen_lines, uint8_t* d_result, hipStream_t s) {
   hipLaunchKernelGGL(bls_verify_kernel, dim3(1), dim3(PAIR_BLOCK), 0, s, d_msg, len, d_H, d_sig33, d_pk_lines,
                      pk_abc, d_pk_ok, d_gen_lines, d_result);
+  return hipGetLastError();
+}
+hipError_t cbft_bls_launch_verify_multisig(const uint32_t* d_parts, uint32_t count, const uint8_t* d_msg, uint32_t len,
+                                           const uint8_t* d_sig33, const uint32_t* d_gen_lines, uint8_t* d_pk_ok,
+                                           uint8_t* d_result, hipStream_t s) {
+  hipLaunchKernelGGL(bls_verify_multisig_kernel, dim3(1), dim3(MS_BLOCK), 0, s, d_parts, count, d_msg, len, d_sig33,
+                     d_gen_lines, d_pk_ok, d_result);
   return hipGetLastError();
 }

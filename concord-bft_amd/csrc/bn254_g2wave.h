@@ -198,9 +198,18 @@ __device__ __forceinline__ void g2w_add(uint32_t* ln, g2j& T, const fp2& qx, con
   T.X = X3;
 }
 
+// Streaming hand-over of lines to a consumer wave of the same block (progress in LDS): after
+// line k is stored, progress = k + 1 (release at workgroup scope).
+__device__ __forceinline__ void g2w_publish(volatile int* progress, int k, int lane) {
+  if (!progress) return;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (lane == 0) *progress = k;
+}
+
 // all BN_ATE_LINES (A, B, C) lines of affine q (not infinity), in Miller-loop order
-// (g2_precompute_lines_batch's step sequence); every lane of the wave calls it
-__device__ __noinline__ void g2w_lines_abc(uint32_t* out, const g2a& q) {
+// (g2_precompute_lines_batch's step sequence); every lane of the wave calls it.  progress
+// (nullable): published after every line (g2w_publish).
+__device__ __noinline__ void g2w_lines_abc(uint32_t* out, const g2a& q, volatile int* progress = nullptr) {
   const int lane = threadIdx.x & 63;
   g2j T;
   T.X = q.x;
@@ -210,7 +219,11 @@ __device__ __noinline__ void g2w_lines_abc(uint32_t* out, const g2a& q) {
 #pragma nounroll
   for (int i = BN_ATE_DBL - 1; i >= 0; i--) {
     g2w_dbl(out + (k++) * BN_ABC_WORDS, T, lane);
-    if (bn_ate_bit(i)) g2w_add(out + (k++) * BN_ABC_WORDS, T, q.x, q.y, lane);
+    g2w_publish(progress, k, lane);
+    if (bn_ate_bit(i)) {
+      g2w_add(out + (k++) * BN_ABC_WORDS, T, q.x, q.y, lane);
+      g2w_publish(progress, k, lane);
+    }
   }
   fp2_neg(T.Y, T.Y);  // 6u + 2 < 0
   fp2 q1x, q1y, q2x, q2y, c;
@@ -221,10 +234,12 @@ __device__ __noinline__ void g2w_lines_abc(uint32_t* out, const g2a& q) {
   fp2_load(c, Bn254Consts::TWY1);
   fp2_mul(q1y, q1y, c);
   g2w_add(out + (k++) * BN_ABC_WORDS, T, q1x, q1y, lane);
+  g2w_publish(progress, k, lane);
   fp2_load(c, Bn254Consts::TWX2);
   fp2_mul(q2x, q.x, c);
   fp2_load(c, Bn254Consts::TWY2);
   fp2_mul(q2y, q.y, c);
   fp2_neg(q2y, q2y);
   g2w_add(out + (k++) * BN_ABC_WORDS, T, q2x, q2y, lane);
+  g2w_publish(progress, k, lane);
 }

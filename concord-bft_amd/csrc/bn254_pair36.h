@@ -402,12 +402,19 @@ __device__ __forceinline__ void p36_final_exp(fp& r, const fp& f, const P36& g) 
 // ABC; P_j not infinity), conjugation and the two Frobenius lines included: the value final_exp takes.
 // Miller values of disjoint pair sets multiply (the loop squares and conjugates a product), so
 // two waves may run one pair each and multiply their f.  All 64 lanes of the wave call it.
+// progress (nullable, LDS): lines are still being produced by another wave of the block
+// (g2w_lines_abc); line k is read once progress > k.
 template <int NP, bool ABC = false>
-__device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* const* lines, const P36& g) {
+__device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* const* lines, const P36& g,
+                                           const volatile int* progress = nullptr) {
   constexpr int W = ABC ? 54 : BN_LINE_WORDS;  // ABC: unnormalised lines (bn254_g2wave.h)
   p36_one(f, g);
   int k = 0;
   auto line = [&](int j) {
+    if (progress) {
+      while (*progress <= k) __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
     if (ABC)
       p36_line_abc(f, lines[j] + k * W, P[j], g);
     else

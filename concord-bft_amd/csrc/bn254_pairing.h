@@ -388,6 +388,8 @@ BN_HDN void g2_add_j(g2j& r, const g2j& p, const g2j& q) {
   r.Z = Z3;
 }
 
+// VAR: variable-time inversion, for public points only (a multisig key sum)
+template <bool VAR = false>
 BN_HDN void g2_to_affine(g2a& r, const g2j& p) {
   if (fp2_is_zero(p.Z)) {
     r.inf = true;
@@ -396,7 +398,7 @@ BN_HDN void g2_to_affine(g2a& r, const g2j& p) {
     return;
   }
   fp2 zi, zi2;
-  fp2_inv(zi, p.Z);
+  fp2_inv<VAR>(zi, p.Z);
   fp2_sqr(zi2, zi);
   fp2_mul(r.x, p.X, zi2);
   fp2_mul(zi2, zi2, zi);

@@ -231,6 +231,22 @@ int cbft_bls_combine_finish(cbft_ctx* c, const uint8_t* partials, uint32_t count
   return CBFT_OK;
 }
 
+// multisig: the key-sum partials are on the device (c->bls_partial); one fused launch sums them,
+// streams the key's lines into the (H, PK) Miller loop and verifies
+static int bls_verify_multisig_parts(cbft_ctx* c, uint32_t len, const uint8_t* sig33, uint32_t count, int* out_ok) {
+  CBFT_HIP(c->bls_shares.reserve(33));
+  CBFT_HIP(c->bls_out.reserve(33));
+  CBFT_HIP(hipMemcpyAsync(c->bls_shares.p, sig33, 33, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_verify_multisig(c->bls_partial.as<uint32_t>(), count, c->bls_msg.as<uint8_t>(), len,
+                                           c->bls_shares.as<uint8_t>(), c->bls_gen_lines.as<uint32_t>(),
+                                           c->bls_ms_ok.as<uint8_t>(), c->bls_out.as<uint8_t>(), c->stream));
+  uint8_t r = 0;
+  CBFT_HIP(hipMemcpyAsync(&r, c->bls_out.p, 1, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
+  *out_ok = r ? 1 : 0;
+  return CBFT_OK;
+}
+
 // the message is on the device (bls_upload_msg): the verify kernel hashes it itself
 static int bls_verify_with_lines(cbft_ctx* c, uint32_t len, const uint8_t* sig33, const uint32_t* d_lines, int abc,
                                  const uint8_t* d_ok, int* out_ok) {
@@ -369,13 +385,12 @@ int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint3
   CBFT_HIP(c->bls_ms_ok.reserve(1));
   CBFT_HIP(c->bls_partial.reserve(CBFT_BLS_G2_PARTIAL_BYTES));
   CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
-  // PK = sum vk_i (one Jacobian partial), then its lines on one wave, then the 2-wave verify
+  // PK = sum vk_i (one Jacobian partial), then the fused 3-wave verify (lines streamed into the
+  // Miller loop)
   CBFT_HIP(cbft_bls_launch_g2_sum(ks->aff.as<uint32_t>() + BLS_G2A_WORDS, ks->ok.as<uint8_t>() + 1, ks->n,
                                   c->bls_bitmap.as<uint8_t>(), 1, ks->n + 1, c->bls_ms_ok.as<uint8_t>(), nullptr,
                                   c->bls_partial.as<uint32_t>(), c->stream));
-  CBFT_HIP(cbft_bls_launch_g2_lines(c->bls_partial.as<uint32_t>(), 1, c->bls_ms_lines.as<uint32_t>(),
-                                    c->bls_ms_ok.as<uint8_t>(), c->stream));
-  return bls_verify_with_lines(c, len, sig33, c->bls_ms_lines.as<uint32_t>(), 1, c->bls_ms_ok.as<uint8_t>(), out_ok);
+  return bls_verify_multisig_parts(c, len, sig33, 1, out_ok);
 }
 
 int cbft_bls_sum_keys(cbft_ctx* c, uint32_t id, const uint8_t* signers256, uint8_t* out65) {
@@ -431,9 +446,7 @@ int cbft_bls_verify_multisig_partials(cbft_ctx* c, const uint8_t* msg, uint32_t 
   CBFT_HIP(c->bls_ms_ok.reserve(1));
   CBFT_HIP(hipMemcpyAsync(c->bls_partial.p, key_partials, (size_t)count * CBFT_BLS_G2_PARTIAL_BYTES,
                           hipMemcpyHostToDevice, c->stream));
-  CBFT_HIP(cbft_bls_launch_g2_lines(c->bls_partial.as<uint32_t>(), count, c->bls_ms_lines.as<uint32_t>(),
-                                    c->bls_ms_ok.as<uint8_t>(), c->stream));
-  return bls_verify_with_lines(c, len, sig33, c->bls_ms_lines.as<uint32_t>(), 1, c->bls_ms_ok.as<uint8_t>(), out_ok);
+  return bls_verify_multisig_parts(c, len, sig33, count, out_ok);
 }
 
 // 32-byte big-endian scalar -> 8 little-endian words

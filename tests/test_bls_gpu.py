@@ -91,6 +91,10 @@ def test_multisig_combine_and_verify(ctx):
     try:
         assert ctx.bls_verify_multisig(kid, msg, comb, B.signers_bitmap(ids))
         assert not ctx.bls_verify_multisig(kid, msg, comb, B.signers_bitmap(ids[:-1]))
+        assert not ctx.bls_verify_multisig(kid, b"other digest", comb, B.signers_bitmap(ids))
+        # no signer: PK = infinity, the key wave releases the Miller-loop wave without lines
+        assert not ctx.bls_verify_multisig(kid, msg, comb, bytes(256))
+        assert ctx.bls_verify_multisig(kid, msg, comb, B.signers_bitmap(ids))  # context still sound
     finally:
         ctx.bls_unload_keys(kid)
 
