@@ -154,43 +154,69 @@ BN_HD void f_2q(uint32_t* s) {
   }
 }
 
-// r = a + b mod (2q range): a, b < 2q -> r < 2q
+// true in every lane of the wave when any lane's pred holds (device); pred itself on the host
+BN_HD bool bn_any(bool pred) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __any(pred);
+#else
+  return pred;
+#endif
+}
+
+// r += 2q where fix (the correction pass of f_add / f_sub, rarely taken)
 template <class F>
-BN_HD void f_add(Fe<F>& r, const Fe<F>& a, const Fe<F>& b) {
+BN_HD void f_add_2q_where(Fe<F>& r, bool fix) {
+  uint32_t q2[BN_LIMBS];
+  f_2q<F>(q2);
+  const uint32_t msk = fix ? BN_MASK : 0u;
   uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < BN_LIMBS; i++) {
-    uint32_t x = a.v[i] + b.v[i] + c;
+    const uint32_t x = r.v[i] + (q2[i] & msk) + c;
     r.v[i] = x & BN_MASK;
     c = x >> 29;
   }
-  uint32_t q2[BN_LIMBS];
-  f_2q<F>(q2);
-  f_csub(r, q2);
 }
 
-// r = a - b: a, b < 2q -> r < 2q
+// r = a + b reduced below 2q (a, b < 2q, normalised).  The reduction is decided from the top
+// limbs: with T = top limb of 2q, a + b lies in [t, t + 2) 2^232 for t = a8 + b8, so t + 2 <= T
+// means a + b < 2q (keep); otherwise 2q is subtracted in the same signed carry pass as the add
+// (~40 instructions against ~70 for add + trial subtraction).  Only for t in {T - 1, T} can
+// that go negative (probability ~2^-21 per random operand pair): the final carry says so and a
+// correction pass adds 2q back, executed by a wave only when one of its lanes needs it.  The
+// result is the same reduced value as the trial-subtraction form.
+template <class F>
+BN_HD void f_add(Fe<F>& r, const Fe<F>& a, const Fe<F>& b) {
+  uint32_t q2[BN_LIMBS];
+  f_2q<F>(q2);
+  const uint32_t t = a.v[BN_LIMBS - 1] + b.v[BN_LIMBS - 1];
+  const uint32_t msk = t + 2 > q2[BN_LIMBS - 1] ? BN_MASK : 0u;
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    const int32_t x = (int32_t)(a.v[i] + b.v[i]) - (int32_t)(q2[i] & msk) + c;
+    r.v[i] = (uint32_t)x & BN_MASK;
+    c = x >> 29;
+  }
+  if (bn_any(c < 0)) f_add_2q_where(r, c < 0);
+}
+
+// r = a - b reduced below 2q (a, b < 2q, normalised): a8 < b8 means a < b, so 2q is added in
+// the same signed pass; otherwise nothing is added, and when the top limbs were equal and
+// a < b after all, the final borrow triggers the correction pass.
 template <class F>
 BN_HD void f_sub(Fe<F>& r, const Fe<F>& a, const Fe<F>& b) {
   uint32_t q2[BN_LIMBS];
   f_2q<F>(q2);
-  int32_t br = 0;
-  uint32_t t[BN_LIMBS];
+  const uint32_t msk = a.v[BN_LIMBS - 1] < b.v[BN_LIMBS - 1] ? BN_MASK : 0u;
+  int32_t c = 0;
 #pragma unroll
   for (int i = 0; i < BN_LIMBS; i++) {
-    int32_t d = (int32_t)a.v[i] - (int32_t)b.v[i] + br;
-    t[i] = (uint32_t)d & BN_MASK;
-    br = d >> 29;
-  }
-  // if negative add 2q
-  const uint32_t msk = br ? BN_MASK : 0u;
-  uint32_t c = 0;
-#pragma unroll
-  for (int i = 0; i < BN_LIMBS; i++) {
-    uint32_t x = t[i] + (q2[i] & msk) + c;
-    r.v[i] = x & BN_MASK;
+    const int32_t x = (int32_t)a.v[i] - (int32_t)b.v[i] + (int32_t)(q2[i] & msk) + c;
+    r.v[i] = (uint32_t)x & BN_MASK;
     c = x >> 29;
   }
+  if (bn_any(c < 0)) f_add_2q_where(r, c < 0);
 }
 
 template <class F>
