@@ -47,6 +47,7 @@ METRIC = "Ed25519 verifies/sec at batch 64K on 1–8 MI355X; p50 latency @ batch
 # INT32 VALU peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz (CDNA4 SIMDs are 32-wide;
 # MI355X_MICROARCH.md; v_add_u32 measured at 0.88 of it, tools/microbench/intrate.hip)
 INT32_PEAK = 256 * 4 * 32 * 2.4e9
+MAD64_PEAK = INT32_PEAK / 2  # v_mad_u64_u32 issues at half the INT32 rate
 # Algorithmic INT32 ops per verify, SURVEY.md §8(d) model (8x32-bit limbs: M = 72, S = 44):
 OPS_DSM = 1020 * 44 + 1460 * 72            # double-scalar multiplication [S]B - [h]A = 150,000
 OPS_DECODE = 256 * 44 + 20 * 72            # A decode
@@ -268,15 +269,24 @@ def main():
                 slot_ops = (k["SQ_INSTS_VALU"] + k["SQ_INSTS_VALU_INT64"]) * 64
         except Exception:  # noqa: BLE001
             traffic = slot_ops = None
-    achieved = OPS_DSM * n / (ladder_ms * 1e-3)  # SURVEY.md §8(d) algorithmic ops / launch duration
+    # Algorithmic work of the comb ladder: one mixed addition per comb position (radix-2^w_A key
+    # table + radix-2^w_B B table), 7 field multiplications each, 81 + 9 v_mad_u64_u32 per
+    # multiplication (9 x 29-bit limbs, fe25519.h); the pair / quad combines are parallelisation
+    # overhead and not counted.  Bound: the MAD64 pipe (half the INT32 issue rate).
+    npos = {8: 32, 9: 29, 10: 26, 11: 23, 12: 22, 13: 20}[args.comb_radix] + \
+        {16: 16, 17: 15, 18: 15, 19: 14, 20: 13, 21: 13, 22: 12}[b_radix]
+    mads_per_unit = npos * 7 * 90
+    achieved = mads_per_unit * n / (ladder_ms * 1e-3)
     h2d_bytes = 4 + 64 + L  # key index + R||S + message, per signature (fixed-length batch)
-    roofline = {"bound": "valu_int32", "achieved": achieved / 1e12, "peak": INT32_PEAK / 1e12, "unit": "TOP/s",
-                "frac": achieved / INT32_PEAK, "traffic": traffic,
+    roofline = {"bound": "valu_mad64", "achieved": achieved / 1e12, "peak": MAD64_PEAK / 1e12, "unit": "T MAD64/s",
+                "frac": achieved / MAD64_PEAK, "traffic": traffic,
                 "kernel": kname, "kernel_ms": ladder_ms, "units_per_launch": n,
-                "ops_per_unit": OPS_DSM,
-                "achieved_basis": "SURVEY.md 8(d) ops of the double-scalar mult (ref10 model: 1020 S + 1460 M, "
-                                  "M = 72, S = 44 INT32 ops) x units / ladder launch duration; the comb executes "
-                                  "fewer field ops than that model (work-equivalent rate)",
+                "ops_per_unit": mads_per_unit,
+                "achieved_basis": f"{npos} comb additions x 7 field multiplications x 90 v_mad_u64_u32 (81 products "
+                                  f"+ 9 folds) per verify x units / ladder launch duration",
+                "work_equiv_frac": OPS_DSM * n / (ladder_ms * 1e-3) / INT32_PEAK,
+                "work_equiv_basis": "SURVEY.md 8(d) ref10 model (1020 S + 1460 M, M = 72, S = 44 INT32 ops = 150,000 "
+                                    "per verify) / INT32 peak: over-credits the comb, which does no doublings",
                 "kernel_ms_basis": f"mean of {pipe_batches} launches inside the timed host pipeline (HIP events "
                                    f"on the launch streams)",
                 "issue_frac": (slot_ops / (ladder_ms * 1e-3) / INT32_PEAK) if slot_ops else None,
@@ -398,10 +408,9 @@ def bench_mixed(ctx, args, cpu_threads):
             "msg_bytes_total": int(ss.len.sum())}
 
 
-# RSA: v_mad_u64_u32 issues at half the INT32 rate (MI355X_MICROARCH.md): 256 CU x 4 SIMD x 16
-# lanes x 2.4 GHz = 3.93e13 MAC/s; measured 3.28e13 on the microbench (tools/microbench/intrate.hip,
-# profiles/r01_intrate_microbench.txt), reported beside it
-MAD64_PEAK = INT32_PEAK / 2
+# MAD64_PEAK (top): v_mad_u64_u32 issues at half the INT32 rate (MI355X_MICROARCH.md): 256 CU x 4
+# SIMD x 16 lanes x 2.4 GHz = 3.93e13 MAC/s; measured 3.28e13 on the microbench
+# (tools/microbench/intrate.hip, profiles/r01_intrate_microbench.txt), reported beside it
 MAD64_MEASURED = 3.277e13
 
 

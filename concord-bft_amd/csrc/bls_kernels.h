@@ -36,19 +36,14 @@ hipError_t cbft_bls_launch_g1_parts(const uint32_t* d_parts, uint32_t count, uin
 hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok, uint32_t n, const uint8_t* d_bitmap,
                                   uint32_t lo_id, uint32_t hi_id, uint8_t* d_ok, uint8_t* d_out65, uint32_t* d_out_part,
                                   hipStream_t s);
-// sum of count partials -> unnormalised (A, B, C) Miller lines (cbft_bls_abc_lines_words() words)
-size_t cbft_bls_abc_lines_words();
-hipError_t cbft_bls_launch_g2_lines(const uint32_t* d_parts, uint32_t count, uint32_t* d_lines, uint8_t* d_ok,
-                                    hipStream_t s);
 // H = g1_map(msg) (-> d_H when non-null) and e(H, PK) e(-sigma, g2) == 1 in one launch
 // multisig verify in one launch: PK = sum of count key-sum partials, its lines streamed from one
 // wave to the Miller loop of another, sigma's pair on a third (d_pk_ok = PK usable)
 hipError_t cbft_bls_launch_verify_multisig(const uint32_t* d_parts, uint32_t count, const uint8_t* d_msg, uint32_t len,
                                            const uint8_t* d_sig33, const uint32_t* d_gen_lines, uint8_t* d_pk_ok,
                                            uint8_t* d_result, hipStream_t s);
-// pk_abc: d_pk_lines are unnormalised (A, B, C) lines (cbft_bls_launch_g2_lines)
 hipError_t cbft_bls_launch_verify(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, const uint8_t* d_sig33,
-                                  const uint32_t* d_pk_lines, int pk_abc, const uint8_t* d_pk_ok,
+                                  const uint32_t* d_pk_lines, const uint8_t* d_pk_ok,
                                   const uint32_t* d_gen_lines, uint8_t* d_result, hipStream_t s);
 hipError_t cbft_bls_launch_sign(const uint8_t* d_msg, uint32_t len, const uint32_t* d_sk, uint32_t id,
                                 uint8_t* d_out37, hipStream_t s);

@@ -5,11 +5,8 @@
 //                            (BlsThresholdVerifier ctor; lines make per-share work G2-free)
 //   bls_g2_sum_kernel        multisig PK = sum vk_i over the signer bitmap (Jacobian partial, or
 //                            compressed for cbft_bls_sum_keys)
-//   bls_g2_lines_kernel      sum of partials -> affine PK -> its unnormalised Miller lines, the
-//                            products of each line step spread over one wave (bn254_g2wave.h)
 //   bls_pubkey_kernel        vk = sk * g2
 #include "bls_common.h"
-#include "bn254_g2wave.h"
 
 #define LINE_SCRATCH_WORDS (BN_ATE_LINES * 36)  // g2_precompute_lines_batch scratch per key
 
@@ -55,7 +52,7 @@ __device__ void g2_sum_tail(const g2j& acc, bool bad, uint8_t* ok, uint8_t* out6
 }
 
 // Signer ids [lo_id, hi_id) only (a rank's slice of a sharded multisig key sum).  With out_part
-// the block writes its Jacobian sum (54 words) + the bad-key flag (1 word) (-> bls_g2_lines_kernel),
+// the block writes its Jacobian sum (54 words) + the bad-key flag (1 word) (-> bls_verify_multisig_kernel),
 // else the compressed sum into out65.
 __global__ void __launch_bounds__(SUM_THREADS) bls_g2_sum_kernel(const uint32_t* aff, const uint8_t* key_ok,
                                                                  uint32_t n, const uint8_t* bitmap, uint32_t lo_id,
@@ -106,30 +103,6 @@ __global__ void __launch_bounds__(SUM_THREADS) bls_g2_sum_kernel(const uint32_t*
   g2_sum_tail(acc, bad != 0, ok, out65);
 }
 
-// PK = sum of count G2 partials (55 words each, bls_g2_sum_kernel's out_part), then its
-// BN_ATE_LINES unnormalised (A, B, C) lines (BN_ABC_WORDS each) computed by the whole wave.
-// ok = 0 when a selected key did not decode or PK is infinity.
-__global__ void __launch_bounds__(64) bls_g2_lines_kernel(const uint32_t* parts, uint32_t count, uint32_t* lines,
-                                                          uint8_t* ok) {
-  if (blockIdx.x != 0) return;
-  g2j acc;
-  fp2_one(acc.X);
-  fp2_one(acc.Y);
-  fp2_zero(acc.Z);
-  bool bad = false;
-  for (uint32_t b = 0; b < count; b++) {
-    g2j o;
-    g2j_load(o, parts + 55 * (size_t)b);
-    bad |= parts[55 * (size_t)b + 54] != 0;
-    g2_add_j(acc, acc, o);
-  }
-  g2a s;
-  g2_to_affine(s, acc);
-  const bool usable = !bad && !s.inf;
-  if (threadIdx.x == 0) ok[0] = usable ? 1 : 0;
-  if (usable) g2w_lines_abc(lines, s);
-}
-
 // vk = sk * g2 as 65 compressed bytes: the signer's public key (BlsThresholdSigner's
 // publicKey_(secretKey) -> g2_mul_gen, BlsThresholdSigner.cpp:25; IThresholdSigner::
 // getShareVerificationKey).  sk: 8 LE words (< r).  One lane, double-and-add (a one-off per key).
@@ -170,12 +143,6 @@ hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok
                                   hipStream_t s) {
   hipLaunchKernelGGL(bls_g2_sum_kernel, dim3(1), dim3(SUM_THREADS), 0, s, d_aff, d_key_ok, n, d_bitmap, lo_id, hi_id,
                      d_ok, d_out65, d_out_part);
-  return hipGetLastError();
-}
-size_t cbft_bls_abc_lines_words() { return (size_t)BN_ATE_LINES * BN_ABC_WORDS; }
-hipError_t cbft_bls_launch_g2_lines(const uint32_t* d_parts, uint32_t count, uint32_t* d_lines, uint8_t* d_ok,
-                                    hipStream_t s) {
-  hipLaunchKernelGGL(bls_g2_lines_kernel, dim3(1), dim3(64), 0, s, d_parts, count, d_lines, d_ok);
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_pubkey(const uint32_t* d_sk, uint8_t* d_out65, hipStream_t s) {

@@ -121,14 +121,13 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
 
 // H = g1_map(msg) on wave 0 (also stored to H_out when non-null), sigma from 33 bytes on wave 1:
 // e(H, PK) * e(-sigma, g2) == 1 for a combined signature.  One block of two waves.
-// pk_abc: the key's lines are unnormalised (a fresh multisig key, bn254_g2wave.h).
 // CBFT_BLS_PHASES (probe builds only): phase timestamps (bn254_pair36.h: BLS_STAMP), printed
 // by lane 0 of wave 0 at the end in 10 ns wall-clock ticks.
 #define BLS_PHASE(slot) BLS_STAMP(slot)
 
 __global__ void __launch_bounds__(PAIR_BLOCK) bls_verify_kernel(const uint8_t* msg, uint32_t len, uint32_t* H_out,
                                                                 const uint8_t* sig33, const uint32_t* pk_lines,
-                                                                int pk_abc, const uint8_t* pk_ok,
+                                                                const uint8_t* pk_ok,
                                                                 const uint32_t* gen_lines, uint8_t* result) {
   __shared__ PairXchg xc;
   if (blockIdx.x != 0) return;
@@ -157,10 +156,7 @@ __global__ void __launch_bounds__(PAIR_BLOCK) bls_verify_kernel(const uint8_t* m
     BLS_PHASE(4);
     if (g.lane == 0 && H_out) g1a_store(H_out, P);
     const uint32_t* l[1] = {pk_lines};
-    if (pk_abc)
-      p36_miller<1, true>(f, &P, l, g);
-    else
-      p36_miller<1>(f, &P, l, g);
+    p36_miller<1>(f, &P, l, g);
     BLS_PHASE(5);
   }
   __syncthreads();
@@ -282,10 +278,10 @@ hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uin
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_verify(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, const uint8_t* d_sig33,
-                                  const uint32_t* d_pk_lines, int pk_abc, const uint8_t* d_pk_ok,
+                                  const uint32_t* d_pk_lines, const uint8_t* d_pk_ok,
                                   const uint32_t* d_gen_lines, uint8_t* d_result, hipStream_t s) {
   hipLaunchKernelGGL(bls_verify_kernel, dim3(1), dim3(PAIR_BLOCK), 0, s, d_msg, len, d_H, d_sig33, d_pk_lines,
-                     pk_abc, d_pk_ok, d_gen_lines, d_result);
+                     d_pk_ok, d_gen_lines, d_result);
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_verify_multisig(const uint32_t* d_parts, uint32_t count, const uint8_t* d_msg, uint32_t len,

@@ -248,13 +248,13 @@ static int bls_verify_multisig_parts(cbft_ctx* c, uint32_t len, const uint8_t* s
 }
 
 // the message is on the device (bls_upload_msg): the verify kernel hashes it itself
-static int bls_verify_with_lines(cbft_ctx* c, uint32_t len, const uint8_t* sig33, const uint32_t* d_lines, int abc,
+static int bls_verify_with_lines(cbft_ctx* c, uint32_t len, const uint8_t* sig33, const uint32_t* d_lines,
                                  const uint8_t* d_ok, int* out_ok) {
   CBFT_HIP(c->bls_shares.reserve(33));
   CBFT_HIP(c->bls_out.reserve(33));
   CBFT_HIP(hipMemcpyAsync(c->bls_shares.p, sig33, 33, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(cbft_bls_launch_verify(c->bls_msg.as<uint8_t>(), len, c->bls_H.as<uint32_t>(), c->bls_shares.as<uint8_t>(),
-                                  d_lines, abc, d_ok, c->bls_gen_lines.as<uint32_t>(), c->bls_out.as<uint8_t>(),
+                                  d_lines, d_ok, c->bls_gen_lines.as<uint32_t>(), c->bls_out.as<uint8_t>(),
                                   c->stream));
   uint8_t r = 0;
   CBFT_HIP(hipMemcpyAsync(&r, c->bls_out.p, 1, hipMemcpyDeviceToHost, c->stream));
@@ -273,7 +273,7 @@ int cbft_bls_verify(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, 
   int rc = bls_gen_lines(c);
   if (!rc) rc = bls_upload_msg(c, msg, len);
   if (rc) return rc;
-  return bls_verify_with_lines(c, len, sig33, ks->lines.as<uint32_t>(), 0, ks->ok.as<uint8_t>(), out_ok);
+  return bls_verify_with_lines(c, len, sig33, ks->lines.as<uint32_t>(), ks->ok.as<uint8_t>(), out_ok);
 }
 
 // The SignaturesProcessingJob policy (CollectorOfThresholdSignatures.hpp:363-406) as one call,
@@ -326,7 +326,7 @@ int cbft_bls_combine_threshold(cbft_ctx* c, uint32_t id, const uint8_t* msg, uin
                                      c->bls_partial.as<uint32_t>(), c->bls_out.as<uint8_t>(), nullptr, nullptr,
                                      c->stream));
     CBFT_HIP(cbft_bls_launch_verify(c->bls_msg.as<uint8_t>(), len, nullptr, c->bls_out.as<uint8_t>(),
-                                    ks->lines.as<uint32_t>(), 0, ks->ok.as<uint8_t>(),
+                                    ks->lines.as<uint32_t>(), ks->ok.as<uint8_t>(),
                                     c->bls_gen_lines.as<uint32_t>(), c->bls_flag.as<uint8_t>(), c->stream));
     return CBFT_OK;
   };
@@ -381,7 +381,6 @@ int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint3
   if (!rc) rc = bls_upload_msg(c, msg, len);
   if (rc) return rc;
   CBFT_HIP(c->bls_bitmap.reserve(256));
-  CBFT_HIP(c->bls_ms_lines.reserve(cbft_bls_abc_lines_words() * 4));
   CBFT_HIP(c->bls_ms_ok.reserve(1));
   CBFT_HIP(c->bls_partial.reserve(CBFT_BLS_G2_PARTIAL_BYTES));
   CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
@@ -442,7 +441,6 @@ int cbft_bls_verify_multisig_partials(cbft_ctx* c, const uint8_t* msg, uint32_t 
   if (!rc) rc = bls_upload_msg(c, msg, len);
   if (rc) return rc;
   CBFT_HIP(c->bls_partial.reserve((size_t)count * CBFT_BLS_G2_PARTIAL_BYTES));
-  CBFT_HIP(c->bls_ms_lines.reserve(cbft_bls_abc_lines_words() * 4));
   CBFT_HIP(c->bls_ms_ok.reserve(1));
   CBFT_HIP(hipMemcpyAsync(c->bls_partial.p, key_partials, (size_t)count * CBFT_BLS_G2_PARTIAL_BYTES,
                           hipMemcpyHostToDevice, c->stream));

@@ -266,7 +266,7 @@ void cbft_close(cbft_ctx* c) {
     kv.second.aff.release();
   }
   for (DevBuf* b : {&c->bls_gen_lines, &c->bls_msg, &c->bls_H, &c->bls_shares, &c->bls_valid, &c->bls_sig,
-                    &c->bls_ids, &c->bls_use, &c->bls_lambda, &c->bls_partial, &c->bls_out, &c->bls_ms_lines,
+                    &c->bls_ids, &c->bls_use, &c->bls_lambda, &c->bls_partial, &c->bls_out,
                     &c->bls_ms_ok, &c->bls_bitmap, &c->bls_inv})
     b->release();
   (void)hipDeviceSynchronize();  // device-path batches may still run on caller streams
