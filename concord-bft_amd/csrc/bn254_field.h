@@ -10,6 +10,7 @@
 // Output of mont_mul for inputs < 2q is < 2q (R = 2^261 > 4q).
 #pragma once
 #include <stdint.h>
+#include "safegcd30.h"
 
 #if defined(__HIPCC__)
 #include <hip/hip_runtime.h>
@@ -342,14 +343,7 @@ BN_HDN bool fp_sqrt(fp& y, const fp& a) {
 BN_HDN void fp_inv(fp& r, const fp& a) { f_inv_fp(r, a); }
 
 // ---- variable-time inversion in Fp, for PUBLIC values only (the final exponentiation of a
-// pairing check: signatures, message hashes, public keys).  Bernstein-Yang "safegcd" divsteps,
-// the variable-time form (eta = -delta, up to 8 bits of g cancelled per step with -f^-1 mod 2^8),
-// in batches of 30 on signed radix-2^30 limbs, as published for libsecp256k1's modinv32_var.
-// About 13 batches of ~450 instructions for a 254-bit p against Fermat's 254 squarings + 128
-// multiplications; one lane, so a wave whose lanes hold the same value never diverges.
-struct BnS30 {
-  int32_t v[9];
-};
+// pairing check: signatures, message hashes, public keys): safegcd30.h.
 struct BnS30Mod {  // p in signed-30 limbs, p^-1 mod 2^30, R^3 mod p (R = 2^261) in 29-bit limbs
   static constexpr int32_t P[9] = {0x00000013, 0x1c000000, 0x0000013a, 0x08400000, 0x00000861,
                                    0x11360000, 0x00001ba3, 0x19209000, 0x00002523};
@@ -357,145 +351,16 @@ struct BnS30Mod {  // p in signed-30 limbs, p^-1 mod 2^30, R^3 mod p (R = 2^261)
   static constexpr uint32_t R3[9] = {0x1b6b46eeu, 0x090454c7u, 0x1074d76du, 0x0c39e3dcu, 0x0cbd1a82u,
                                      0x1c75654du, 0x0a20d59bu, 0x174dc09au, 0x0008606fu};
 };
-#define BN_M30 0x3fffffff
-
-// 30 divsteps on the low words of f (odd) and g: eta' and the transition matrix t = (u, v, q, r)
-// with (f', g') = (u f + v g, q f + r g) / 2^30.
-BN_HD int32_t bn_divsteps30_var(int32_t eta, uint32_t f, uint32_t g, int32_t* t) {
-  uint32_t u = 1, v = 0, q = 0, r = 1;
-  int i = 30;
-  for (;;) {
-    const int zeros = __builtin_ctz(g | (0xffffffffu << i));  // sentinel: at most i zeros
-    g >>= zeros;
-    u <<= zeros;
-    v <<= zeros;
-    eta -= zeros;
-    i -= zeros;
-    if (i == 0) break;
-    if (eta < 0) {  // (f, g) <- (g, -f) and the matrix rows with them
-      uint32_t x;
-      eta = -eta;
-      x = f; f = g; g = 0u - x;
-      x = u; u = q; q = 0u - x;
-      x = v; v = r; r = 0u - x;
-    }
-    const int limit = (eta + 1) > i ? i : (eta + 1);
-    const uint32_t m = (0xffffffffu >> (32 - limit)) & 255u;
-    uint32_t fi = f;  // f^-1 mod 2^12 by two Newton steps (f odd: f f == 1 mod 8)
-    fi *= 2u - f * fi;
-    fi *= 2u - f * fi;
-    const uint32_t w = (g * (0u - fi)) & m;  // cancels the low min(limit, 8) bits of g
-    g += f * w;
-    q += u * w;
-    r += v * w;
-  }
-  t[0] = (int32_t)u;
-  t[1] = (int32_t)v;
-  t[2] = (int32_t)q;
-  t[3] = (int32_t)r;
-  return eta;
-}
-
-// (d, e) <- (t [d, e] + p [md, me]) / 2^30 with md, me chosen to clear the low 30 bits
-BN_HD void bn_update_de30(BnS30& d, BnS30& e, const int32_t* t) {
-  const int32_t u = t[0], v = t[1], q = t[2], r = t[3];
-  const int32_t sd = d.v[8] >> 31, se = e.v[8] >> 31;
-  int32_t md = (u & sd) + (v & se), me = (q & sd) + (r & se);
-  int64_t cd = (int64_t)u * d.v[0] + (int64_t)v * e.v[0];
-  int64_t ce = (int64_t)q * d.v[0] + (int64_t)r * e.v[0];
-  md -= (int32_t)((BnS30Mod::PINV30 * (uint32_t)cd + (uint32_t)md) & BN_M30);
-  me -= (int32_t)((BnS30Mod::PINV30 * (uint32_t)ce + (uint32_t)me) & BN_M30);
-  cd += (int64_t)BnS30Mod::P[0] * md;
-  ce += (int64_t)BnS30Mod::P[0] * me;
-  cd >>= 30;
-  ce >>= 30;
-#pragma unroll
-  for (int i = 1; i < 9; i++) {
-    cd += (int64_t)u * d.v[i] + (int64_t)v * e.v[i] + (int64_t)BnS30Mod::P[i] * md;
-    ce += (int64_t)q * d.v[i] + (int64_t)r * e.v[i] + (int64_t)BnS30Mod::P[i] * me;
-    d.v[i - 1] = (int32_t)cd & BN_M30;
-    cd >>= 30;
-    e.v[i - 1] = (int32_t)ce & BN_M30;
-    ce >>= 30;
-  }
-  d.v[8] = (int32_t)cd;
-  e.v[8] = (int32_t)ce;
-}
-
-// (f, g) <- t [f, g] / 2^30
-BN_HD void bn_update_fg30(BnS30& f, BnS30& g, const int32_t* t) {
-  const int32_t u = t[0], v = t[1], q = t[2], r = t[3];
-  int64_t cf = (int64_t)u * f.v[0] + (int64_t)v * g.v[0];
-  int64_t cg = (int64_t)q * f.v[0] + (int64_t)r * g.v[0];
-  cf >>= 30;
-  cg >>= 30;
-#pragma unroll
-  for (int i = 1; i < 9; i++) {
-    cf += (int64_t)u * f.v[i] + (int64_t)v * g.v[i];
-    cg += (int64_t)q * f.v[i] + (int64_t)r * g.v[i];
-    f.v[i - 1] = (int32_t)cf & BN_M30;
-    cf >>= 30;
-    g.v[i - 1] = (int32_t)cg & BN_M30;
-    cg >>= 30;
-  }
-  f.v[8] = (int32_t)cf;
-  g.v[8] = (int32_t)cg;
-}
-
-// d in (-2p, p) -> (sign < 0 ? -d : d) mod p in [0, p)
-BN_HD void bn_normalize30(BnS30& d, int32_t sign) {
-  const int32_t neg = sign >> 31;
-  int32_t add = d.v[8] >> 31;
-#pragma unroll
-  for (int i = 0; i < 9; i++) d.v[i] = ((d.v[i] + (BnS30Mod::P[i] & add)) ^ neg) - neg;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    d.v[i + 1] += d.v[i] >> 30;
-    d.v[i] &= BN_M30;
-  }
-  add = d.v[8] >> 31;
-#pragma unroll
-  for (int i = 0; i < 9; i++) d.v[i] += BnS30Mod::P[i] & add;
-#pragma unroll
-  for (int i = 0; i < 8; i++) {
-    d.v[i + 1] += d.v[i] >> 30;
-    d.v[i] &= BN_M30;
-  }
-}
 
 // r = a^-1 (Montgomery form in and out; a^-1 of 0 is 0, as Fermat's).  VARIABLE TIME.
 BN_HDN void fp_inv_var(fp& r, const fp& a) {
   fp c = a;
   f_canon(c);  // [0, q): the integer A = a R mod q
-  BnS30 f, g, d, e;
-#pragma unroll
-  for (int j = 0; j < 9; j++) {  // 29-bit limbs -> 30-bit limbs
-    const int b = 30 * j, i = b / 29, s = b % 29;
-    const uint64_t w = ((uint64_t)(i + 1 < 9 ? c.v[i + 1] : 0u) << 29) | c.v[i];
-    g.v[j] = (int32_t)((w >> s) & BN_M30);
-    f.v[j] = BnS30Mod::P[j];
-    d.v[j] = 0;
-    e.v[j] = j == 0 ? 1 : 0;
-  }
-  int32_t eta = -1;
-  for (int it = 0; it < 64; it++) {  // g = 0 after <= 25 batches for 254 bits (bound 741 divsteps)
-    int32_t t[4];
-    eta = bn_divsteps30_var(eta, (uint32_t)f.v[0], (uint32_t)g.v[0], t);
-    bn_update_de30(d, e, t);
-    bn_update_fg30(f, g, t);
-    int32_t any = 0;
-#pragma unroll
-    for (int j = 0; j < 9; j++) any |= g.v[j];
-    if (any == 0) break;
-  }
-  bn_normalize30(d, f.v[8]);  // f = +-1: d = +-A^-1
+  Sg30 x;
+  sg_from_limbs29(x, c.v);
+  sg_inv30_var<BnS30Mod>(x);  // A^-1 mod q
   fp y;
-#pragma unroll
-  for (int i = 0; i < 9; i++) {  // 30-bit limbs -> 29-bit limbs (value < q)
-    const int b = 29 * i, j = b / 30, s = b % 30;
-    const uint64_t w = ((uint64_t)(uint32_t)(j + 1 < 9 ? d.v[j + 1] : 0) << 30) | (uint32_t)d.v[j];
-    y.v[i] = (uint32_t)(w >> s) & BN_MASK;
-  }
+  sg_to_limbs29(y.v, x);
   fp r3;
 #pragma unroll
   for (int i = 0; i < 9; i++) r3.v[i] = BnS30Mod::R3[i];

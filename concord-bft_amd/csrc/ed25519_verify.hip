@@ -356,7 +356,14 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_finish_kernel(const
     fe_load_soa(Y, xyz_soa + 9 * b.n, b.n, i);
     fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
     uint32_t Rp[8], Rw[8];
-    ge_tobytes<false>(Rp, X, Y, Z);
+    {  // encode R' (public: variable-time inversion)
+      fe zi, x, y;
+      fe_invert_var(zi, Z);
+      fe_mul<false>(x, X, zi);
+      fe_mul<false>(y, Y, zi);
+      fe_to_words(Rp, y);
+      Rp[7] ^= fe_isnegative(x) << 31;
+    }
     load_words8(Rw, b.sig + i * 64);
     uint32_t diff = 0;
 #pragma unroll
@@ -405,7 +412,7 @@ __global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519B
     for (int k = 0; k < FE_LIMBS; k++) pre[j][k][ln] = acc.v[k];
   }
   fe inv;
-  fe_invert<false>(inv, acc);
+  fe_invert_var(inv, acc);
 #pragma nounroll
   for (int j = K - 1; j >= 0; j--) {
     const size_t i = base + (size_t)j * 64 + ln;

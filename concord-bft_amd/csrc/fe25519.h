@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "safegcd30.h"
+
 #define FE_LIMBS 9
 #define FE_MASK 0x1fffffffu
 
@@ -323,6 +325,35 @@ FE_INLINE void fe_invert(fe& r, const fe& z) {
   fe_pow_2_250_1<C>(z250, z11, z);
   fe_sqn<C>(z250, z250, 5);    // 2^255 - 32
   fe_mul<C>(r, z250, z11);     // 2^255 - 21
+}
+
+// r = z^-1 for PUBLIC z (verification: R' of a signature, keys): safegcd30.h, variable time;
+// 0 -> 0 like fe_invert.  One lane per inversion; ~6x fewer instructions than the Fermat chain,
+// which is what the finish kernels' lone waves (batch-shared inversions, small batches) wait on.
+struct Fe25519S30 {
+  static constexpr int32_t P[9] = {0x3fffffed, 0x3fffffff, 0x3fffffff, 0x3fffffff, 0x3fffffff,
+                                   0x3fffffff, 0x3fffffff, 0x3fffffff, 0x00007fff};
+  static constexpr uint32_t PINV30 = 0x179435e5u;
+};
+FE_INLINE void fe_invert_var(fe& r, const fe& z) {
+  uint32_t w[8];
+  fe_to_words(w, z);  // canonical, [0, p)
+  Sg30 x;
+#pragma unroll
+  for (int j = 0; j < 9; j++) {  // 8 x 32-bit words -> 9 x 30-bit limbs
+    const int b = 30 * j, i = b >> 5, sh = b & 31;
+    const uint64_t v = ((uint64_t)(i + 1 < 8 ? w[i + 1] : 0u) << 32) | (i < 8 ? w[i] : 0u);
+    x.v[j] = (int32_t)((v >> sh) & SG_M30);
+  }
+  sg_inv30_var<Fe25519S30>(x);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {  // back to words
+    const int b = 32 * i, j = b / 30, sh = b % 30;
+    const uint64_t v = ((uint64_t)(uint32_t)(j + 2 < 9 ? x.v[j + 2] : 0) << 60) |
+                       ((uint64_t)(uint32_t)(j + 1 < 9 ? x.v[j + 1] : 0) << 30) | (uint32_t)x.v[j];
+    w[i] = (uint32_t)(v >> sh);
+  }
+  fe_from_words(r, w);
 }
 
 // r = z^((p-5)/8) = z^(2^252 - 3)
