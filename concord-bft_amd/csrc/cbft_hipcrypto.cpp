@@ -531,7 +531,9 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   // small (latency-bound) batch inverts per signature.  K = 16 at the 64K headline: the finish is
   // then 64 waves that run beside the next batch's hash/ladder (stage order), 5 % of the VALU work
   // of a per-signature inversion (A/B on MI355X: K = 8 327, K = 16 360, K = 32 273 M verifies/s)
-  w.finish_batch = c->finish_batch ? c->finish_batch : (n >= 65536 ? 16 : n >= 32768 ? 8 : 1);
+  // one shared (variable-time) inversion per 2 signatures per lane from 16K: the inversion is now
+  // cheap, so more waves beat more sharing (64K: K = 2 55 us, 4 60, 8 74, 16 103, 32 162 us)
+  w.finish_batch = c->finish_batch ? c->finish_batch : (n >= 16384 ? 2 : 1);
   w.base_table = c->base_table.as<uint32_t>();
   w.h_soa = slot.h.as<uint32_t>();
   w.flags = slot.flags.as<uint8_t>();
