@@ -311,3 +311,21 @@ def test_per_batch_profiling_ring(golden):
             c.stage_times_avg_ms()
         lib = cb.load_library()
         assert lib.cbft_set_profiling(c.handle, 3) == -22
+
+
+@pytest.mark.parametrize("lanes", ["2", "4"])
+def test_ladder_layouts_both_sizes(golden, monkeypatch, lanes):
+    """Each comb-ladder layout ($CBFT_LADDER_LANES) at the sizes the default does not pick it for:
+    the pair ladder on the small golden batch, the quad ladder on a 64K batch."""
+    monkeypatch.setenv("CBFT_LADDER_LANES", lanes)
+    keys = sorted({v.pk for v in golden})
+    index = {k: i for i, k in enumerate(keys)}
+    with cb.Context(device=0, max_batch=1 << 16) as c:
+        tid = c.load_keys(keys)
+        got = _bools(c.verify(tid, [index[v.pk] for v in golden], [v.sig for v in golden],
+                              [v.msg for v in golden]), len(golden))
+        assert np.array_equal(got, np.array([bool(v.verdict) for v in golden]))
+        ss = sigsets.make_sigset(1 << 16, nkeys=64, msg_len=256, seed=77, threads=16, invalid_frac=0.05)
+        tid2 = c.load_keys(ss.pk)
+        got = _bools(c.verify_packed(tid2, ss.key_idx, ss.sig, ss.blob, ss.off, ss.len), 1 << 16)
+        assert np.array_equal(got, ss.expected)
