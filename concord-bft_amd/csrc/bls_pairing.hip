@@ -12,6 +12,8 @@
 // wave per SIMD, issue-bound), so splitting the pairs takes one Miller loop's line evaluations
 // off the critical path, and with them the sqrt of sigma's decompression (and, in
 // bls_verify_kernel, the hash to G1, which wave 0 computes while wave 1 decodes sigma).
+#include <cstdlib>
+
 #include "bls_common.h"
 #include "bn254_g2wave.h"
 #include "bn254_pair36.h"
@@ -269,7 +271,12 @@ hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uin
                                         const uint32_t* d_gen_lines, int do_verify, uint8_t* d_valid,
                                         uint32_t* d_sig, uint32_t* d_ids, hipStream_t s) {
   if (!k) return hipSuccess;
-  if (do_verify && 2 * (size_t)k <= SIMDS)
+  static const int forced = [] {  // $CBFT_BLS_SHARE_WAVES: 1 or 2 forces the form (A/B), else by k
+    const char* e = getenv("CBFT_BLS_SHARE_WAVES");
+    return e ? atoi(e) : 0;
+  }();
+  const bool two = forced ? forced == 2 : 2 * (size_t)k <= SIMDS;
+  if (do_verify && two)
     hipLaunchKernelGGL(bls_share_verify_kernel<2>, dim3(k), dim3(128), 0, s, d_shares, k, n, d_H, d_vk_lines,
                        d_vk_ok, d_gen_lines, do_verify, d_valid, d_sig, d_ids);
   else

@@ -329,3 +329,17 @@ def test_ladder_layouts_both_sizes(golden, monkeypatch, lanes):
         tid2 = c.load_keys(ss.pk)
         got = _bools(c.verify_packed(tid2, ss.key_idx, ss.sig, ss.blob, ss.off, ss.len), 1 << 16)
         assert np.array_equal(got, ss.expected)
+
+
+def test_config3_full_shape(ctx):
+    """BASELINE config #3 at full size: 65,536 signatures from 4,096 clients, message lengths
+    log-uniform in 64..4,096 B (variable-length SHA-512: 2..33 blocks), 10 % adversarially invalid;
+    verdicts equal host OpenSSL's on every signature."""
+    ss = sigsets.make_sigset(65536, nkeys=4096, msg_len=(64, 4096), seed=3, invalid_frac=0.10, threads=16)
+    tid = ctx.load_keys(ss.pk)
+    try:
+        got = _bools(ctx.verify_packed(tid, ss.key_idx, ss.sig, ss.blob, ss.off, ss.len), ss.n)
+    finally:
+        ctx.unload_keys(tid)
+    assert np.array_equal(got, ss.expected)
+    assert 0.05 < (~ss.expected).mean() < 0.15
