@@ -127,47 +127,61 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
 // by lane 0 of wave 0 at the end in 10 ns wall-clock ticks.
 #define BLS_PHASE(slot) BLS_STAMP(slot)
 
-__global__ void __launch_bounds__(PAIR_BLOCK) bls_verify_kernel(const uint8_t* msg, uint32_t len, uint32_t* H_out,
-                                                                const uint8_t* sig33, const uint32_t* pk_lines,
-                                                                const uint8_t* pk_ok,
-                                                                const uint32_t* gen_lines, uint8_t* result) {
-  __shared__ PairXchg xc;
+// H = g1_map(msg), sigma from 33 bytes: e(H, PK) * e(-sigma, g2) == 1 for a combined signature,
+// in one block of FOUR waves: each pair's Miller loop is split in two (p36_miller_part: top part
+// + squarings | bottom part + Frobenius lines, 209 vs 320 Fp multiplications per lane).  Waves 0
+// and 1 both hash to G1 (wave 0 stores H) and run the (H, PK) parts; waves 2 and 3 both decode
+// sigma and run the (-sigma, g2) parts; waves 1..3 hand their values over through LDS and wave 0
+// multiplies the four and runs the final exponentiation.
+#define VERIFY_BLOCK 256
+__global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t* msg, uint32_t len, uint32_t* H_out,
+                                                                  const uint8_t* sig33, const uint32_t* pk_lines,
+                                                                  const uint8_t* pk_ok, const uint32_t* gen_lines,
+                                                                  uint8_t* result) {
+  __shared__ PairXchg xc[3];  // the values of waves 1, 2, 3
   if (blockIdx.x != 0) return;
   const int wave = threadIdx.x >> 6;
   const P36 g = p36_lane();
-  BLS_PHASE(wave);
+  BLS_PHASE(wave == 0 ? 0 : 1);
   fp f;
-  if (wave == 1) {
+  if (wave < 2) {
+    g1a P;
+    g1_map_wave(P, msg, len);
+    BLS_PHASE(wave == 0 ? 4 : 12);
+    if (wave == 0 && g.lane == 0 && H_out) g1a_store(H_out, P);
+    if (wave == 0)
+      p36_miller_part<true>(f, P, pk_lines, g);
+    else
+      p36_miller_part<false>(f, P, pk_lines, g);
+    BLS_PHASE(wave == 0 ? 5 : 13);
+  } else {
     g1a s;
     const bool ok = g1_decompress(s, sig33);
-    BLS_PHASE(2);
+    BLS_PHASE(wave == 2 ? 2 : 14);
     if (ok && !s.inf) {
       g1a P = s;
       f_neg(P.y, s.y);
-      const uint32_t* l[1] = {gen_lines};
-      p36_miller<1>(f, &P, l, g);
+      if (wave == 2)
+        p36_miller_part<true>(f, P, gen_lines, g);
+      else
+        p36_miller_part<false>(f, P, gen_lines, g);
     } else {
-      p36_one(f, g);
+      p36_one(f, g);  // e(O, g2) = 1
     }
-    BLS_PHASE(3);
-    xchg_put(xc, f, g);
-    if (g.lane == 0) xc.ok = ok ? 1 : 0;
-  } else {
-    g1a P;
-    g1_map_wave(P, msg, len);
-    BLS_PHASE(4);
-    if (g.lane == 0 && H_out) g1a_store(H_out, P);
-    const uint32_t* l[1] = {pk_lines};
-    p36_miller<1>(f, &P, l, g);
-    BLS_PHASE(5);
+    BLS_PHASE(wave == 2 ? 3 : 15);
+    if (g.lane == 0) xc[wave - 1].ok = ok ? 1 : 0;
   }
+  if (wave > 0) xchg_put(xc[wave - 1], f, g);
   __syncthreads();
   if (wave != 0) return;
-  bool good = xc.ok != 0 && pk_ok[0] != 0;
+  bool good = xc[1].ok != 0 && pk_ok[0] != 0;
   if (good) {
-    fp f1;
-    xchg_get(f1, xc, g);
-    p36_mul(f, f, f1, g);
+#pragma nounroll
+    for (int w = 0; w < 3; w++) {
+      fp f1;
+      xchg_get(f1, xc[w], g);
+      p36_mul(f, f, f1, g);
+    }
     BLS_PHASE(6);
     good = p36_is_one_after_final_exp(f, g);
     BLS_PHASE(11);
@@ -176,11 +190,13 @@ __global__ void __launch_bounds__(PAIR_BLOCK) bls_verify_kernel(const uint8_t* m
 #if CBFT_BLS_PHASES
   if (g.lane == 0) {
     const uint64_t t0 = g_bls_phase[0];
-    printf("bls_verify phases (us from start): w1 decompressed %.1f w1 miller %.1f | w0 hashed %.1f miller %.1f "
-           "joined %.1f fe_inv %.1f fe_easy %.1f fe_pow_u %.1f fe_done %.1f\n",
-           (g_bls_phase[2] - t0) * 0.01, (g_bls_phase[3] - t0) * 0.01, (g_bls_phase[4] - t0) * 0.01,
-           (g_bls_phase[5] - t0) * 0.01, (g_bls_phase[6] - t0) * 0.01, (g_bls_phase[8] - t0) * 0.01,
-           (g_bls_phase[9] - t0) * 0.01, (g_bls_phase[10] - t0) * 0.01, (g_bls_phase[11] - t0) * 0.01);
+    printf("bls_verify phases (us from start): sigma decoded %.1f/%.1f miller top %.1f bottom %.1f | H %.1f/%.1f "
+           "miller top %.1f bottom %.1f | joined %.1f fe_inv %.1f fe_easy %.1f fe_pow_u %.1f fe_done %.1f\n",
+           (g_bls_phase[2] - t0) * 0.01, (g_bls_phase[14] - t0) * 0.01, (g_bls_phase[3] - t0) * 0.01,
+           (g_bls_phase[15] - t0) * 0.01, (g_bls_phase[4] - t0) * 0.01, (g_bls_phase[12] - t0) * 0.01,
+           (g_bls_phase[5] - t0) * 0.01, (g_bls_phase[13] - t0) * 0.01, (g_bls_phase[6] - t0) * 0.01,
+           (g_bls_phase[8] - t0) * 0.01, (g_bls_phase[9] - t0) * 0.01, (g_bls_phase[10] - t0) * 0.01,
+           (g_bls_phase[11] - t0) * 0.01);
   }
 #endif
 }
@@ -287,7 +303,7 @@ hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uin
 hipError_t cbft_bls_launch_verify(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, const uint8_t* d_sig33,
                                   const uint32_t* d_pk_lines, const uint8_t* d_pk_ok,
                                   const uint32_t* d_gen_lines, uint8_t* d_result, hipStream_t s) {
-  hipLaunchKernelGGL(bls_verify_kernel, dim3(1), dim3(PAIR_BLOCK), 0, s, d_msg, len, d_H, d_sig33, d_pk_lines,
+  hipLaunchKernelGGL(bls_verify_kernel, dim3(1), dim3(VERIFY_BLOCK), 0, s, d_msg, len, d_H, d_sig33, d_pk_lines,
                      d_pk_ok, d_gen_lines, d_result);
   return hipGetLastError();
 }

@@ -297,26 +297,28 @@ __device__ __forceinline__ void p36_frob(fp& r, const fp& x, const P36& g) {
   p12_cmul(r, c, co, gmm, gmo, g.h);
 }
 
+// x^-1 = conj(x) / N with N = x conj(x) in Fp6 (the even w-coefficients; the odd ones vanish):
+// N on the wave (one p36_mul), N^-1 by the Fp6 tower on every lane (variable-time Fp inversion:
+// x is a Miller value of public inputs), then conj(x) N^-1 on the wave.  Half the one-lane tower
+// work of inverting in Fp12 directly.
 __device__ __noinline__ void p36_inv(fp& r, const fp& x, const P36& g) {
-  fp12 f, t;
-  fp_shfl(f.c0.c0.a, x, p36_src(0, 0, 0));
-  fp_shfl(f.c0.c0.b, x, p36_src(0, 1, 0));
-  fp_shfl(f.c1.c0.a, x, p36_src(1, 0, 0));
-  fp_shfl(f.c1.c0.b, x, p36_src(1, 1, 0));
-  fp_shfl(f.c0.c1.a, x, p36_src(2, 0, 0));
-  fp_shfl(f.c0.c1.b, x, p36_src(2, 1, 0));
-  fp_shfl(f.c1.c1.a, x, p36_src(3, 0, 0));
-  fp_shfl(f.c1.c1.b, x, p36_src(3, 1, 0));
-  fp_shfl(f.c0.c2.a, x, p36_src(4, 0, 0));
-  fp_shfl(f.c0.c2.b, x, p36_src(4, 1, 0));
-  fp_shfl(f.c1.c2.a, x, p36_src(5, 0, 0));
-  fp_shfl(f.c1.c2.b, x, p36_src(5, 1, 0));
-  fp12_inv(t, f);
-  const fp2* e[6] = {&t.c0.c0, &t.c1.c0, &t.c0.c1, &t.c1.c1, &t.c0.c2, &t.c1.c2};
-  fp2 pick = t.c0.c0;
-#pragma unroll
-  for (int k = 1; k < 6; k++) p12_sel2(pick, *e[k], g.k == k);
-  r = g.h ? pick.b : pick.a;
+  fp xc, n;
+  p36_conj(xc, x, g);
+  p36_mul(n, x, xc, g);
+  fp6 t;
+  fp_shfl(t.c0.a, n, p36_src(0, 0, 0));
+  fp_shfl(t.c0.b, n, p36_src(0, 1, 0));
+  fp_shfl(t.c1.a, n, p36_src(2, 0, 0));
+  fp_shfl(t.c1.b, n, p36_src(2, 1, 0));
+  fp_shfl(t.c2.a, n, p36_src(4, 0, 0));
+  fp_shfl(t.c2.b, n, p36_src(4, 1, 0));
+  fp6_inv<true>(t, t);
+  fp2 pick = t.c0;
+  p12_sel2(pick, t.c1, g.k == 2);
+  p12_sel2(pick, t.c2, g.k == 4);
+  fp ninv = g.h ? pick.b : pick.a;
+  if (g.k & 1) f_zero(ninv);
+  p36_mul(r, xc, ninv, g);
 }
 
 __device__ __forceinline__ void p36_pow_u(fp& r, const fp& x, const P36& g) {
@@ -437,6 +439,35 @@ __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* 
 #pragma unroll
     for (int j = 0; j < NP; j++) line(j);
     k++;
+  }
+}
+
+// One pair's Miller loop split over two waves: the TOP part runs iterations 63..s and then s
+// more squarings, the BOTTOM part iterations s-1..0 (starting from 1), the conjugation and the
+// two Frobenius lines; F_top^(2^s) F_bottom is the whole loop's value (squaring distributes over
+// the product), conjugation applied to both.  With s = 40 both parts cost 209 Fp multiplications
+// per lane (sqr 2, line 3) against 320 for the whole loop on one wave.
+#define P36_MILLER_SPLIT 40
+template <bool TOP>
+__device__ __forceinline__ void p36_miller_part(fp& f, const g1a& P, const uint32_t* lines, const P36& g) {
+  p36_one(f, g);
+  int k = 0;
+  const int hi = TOP ? BN_ATE_DBL - 1 : P36_MILLER_SPLIT - 1, lo = TOP ? P36_MILLER_SPLIT : 0;
+  for (int i = BN_ATE_DBL - 1; i > hi; i--) k += bn_ate_bit(i) ? 2 : 1;
+#pragma nounroll
+  for (int i = hi; i >= lo; i--) {
+    p36_sqr(f, f, g);
+    p36_line1(f, lines + (k++) * BN_LINE_WORDS, P, g);
+    if (bn_ate_bit(i)) p36_line1(f, lines + (k++) * BN_LINE_WORDS, P, g);
+  }
+  if (TOP) {
+#pragma nounroll
+    for (int t = 0; t < P36_MILLER_SPLIT; t++) p36_sqr(f, f, g);
+  }
+  p36_conj(f, f, g);
+  if (!TOP) {
+    p36_line1(f, lines + (k++) * BN_LINE_WORDS, P, g);
+    p36_line1(f, lines + (k++) * BN_LINE_WORDS, P, g);
   }
 }
 
