@@ -220,6 +220,28 @@ BN_HD void f_sub(Fe<F>& r, const Fe<F>& a, const Fe<F>& b) {
   if (bn_any(c < 0)) f_add_2q_where(r, c < 0);
 }
 
+// r = add ? a + b : a - b, reduced below 2q (a, b < 2q, normalised), for lanes that pick one
+// of the two per lane (the Fp2 / Fp12 component formulas): one signed pass instead of both
+// operations and a select.  Same reduction rule as f_add / f_sub, so the same results.
+template <class F>
+BN_HD void f_addsub(Fe<F>& r, const Fe<F>& a, const Fe<F>& b, bool add) {
+  uint32_t q2[BN_LIMBS];
+  f_2q<F>(q2);
+  const uint32_t a8 = a.v[BN_LIMBS - 1], b8 = b.v[BN_LIMBS - 1];
+  const bool corr = add ? a8 + b8 + 2 > q2[BN_LIMBS - 1] : a8 < b8;  // -2q (add) / +2q (sub)
+  const int32_t bs = add ? 0 : -1;  // b's sign: (b ^ bs) - bs = +-b
+  int32_t c = 0;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    const int32_t bi = ((int32_t)b.v[i] ^ bs) - bs;
+    const int32_t qi = corr ? (add ? -(int32_t)q2[i] : (int32_t)q2[i]) : 0;
+    const int32_t x = (int32_t)a.v[i] + bi + qi + c;
+    r.v[i] = (uint32_t)x & BN_MASK;
+    c = x >> 29;
+  }
+  if (bn_any(c < 0)) f_add_2q_where(r, c < 0);
+}
+
 template <class F>
 BN_HD void f_neg(Fe<F>& r, const Fe<F>& a) {
   Fe<F> z;

@@ -56,10 +56,7 @@ __device__ __forceinline__ void p12_cmul(fp& r, const fp& xm, const fp& xo, cons
   fp u = h ? xo : xm, v = h ? xm : xo, t1, t2;
   f_mul(t1, u, ym);
   f_mul(t2, v, yo);
-  fp s, d;
-  f_add(s, t1, t2);
-  f_sub(d, t1, t2);
-  r = h ? s : d;
+  f_addsub(r, t1, t2, h != 0);
 }
 // my component of x^2 (xm, xo): h = 0: (x0 + x1)(x0 - x1); h = 1: 2 x0 x1
 __device__ __forceinline__ void p12_csqr(fp& r, const fp& xm, const fp& xo, int h) {
@@ -73,12 +70,7 @@ __device__ __forceinline__ void p12_csqr(fp& r, const fp& xm, const fp& xo, int 
   r = h ? t2 : t;
 }
 // my component of xi * z from my and the other component: h = 0: z0 - z1; h = 1: z0 + z1
-__device__ __forceinline__ void p12_cxi(fp& r, const fp& zm, const fp& zo, int h) {
-  fp s, d;
-  f_add(s, zm, zo);
-  f_sub(d, zm, zo);
-  r = h ? s : d;
-}
+__device__ __forceinline__ void p12_cxi(fp& r, const fp& zm, const fp& zo, int h) { f_addsub(r, zm, zo, h != 0); }
 __device__ __forceinline__ void p12_xi(fp& r, const fp& z, const P12& g) {
   fp zo;
   fp_shfl(zo, z, g.lane ^ 1);
@@ -173,13 +165,11 @@ __device__ __forceinline__ void p12_cyc_sqr(fp& r, const fp& a, const P12& g) {
   fp px;
   p12_cxi(px, p, q, g.h);
   fp_sel(p, px, g.k == 1);
-  fp three, two, plus, minus;
+  fp three, two;
   f_add(three, p, p);
   f_add(three, three, p);
   f_add(two, a, a);
-  f_add(plus, three, two);
-  f_sub(minus, three, two);
-  r = odd ? plus : minus;
+  f_addsub(r, three, two, odd);
 }
 
 // f <- f * (yP + s w + mu w^3) with s = -lambda xP: c_k = f_k yP - xP f_{k-1} lambda + f_{k-3} mu

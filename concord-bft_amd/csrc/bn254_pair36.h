@@ -113,15 +113,14 @@ __device__ __forceinline__ void p36_sqr(fp& r, const fp& a, const P36& g) {
   fp P1, P2;
   f_mul(P1, X1, Y1);
   f_mul(P2, X2, Y2);
-  fp acc, accw, t, t2;
+  fp acc, accw;
   // diag: acc = (h ? 2 P1 : P1), accw = (h ? 2 P2 : P2) (the second diagonal term wraps)
   // cross: T = 2 (h ? P1 + P2 : P1 - P2), into accw if it wraps
   f_add(s1, P1, P1);
   f_add(s2, P2, P2);
   fp dA = g.h ? s1 : P1, dB = g.h ? s2 : P2;
-  f_add(t, P1, P2);
-  f_sub(t2, P1, P2);
-  fp c = g.h ? t : t2;
+  fp c;
+  f_addsub(c, P1, P2, g.h != 0);
   f_add(c, c, c);
   fp zero;
   f_zero(zero);
@@ -161,13 +160,11 @@ __device__ __forceinline__ void p36_cyc_sqr(fp& r, const fp& a, const P36& g) {
   fp vx;
   p36_xi(vx, v, g);  // t C^2 term for k = 1
   fp_sel(v, vx, g.k == 1);
-  fp three, two, plus, minus;
+  fp three, two;
   f_add(three, v, v);
   f_add(three, three, v);
   f_add(two, a, a);
-  f_add(plus, three, two);
-  f_sub(minus, three, two);
-  r = odd ? plus : minus;
+  f_addsub(r, three, two, odd);
 }
 
 __device__ __forceinline__ void p36_coef(fp& m, fp& o, const uint32_t* c, int h) {
@@ -188,12 +185,10 @@ __device__ __forceinline__ void p36_line1(fp& f, const uint32_t* ln, const g1a& 
   const fp u = g.h ? oo : om, v = g.h ? om : oo;
   fp X1 = g.s == 0 ? f : u;
   fp Y1 = g.s == 0 ? P.y : cm;
-  fp P1, P2, P3, C, t;
+  fp P1, P2, P3, C;
   f_mul(P1, X1, Y1);
   f_mul(P2, v, co);
-  f_add(C, P1, P2);
-  f_sub(t, P1, P2);
-  C = g.h ? C : t;
+  f_addsub(C, P1, P2, g.h != 0);
   f_mul(P3, C, P.x);
   f_neg(P3, P3);
   fp T = g.s == 0 ? P1 : (g.s == 1 ? P3 : C);
@@ -212,12 +207,10 @@ __device__ __forceinline__ void p36_line_abc(fp& f, const uint32_t* ln, const g1
   p36_fetch(om, oo, f, g.s == 0 ? g.k : (g.s == 1 ? (g.k + 5) % 6 : (g.k + 3) % 6), g);
   p36_coef(cm, co, ln + 18 * g.s, g.h);
   const fp u = g.h ? oo : om, v = g.h ? om : oo;
-  fp P1, P2, P3, C, t;
+  fp P1, P2, P3, C;
   f_mul(P1, u, cm);
   f_mul(P2, v, co);
-  f_add(C, P1, P2);
-  f_sub(t, P1, P2);
-  C = g.h ? C : t;
+  f_addsub(C, P1, P2, g.h != 0);
   f_mul(P3, C, g.s == 0 ? P.y : P.x);
   fp T = g.s == 2 ? C : P3;
   const bool wrap = (g.s == 1 && g.k == 0) || (g.s == 2 && g.k < 3);

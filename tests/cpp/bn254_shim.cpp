@@ -22,6 +22,27 @@ static void fp12_flat(uint8_t* out, const fp12& x) {  // 12 x 32-byte big-endian
 
 extern "C" {
 
+// f_add / f_sub / f_addsub on Montgomery forms of a, b (< p, 32-byte big-endian): writes the
+// canonical results of add, sub, addsub(add = 1), addsub(add = 0); returns 1 if the reduced
+// representations of addsub equal f_add's / f_sub's limb for limb.
+int shim_fp_addsub(const uint8_t* a32, const uint8_t* b32, uint8_t* out128) {
+  uint32_t w[8];
+  fp a, b, r[4];
+  be32_to_words(w, a32);
+  f_from_words(a, w);
+  be32_to_words(w, b32);
+  f_from_words(b, w);
+  f_add(r[0], a, b);
+  f_sub(r[1], a, b);
+  f_addsub(r[2], a, b, true);
+  f_addsub(r[3], a, b, false);
+  for (int k = 0; k < 4; k++) {
+    f_to_words(w, r[k]);
+    words_to_be32(out128 + 32 * k, w);
+  }
+  return std::memcmp(&r[0], &r[2], sizeof(fp)) == 0 && std::memcmp(&r[1], &r[3], sizeof(fp)) == 0;
+}
+
 // fp_inv_var and fp_inv of the canonical integer x (32-byte big-endian, < p): out_var, out_fermat
 // (big-endian canonical).  Returns 1 if both agree.
 int shim_fp_inv(const uint8_t* x32, uint8_t* out_var, uint8_t* out_fermat) {
