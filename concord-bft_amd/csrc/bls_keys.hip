@@ -54,7 +54,7 @@ __device__ void g2_sum_tail(const g2j& acc, bool bad, uint8_t* ok, uint8_t* out6
 // Signer ids [lo_id, hi_id) only (a rank's slice of a sharded multisig key sum).  With out_part
 // the block writes its Jacobian sum (54 words) + the bad-key flag (1 word) (-> bls_verify_multisig_kernel),
 // else the compressed sum into out65.
-__global__ void __launch_bounds__(SUM_THREADS) bls_g2_sum_kernel(const uint32_t* aff, const uint8_t* key_ok,
+__global__ void __launch_bounds__(SUM_THREADS, 1) bls_g2_sum_kernel(const uint32_t* aff, const uint8_t* key_ok,
                                                                  uint32_t n, const uint8_t* bitmap, uint32_t lo_id,
                                                                  uint32_t hi_id, uint8_t* ok, uint8_t* out65,
                                                                  uint32_t* out_part) {
@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(SUM_THREADS) bls_g2_sum_kernel(const uint32_t*
     p.X = q.x;
     p.Y = q.y;
     fp2_one(p.Z);
-    g2_add_j(acc, acc, p);
+    g2_add_j_body(acc, acc, p);
   }
   if (mine_bad) atomicOr(&bad, 1);
   for (int stride = SUM_THREADS / 2; stride >= 1; stride >>= 1) {
@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(SUM_THREADS) bls_g2_sum_kernel(const uint32_t*
     if (t < stride) {
       g2j o;
       g2j_load(o, sp[t]);
-      g2_add_j(acc, acc, o);
+      g2_add_j_body(acc, acc, o);
     }
     __syncthreads();
   }

@@ -334,7 +334,10 @@ BN_HDN void g2_dbl_j(g2j& r, const g2j& p) {
   fp2_sub(r.Y, t, C);
 }
 
-BN_HDN void g2_add_j(g2j& r, const g2j& p, const g2j& q) {
+// The Jacobian addition's body, inlinable where the caller has registers to spare (the multisig
+// key-sum tree: as a called function it gets a 128-VGPR budget and spills every product to
+// scratch).  g2_add_j below is the out-of-line form.
+BN_HD void g2_add_j_body(g2j& r, const g2j& p, const g2j& q) {
   if (fp2_is_zero(p.Z)) {
     r = q;
     return;
@@ -387,6 +390,7 @@ BN_HDN void g2_add_j(g2j& r, const g2j& p, const g2j& q) {
   r.Y = Y3;
   r.Z = Z3;
 }
+BN_HDN void g2_add_j(g2j& r, const g2j& p, const g2j& q) { g2_add_j_body(r, p, q); }
 
 // VAR: variable-time inversion, for public points only (a multisig key sum)
 template <bool VAR = false>
