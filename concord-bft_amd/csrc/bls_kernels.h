@@ -15,9 +15,14 @@ hipError_t cbft_bls_launch_keys(const uint8_t* d_keys65, uint32_t nkeys, uint32_
                                 uint32_t* d_aff, uint32_t* d_scratch, hipStream_t s);
 hipError_t cbft_bls_launch_gen_lines(uint32_t* d_lines, hipStream_t s);
 hipError_t cbft_bls_launch_hash(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, hipStream_t s);
+// H = g1_map(msg) when d_H is non-null, beside the decoding of k shares (lane per share):
+// d_valid[j] = decodable && id in [1, n], d_sig (19 words each), d_ids
+hipError_t cbft_bls_launch_prep(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, const uint8_t* d_shares, uint32_t k,
+                                uint32_t n, uint8_t* d_valid, uint32_t* d_sig, uint32_t* d_ids, hipStream_t s);
+// parsed: d_valid / d_sig / d_ids already hold bls_prep's decoding (d_valid is overwritten with the verdicts)
 hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uint32_t n, const uint32_t* d_H,
                                         const uint32_t* d_vk_lines, const uint8_t* d_vk_ok,
-                                        const uint32_t* d_gen_lines, int do_verify, uint8_t* d_valid,
+                                        const uint32_t* d_gen_lines, int do_verify, int parsed, uint8_t* d_valid,
                                         uint32_t* d_sig, uint32_t* d_ids, hipStream_t s);
 // lambda over all k shares; the MSM over shares [lo, hi); d_out_jac (nullable): write the sum as
 // one Jacobian partial (BLS_JAC_WORDS) instead of compressing it into d_out33

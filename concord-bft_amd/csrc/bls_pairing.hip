@@ -43,12 +43,14 @@ __device__ __forceinline__ void xchg_get(fp& f, const PairXchg& x, const P36& g)
 //              used while 2k waves fit the chip's 1,024 SIMDs;
 //   WAVES = 1: one wave per share, both pairs on it: the throughput form for larger k and for
 //              parse-only launches (two waves of a share would share SIMDs with other shares).
+// parsed != 0: bls_prep_kernel has already decoded the shares (valid = decodable && id in range,
+// sig, ids), so the check starts at the Miller loop.
 template <int WAVES>
 __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint8_t* shares, uint32_t k, uint32_t n,
                                                                       const uint32_t* H, const uint32_t* vk_lines,
                                                                       const uint8_t* vk_ok, const uint32_t* gen_lines,
-                                                                      int do_verify, uint8_t* valid, uint32_t* sig,
-                                                                      uint32_t* ids) {
+                                                                      int do_verify, int parsed, uint8_t* valid,
+                                                                      uint32_t* sig, uint32_t* ids) {
   __shared__ PairXchg xc;
   const uint32_t j = blockIdx.x;
   if (j >= k) return;  // whole blocks exit together
@@ -60,12 +62,18 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
   const bool key_ok = do_verify && id_ok && vk_ok[id - 1] != 0;
   const uint32_t* vkl = key_ok ? vk_lines + (size_t)(id - 1) * LINES_PER_KEY : nullptr;
   if (WAVES == 1) {
-    uint32_t pid;
     g1a s;
-    bool good = bls_parse_share(pid, s, sh) && id_ok;
-    if (g.lane == 0) {
-      ids[j] = id;
-      g1a_store(sig + 19 * (size_t)j, s);
+    bool good;
+    if (parsed) {
+      good = valid[j] != 0;
+      g1a_load(s, sig + 19 * (size_t)j);
+    } else {
+      uint32_t pid;
+      good = bls_parse_share(pid, s, sh) && id_ok;
+      if (g.lane == 0) {
+        ids[j] = id;
+        g1a_store(sig + 19 * (size_t)j, s);
+      }
     }
     if (do_verify) {
       good = good && key_ok;
@@ -83,14 +91,20 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
   }
   fp f;
   if (wave == 1) {
-    uint32_t pid;
     g1a s;
-    const bool parsed = bls_parse_share(pid, s, sh) && id_ok;
-    if (g.lane == 0) {
-      ids[j] = id;
-      g1a_store(sig + 19 * (size_t)j, s);
+    bool decoded;
+    if (parsed) {
+      decoded = valid[j] != 0;
+      g1a_load(s, sig + 19 * (size_t)j);
+    } else {
+      uint32_t pid;
+      decoded = bls_parse_share(pid, s, sh) && id_ok;
+      if (g.lane == 0) {
+        ids[j] = id;
+        g1a_store(sig + 19 * (size_t)j, s);
+      }
     }
-    if (parsed && key_ok && !s.inf) {
+    if (decoded && key_ok && !s.inf) {
       g1a P = s;
       f_neg(P.y, s.y);
       const uint32_t* l[1] = {gen_lines};
@@ -99,7 +113,7 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
       p36_one(f, g);  // e(O, g2) = 1: an infinite sigma checks against e(H, vk) alone
     }
     xchg_put(xc, f, g);
-    if (g.lane == 0) xc.ok = parsed ? 1 : 0;
+    if (g.lane == 0) xc.ok = decoded ? 1 : 0;
   } else if (key_ok) {
     g1a P;
     g1a_load(P, H);
@@ -281,10 +295,39 @@ __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uin
   if (g.lane == 0) result[0] = good ? 1 : 0;
 }
 
+// H = g1_map(msg) (block 0, when H is non-null) beside the decoding of k shares, one lane per
+// share (blocks 1..): id, affine point, valid = decodable && id in [1, n].  The shares' square
+// roots then run while the message is hashed instead of after it, inside the verify.
+__global__ void __launch_bounds__(64) bls_prep_kernel(const uint8_t* msg, uint32_t len, uint32_t* H,
+                                                      const uint8_t* shares, uint32_t k, uint32_t n, uint8_t* valid,
+                                                      uint32_t* sig, uint32_t* ids) {
+  if (blockIdx.x == 0) {
+    if (!H) return;
+    g1a P;
+    g1_map_wave(P, msg, len);
+    if ((threadIdx.x & 63) == 0) g1a_store(H, P);
+    return;
+  }
+  const uint32_t j = (blockIdx.x - 1) * 64 + threadIdx.x;
+  if (j >= k) return;
+  uint32_t id;
+  g1a s;
+  const bool ok = bls_parse_share(id, s, shares + 37 * (size_t)j) && id >= 1 && id <= n;
+  ids[j] = id;
+  g1a_store(sig + 19 * (size_t)j, s);
+  valid[j] = ok ? 1 : 0;
+}
+
 // ------------------------------------------------------------------------------ launchers
+hipError_t cbft_bls_launch_prep(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, const uint8_t* d_shares, uint32_t k,
+                                uint32_t n, uint8_t* d_valid, uint32_t* d_sig, uint32_t* d_ids, hipStream_t s) {
+  hipLaunchKernelGGL(bls_prep_kernel, dim3(1 + (k + 63) / 64), dim3(64), 0, s, d_msg, len, d_H, d_shares, k, n, d_valid,
+                     d_sig, d_ids);
+  return hipGetLastError();
+}
 hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uint32_t n, const uint32_t* d_H,
                                         const uint32_t* d_vk_lines, const uint8_t* d_vk_ok,
-                                        const uint32_t* d_gen_lines, int do_verify, uint8_t* d_valid,
+                                        const uint32_t* d_gen_lines, int do_verify, int parsed, uint8_t* d_valid,
                                         uint32_t* d_sig, uint32_t* d_ids, hipStream_t s) {
   if (!k) return hipSuccess;
   static const int forced = [] {  // $CBFT_BLS_SHARE_WAVES: 1 or 2 forces the form (A/B), else by k
@@ -294,10 +337,10 @@ hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uin
   const bool two = forced ? forced == 2 : 2 * (size_t)k <= SIMDS;
   if (do_verify && two)
     hipLaunchKernelGGL(bls_share_verify_kernel<2>, dim3(k), dim3(128), 0, s, d_shares, k, n, d_H, d_vk_lines,
-                       d_vk_ok, d_gen_lines, do_verify, d_valid, d_sig, d_ids);
+                       d_vk_ok, d_gen_lines, do_verify, parsed, d_valid, d_sig, d_ids);
   else
     hipLaunchKernelGGL(bls_share_verify_kernel<1>, dim3(k), dim3(64), 0, s, d_shares, k, n, d_H, d_vk_lines,
-                       d_vk_ok, d_gen_lines, do_verify, d_valid, d_sig, d_ids);
+                       d_vk_ok, d_gen_lines, do_verify, parsed, d_valid, d_sig, d_ids);
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_verify(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, const uint8_t* d_sig33,

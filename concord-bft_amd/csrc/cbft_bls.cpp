@@ -124,17 +124,28 @@ int cbft_bls_hash_to_g1(cbft_ctx* c, const uint8_t* msg, uint32_t len, uint8_t* 
   return CBFT_OK;
 }
 
-// Stage k shares on the device and run the parse (+ verify) kernel.
-static int bls_shares(cbft_ctx* c, BlsKeySet* ks, const uint8_t* shares37, uint32_t k, int do_verify) {
-  CBFT_HIP(c->bls_shares.reserve((size_t)k * 37));
-  CBFT_HIP(c->bls_valid.reserve(k));
-  CBFT_HIP(c->bls_sig.reserve((size_t)k * BLS_SIG_WORDS * 4));
-  CBFT_HIP(c->bls_ids.reserve((size_t)k * 4));
-  CBFT_HIP(hipMemcpyAsync(c->bls_shares.p, shares37, (size_t)k * 37, hipMemcpyHostToDevice, c->stream));
+// Stage k shares on the device and decode them, one lane per share (ids, affine points, valid =
+// decodable && id in range), hashing the uploaded message to bls_H in the same launch when
+// `hash` (the share roots run beside the hash instead of after it).
+static int bls_prep(cbft_ctx* c, BlsKeySet* ks, const uint8_t* shares37, uint32_t k, bool hash, uint32_t len) {
+  CBFT_HIP(c->bls_shares.reserve((size_t)(k ? k : 1) * 37));
+  CBFT_HIP(c->bls_valid.reserve(k ? k : 1));
+  CBFT_HIP(c->bls_sig.reserve((size_t)(k ? k : 1) * BLS_SIG_WORDS * 4));
+  CBFT_HIP(c->bls_ids.reserve((size_t)(k ? k : 1) * 4));
+  if (k) CBFT_HIP(hipMemcpyAsync(c->bls_shares.p, shares37, (size_t)k * 37, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(cbft_bls_launch_prep(c->bls_msg.as<uint8_t>(), len, hash ? c->bls_H.as<uint32_t>() : nullptr,
+                                c->bls_shares.as<uint8_t>(), k, ks ? ks->n : BLS_MAX_SHARES,
+                                c->bls_valid.as<uint8_t>(), c->bls_sig.as<uint32_t>(), c->bls_ids.as<uint32_t>(),
+                                c->stream));
+  return CBFT_OK;
+}
+
+// Verify the k shares bls_prep decoded against H (bls_H): verdicts into bls_valid.
+static int bls_verify_parsed(cbft_ctx* c, BlsKeySet* ks, uint32_t k) {
   CBFT_HIP(cbft_bls_launch_share_verify(
-      c->bls_shares.as<uint8_t>(), k, ks ? ks->n : BLS_MAX_SHARES, c->bls_H.as<uint32_t>(),
-      ks ? ks->lines.as<uint32_t>() + cbft_bls_lines_words_per_key() : nullptr, ks ? ks->ok.as<uint8_t>() + 1 : nullptr,
-      c->bls_gen_lines.as<uint32_t>(), do_verify, c->bls_valid.as<uint8_t>(), c->bls_sig.as<uint32_t>(),
+      c->bls_shares.as<uint8_t>(), k, ks->n, c->bls_H.as<uint32_t>(),
+      ks->lines.as<uint32_t>() + cbft_bls_lines_words_per_key(), ks->ok.as<uint8_t>() + 1,
+      c->bls_gen_lines.as<uint32_t>(), 1, 1, c->bls_valid.as<uint8_t>(), c->bls_sig.as<uint32_t>(),
       c->bls_ids.as<uint32_t>(), c->stream));
   return CBFT_OK;
 }
@@ -149,8 +160,9 @@ int cbft_bls_verify_shares(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_
   if (!k) return CBFT_OK;
   CBFT_HIP(hipSetDevice(c->device));
   int rc = bls_gen_lines(c);
-  if (!rc) rc = bls_upload_msg_hash(c, msg, len);
-  if (!rc) rc = bls_shares(c, ks, shares37, k, 1);
+  if (!rc) rc = bls_upload_msg(c, msg, len);
+  if (!rc) rc = bls_prep(c, ks, shares37, k, true, len);
+  if (!rc) rc = bls_verify_parsed(c, ks, k);
   if (rc) return rc;
   std::vector<uint8_t> v(k);
   CBFT_HIP(hipMemcpyAsync(v.data(), c->bls_valid.p, k, hipMemcpyDeviceToHost, c->stream));
@@ -175,7 +187,7 @@ static int bls_combine_range(cbft_ctx* c, const uint8_t* shares37, uint32_t k, u
   }
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
-  int rc = bls_shares(c, nullptr, shares37, k, 0);
+  int rc = bls_prep(c, nullptr, shares37, k, false, 0);
   if (rc) return rc;
   CBFT_HIP(c->bls_lambda.reserve((size_t)k * 8 * 4));
   CBFT_HIP(c->bls_partial.reserve((size_t)((k + 15) / 16 + 1) * BLS_JAC_WORDS * 4));
@@ -306,7 +318,8 @@ int cbft_bls_combine_threshold(cbft_ctx* c, uint32_t id, const uint8_t* msg, uin
     }
   }
   int rc = bls_gen_lines(c);
-  if (!rc) rc = bls_upload_msg_hash(c, msg, len);
+  if (!rc) rc = bls_upload_msg(c, msg, len);
+  if (!rc && k) rc = bls_prep(c, ks, shares37, k, true, len);  // H beside the shares' decoding
   if (rc) return rc;
   CBFT_HIP(c->bls_first.reserve(k ? k : 1));
   CBFT_HIP(c->bls_use.reserve(k ? k : 1));
@@ -334,8 +347,6 @@ int cbft_bls_combine_threshold(cbft_ctx* c, uint32_t id, const uint8_t* msg, uin
   uint8_t ok = 0;
   bool done = false;
   if (optimistic && k) {
-    rc = bls_shares(c, ks, shares37, k, 0);  // parse only
-    if (rc) return rc;
     CBFT_HIP(cbft_bls_launch_and(c->bls_first.as<uint8_t>(), c->bls_valid.as<uint8_t>(), c->bls_use.as<uint8_t>(), k,
                                  c->stream));
     rc = combine_verify();
@@ -350,7 +361,7 @@ int cbft_bls_combine_threshold(cbft_ctx* c, uint32_t id, const uint8_t* msg, uin
   }
   if (!done) {
     if (k) {
-      rc = bls_shares(c, ks, shares37, k, 1);  // parse + verify every share
+      rc = bls_verify_parsed(c, ks, k);  // verify every decoded share
       if (rc) return rc;
       CBFT_HIP(cbft_bls_launch_and(c->bls_first.as<uint8_t>(), c->bls_valid.as<uint8_t>(), c->bls_use.as<uint8_t>(),
                                    k, c->stream));
