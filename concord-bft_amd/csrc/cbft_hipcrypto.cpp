@@ -527,10 +527,7 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   Ed25519Batch b{n, d_pk, d_kidx, KeyChunks{nullptr, 0}, d_sig, d_msg, d_off, d_len,
                  kt ? kt->nkeys : (uint32_t)n, fixed_len};
   Ed25519Work w{};
-  // one inversion per K signatures per lane only where the batch keeps >= 64 finish waves; a
-  // small (latency-bound) batch inverts per signature.  K = 16 at the 64K headline: the finish is
-  // then 64 waves that run beside the next batch's hash/ladder (stage order), 5 % of the VALU work
-  // of a per-signature inversion (A/B on MI355X: K = 8 327, K = 16 360, K = 32 273 M verifies/s)
+  // a small (latency-bound) batch inverts per signature;
   // one shared (variable-time) inversion per 2 signatures per lane from 16K: the inversion is now
   // cheap, so more waves beat more sharing (64K: K = 2 55 us, 4 60, 8 74, 16 103, 32 162 us)
   w.finish_batch = c->finish_batch ? c->finish_batch : (n >= 16384 ? 2 : 1);

@@ -1,4 +1,4 @@
-// Batched Ed25519 signature verification for gfx950 (MI355X): one signature per lane.
+// Batched Ed25519 signature verification for gfx950 (MI355X).
 //
 // Semantics: exactly OpenSSL 3.0.2 EVP_DigestVerify(ED25519) == 1 (see oracle/ed25519_ref.py):
 //   S < L (strict);  A decoded without a canonicity check on y;  h = SHA-512(R||A||M) mod L;
@@ -25,6 +25,12 @@
 // addition everywhere).  The B table (2^(WB-1)+1 affine entries) lives in LDS; the -A table
 // entry is streamed from HBM/L2 one field element at a time inside the addition, so at most
 // 9 VGPRs of it are ever live.
+//
+// That windowed ladder is the path for per-signature keys.  Keys loaded into a key table (and B)
+// instead get fixed-base comb tables (ed25519_comb_table_kernel, below) and the comb ladders: the
+// quad ladder (4 lanes per signature, ed25519_comb_ladder_kernel) below 32K signatures and the
+// pair ladder (2 lanes per signature, ed25519_comb2_ladder_kernel) from 32K; hash, decode and
+// finish stay one signature per lane.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -459,10 +465,10 @@ __global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519B
 // offset = 2^(w-1) sum_{j < npos-1} 2^(w j); d_j = chunk_j(s') - 2^(w-1) below the top position,
 // d_top = chunk_top(s') in [0, 2^(w-1)] (CombGeom in ed25519_verify.h; tests/test_comb_recode.py
 // checks the recoding exhaustively at the range edges).  One mixed addition per position and no
-// doublings: B's table is radix 2^16 (16 positions, 67 MB: Infinity-Cache resident), a key's
+// doublings: B's table is radix 2^22 (12 positions, 3.2 GB in HBM), a key's
 // table radix 2^w_A (default 2^13 while the tables fit the budget: 20 positions, 10.5 MB per key,
 // 43 GB for 4,096 keys -- HBM is 288 GB and keys are long-lived, SigManager.cpp:139-150), so a
-// verify is 16 + 20 = 36 mixed additions (the radix-256 comb of the first round: 64).
+// verify is 12 + 20 = 32 mixed additions (the radix-256 comb of the first round: 64).
 //
 // The additions are dealt to the 4 lanes of a quad in order (lane q takes additions
 // q*nper .. q*nper+nper-1, the A positions first), then two DPP butterfly levels (quad_perm
