@@ -1,0 +1,190 @@
+// Lazy-reduction lane arithmetic of the cyclotomic squaring on the pair36 layout
+// (bn254_pair36.h: p36_cyc_sqr).  Host + device: tests/cpp/bn254_shim.cpp runs the same stage
+// functions on the CPU over an emulated 36-lane wave and checks them against fp12_sqr.
+//
+// A final exponentiation is one wave issuing one dependent instruction stream (a lone wave on
+// gfx950: ~6 cycles per VALU instruction, 10.6 per v_mad_u64_u32, profiles/r02_intrate2.txt), so
+// its cost is the instruction count per lane.  The reduced form (f_add / f_sub: a carry pass, a
+// reduction decision and a branch each) cost ~14 x 45 instructions per squaring against ~210 for
+// the one Fp multiplication.  Here the squaring carries unreduced values between its gathers
+// (sums of a few reduced values, limbs kept non-negative by redundant representations of
+// multiples of q) and reduces ONCE, at the end (fp_reduce64: the multiple of q estimated from the
+// top limb, subtracted with 24-bit products).  Every bound is stated at the function.
+#pragma once
+#include "bn254_field.h"
+
+// ---- constants: k q as limbs, and redundant forms of k q with every low limb >= L ----------
+struct CsLimbs {
+  uint32_t v[BN_LIMBS];
+};
+
+// k q normalised (limbs 0..7 < 2^29)
+constexpr CsLimbs cs_kq(uint32_t k) {
+  CsLimbs r{};
+  uint64_t c = 0;
+  for (int i = 0; i < BN_LIMBS; i++) {
+    const uint64_t x = (uint64_t)k * FpParams::Q[i] + c;
+    r.v[i] = i < BN_LIMBS - 1 ? (uint32_t)(x & BN_MASK) : (uint32_t)x;
+    c = x >> 29;
+  }
+  return r;
+}
+
+// the same value (k q, or 0 for k = 0) with limbs 0..7 in [L, L + 2^29) and the rest (signed)
+// in the top limb: added to a limb-wise difference it keeps every low limb non-negative
+constexpr CsLimbs cs_redundant(uint32_t k, int64_t L) {
+  const CsLimbs n = cs_kq(k);
+  CsLimbs r{};
+  int64_t b = 0;  // borrowed from this limb (in units of its weight)
+  for (int i = 0; i < BN_LIMBS - 1; i++) {
+    const int64_t cur = (int64_t)n.v[i] - b;
+    int64_t d = (cur - L) % (int64_t)(1 << 29);
+    if (d < 0) d += (int64_t)1 << 29;
+    const int64_t di = L + d;
+    r.v[i] = (uint32_t)di;
+    b = (di - cur) >> 29;
+  }
+  r.v[BN_LIMBS - 1] = (uint32_t)(int32_t)((int64_t)n.v[BN_LIMBS - 1] - b);
+  return r;
+}
+
+struct CsConst {
+  static constexpr CsLimbs Q4R = cs_redundant(4, (1 << 30) - 2);   // cs_operands: Wm - Wo + 4q
+  static constexpr CsLimbs Z3 = cs_redundant(0, 3 << 29);          // cs_combine: +-(X2 + Y2) +- G3
+  static constexpr CsLimbs Z4 = cs_redundant(0, 1 << 29);          // cs_finish: v +- vo
+  static constexpr CsLimbs D28M = cs_redundant(28, (1 << 30) - 2);  // cs_finish: 3w - 2a + 28q
+  static constexpr CsLimbs D28P = cs_kq(28);                        // cs_finish: 3w + 2a + 28q
+  // floor(2^32 / (Q8 + 1)): m = umulhi(x8, MINV) estimates floor(x / q) from the top limb
+  static constexpr uint32_t MINV = (uint32_t)((1ull << 32) / (FpParams::Q[BN_LIMBS - 1] + 1));
+};
+
+constexpr int cs_ctz(uint32_t x) {
+  int n = 0;
+  while (!(x & 1u)) {
+    x >>= 1;
+    n++;
+  }
+  return n;
+}
+constexpr int cs_bitlen(uint32_t x) {
+  int n = 0;
+  while (x) {
+    x >>= 1;
+    n++;
+  }
+  return n;
+}
+
+// ---- carry passes -------------------------------------------------------------------------
+// limbs 0..7 non-negative (as uint32, any size): -> [0, 2^29), carries into the top limb
+// (two's complement, so a signed top limb stays signed).  Sequential, 3 instructions a limb.
+BN_HD void cs_carry(fp& x) {
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS - 1; i++) {
+    x.v[i + 1] += x.v[i] >> 29;
+    x.v[i] &= BN_MASK;
+  }
+}
+// limbs 0..7 signed (|x_i| < 2^31): the same with arithmetic shifts
+BN_HD void cs_carry_s(fp& x) {
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS - 1; i++) {
+    x.v[i + 1] += (uint32_t)((int32_t)x.v[i] >> 29);
+    x.v[i] &= BN_MASK;
+  }
+}
+
+// ---- the single reduction -------------------------------------------------------------------
+// r = x mod q, r < 2q and normalised, for 0 <= x < 64 q given with limbs 0..7 in [0, 2^29 + 8)
+// (the top limb then within 1 of floor(x / 2^232) from below).
+//   m = umulhi(x8, MINV) satisfies floor(x/q) - 1 <= m <= floor(x/q): m <= x8 / (Q8 + 1) <= x/q,
+//   and x8 MINV / 2^32 > x8 / (Q8 + 1) - 2^-4 > x/q - 2^-4 - 66 / (Q8 + 1)  (x8 < 2^28).
+// m q is subtracted limb by limb: Q_i = s_i 2^sh_i with s_i < 2^22, so every m s_i (m < 64) is
+// one 24-bit product, placed as (m s_i << sh_i) & mask into limb i and m s_i >> (29 - sh_i)
+// into limb i + 1.  One signed carry pass normalises (x - m q in [0, 2q)).
+BN_HD void fp_reduce64(fp& r, fp& x) {
+  const uint32_t x8 = x.v[BN_LIMBS - 1];
+  const uint32_t m = (uint32_t)(((uint64_t)x8 * CsConst::MINV) >> 32) & 63u;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS - 1; i++) {
+    const int sh = cs_ctz(FpParams::Q[i]);
+    const uint32_t s = FpParams::Q[i] >> sh;
+    const uint32_t p = m * s;  // < 2^28
+    if (sh == 0) {
+      x.v[i] -= p;  // s < 2^23 here: m s < 2^29, no spill into limb i + 1
+    } else {
+      x.v[i] -= (p << sh) & BN_MASK;
+      if (cs_bitlen(s) + 6 + sh > 29) x.v[i + 1] -= p >> (29 - sh);
+    }
+  }
+  x.v[BN_LIMBS - 1] -= m * FpParams::Q[BN_LIMBS - 1];
+  cs_carry_s(x);
+  r = x;
+}
+
+// ---- the four lane stages of p36_cyc_sqr -------------------------------------------------
+// Lane (k, h, s) of the pair36 layout; a = its component of the input (reduced, < 2q).
+// Granger-Scott: for (x, y) = (e_sx, e_sx+3), sub-lane s squares w = x | y | x + y (s = 0, 1, 2);
+// the component h of e_k^2-part then combines x^2, y^2, (x + y)^2 (bn254_pair12.h: p12_cyc_sqr).
+
+// stage 1 (source side): R = a, plus a_{k+3} (t, gathered from coefficient k + 3) on sub-lane 2,
+// so one gather per component gives w: x from (sx, h, 0), y from (sx + 3, h, 1), x + y from
+// (sx, h, 2).  Limbs < 2^30, value < 4q.
+BN_HD void cs_pre(fp& R, const fp& a, const fp& t, int s) {
+  const uint32_t msk = s == 2 ? ~0u : 0u;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) R.v[i] = a.v[i] + (t.v[i] & msk);
+}
+
+// stage 2: the operands of the one multiplication from my (Wm) and the other (Wo) component of w:
+//   h = 0: (Wm + Wo)(Wm - Wo) = w_0^2 - w_1^2;  h = 1: (2 Wm) Wo = 2 w_0 w_1.
+// U stays raw (limbs < 2^31, value < 8q); V = Wm - Wo + 4q (h = 0; low limbs of Q4R >= 2^30 - 2
+// >= Wo_i, so non-negative) or Wo (h = 1), then carried (value < 8q).  f_mul(U, V): product
+// columns < 9 2^60 + 9 2^58 + 2^35 < 2^64, result T < 64 q^2 / 2^261 + q < 1.3 q, normalised.
+BN_HD void cs_operands(fp& U, fp& V, const fp& Wm, const fp& Wo, int h) {
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    U.v[i] = Wm.v[i] + (h ? Wm.v[i] : Wo.v[i]);
+    V.v[i] = h ? Wo.v[i] : Wm.v[i] - Wo.v[i] + CsConst::Q4R.v[i];
+  }
+  cs_carry(V);
+}
+
+// stage 3: v = x^2 + xi y^2 (even k) or (x + y)^2 - x^2 - y^2 = 2xy (odd k), my component, from
+// X2 = x^2_h, Y2 = y^2_h and G3 = y^2_h' (even k) | (x + y)^2_h (odd k), each < 1.3 q:
+//   even, h = 0: X2 + Y2 - G3;  even, h = 1: X2 + Y2 + G3;  odd: G3 - X2 - Y2.
+// Negation as (z ^ -1) + 1; Z3 (a redundant zero, low limbs >= 3 2^29) keeps the low limbs
+// non-negative.  Carried: low limbs normalised, signed top, |v| < 3.9 q.
+BN_HD void cs_combine(fp& v, const fp& X2, const fp& Y2, const fp& G3, int k, int h) {
+  const bool odd = (k & 1) != 0;
+  const uint32_t mP = odd ? ~0u : 0u;
+  const uint32_t mG = (!odd && h == 0) ? ~0u : 0u;
+  const uint32_t c = (mP & 1u) + (mG & 1u);
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) v.v[i] = ((X2.v[i] + Y2.v[i]) ^ mP) + (G3.v[i] ^ mG) + (CsConst::Z3.v[i] + c);
+  cs_carry(v);
+}
+
+// stage 4: r = 3 v' + 2a (odd k) | 3 v' - 2a (even k), reduced below 2q, where v' = xi v for k = 1
+// (xi = 1 + i: component 0 v_0 - v_1, component 1 v_0 + v_1; vo = the other component's v) and
+// v' = v otherwise.  w = v' with Z4 (low limbs >= 2^29) is carried (|w| < 7.8 q); then
+// 3w +- 2a + 28q has low limbs in [0, 3 2^30) (D28M's low limbs >= 2^30 - 2 >= 2a_i) and value in
+// (0, 56 q): one carry pass and fp_reduce64.
+BN_HD void cs_finish(fp& r, const fp& v, const fp& vo, const fp& a, int k, int h) {
+  const uint32_t use = k == 1 ? ~0u : 0u;
+  const uint32_t neg = (k == 1 && h == 0) ? ~0u : 0u;
+  fp w;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) w.v[i] = v.v[i] + ((vo.v[i] & use) ^ neg) + (CsConst::Z4.v[i] + (neg & 1u));
+  cs_carry(w);
+  const bool odd = (k & 1) != 0;
+  const uint32_t sa = odd ? 0u : ~0u;
+  fp x;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    const uint32_t d = (odd ? CsConst::D28P.v[i] : CsConst::D28M.v[i]) + (sa & 1u);
+    x.v[i] = 3u * w.v[i] + ((a.v[i] << 1) ^ sa) + d;
+  }
+  cs_carry(x);
+  fp_reduce64(r, x);
+}

@@ -17,6 +17,7 @@
 // exactly (same GT element; tests/test_bls_gpu.py and tests/test_relic_gpu.py against the
 // Python oracle).
 #pragma once
+#include "bn254_cycsq.h"
 #include "bn254_pair12.h"
 
 struct P36 {
@@ -135,36 +136,23 @@ __device__ __forceinline__ void p36_sqr(fp& r, const fp& a, const P36& g) {
 // Granger-Scott cyclotomic squaring (p6_cyc_sqr's formulas): s = 0, 1, 2 square x, y, x + y
 // (one component each), then P = x^2 + xi y^2 (even k) or Q = (x + y)^2 - x^2 - y^2 (odd k)
 __device__ __forceinline__ void p36_cyc_sqr(fp& r, const fp& a, const P36& g) {
+  // lazy form (bn254_cycsq.h): 4 gathers of 9 limbs, one Fp multiplication, one reduction
   const int sx = (g.k == 0 || g.k == 3) ? 0 : ((g.k == 1 || g.k == 4) ? 2 : 1);
-  fp fm, fo, ym, yo;
-  p36_fetch(fm, fo, a, g.s == 1 ? sx + 3 : sx, g);
-  p36_fetch(ym, yo, a, sx + 3, g);
-  fp wm, wo, sm, so;
-  f_add(sm, fm, ym);
-  f_add(so, fo, yo);
-  wm = g.s == 2 ? sm : fm;
-  wo = g.s == 2 ? so : fo;
-  fp prod;
-  p12_csqr(prod, wm, wo, g.h);
   const bool odd = (g.k & 1) != 0;
-  fp X2, Y2, G3;
-  fp_shfl(X2, prod, p36_src(g.k, g.h, 0));
-  fp_shfl(Y2, prod, p36_src(g.k, g.h, 1));
-  fp_shfl(G3, prod, odd ? p36_src(g.k, g.h, 2) : p36_src(g.k, 1 - g.h, 1));  // (x+y)^2_h | y^2_h'
-  fp p, q;
-  p12_cxi(p, Y2, G3, g.h);
-  f_add(p, X2, p);  // P = x^2 + xi y^2
-  f_sub(q, G3, X2);
-  f_sub(q, q, Y2);  // Q = 2xy
-  fp v = odd ? q : p;
-  fp vx;
-  p36_xi(vx, v, g);  // t C^2 term for k = 1
-  fp_sel(v, vx, g.k == 1);
-  fp three, two;
-  f_add(three, v, v);
-  f_add(three, three, v);
-  f_add(two, a, a);
-  f_addsub(r, three, two, odd);
+  fp t, R, Wm, Wo, U, V, T, X2, Y2, G3, v, vo;
+  fp_shfl(t, a, p36_src(g.k < 3 ? g.k + 3 : g.k - 3, g.h, g.s));
+  cs_pre(R, a, t, g.s);
+  const int c = g.s == 1 ? sx + 3 : sx;
+  fp_shfl(Wm, R, p36_src(c, g.h, g.s));
+  fp_shfl(Wo, R, p36_src(c, 1 - g.h, g.s));
+  cs_operands(U, V, Wm, Wo, g.h);
+  f_mul(T, U, V);
+  fp_shfl(X2, T, p36_src(g.k, g.h, 0));
+  fp_shfl(Y2, T, p36_src(g.k, g.h, 1));
+  fp_shfl(G3, T, odd ? p36_src(g.k, g.h, 2) : p36_src(g.k, 1 - g.h, 1));  // (x+y)^2_h | y^2_h'
+  cs_combine(v, X2, Y2, G3, g.k, g.h);
+  fp_shfl(vo, v, p36_src(g.k, 1 - g.h, g.s));
+  cs_finish(r, v, vo, a, g.k, g.h);
 }
 
 __device__ __forceinline__ void p36_coef(fp& m, fp& o, const uint32_t* c, int h) {

@@ -6,6 +6,7 @@
 #include <vector>
 
 #include "bls_ops.h"
+#include "bn254_cycsq.h"
 
 static void fp12_flat(uint8_t* out, const fp12& x) {  // 12 x 32-byte big-endian, oracle basis
   const fp2* e[6] = {&x.c0.c0, &x.c1.c0, &x.c0.c1, &x.c1.c1, &x.c0.c2, &x.c1.c2};
@@ -58,6 +59,114 @@ int shim_fp_inv(const uint8_t* x32, uint8_t* out_var, uint8_t* out_fermat) {
   f_to_words(w2, r2);
   words_to_be32(out_fermat, w2);
   return std::memcmp(w, w2, sizeof w) == 0 ? 1 : 0;
+}
+
+// ---- the lazy cyclotomic squaring (bn254_cycsq.h) on an emulated pair36 wave ----------------
+static uint64_t sm64(uint64_t& x) {
+  uint64_t z = (x += 0x9e3779b97f4a7c15ull);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+static void fp_random(fp& r, uint64_t& st) {
+  uint32_t w[8];
+  for (int i = 0; i < 8; i++) w[i] = (uint32_t)sm64(st);
+  w[7] &= 0x1fffffffu;  // < 2^253 < p
+  f_from_words(r, w);
+}
+static int cs_src(int k, int h, int s) { return 12 * s + 2 * k + h; }
+static fp2* fp12_coef(fp12& x, int k) {
+  fp2* e[6] = {&x.c0.c0, &x.c1.c0, &x.c0.c1, &x.c1.c1, &x.c0.c2, &x.c1.c2};
+  return e[k];
+}
+// normalised limbs and value < 2q
+static bool fp_reduced(const fp& x) {
+  for (int i = 0; i < BN_LIMBS - 1; i++)
+    if (x.v[i] > BN_MASK) return false;
+  uint32_t q2[BN_LIMBS];
+  f_2q<FpParams>(q2);
+  for (int i = BN_LIMBS - 1; i >= 0; i--) {
+    if (x.v[i] != q2[i]) return x.v[i] < q2[i];
+  }
+  return false;
+}
+
+// fp_reduce64 on raw limbs x9 -> out9; returns 1 when the output is normalised and < 2q
+int shim_fp_reduce64(const uint32_t* x9, uint32_t* out9) {
+  fp x, r;
+  std::memcpy(x.v, x9, sizeof x.v);
+  fp_reduce64(r, x);
+  std::memcpy(out9, r.v, sizeof r.v);
+  return fp_reduced(r) ? 1 : 0;
+}
+
+// f_mul on raw limbs (the cyclotomic squaring's unreduced operands); 1 when normalised, < 2q
+int shim_fp_mul_raw(const uint32_t* a9, const uint32_t* b9, uint32_t* out9) {
+  fp a, b, r;
+  std::memcpy(a.v, a9, sizeof a.v);
+  std::memcpy(b.v, b9, sizeof b.v);
+  f_mul(r, a, b);
+  std::memcpy(out9, r.v, sizeof r.v);
+  return fp_reduced(r) ? 1 : 0;
+}
+
+// A random element of the cyclotomic subgroup (f^((p^6 - 1)(p^2 + 1))) squared `iters` times by
+// the lane stages of p36_cyc_sqr over an emulated 36-lane wave, against fp12_sqr.  Returns 1 on
+// success; -1 a lane left the reduced form, -2 the sub-lane replicas differ, -3 a value differs.
+int shim_cyc_sqr_emul(uint64_t seed, int iters) {
+  uint64_t st = seed;
+  fp12 f, fi, g, t;
+  for (int k = 0; k < 6; k++) {
+    fp_random(fp12_coef(f, k)->a, st);
+    fp_random(fp12_coef(f, k)->b, st);
+  }
+  fp12_inv(fi, f);
+  fp12_conj(g, f);
+  fp12_mul(g, g, fi);
+  fp12_frob2(t, g);
+  fp12_mul(g, t, g);
+  fp lane[36];
+  for (int L = 0; L < 36; L++) {
+    const int c = L % 12, k = c >> 1, h = c & 1;
+    const fp2* e = fp12_coef(g, k);
+    lane[L] = h ? e->b : e->a;
+  }
+  fp12 ref = g;
+  for (int it = 0; it < iters; it++) {
+    fp R[36], T[36], v[36], r[36];
+    for (int L = 0; L < 36; L++) {
+      const int c = L % 12, s = L / 12, k = c >> 1, h = c & 1;
+      cs_pre(R[L], lane[L], lane[cs_src(k < 3 ? k + 3 : k - 3, h, s)], s);
+    }
+    for (int L = 0; L < 36; L++) {
+      const int c = L % 12, s = L / 12, k = c >> 1, h = c & 1;
+      const int sx = (k == 0 || k == 3) ? 0 : ((k == 1 || k == 4) ? 2 : 1);
+      const int cc = s == 1 ? sx + 3 : sx;
+      fp U, V;
+      cs_operands(U, V, R[cs_src(cc, h, s)], R[cs_src(cc, 1 - h, s)], h);
+      f_mul(T[L], U, V);
+    }
+    for (int L = 0; L < 36; L++) {
+      const int c = L % 12, k = c >> 1, h = c & 1;
+      const bool odd = (k & 1) != 0;
+      cs_combine(v[L], T[cs_src(k, h, 0)], T[cs_src(k, h, 1)], odd ? T[cs_src(k, h, 2)] : T[cs_src(k, 1 - h, 1)], k, h);
+    }
+    for (int L = 0; L < 36; L++) {
+      const int c = L % 12, s = L / 12, k = c >> 1, h = c & 1;
+      cs_finish(r[L], v[L], v[cs_src(k, 1 - h, s)], lane[L], k, h);
+    }
+    for (int L = 0; L < 36; L++) {
+      if (!fp_reduced(r[L])) return -1;
+      if (std::memcmp(&r[L], &r[L % 12], sizeof(fp)) != 0) return -2;
+      lane[L] = r[L];
+    }
+    fp12_sqr(ref, ref);
+  }
+  for (int k = 0; k < 6; k++) {
+    const fp2* e = fp12_coef(ref, k);
+    if (!f_eq(lane[2 * k], e->a) || !f_eq(lane[2 * k + 1], e->b)) return -3;
+  }
+  return 1;
 }
 
 int shim_g1_decompress(const uint8_t* in33, uint8_t* out64) {

@@ -45,3 +45,65 @@ def test_fp_addsub_matches_add_and_sub(shim):
         vals = [int.from_bytes(out.raw[32 * k:32 * k + 32], "big") for k in range(4)]
         assert vals == [(a + b) % P, (a - b) % P, (a + b) % P, (a - b) % P]
         assert same == 1
+
+
+def _limbs(x, n=9):
+    return [(x >> (29 * i)) & (2**29 - 1) for i in range(n - 1)] + [x >> 232]
+
+
+def _val(l):
+    return sum(int(v) << (29 * i) for i, v in enumerate(l))
+
+
+def test_fp_reduce64_edges(shim):
+    """fp_reduce64 (bn254_cycsq.h): x mod q below 2q for every 0 <= x < 64q, including the values
+    on each side of every multiple of q (where the top-limb estimate of the multiple is off by one)."""
+    rng = random.Random(0x64)
+    xs = [0, 1, 64 * P - 1] + [k * P + d for k in range(1, 64) for d in (-2, -1, 0, 1)]
+    xs += [rng.randrange(64 * P) for _ in range(3000)] + [(k * P) | (2**232 - 1) for k in range(1, 63)]
+    arr = ctypes.c_uint32 * 9
+    for x in xs:
+        if not 0 <= x < 64 * P:
+            continue
+        limbs = _limbs(x)
+        out = arr()
+        ok = shim.shim_fp_reduce64(arr(*limbs), out)
+        assert ok == 1, hex(x)
+        r = _val(out)
+        assert r % P == x % P and r < 2 * P, hex(x)
+    # low limbs up to 2^29 + 7 (the carried form of the squaring's last stage)
+    for _ in range(2000):
+        lo = [2**29 + rng.randrange(8) if rng.random() < 0.5 else rng.randrange(2**29) for _ in range(8)]
+        top = rng.randrange((60 * P - _val(lo + [0])) >> 232)
+        limbs = lo + [top]
+        out = arr()
+        assert shim.shim_fp_reduce64(arr(*limbs), out) == 1
+        assert _val(out) % P == _val(limbs) % P
+
+
+def test_fp_mul_raw_operand_bounds(shim):
+    """f_mul with the squaring's unreduced operands (bn254_cycsq.h: cs_operands): U with every low
+    limb up to 2^31 - 1 and value < 8q, V normalised < 8q -> U V 2^-261 mod q, below 1.3q."""
+    rng = random.Random(0x31)
+    arr = ctypes.c_uint32 * 9
+    RINV = pow(2**261, -1, P)
+    for it in range(1500):
+        lo = [rng.randrange(2**31 - 2**29, 2**31) if it % 2 else 2**31 - 1 for _ in range(8)]
+        low = _val(lo + [0])
+        top_max = (8 * P - 1 - low) >> 232
+        u = lo + [rng.randrange(top_max + 1) if it % 3 else top_max]
+        v = rng.randrange(8 * P) if it % 5 else 8 * P - 1
+        out = arr()
+        assert shim.shim_fp_mul_raw(arr(*u), arr(*_limbs(v)), out) == 1
+        r = _val(out)
+        assert r % P == _val(u) * v * RINV % P
+        assert r < 13 * P // 10
+
+
+def test_cyclotomic_square_lane_emulation(shim):
+    """p36_cyc_sqr's lane stages (cs_pre, cs_operands, f_mul, cs_combine, cs_finish) over an
+    emulated 36-lane wave, 186 squarings deep (the three x^u chains of a final exponentiation)
+    from random cyclotomic elements, equal fp12_sqr; every lane stays reduced, replicas agree."""
+    shim.shim_cyc_sqr_emul.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    for seed in range(1, 9):
+        assert shim.shim_cyc_sqr_emul(seed, 186 if seed < 3 else 20) == 1, seed
