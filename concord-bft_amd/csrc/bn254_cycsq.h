@@ -188,3 +188,76 @@ BN_HD void cs_finish(fp& r, const fp& v, const fp& vo, const fp& a, int k, int h
   cs_carry(x);
   fp_reduce64(r, x);
 }
+
+// ---- the lazy Fp12 multiplication (bn254_pair36.h: p36_mul) ------------------------------
+// Lane (k, h, s) forms the terms i = 2s, 2s + 1 of c_k = sum_i a_i b_{k-i} (xi on wrap), each an
+// Fp2 product's component h from two Fp multiplications (t1 = u b_m, t2 = v b_o, all < 1.02 q:
+// inputs < 2q); the sums stay unreduced up to one reduction after the sub-lane sum.
+
+struct CmConst {
+  static constexpr CsLimbs Z2 = cs_redundant(0, 1 << 30);  // cm_terms: up to two negated terms
+  static constexpr CsLimbs Z1 = cs_redundant(0, 1 << 29);  // cm_xi: one negated term
+};
+
+// stage 1: e_t = t1_t + t2_t (h = 1) | t1_t - t2_t (h = 0), summed into acc (no wrap) or accw (wrap).
+// Low limbs of e in (-2^29, 2^30); Z2 keeps them >= 0, below 3.5 2^30; both carried.
+BN_HD void cm_terms(fp& acc, fp& accw, const fp& t1a, const fp& t2a, const fp& t1b, const fp& t2b, int h, bool wa,
+                    bool wb) {
+  const uint32_t sg = h ? 0u : ~0u;
+  const uint32_t ma = wa ? ~0u : 0u, mb = wb ? ~0u : 0u;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    const uint32_t ea = t1a.v[i] + (t2a.v[i] ^ sg) + (sg & 1u);
+    const uint32_t eb = t1b.v[i] + (t2b.v[i] ^ sg) + (sg & 1u);
+    acc.v[i] = CmConst::Z2.v[i] + (ea & ~ma) + (eb & ~mb);
+    accw.v[i] = CmConst::Z2.v[i] + (ea & ma) + (eb & mb);
+  }
+  cs_carry(acc);
+  cs_carry(accw);
+}
+
+// stage 2: z = acc + xi accw, my component (xi = 1 + i: accw +- the other component's accw, ao)
+BN_HD void cm_xi(fp& z, const fp& acc, const fp& accw, const fp& ao, int h) {
+  const uint32_t sg = h ? 0u : ~0u;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) z.v[i] = acc.v[i] + accw.v[i] + (ao.v[i] ^ sg) + (CmConst::Z1.v[i] + (sg & 1u));
+  cs_carry(z);
+}
+
+// stage 3: r = z_0 + z_1 + z_2 over the sub-lanes (|sum| < 24.5 q) + 28 q, reduced below 2q
+BN_HD void cm_sum3(fp& r, const fp& z0, const fp& z1, const fp& z2) {
+  fp x;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) x.v[i] = z0.v[i] + z1.v[i] + (z2.v[i] + CsConst::D28P.v[i]);
+  cs_carry(x);
+  fp_reduce64(r, x);
+}
+
+// ---- the lazy Fp12 squaring (bn254_pair36.h: p36_sqr) ------------------------------------
+// Two multiplications per lane: diag (even k, s = 0) squares x = a_f1 and z = a_f2 (component h:
+// (m + o)(m - o) for h = 0, (2m) o for h = 1); a cross lane forms 2 (x z)_h = (2u) z_m +- (2v) z_o
+// (u = h ? x_o : x_m, v = h ? x_m : x_o).  The doublings ride in the raw left operands (limbs
+// < 2^30, values < 4q); the right operands are carried (m - o + 2q: Q2R's low limbs >= 2^29).
+// Products < 16 q^2 / 2^261 + q < 1.08 q.  The products then go through cm_terms (diag: x^2 term
+// to acc, z^2 term to accw; cross: P1 +- P2 to acc or accw), cm_xi and cm_sum3 (sum < 26 q).
+struct SqConst {
+  static constexpr CsLimbs Q2R = cs_redundant(2, 1 << 29);
+};
+BN_HD void sq_operands(fp& U1, fp& V1, fp& U2, fp& V2, const fp& xm, const fp& xo, const fp& zm, const fp& zo,
+                       bool diag, int h) {
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    const uint32_t du1 = xm.v[i] + (h ? xm.v[i] : xo.v[i]);
+    const uint32_t dv1 = h ? xo.v[i] : xm.v[i] - xo.v[i] + SqConst::Q2R.v[i];
+    const uint32_t du2 = zm.v[i] + (h ? zm.v[i] : zo.v[i]);
+    const uint32_t dv2 = h ? zo.v[i] : zm.v[i] - zo.v[i] + SqConst::Q2R.v[i];
+    const uint32_t cu1 = (h ? xo.v[i] : xm.v[i]) << 1;
+    const uint32_t cu2 = (h ? xm.v[i] : xo.v[i]) << 1;
+    U1.v[i] = diag ? du1 : cu1;
+    V1.v[i] = diag ? dv1 : zm.v[i];
+    U2.v[i] = diag ? du2 : cu2;
+    V2.v[i] = diag ? dv2 : zo.v[i];
+  }
+  cs_carry(V1);
+  cs_carry(V2);
+}

@@ -63,29 +63,32 @@ __device__ __forceinline__ void p36_xi(fp& r, const fp& z, const P36& g) {
   p12_cxi(r, z, zo, g.h);
 }
 
-// r = a * b: sub-lane s forms the terms i = 2s, 2s + 1 of c_k = sum_i a_i b_{k-i} (xi on wrap)
+// r = a * b: sub-lane s forms the terms i = 2s, 2s + 1 of c_k = sum_i a_i b_{k-i} (xi on wrap);
+// lazy sums and one reduction (bn254_cycsq.h: cm_terms, cm_xi, cm_sum3)
 __device__ __forceinline__ void p36_mul(fp& r, const fp& a, const fp& b, const P36& g) {
-  fp acc, accw;
-  f_zero(acc);
-  f_zero(accw);
+  fp T[4];
+  bool wrap[2];
 #pragma unroll
   for (int t = 0; t < 2; t++) {
     const int i = 2 * g.s + t;
     int j = g.k - i;
-    const bool wrap = j < 0;
-    if (wrap) j += 6;
-    fp am, ao, bm, bo, p, q;
+    wrap[t] = j < 0;
+    if (wrap[t]) j += 6;
+    fp am, ao, bm, bo;
     p36_fetch(am, ao, a, i, g);
     p36_fetch(bm, bo, b, j, g);
-    p12_cmul(p, am, ao, bm, bo, g.h);
-    f_add(q, wrap ? accw : acc, p);
-    fp_sel(acc, q, !wrap);
-    fp_sel(accw, q, wrap);
+    const fp u = g.h ? ao : am, v = g.h ? am : ao;
+    f_mul(T[2 * t], u, bm);
+    f_mul(T[2 * t + 1], v, bo);
   }
-  fp w;
-  p36_xi(w, accw, g);
-  f_add(acc, acc, w);
-  p36_sum3(r, acc, g);
+  fp acc, accw, ao, z, z0, z1, z2;
+  cm_terms(acc, accw, T[0], T[1], T[2], T[3], g.h, wrap[0], wrap[1]);
+  fp_shfl(ao, accw, p36_src(g.k, 1 - g.h, g.s));
+  cm_xi(z, acc, accw, ao, g.h);
+  fp_shfl(z0, z, p36_src(g.k, g.h, 0));
+  fp_shfl(z1, z, p36_src(g.k, g.h, 1));
+  fp_shfl(z2, z, p36_src(g.k, g.h, 2));
+  cm_sum3(r, z0, z1, z2);
 }
 
 // r = a^2 (the term table kP12Sq of bn254_pair12.h).  Even k: s = 0 squares the two diagonal
@@ -101,36 +104,21 @@ __device__ __forceinline__ void p36_sqr(fp& r, const fp& a, const P36& g) {
   fp xm, xo, zm, zo;
   p36_fetch(xm, xo, a, f1, g);
   p36_fetch(zm, zo, a, f2, g);
-  fp s1, d1, s2, d2;
-  f_add(s1, xm, xo);
-  f_sub(d1, xm, xo);
-  f_add(s2, zm, zo);
-  f_sub(d2, zm, zo);
-  // diag: (h ? x1 x0 : (x0 + x1)(x0 - x1)), same for z;  cross: split product (x * z)_h
-  fp X1 = diag ? (g.h ? xm : s1) : (g.h ? xo : xm);
-  fp Y1 = diag ? (g.h ? xo : d1) : zm;
-  fp X2 = diag ? (g.h ? zm : s2) : (g.h ? xm : xo);
-  fp Y2 = diag ? (g.h ? zo : d2) : zo;
-  fp P1, P2;
-  f_mul(P1, X1, Y1);
-  f_mul(P2, X2, Y2);
-  fp acc, accw;
-  // diag: acc = (h ? 2 P1 : P1), accw = (h ? 2 P2 : P2) (the second diagonal term wraps)
-  // cross: T = 2 (h ? P1 + P2 : P1 - P2), into accw if it wraps
-  f_add(s1, P1, P1);
-  f_add(s2, P2, P2);
-  fp dA = g.h ? s1 : P1, dB = g.h ? s2 : P2;
-  fp c;
-  f_addsub(c, P1, P2, g.h != 0);
-  f_add(c, c, c);
-  fp zero;
+  // lazy form (bn254_cycsq.h: sq_operands, then p36_mul's cm_* stages)
+  fp U1, V1, U2, V2, P1, P2;
+  sq_operands(U1, V1, U2, V2, xm, xo, zm, zo, diag, g.h);
+  f_mul(P1, U1, V1);
+  f_mul(P2, U2, V2);
+  fp zero, acc, accw, ao, z, z0, z1, z2;
   f_zero(zero);
-  acc = diag ? dA : (cwrap ? zero : c);
-  accw = diag ? dB : (cwrap ? c : zero);
-  fp w;
-  p36_xi(w, accw, g);
-  f_add(acc, acc, w);
-  p36_sum3(r, acc, g);
+  // diag: x^2 term -> acc, z^2 term -> accw (the second diagonal term wraps); cross: P1 +- P2
+  cm_terms(acc, accw, P1, diag ? zero : P2, diag ? P2 : zero, zero, g.h, !diag && cwrap, true);
+  fp_shfl(ao, accw, p36_src(g.k, 1 - g.h, g.s));
+  cm_xi(z, acc, accw, ao, g.h);
+  fp_shfl(z0, z, p36_src(g.k, g.h, 0));
+  fp_shfl(z1, z, p36_src(g.k, g.h, 1));
+  fp_shfl(z2, z, p36_src(g.k, g.h, 2));
+  cm_sum3(r, z0, z1, z2);
 }
 
 // Granger-Scott cyclotomic squaring (p6_cyc_sqr's formulas): s = 0, 1, 2 square x, y, x + y

@@ -169,6 +169,127 @@ int shim_cyc_sqr_emul(uint64_t seed, int iters) {
   return 1;
 }
 
+// p36_mul's lane stages (cm_terms, cm_xi, cm_sum3) over an emulated 36-lane wave: x <- x * y
+// `iters` times from random x, y, against fp12_mul.  Return codes as shim_cyc_sqr_emul.
+int shim_p36_mul_emul(uint64_t seed, int iters) {
+  uint64_t st = seed;
+  fp12 x, y;
+  for (int k = 0; k < 6; k++) {
+    fp_random(fp12_coef(x, k)->a, st);
+    fp_random(fp12_coef(x, k)->b, st);
+    fp_random(fp12_coef(y, k)->a, st);
+    fp_random(fp12_coef(y, k)->b, st);
+  }
+  fp la[36], lb[36];
+  for (int L = 0; L < 36; L++) {
+    const int c = L % 12, k = c >> 1, h = c & 1;
+    la[L] = h ? fp12_coef(x, k)->b : fp12_coef(x, k)->a;
+    lb[L] = h ? fp12_coef(y, k)->b : fp12_coef(y, k)->a;
+  }
+  fp12 ref = x;
+  for (int it = 0; it < iters; it++) {
+    fp acc[36], accw[36], z[36], r[36];
+    for (int L = 0; L < 36; L++) {
+      const int c = L % 12, s = L / 12, k = c >> 1, h = c & 1;
+      fp T[4];
+      bool wrap[2];
+      for (int t = 0; t < 2; t++) {
+        const int i = 2 * s + t;
+        int j = k - i;
+        wrap[t] = j < 0;
+        if (wrap[t]) j += 6;
+        const fp& am = la[cs_src(i, h, s)];
+        const fp& ao = la[cs_src(i, 1 - h, s)];
+        const fp& bm = lb[cs_src(j, h, s)];
+        const fp& bo = lb[cs_src(j, 1 - h, s)];
+        f_mul(T[2 * t], h ? ao : am, bm);
+        f_mul(T[2 * t + 1], h ? am : ao, bo);
+      }
+      cm_terms(acc[L], accw[L], T[0], T[1], T[2], T[3], h, wrap[0], wrap[1]);
+    }
+    for (int L = 0; L < 36; L++) {
+      const int c = L % 12, s = L / 12, k = c >> 1, h = c & 1;
+      cm_xi(z[L], acc[L], accw[L], accw[cs_src(k, 1 - h, s)], h);
+    }
+    for (int L = 0; L < 36; L++) {
+      const int c = L % 12, k = c >> 1, h = c & 1;
+      cm_sum3(r[L], z[cs_src(k, h, 0)], z[cs_src(k, h, 1)], z[cs_src(k, h, 2)]);
+    }
+    for (int L = 0; L < 36; L++) {
+      if (!fp_reduced(r[L])) return -1;
+      if (std::memcmp(&r[L], &r[L % 12], sizeof(fp)) != 0) return -2;
+      la[L] = r[L];
+    }
+    fp12_mul(ref, ref, y);
+  }
+  for (int k = 0; k < 6; k++) {
+    const fp2* e = fp12_coef(ref, k);
+    if (!f_eq(la[2 * k], e->a) || !f_eq(la[2 * k + 1], e->b)) return -3;
+  }
+  return 1;
+}
+
+// p36_sqr's lane stages (sq_operands, cm_terms, cm_xi, cm_sum3) over an emulated wave: x <- x^2
+// `iters` times from a random (non-cyclotomic) x, against fp12_sqr.  kSq = bn254_pair12.h's
+// kP12Sq term table (i, j, flags: bit 1 = times xi), repeated here for the host build.
+static const uint8_t kSq[6][4][3] = {
+    {{0, 0, 4}, {3, 3, 6}, {1, 5, 7}, {2, 4, 7}}, {{0, 1, 5}, {2, 5, 7}, {3, 4, 7}, {0, 0, 0}},
+    {{1, 1, 4}, {4, 4, 6}, {0, 2, 5}, {3, 5, 7}}, {{0, 3, 5}, {1, 2, 5}, {4, 5, 7}, {0, 0, 0}},
+    {{2, 2, 4}, {5, 5, 6}, {0, 4, 5}, {1, 3, 5}}, {{0, 5, 5}, {1, 4, 5}, {2, 3, 5}, {0, 0, 0}},
+};
+int shim_p36_sqr_emul(uint64_t seed, int iters) {
+  uint64_t st = seed;
+  fp12 x;
+  for (int k = 0; k < 6; k++) {
+    fp_random(fp12_coef(x, k)->a, st);
+    fp_random(fp12_coef(x, k)->b, st);
+  }
+  fp la[36];
+  for (int L = 0; L < 36; L++) {
+    const int c = L % 12, k = c >> 1, h = c & 1;
+    la[L] = h ? fp12_coef(x, k)->b : fp12_coef(x, k)->a;
+  }
+  fp12 ref = x;
+  fp zero;
+  f_zero(zero);
+  for (int it = 0; it < iters; it++) {
+    fp acc[36], accw[36], z[36], r[36];
+    for (int L = 0; L < 36; L++) {
+      const int c = L % 12, s = L / 12, k = c >> 1, h = c & 1;
+      const bool even = (k & 1) == 0, diag = even && s == 0;
+      const int tt = even ? s + 1 : s;
+      const int f1 = diag ? kSq[k][0][0] : kSq[k][tt][0];
+      const int f2 = diag ? kSq[k][1][0] : kSq[k][tt][1];
+      const bool cwrap = (kSq[k][tt][2] & 2) != 0;
+      fp U1, V1, U2, V2, P1, P2;
+      sq_operands(U1, V1, U2, V2, la[cs_src(f1, h, s)], la[cs_src(f1, 1 - h, s)], la[cs_src(f2, h, s)],
+                  la[cs_src(f2, 1 - h, s)], diag, h);
+      f_mul(P1, U1, V1);
+      f_mul(P2, U2, V2);
+      cm_terms(acc[L], accw[L], P1, diag ? zero : P2, diag ? P2 : zero, zero, h, !diag && cwrap, true);
+    }
+    for (int L = 0; L < 36; L++) {
+      const int c = L % 12, s = L / 12, k = c >> 1, h = c & 1;
+      cm_xi(z[L], acc[L], accw[L], accw[cs_src(k, 1 - h, s)], h);
+    }
+    for (int L = 0; L < 36; L++) {
+      const int c = L % 12, k = c >> 1, h = c & 1;
+      cm_sum3(r[L], z[cs_src(k, h, 0)], z[cs_src(k, h, 1)], z[cs_src(k, h, 2)]);
+    }
+    for (int L = 0; L < 36; L++) {
+      if (!fp_reduced(r[L])) return -1;
+      if (std::memcmp(&r[L], &r[L % 12], sizeof(fp)) != 0) return -2;
+      la[L] = r[L];
+    }
+    fp12_sqr(ref, ref);
+  }
+  for (int k = 0; k < 6; k++) {
+    const fp2* e = fp12_coef(ref, k);
+    if (!f_eq(la[2 * k], e->a) || !f_eq(la[2 * k + 1], e->b)) return -3;
+  }
+  return 1;
+}
+
 int shim_g1_decompress(const uint8_t* in33, uint8_t* out64) {
   g1a a;
   if (!g1_decompress(a, in33)) return 0;

@@ -107,3 +107,19 @@ def test_cyclotomic_square_lane_emulation(shim):
     shim.shim_cyc_sqr_emul.argtypes = [ctypes.c_uint64, ctypes.c_int]
     for seed in range(1, 9):
         assert shim.shim_cyc_sqr_emul(seed, 186 if seed < 3 else 20) == 1, seed
+
+
+def test_fp12_mul_lane_emulation(shim):
+    """p36_mul's lane stages (cm_terms, cm_xi, cm_sum3) over an emulated 36-lane wave, chained
+    60 multiplications deep from random (non-cyclotomic) elements, equal fp12_mul."""
+    shim.shim_p36_mul_emul.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    for seed in range(1, 9):
+        assert shim.shim_p36_mul_emul(seed, 60 if seed < 3 else 5) == 1, seed
+
+
+def test_fp12_sqr_lane_emulation(shim):
+    """p36_sqr's lane stages (sq_operands + the cm_* stages) over an emulated 36-lane wave, 64
+    squarings deep (a Miller loop's worth) from random elements, equal fp12_sqr."""
+    shim.shim_p36_sqr_emul.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    for seed in range(1, 9):
+        assert shim.shim_p36_sqr_emul(seed, 64 if seed < 3 else 5) == 1, seed
