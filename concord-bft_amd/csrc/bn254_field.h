@@ -351,12 +351,78 @@ BN_HD void f_inv_fp(Fe<F>& r, const Fe<F>& a) {
   f_pow(r, a, e);
 }
 
+// Left-to-right sliding-window schedule (window 4) of a fixed public exponent: acc = a^v[0],
+// then for each further window nsq[w] squarings and a multiplication by a^v[w] (v odd, < 16),
+// then `tail` squarings.  Built at compile time; the schedule depends on the exponent only.
+struct SwSchedule {
+  int n, tail;
+  uint8_t nsq[80], v[80];
+};
+constexpr SwSchedule sw_schedule(const uint32_t (&e)[8]) {
+  SwSchedule s{};
+  int i = 255;
+  while (!((e[i >> 5] >> (i & 31)) & 1u)) i--;
+  int pend = 0;  // squarings owed before the next window
+  while (i >= 0) {
+    if (!((e[i >> 5] >> (i & 31)) & 1u)) {
+      pend++;
+      i--;
+      continue;
+    }
+    int j = i - 3 < 0 ? 0 : i - 3;
+    while (!((e[j >> 5] >> (j & 31)) & 1u)) j++;
+    uint32_t v = 0;
+    for (int b = i; b >= j; b--) v = 2 * v + ((e[b >> 5] >> (b & 31)) & 1u);
+    s.nsq[s.n] = (uint8_t)(s.n == 0 ? 0 : pend + (i - j + 1));
+    s.v[s.n] = (uint8_t)v;
+    s.n++;
+    pend = 0;
+    i = j - 1;
+  }
+  s.tail = pend;
+  return s;
+}
+struct FpSqrtSchedule {
+  static constexpr SwSchedule S = sw_schedule(FpExp::SQRT);  // 19 windows instead of 42 multiplications
+};
+
+// a^e for the schedule S: 8 odd powers a, a^3, .., a^15, then the windows (the table entry is
+// picked by a wave-uniform switch, so it stays in registers)
+template <class F, class Sched>
+BN_HDN void f_pow_sw(Fe<F>& r, const Fe<F>& a) {
+  Fe<F> t[8], a2, acc;
+  t[0] = a;
+  f_sqr(a2, a);
+#pragma unroll
+  for (int k = 1; k < 8; k++) f_mul(t[k], t[k - 1], a2);
+  for (int w = 0; w < Sched::S.n; w++) {
+    for (int q = 0; q < Sched::S.nsq[w]; q++) f_sqr(acc, acc);
+    const int idx = Sched::S.v[w] >> 1;
+    if (w == 0) {
+      acc = t[0];
+#pragma unroll
+      for (int k = 1; k < 8; k++)
+        if (idx == k) acc = t[k];
+      continue;
+    }
+    switch (idx) {
+      case 0: f_mul(acc, acc, t[0]); break;
+      case 1: f_mul(acc, acc, t[1]); break;
+      case 2: f_mul(acc, acc, t[2]); break;
+      case 3: f_mul(acc, acc, t[3]); break;
+      case 4: f_mul(acc, acc, t[4]); break;
+      case 5: f_mul(acc, acc, t[5]); break;
+      case 6: f_mul(acc, acc, t[6]); break;
+      default: f_mul(acc, acc, t[7]); break;
+    }
+  }
+  for (int q = 0; q < Sched::S.tail; q++) f_sqr(acc, acc);
+  r = acc;
+}
+
 // square root for p = 3 mod 4: y = a^((p+1)/4); returns false if a is not a square
 BN_HDN bool fp_sqrt(fp& y, const fp& a) {
-  uint32_t e[8];
-#pragma unroll
-  for (int i = 0; i < 8; i++) e[i] = FpExp::SQRT[i];
-  f_pow(y, a, e);
+  f_pow_sw<FpParams, FpSqrtSchedule>(y, a);
   fp t;
   f_sqr(t, y);
   return f_eq(t, a);
