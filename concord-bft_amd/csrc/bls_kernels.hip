@@ -346,7 +346,7 @@ __global__ void __launch_bounds__(64) bls_msm_finish_kernel(const uint32_t* part
     return;
   }
   g1a a;
-  g1_to_affine(a, acc);
+  g1_to_affine<true>(a, acc);  // the combined signature is public: variable-time inversion
   if (q == 0) {
     g1_compress(out33, a);
     if (sig_aff) g1a_store(sig_aff, a);

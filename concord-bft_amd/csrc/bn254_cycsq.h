@@ -11,7 +11,7 @@
 // multiples of q) and reduces ONCE, at the end (fp_reduce64: the multiple of q estimated from the
 // top limb, subtracted with 24-bit products).  Every bound is stated at the function.
 #pragma once
-#include "bn254_field.h"
+#include "bn254_pairing.h"  // g1j (the lazy G1 doubling); bn254_field.h for the rest
 
 // ---- constants: k q as limbs, and redundant forms of k q with every low limb >= L ----------
 struct CsLimbs {
@@ -260,4 +260,67 @@ BN_HD void sq_operands(fp& U1, fp& V1, fp& U2, fp& V2, const fp& xm, const fp& x
   }
   cs_carry(V1);
   cs_carry(V2);
+}
+
+// ---- the lazy G1 doubling (bn254_g1quad.h: g1q_dbl, dbl-2009-l, a = 0) --------------------
+// Rounds of products: {A = X^2, B = Y^2, YZ} -> {C = B^2, T2 = t^2, F = E^2} -> {E w}, with
+// E = 3A, t = X + B, D = 2(T2 - A - C), X3 = F - 2D, w = D - X3, Y3 = E w - 8C, Z3 = 2 YZ.
+// Inputs < 2q: A, B, YZ, C < 1.02 q; E < 3.06 q and t < 3.02 q carried (T2, F < 1.04 q).
+// D' = D + 5q in (0.92 q, 7.08 q) is carried, X3 and Y3 are reduced once each (fp_reduce64),
+// w' = D' - X3 + 2q = w + 7q in (0.92 q, 9.08 q) feeds E w' (< 28 q^2: product < 1.13 q).
+struct G1dConst {
+  static constexpr CsLimbs D5 = cs_redundant(5, (int64_t)1 << 31);   // 2T2 - 2A - 2C + 5q
+  static constexpr CsLimbs D16 = cs_redundant(16, (int64_t)1 << 30); // F - 2D' + 16q
+  static constexpr CsLimbs D2 = cs_redundant(2, (int64_t)1 << 29);   // D' - X3 + 2q
+  static constexpr CsLimbs D9 = cs_redundant(9, (int64_t)1 << 29);   // E w' - 8C + 9q
+};
+BN_HD void g1d_et(fp& E, fp& t, const fp& A, const fp& X, const fp& B) {
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    E.v[i] = 3u * A.v[i];
+    t.v[i] = X.v[i] + B.v[i];
+  }
+  cs_carry(E);
+  cs_carry(t);
+}
+BN_HD void g1d_x3w(fp& X3, fp& w, const fp& T2, const fp& A, const fp& C, const fp& F) {
+  fp Dp, x;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) Dp.v[i] = 2u * (T2.v[i] - A.v[i] - C.v[i]) + G1dConst::D5.v[i];
+  cs_carry(Dp);
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) x.v[i] = F.v[i] - 2u * Dp.v[i] + G1dConst::D16.v[i];
+  cs_carry(x);
+  fp_reduce64(X3, x);
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) w.v[i] = Dp.v[i] - X3.v[i] + G1dConst::D2.v[i];
+  cs_carry(w);
+}
+BN_HD void g1d_y3(fp& Y3, const fp& Ew, const fp& C) {
+  fp c8, x;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) c8.v[i] = C.v[i] << 3;
+  cs_carry(c8);
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) x.v[i] = Ew.v[i] - c8.v[i] + G1dConst::D9.v[i];
+  cs_carry(x);
+  fp_reduce64(Y3, x);
+}
+
+// one lane's lazy doubling (the same stages with the products inline): the host check of g1q_dbl
+BN_HD void g1_dbl_lazy(g1j& r, const g1j& p) {
+  fp A, B, YZ, Z3, E, t, C, T2, F, X3, w, Ew;
+  f_mul(A, p.X, p.X);
+  f_mul(B, p.Y, p.Y);
+  f_mul(YZ, p.Y, p.Z);
+  f_add(Z3, YZ, YZ);
+  g1d_et(E, t, A, p.X, B);
+  f_mul(C, B, B);
+  f_mul(T2, t, t);
+  f_mul(F, E, E);
+  g1d_x3w(X3, w, T2, A, C, F);
+  f_mul(Ew, E, w);
+  g1d_y3(r.Y, Ew, C);
+  r.X = X3;
+  r.Z = Z3;
 }

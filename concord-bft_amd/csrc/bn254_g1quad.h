@@ -9,6 +9,7 @@
 // (bn254_pairing.h) as points (same field elements; tests/test_bls_gpu.py compares the
 // combined signature with the oracle byte for byte).
 #pragma once
+#include "bn254_cycsq.h"
 #include "bn254_pairing.h"
 
 template <int CTRL>
@@ -37,7 +38,9 @@ __device__ __forceinline__ void g1q_round(fp* r, const fp* U, const fp* V, int q
   if (N > 3) g1q_bcast<0xFF>(r[3], p);
 }
 
-// r = 2p (dbl-2009-l, a = 0); infinity (Z = 0) stays infinity
+// r = 2p (dbl-2009-l, a = 0); infinity (Z = 0) stays infinity.  Lazy sums between the rounds
+// and one reduction per output coordinate (bn254_cycsq.h: g1d_*, checked on the host as
+// g1_dbl_lazy against g1_dbl).
 __device__ __forceinline__ void g1q_dbl(g1j& r, const g1j& p, int q) {
   fp U[3], V[3], o[3];
   U[0] = p.X;
@@ -49,9 +52,7 @@ __device__ __forceinline__ void g1q_dbl(g1j& r, const g1j& p, int q) {
   g1q_round<3>(o, U, V, q);
   fp A = o[0], B = o[1], E, Z3, t;
   f_add(Z3, o[2], o[2]);
-  f_add(E, A, A);
-  f_add(E, E, A);
-  f_add(t, p.X, B);
+  g1d_et(E, t, A, p.X, B);
   U[0] = B;
   V[0] = B;
   U[1] = t;
@@ -59,20 +60,12 @@ __device__ __forceinline__ void g1q_dbl(g1j& r, const g1j& p, int q) {
   U[2] = E;
   V[2] = E;
   g1q_round<3>(o, U, V, q);
-  fp C = o[0], D, X3, w;
-  f_sub(D, o[1], A);
-  f_sub(D, D, C);
-  f_add(D, D, D);
-  f_sub(X3, o[2], D);
-  f_sub(X3, X3, D);
-  f_sub(w, D, X3);
+  fp C = o[0], X3, w;
+  g1d_x3w(X3, w, o[1], A, C, o[2]);
   U[0] = E;
   V[0] = w;
   g1q_round<1>(o, U, V, q);
-  f_add(C, C, C);
-  f_add(C, C, C);
-  f_add(C, C, C);
-  f_sub(r.Y, o[0], C);
+  g1d_y3(r.Y, o[0], C);
   r.X = X3;
   r.Z = Z3;
 }

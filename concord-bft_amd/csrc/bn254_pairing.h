@@ -133,6 +133,9 @@ BN_HD void g1_from_affine(g1j& r, const g1a& a) {
   f_one(r.Z);
 }
 
+// VAR: variable-time inversion (safegcd) -- only for points that are public anyway (a combined
+// signature, sums of published shares); signing keeps the constant-time Fermat form
+template <bool VAR = false>
 BN_HDN void g1_to_affine(g1a& r, const g1j& p) {
   if (g1_is_inf(p)) {
     r.inf = true;
@@ -141,7 +144,10 @@ BN_HDN void g1_to_affine(g1a& r, const g1j& p) {
     return;
   }
   fp zi, zi2;
-  fp_inv(zi, p.Z);
+  if (VAR)
+    fp_inv_var(zi, p.Z);
+  else
+    fp_inv(zi, p.Z);
   f_sqr(zi2, zi);
   f_mul(r.x, p.X, zi2);
   f_mul(zi2, zi2, zi);

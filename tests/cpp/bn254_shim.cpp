@@ -290,6 +290,28 @@ int shim_p36_sqr_emul(uint64_t seed, int iters) {
   return 1;
 }
 
+// g1_dbl_lazy (the stages of g1q_dbl) against g1_dbl, `iters` doublings deep from g1_map(seed):
+// 1 when every step gives the same affine point and reduced coordinates, else a negative code
+int shim_g1_dbl_lazy(uint64_t seed, int iters) {
+  uint8_t msg[8];
+  for (int i = 0; i < 8; i++) msg[i] = (uint8_t)(seed >> (8 * i));
+  g1a h;
+  g1_map(h, msg, 8);
+  g1j p, q;
+  g1_from_affine(p, h);
+  q = p;
+  for (int it = 0; it < iters; it++) {
+    g1_dbl(p, p);
+    g1_dbl_lazy(q, q);
+    if (!fp_reduced(q.X) || !fp_reduced(q.Y) || !fp_reduced(q.Z)) return -1;
+    g1a a, b;
+    g1_to_affine(a, p);
+    g1_to_affine(b, q);
+    if (a.inf != b.inf || !f_eq(a.x, b.x) || !f_eq(a.y, b.y)) return -3;
+  }
+  return 1;
+}
+
 int shim_g1_decompress(const uint8_t* in33, uint8_t* out64) {
   g1a a;
   if (!g1_decompress(a, in33)) return 0;

@@ -123,3 +123,11 @@ def test_fp12_sqr_lane_emulation(shim):
     shim.shim_p36_sqr_emul.argtypes = [ctypes.c_uint64, ctypes.c_int]
     for seed in range(1, 9):
         assert shim.shim_p36_sqr_emul(seed, 64 if seed < 3 else 5) == 1, seed
+
+
+def test_g1_lazy_doubling_matches(shim):
+    """g1q_dbl's lazy stages (g1d_et, g1d_x3w, g1d_y3; bn254_cycsq.h) as one lane's doubling,
+    300 doublings deep from hashed points, equal g1_dbl as affine points; coordinates reduced."""
+    shim.shim_g1_dbl_lazy.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    for seed in range(1, 7):
+        assert shim.shim_g1_dbl_lazy(seed, 300 if seed < 3 else 30) == 1, seed
