@@ -324,3 +324,15 @@ BN_HD void g1_dbl_lazy(g1j& r, const g1j& p) {
   r.X = X3;
   r.Z = Z3;
 }
+
+// unreduced operand sums (bn254_g2wave.h, bn254_g1quad.h): a + b, and a - b + 2q (low limbs of
+// Q2R >= 2^29 > b_i), for a, b < 2q normalised: limbs < 2^30 / < 1.5 2^30, values < 4q -- f_mul
+// takes either on both sides (tests/test_bn254_inv.py: test_fp_mul_raw_both_operands)
+BN_HD void fl_sum(fp& r, const fp& a, const fp& b) {
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) r.v[i] = a.v[i] + b.v[i];
+}
+BN_HD void fl_diff2q(fp& r, const fp& a, const fp& b) {
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) r.v[i] = a.v[i] - b.v[i] + SqConst::Q2R.v[i];
+}

@@ -93,8 +93,8 @@ __device__ __forceinline__ void g1q_add(g1j& r, const g1j& p, const g1j& qq, int
   const fp U1 = o[0], U2 = o[1];
   fp H, H2, ZS;
   f_sub(H, U2, U1);
-  f_add(H2, H, H);
-  f_add(ZS, p.Z, qq.Z);
+  fl_sum(H2, H, H);  // unreduced operands of H2^2 and ZS^2 (limbs < 2^30, values < 4q)
+  fl_sum(ZS, p.Z, qq.Z);
   U[0] = o[2];
   V[0] = Z2Z2;
   U[1] = o[3];

@@ -14,6 +14,7 @@
 // ((p^12 - 1)/r is a multiple of p^2 - 1), so the pairing is unchanged and no inversion is
 // needed.  bn254_pair36.h evaluates them at the same cost as normalised lines.
 #pragma once
+#include "bn254_cycsq.h"
 #include "bn254_pairing.h"
 
 #define BN_ABC_WORDS 54  // A | B | C (fp2 each)
@@ -39,18 +40,22 @@ __device__ __forceinline__ void g2w_round(fp* r, const fp* U, const fp* V, int l
 }
 
 // operand slots of an Fp2 product x*y (Karatsuba: x0 y0, x1 y1, (x0 + x1)(y0 + y1)) and square
-// x^2 ((x0 + x1)(x0 - x1), x0 x1), written at U/V + o
+// x^2 ((x0 + x1)(x0 - x1), x0 x1), written at U/V + o.  The sums stay unreduced (bn254_cycsq.h:
+// fl_sum / fl_diff2q): limbs < 2^30 (sum) and < 1.5 2^30 (difference), values < 4q, keep
+// f_mul's columns below 2^64 (at most 7 full-size products: 7 1.5 2^60 + 9 2^58 + 2^35) and its
+// result below 2q (16 q^2 < q 2^261), so no reduction is spent on an operand
+// (tests/test_bn254_inv.py: test_fp_mul_raw_both_operands).
 __device__ __forceinline__ void g2w_mul_ops(fp* U, fp* V, int o, const fp2& x, const fp2& y) {
   U[o] = x.a;
   V[o] = y.a;
   U[o + 1] = x.b;
   V[o + 1] = y.b;
-  f_add(U[o + 2], x.a, x.b);
-  f_add(V[o + 2], y.a, y.b);
+  fl_sum(U[o + 2], x.a, x.b);
+  fl_sum(V[o + 2], y.a, y.b);
 }
 __device__ __forceinline__ void g2w_sqr_ops(fp* U, fp* V, int o, const fp2& x) {
-  f_add(U[o], x.a, x.b);
-  f_sub(V[o], x.a, x.b);
+  fl_sum(U[o], x.a, x.b);
+  fl_diff2q(V[o], x.a, x.b);
   U[o + 1] = x.a;
   V[o + 1] = x.b;
 }

@@ -131,3 +131,22 @@ def test_g1_lazy_doubling_matches(shim):
     shim.shim_g1_dbl_lazy.argtypes = [ctypes.c_uint64, ctypes.c_int]
     for seed in range(1, 7):
         assert shim.shim_g1_dbl_lazy(seed, 300 if seed < 3 else 30) == 1, seed
+
+
+def test_fp_mul_raw_both_operands(shim):
+    """f_mul with BOTH operands unreduced as the G2 line rounds build them (bn254_g2wave.h:
+    g2w_mul_ops / g2w_sqr_ops): a + b (limbs < 2^30) times a - b + 2q (limbs < 1.5 2^30), both
+    values < 4q, including every low limb at its maximum -> the product mod q, below 2q."""
+    rng = random.Random(0x2B)
+    arr = ctypes.c_uint32 * 9
+    RINV = pow(2**261, -1, P)
+    for it in range(1500):
+        hi = it % 4 == 0
+        lo_u = [2**30 - 1 if hi else rng.randrange(2**30) for _ in range(8)]
+        lo_v = [3 * 2**29 - 1 if hi else rng.randrange(3 * 2**29) for _ in range(8)]
+        u = lo_u + [rng.randrange(((4 * P - 1 - _val(lo_u + [0])) >> 232) + 1)]
+        v = lo_v + [rng.randrange(((4 * P - 1 - _val(lo_v + [0])) >> 232) + 1)]
+        assert _val(u) < 4 * P and _val(v) < 4 * P
+        out = arr()
+        assert shim.shim_fp_mul_raw(arr(*u), arr(*v), out) == 1
+        assert _val(out) % P == _val(u) * _val(v) * RINV % P
