@@ -336,3 +336,24 @@ BN_HD void fl_diff2q(fp& r, const fp& a, const fp& b) {
 #pragma unroll
   for (int i = 0; i < BN_LIMBS; i++) r.v[i] = a.v[i] - b.v[i] + SqConst::Q2R.v[i];
 }
+
+// ---- small linear combinations with one reduction ------------------------------------------
+// r = C0 a0 + C1 a1 + C2 a2 (mod q), reduced below 2q, for a_j normalised with values < 2q:
+// K q (K >= 2 * the negative coefficients' sum) keeps the value in (0, 64q), and a redundant form
+// of K q with low limbs >= 2^29 * that sum keeps every low limb in [0, 7 2^29).
+template <int K, int NEG>
+struct CsRed {
+  static constexpr CsLimbs V = cs_redundant(K, (int64_t)NEG << 29);
+};
+template <int C0, int C1, int C2, int K>
+BN_HD void fp_lin3(fp& r, const fp& a0, const fp& a1, const fp& a2) {
+  constexpr int NEG = (C0 < 0 ? -C0 : 0) + (C1 < 0 ? -C1 : 0) + (C2 < 0 ? -C2 : 0);
+  constexpr int POS = (C0 > 0 ? C0 : 0) + (C1 > 0 ? C1 : 0) + (C2 > 0 ? C2 : 0);
+  static_assert(NEG + POS <= 6 && K >= 2 * NEG && K + 2 * POS <= 62, "fp_lin3 bounds");
+  fp x;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++)
+    x.v[i] = (uint32_t)C0 * a0.v[i] + (uint32_t)C1 * a1.v[i] + (uint32_t)C2 * a2.v[i] + CsRed<K, NEG>::V.v[i];
+  cs_carry(x);
+  fp_reduce64(r, x);
+}

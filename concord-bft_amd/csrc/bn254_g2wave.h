@@ -60,10 +60,8 @@ __device__ __forceinline__ void g2w_sqr_ops(fp* U, fp* V, int o, const fp2& x) {
   V[o + 1] = x.b;
 }
 __device__ __forceinline__ void g2w_mul_res(fp2& r, const fp* p, int o) {
-  fp t;
-  f_add(t, p[o], p[o + 1]);
   f_sub(r.a, p[o], p[o + 1]);
-  f_sub(r.b, p[o + 2], t);
+  fp_lin3<1, -1, -1, 4>(r.b, p[o + 2], p[o], p[o + 1]);  // one reduction (bn254_cycsq.h)
 }
 __device__ __forceinline__ void g2w_sqr_res(fp2& r, const fp* p, int o) {
   r.a = p[o];
@@ -102,8 +100,8 @@ __device__ __forceinline__ void g2w_dbl(uint32_t* ln, g2j& T, int lane) {
   g2w_sqr_res(ZZ, p, 4);
   g2w_mul_res(t, p, 6);
   fp2_dbl(t, t);  // 2YZ = Z3
-  fp2_add(E, XX, XX);
-  fp2_add(E, E, XX);  // 3X^2
+  fp_lin3<3, 0, 0, 0>(E.a, XX.a, XX.a, XX.a);  // 3X^2 (one reduction per component)
+  fp_lin3<3, 0, 0, 0>(E.b, XX.b, XX.b, XX.b);
   fp2_add(D0, T.X, YY);
   g2w_mul_ops(U, V, 0, t, ZZ);    // A = 2YZ^3
   g2w_mul_ops(U, V, 3, E, ZZ);    // -B = 3X^2 Z^2
@@ -117,26 +115,26 @@ __device__ __forceinline__ void g2w_dbl(uint32_t* ln, g2j& T, int lane) {
   g2w_mul_res(B, p, 3);
   fp2_neg(B, B);
   g2w_mul_res(C, p, 6);
-  fp2_dbl(w, YY);
-  fp2_sub(C, C, w);  // 3X^3 - 2Y^2
+  fp_lin3<1, -2, 0, 4>(C.a, C.a, YY.a, YY.a);  // 3X^3 - 2Y^2
+  fp_lin3<1, -2, 0, 4>(C.b, C.b, YY.b, YY.b);
   g2w_store(ln, A, B, C, lane);
   g2w_sqr_res(YYYY, p, 9);
   g2w_sqr_res(D, p, 11);
   g2w_sqr_res(F, p, 13);
-  fp2_sub(D, D, XX);
-  fp2_sub(D, D, YYYY);
-  fp2_dbl(D, D);
-  fp2_sub(X3, F, D);
-  fp2_sub(X3, X3, D);
+  fp_lin3<2, -2, -2, 8>(D.a, D.a, XX.a, YYYY.a);  // D = 2((X + YY)^2 - XX - YYYY)
+  fp_lin3<2, -2, -2, 8>(D.b, D.b, XX.b, YYYY.b);
+  fp_lin3<1, -2, 0, 4>(X3.a, F.a, D.a, D.a);  // X3 = F - 2D
+  fp_lin3<1, -2, 0, 4>(X3.b, F.b, D.b, D.b);
   fp2_sub(w, D, X3);
   g2w_mul_ops(U, V, 0, E, w);
   g2w_round<3>(p, U, V, lane);
   fp2 Y3;
   g2w_mul_res(Y3, p, 0);
-  fp2_dbl(YYYY, YYYY);
-  fp2_dbl(YYYY, YYYY);
-  fp2_dbl(YYYY, YYYY);
-  fp2_sub(T.Y, Y3, YYYY);
+  fp u;  // Y3 - 8 YYYY as two reductions of - 4 YYYY
+  fp_lin3<1, -4, 0, 8>(u, Y3.a, YYYY.a, YYYY.a);
+  fp_lin3<1, -4, 0, 8>(T.Y.a, u, YYYY.a, YYYY.a);
+  fp_lin3<1, -4, 0, 8>(u, Y3.b, YYYY.b, YYYY.b);
+  fp_lin3<1, -4, 0, 8>(T.Y.b, u, YYYY.b, YYYY.b);
   T.X = X3;
   T.Z = t;
 }

@@ -312,6 +312,32 @@ int shim_g1_dbl_lazy(uint64_t seed, int iters) {
   return 1;
 }
 
+// fp_lin3 for the coefficient sets the G2 line steps use, on canonical inputs a, b, c (32-byte
+// big-endian, < p): out = 5 x 32-byte canonical results; 1 when every result is reduced
+int shim_fp_lin3(const uint8_t* a32, const uint8_t* b32, const uint8_t* c32, uint8_t* out160) {
+  uint32_t w[8];
+  fp a, b, c, r[5];
+  be32_to_words(w, a32);
+  f_from_words(a, w);
+  be32_to_words(w, b32);
+  f_from_words(b, w);
+  be32_to_words(w, c32);
+  f_from_words(c, w);
+  f_add(a, a, a);  // inputs up to 2q: a + a reduced
+  fp_lin3<3, 0, 0, 0>(r[0], a, b, c);
+  fp_lin3<1, -2, 0, 4>(r[1], a, b, c);
+  fp_lin3<2, -2, -2, 8>(r[2], a, b, c);
+  fp_lin3<1, -4, 0, 8>(r[3], a, b, c);
+  fp_lin3<1, -1, -1, 4>(r[4], a, b, c);
+  int ok = 1;
+  for (int k = 0; k < 5; k++) {
+    if (!fp_reduced(r[k])) ok = 0;
+    f_to_words(w, r[k]);
+    words_to_be32(out160 + 32 * k, w);
+  }
+  return ok;
+}
+
 int shim_g1_decompress(const uint8_t* in33, uint8_t* out64) {
   g1a a;
   if (!g1_decompress(a, in33)) return 0;

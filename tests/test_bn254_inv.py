@@ -150,3 +150,18 @@ def test_fp_mul_raw_both_operands(shim):
         out = arr()
         assert shim.shim_fp_mul_raw(arr(*u), arr(*v), out) == 1
         assert _val(out) % P == _val(u) * _val(v) * RINV % P
+
+
+def test_fp_lin3_combinations(shim):
+    """fp_lin3 (bn254_cycsq.h), the one-reduction linear combinations of the G2 line steps:
+    3a, a - 2b, 2a - 2b - 2c, a - 4b, a - b - c mod p, including inputs at 0 and p - 1."""
+    rng = random.Random(0x13)
+    xs = [0, 1, P - 1, P - 2] + [rng.randrange(P) for _ in range(400)]
+    for i, a in enumerate(xs):
+        b, c = xs[(3 * i + 1) % len(xs)], xs[(7 * i + 2) % len(xs)]
+        out = ctypes.create_string_buffer(160)
+        assert shim.shim_fp_lin3(a.to_bytes(32, "big"), b.to_bytes(32, "big"), c.to_bytes(32, "big"), out) == 1
+        got = [int.from_bytes(out.raw[32 * k:32 * k + 32], "big") for k in range(5)]
+        a2 = 2 * a
+        assert got == [3 * a2 % P, (a2 - 2 * b) % P, (2 * a2 - 2 * b - 2 * c) % P, (a2 - 4 * b) % P,
+                       (a2 - b - c) % P]
