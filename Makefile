@@ -52,17 +52,28 @@ cpu: $(CPU_LIB)
 $(CPU_LIB): tools/cpu_baseline/openssl_ed25519.c
 	gcc -O2 -std=gnu11 -fPIC -shared -Wall -Wno-deprecated-declarations -o $@ $< -lcrypto -lpthread
 
+# C++ plugin layer.  Product sources (concord::hip, BLS::Hip) compile against the reference's own
+# headers in an integration build (tests/test_reference_boundary.py) and here against the
+# restatements in ref_mirror/ (the reference's util / bftengine / threshsign libraries need
+# Crypto++, RELIC and CMF-generated code that the image does not have).
 HOST_LIB := concord-bft_amd/libcbft_host.so
-HOST_SRC := concord-bft_amd/host/src/crypto_utils.cpp concord-bft_amd/host/src/rsa_host.cpp concord-bft_amd/host/src/sig_manager.cpp concord-bft_amd/host/src/bls_hip.cpp concord-bft_amd/host/src/request_batch.cpp
-HOST_INC := -Iinclude -Iconcord-bft_amd/host/include
-host: $(HOST_LIB) tests/cpp/test_host tests/cpp/test_bls_host
-$(HOST_LIB): $(HOST_SRC) concord-bft_amd/host/include/*.hpp concord-bft_amd/host/include/threshsign/*.h* $(LIB)
-	g++ -O2 -std=c++17 -fPIC -shared -Wall $(HOST_INC) -o $@ $(HOST_SRC) -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN'
+HOST_DIR := concord-bft_amd/host
+HOST_SRC := $(HOST_DIR)/src/hip_ed25519.cpp $(HOST_DIR)/src/hip_rsa.cpp $(HOST_DIR)/src/bls_hip.cpp $(HOST_DIR)/src/request_batch.cpp
+MIRROR_SRC := $(wildcard $(HOST_DIR)/ref_mirror/src/*.cpp)
+HOST_INC := -Iinclude -I$(HOST_DIR)/include -I$(HOST_DIR)/ref_mirror/include
+HOST_HDRS := $(wildcard $(HOST_DIR)/include/*.hpp $(HOST_DIR)/include/threshsign/*.hpp $(HOST_DIR)/ref_mirror/include/*.hpp $(HOST_DIR)/ref_mirror/include/threshsign/*.h)
+host: $(HOST_LIB) tests/cpp/test_host tests/cpp/test_bls_host tools/host_bench
+$(HOST_LIB): $(HOST_SRC) $(MIRROR_SRC) $(HOST_HDRS) $(LIB)
+	g++ -O2 -std=c++17 -fPIC -shared -Wall $(HOST_INC) -o $@ $(HOST_SRC) $(MIRROR_SRC) -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN'
 tests/cpp/test_host: tests/cpp/test_host.cpp $(HOST_LIB)
-	g++ -O2 -std=c++17 -Wall $(HOST_INC) -o $@ $< -Lconcord-bft_amd -lcbft_host -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN/../../concord-bft_amd'
+	g++ -O2 -std=c++17 -Wall -DCONCORD_BFT_TESTING $(HOST_INC) -o $@ $< -Lconcord-bft_amd -lcbft_host -lcbft_hipcrypto -lcrypto -lpthread -Wl,-rpath,'$$ORIGIN/../../concord-bft_amd'
 
 tests/cpp/test_bls_host: tests/cpp/test_bls_host.cpp $(HOST_LIB)
 	g++ -O2 -std=c++17 -Wall $(HOST_INC) -o $@ $< -Lconcord-bft_amd -lcbft_host -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN/../../concord-bft_amd'
+
+# per-request path benchmark (bench.py runs it): threads calling verify() / verifySig()
+tools/host_bench: tools/host_bench.cpp $(HOST_LIB)
+	g++ -O2 -std=c++17 -Wall -DCONCORD_BFT_TESTING $(HOST_INC) -o $@ $< -Lconcord-bft_amd -lcbft_host -lcbft_hipcrypto -lcrypto -lpthread -Wl,-rpath,'$$ORIGIN/../concord-bft_amd'
 
 # host build of the BN-P254 device code, for the CPU tests (and the "not RELIC" CPU baseline)
 SHIM := tests/cpp/libbn254_shim.so
@@ -79,6 +90,6 @@ sanitize: $(LIB)
 	for s in address,undefined thread; do \
 	  t=$$(echo $$s | cut -d, -f1); \
 	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 -fPIC -shared $(HOST_INC) -o $(SAN_DIR)/libcbft_host_$$t.so $(HOST_SRC) -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' && \
-	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 $(HOST_INC) -o $(SAN_DIR)/test_host_$$t tests/cpp/test_host.cpp -L$(SAN_DIR) -lcbft_host_$$t -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' && \
+	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 -DCONCORD_BFT_TESTING $(HOST_INC) -o $(SAN_DIR)/test_host_$$t tests/cpp/test_host.cpp -L$(SAN_DIR) -lcbft_host_$$t -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' && \
 	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 $(HOST_INC) -o $(SAN_DIR)/test_bls_host_$$t tests/cpp/test_bls_host.cpp -L$(SAN_DIR) -lcbft_host_$$t -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' || exit 1; \
 	done

@@ -54,6 +54,8 @@ ABI = [
     ("cbft_ed25519_unload_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32]),
     ("cbft_ed25519_append_keys", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint32,
                                                 _u32p]),
+    ("cbft_ed25519_replace_keys", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32]),
     ("cbft_ed25519_table_size", ctypes.c_int, [ctypes.c_void_p, ctypes.c_uint32, _u32p,
                                                ctypes.POINTER(ctypes.c_int)]),
     ("cbft_ed25519_verify_batch", ctypes.c_int,
@@ -273,6 +275,14 @@ class Context:
         _check(self.lib.cbft_ed25519_append_keys(self.handle, tid, _ptr(arr), arr.shape[0], ctypes.byref(first)),
                "cbft_ed25519_append_keys")
         return first.value
+
+    def replace_keys(self, tid: int, idx, pks):
+        """Rebuild loaded key slots idx with new keys (cbft_ed25519_replace_keys)."""
+        arr = _as_rows(pks, 32)
+        ix = np.ascontiguousarray(np.asarray(idx, dtype=np.uint32))
+        assert ix.shape[0] == arr.shape[0]
+        _check(self.lib.cbft_ed25519_replace_keys(self.handle, tid, _ptr(ix), _ptr(arr), ix.shape[0]),
+               "cbft_ed25519_replace_keys")
 
     def table_size(self, tid: int):
         n, r = ctypes.c_uint32(), ctypes.c_int()

@@ -363,7 +363,7 @@ __global__ void bls_sign_kernel(const uint8_t* msg, uint32_t len, const uint32_t
   g1_from_affine(p, h);
   uint32_t k[8];
   for (int q = 0; q < 8; q++) k[q] = sk[q];
-  g1_mul(r, p, k);
+  g1_mul_ct(r, p, k);  // secret scalar: constant operation sequence
   g1a a;
   g1_to_affine(a, r);
   out37[0] = (uint8_t)(id >> 24);

@@ -105,20 +105,17 @@ __global__ void __launch_bounds__(SUM_THREADS, 1) bls_g2_sum_kernel(const uint32
 
 // vk = sk * g2 as 65 compressed bytes: the signer's public key (BlsThresholdSigner's
 // publicKey_(secretKey) -> g2_mul_gen, BlsThresholdSigner.cpp:25; IThresholdSigner::
-// getShareVerificationKey).  sk: 8 LE words (< r).  One lane, double-and-add (a one-off per key).
+// getShareVerificationKey).  sk: 8 LE words (< r).  One lane, constant-sequence Montgomery
+// ladder (g2_mul_ct: the secret key's bits select by mask, never by branch).
 __global__ void bls_pubkey_kernel(const uint32_t* sk, uint8_t* out65) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   g2j G, acc;
   fp2_load(G.X, Bn254Consts::G2X);
   fp2_load(G.Y, Bn254Consts::G2Y);
   fp2_one(G.Z);
-  fp2_one(acc.X);
-  fp2_one(acc.Y);
-  fp2_zero(acc.Z);
-  for (int i = 255; i >= 0; i--) {
-    g2_dbl_j(acc, acc);
-    if ((sk[i >> 5] >> (i & 31)) & 1) g2_add_j(acc, acc, G);
-  }
+  uint32_t k[8];
+  for (int q = 0; q < 8; q++) k[q] = sk[q];
+  g2_mul_ct(acc, G, k);
   g2a a;
   g2_to_affine(a, acc);
   g2_compress(out65, a);

@@ -166,6 +166,62 @@ BN_HDN void g1_mul(g1j& r, const g1j& p, const uint32_t* k) {
   r = acc;
 }
 
+// ------------------------------------------------------------------------------ secret scalars
+// Scalar multiplication by a SECRET scalar (signing, sk * g2) in a fixed operation sequence: a
+// Montgomery ladder over k' = k + 2r, which has bit 254 set and bit 255 clear for every k < r
+// (2r > 2^254, 3r < 2^255), so the loop length does not depend on k; the two ladder registers are
+// exchanged by a masked select, never by a branch on a key bit.  R1 - R0 = P throughout, so the
+// additions never reach their doubling or infinity cases (for P of order r and k >= 2); k'P = kP.
+template <class F>
+BN_HD void f_cswap(Fe<F>& a, Fe<F>& b, uint32_t mask) {
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    const uint32_t t = (a.v[i] ^ b.v[i]) & mask;
+    a.v[i] ^= t;
+    b.v[i] ^= t;
+  }
+}
+
+// k' = k + 2r as 8 LE words (k < r, 8 LE words)
+BN_HD void bn_scalar_plus_2r(uint32_t* out, const uint32_t* k) {
+  const uint32_t r2[8] = {0x0000001au, 0x42000000u, 0x00000021u, 0xff3f0000u,
+                          0x0000000fu, 0x74689b00u, 0x80000003u, 0x4a46c904u};  // 2r
+  uint64_t c = 0;
+  for (int q = 0; q < 8; q++) {
+    c += (uint64_t)k[q] + r2[q];
+    out[q] = (uint32_t)c;
+    c >>= 32;
+  }
+}
+
+template <class PT, class SWAP, class DBL, class ADD>
+BN_HD void bn_ladder(PT& r, const PT& p, const uint32_t* k, SWAP cswap, DBL dbl, ADD add) {
+  uint32_t kk[8];
+  bn_scalar_plus_2r(kk, k);
+  PT r0 = p, r1;
+  dbl(r1, p);
+  for (int i = 253; i >= 0; i--) {
+    const uint32_t mask = 0u - ((kk[i >> 5] >> (i & 31)) & 1u);
+    cswap(r0, r1, mask);
+    add(r1, r0, r1);
+    dbl(r0, r0);
+    cswap(r0, r1, mask);
+  }
+  r = r0;
+}
+
+// r = k * p for a secret k (constant operation sequence; p of order r)
+BN_HDN void g1_mul_ct(g1j& r, const g1j& p, const uint32_t* k) {
+  bn_ladder(
+      r, p, k,
+      [](g1j& a, g1j& b, uint32_t m) {
+        f_cswap(a.X, b.X, m);
+        f_cswap(a.Y, b.Y, m);
+        f_cswap(a.Z, b.Z, m);
+      },
+      [](g1j& o, const g1j& a) { g1_dbl(o, a); }, [](g1j& o, const g1j& a, const g1j& b) { g1_add(o, a, b); });
+}
+
 BN_HDN bool g1_on_curve(const g1a& a) {
   if (a.inf) return true;
   fp l, rr, b;
@@ -414,6 +470,21 @@ BN_HDN void g2_to_affine(g2a& r, const g2j& p) {
   fp2_mul(zi2, zi2, zi);
   fp2_mul(r.y, p.Y, zi2);
   r.inf = false;
+}
+
+// r = k * p for a secret k (G2 form of g1_mul_ct)
+BN_HDN void g2_mul_ct(g2j& r, const g2j& p, const uint32_t* k) {
+  bn_ladder(
+      r, p, k,
+      [](g2j& a, g2j& b, uint32_t m) {
+        f_cswap(a.X.a, b.X.a, m);
+        f_cswap(a.X.b, b.X.b, m);
+        f_cswap(a.Y.a, b.Y.a, m);
+        f_cswap(a.Y.b, b.Y.b, m);
+        f_cswap(a.Z.a, b.Z.a, m);
+        f_cswap(a.Z.b, b.Z.b, m);
+      },
+      [](g2j& o, const g2j& a) { g2_dbl_j(o, a); }, [](g2j& o, const g2j& a, const g2j& b) { g2_add_j(o, a, b); });
 }
 
 BN_HDN bool g2_in_subgroup(const g2a& q) {  // r * Q == O

@@ -458,6 +458,12 @@ int cbft_bls_verify_multisig_partials(cbft_ctx* c, const uint8_t* msg, uint32_t 
   return bls_verify_multisig_parts(c, len, sig33, count, out_ok);
 }
 
+// Clears a host copy of a secret scalar (a volatile store the compiler cannot drop).
+static void secure_zero(void* p, size_t n) {
+  volatile uint8_t* v = static_cast<volatile uint8_t*>(p);
+  while (n--) *v++ = 0;
+}
+
 // 32-byte big-endian scalar -> 8 little-endian words
 static void be32_scalar_words(uint32_t* w, const uint8_t* sk32) {
   for (int q = 0; q < 8; q++)
@@ -477,7 +483,9 @@ int cbft_bls_public_key(cbft_ctx* c, const uint8_t* sk32, uint8_t* out65) {
   CBFT_HIP(hipMemcpyAsync(c->bls_lambda.p, w, sizeof(w), hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(cbft_bls_launch_pubkey(c->bls_lambda.as<uint32_t>(), c->bls_out.as<uint8_t>(), c->stream));
   CBFT_HIP(hipMemcpyAsync(out65, c->bls_out.p, 65, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipMemsetAsync(c->bls_lambda.p, 0, sizeof(w), c->stream));  // the secret scalar leaves the device
   CBFT_HIP(hipStreamSynchronize(c->stream));
+  secure_zero(w, sizeof(w));
   return CBFT_OK;
 }
 
@@ -496,7 +504,9 @@ int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* 
   CBFT_HIP(cbft_bls_launch_sign(c->bls_msg.as<uint8_t>(), len, c->bls_lambda.as<uint32_t>(), id,
                                 c->bls_out.as<uint8_t>(), c->stream));
   CBFT_HIP(hipMemcpyAsync(out37, c->bls_out.p, 37, hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipMemsetAsync(c->bls_lambda.p, 0, sizeof(w), c->stream));  // the secret scalar leaves the device
   CBFT_HIP(hipStreamSynchronize(c->stream));
+  secure_zero(w, sizeof(w));
   return CBFT_OK;
 }
 

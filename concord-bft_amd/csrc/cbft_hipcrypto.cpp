@@ -267,7 +267,7 @@ void cbft_close(cbft_ctx* c) {
   }
   for (DevBuf* b : {&c->bls_gen_lines, &c->bls_msg, &c->bls_H, &c->bls_shares, &c->bls_valid, &c->bls_sig,
                     &c->bls_ids, &c->bls_use, &c->bls_lambda, &c->bls_partial, &c->bls_out,
-                    &c->bls_ms_ok, &c->bls_bitmap, &c->bls_inv})
+                    &c->bls_ms_ok, &c->bls_bitmap, &c->bls_inv, &c->bls_first, &c->bls_flag})
     b->release();
   (void)hipDeviceSynchronize();  // device-path batches may still run on caller streams
   for (DevBuf* b : {&c->base_table, &c->base_comb, &c->verdicts, &c->sig, &c->msg, &c->off, &c->len, &c->kidx, &c->pk,
@@ -412,10 +412,55 @@ static std::shared_ptr<KeyTable> find_table(cbft_ctx* c, uint32_t id) {
   return it == c->tables.end() ? nullptr : it->second;
 }
 
-// Append keys to a table: new chunks as needed (their pointers appended to the device chunk
-// array), the keys copied into their chunk slots and their comb tables built on the context's
-// build stream — all outside the context mutex, so verifies of the published keys continue —
-// then the key count is published.  Appends to one table are serialised by its append_mu.
+// HBM budget of one key table's comb tables ($CBFT_COMB_BUDGET_GB, default 64 GB of 288 GB).
+static double comb_budget_bytes() {
+  double budget = 64.0;
+  if (const char* e = getenv("CBFT_COMB_BUDGET_GB")) budget = atof(e);
+  return budget * 1e9;
+}
+
+// Write keys [k0, k0 + n) of a table (their raw encodings from pk, host or device memory): new
+// chunks as needed (their pointers appended to the device chunk array), the keys copied into
+// their chunk slots and their comb tables built, all on the build stream; synchronous.
+static int fill_keys(cbft_ctx* c, KeyTable& kt, const uint8_t* pk, hipMemcpyKind kind, uint32_t k0, uint32_t n) {
+  const size_t wpk = kt.geo.words_per_unit();
+  hipStream_t s = c->build_stream;
+  while (kt.chunks.size() * CBFT_KEY_CHUNK < (size_t)k0 + n) {
+    DevBuf b;
+    CBFT_HIP(b.reserve(cbft_key_chunk_bytes(wpk)));
+    const size_t ci = kt.chunks.size();
+    kt.chunks.push_back(b);
+    CBFT_HIP(hipMemcpyAsync(kt.chunk_ptrs.as<void*>() + ci, &kt.chunks.back().p, sizeof(void*),
+                            hipMemcpyHostToDevice, s));
+    CBFT_HIP(hipStreamSynchronize(s));  // the source is a host variable
+  }
+  for (uint32_t a = k0; a < k0 + n;) {
+    const uint32_t ci = a >> CBFT_KEY_CHUNK_SHIFT, slot = a & (CBFT_KEY_CHUNK - 1);
+    const uint32_t m = std::min<uint32_t>(k0 + n - a, CBFT_KEY_CHUNK - slot);
+    uint8_t* base = kt.chunks[ci].as<uint8_t>();
+    uint8_t* dpk = base + (size_t)CBFT_KEY_CHUNK * wpk * 4 + (size_t)slot * 32;
+    uint8_t* daok = base + (size_t)CBFT_KEY_CHUNK * (wpk * 4 + 32) + slot;
+    uint32_t* dcomb = reinterpret_cast<uint32_t*>(base) + (size_t)slot * wpk;
+    hipError_t e = hipMemcpyAsync(dpk, pk + (size_t)(a - k0) * 32, (size_t)m * 32, kind, s);
+    if (e == hipSuccess) e = build_comb(dpk, m, 1, kt.geo, dcomb, daok, s);
+    if (e != hipSuccess) return cbft_fail(e, "comb table build", __FILE__, __LINE__);
+    a += m;
+  }
+  return CBFT_OK;
+}
+
+// Raw key encodings [0, nkeys) of a table, device to device, as the source of a rebuild.
+static const uint8_t* chunk_raw_keys(const KeyTable& kt, uint32_t ci) {
+  return kt.chunks[ci].as<uint8_t>() + (size_t)CBFT_KEY_CHUNK * kt.geo.words_per_unit() * 4;
+}
+
+// Append keys to a table — verifies of the published keys continue meanwhile: everything is
+// built outside the context mutex, then the new key count is published.  Appends to one table
+// are serialised by its append_mu.  When the grown table would exceed the HBM budget at its comb
+// radix, the whole table is rebuilt at the widest radix that fits (13 -> 11 -> 8; the published
+// keys' raw encodings are copied device to device) and swapped in under the mutex; batches
+// already queued against the old table finish before it is released.  Past the budget at radix
+// 8 the append fails with CBFT_ENOMEM and the table is unchanged.
 int cbft_ed25519_append_keys(cbft_ctx* c, uint32_t id, const uint8_t* pk, uint32_t nkeys, uint32_t* out_first) {
   if (!c || !out_first || (nkeys && !pk)) return CBFT_EINVAL;
   if (!c->kids.empty()) {
@@ -428,9 +473,15 @@ int cbft_ed25519_append_keys(cbft_ctx* c, uint32_t id, const uint8_t* pk, uint32
     }
     return CBFT_OK;
   }
-  auto kt = find_table(c, id);
-  if (!kt) return CBFT_EINVAL;
-  std::lock_guard<std::mutex> ag(kt->append_mu);
+  std::shared_ptr<KeyTable> kt;
+  std::unique_lock<std::mutex> ag;
+  for (;;) {  // a concurrent re-radix may replace the table while we wait for its append_mu
+    kt = find_table(c, id);
+    if (!kt) return CBFT_EINVAL;
+    ag = std::unique_lock<std::mutex>(kt->append_mu);
+    if (find_table(c, id) == kt) break;
+    ag.unlock();
+  }
   CBFT_HIP(hipSetDevice(c->device));
   uint32_t k0;
   {
@@ -440,31 +491,80 @@ int cbft_ed25519_append_keys(cbft_ctx* c, uint32_t id, const uint8_t* pk, uint32
   *out_first = k0;
   if (!nkeys) return CBFT_OK;
   if ((uint64_t)k0 + nkeys > (uint64_t)CBFT_MAX_KEY_CHUNKS * CBFT_KEY_CHUNK) return CBFT_E2BIG;
-  const size_t wpk = kt->geo.words_per_unit();
-  hipStream_t s = c->build_stream;
-  while (kt->chunks.size() * CBFT_KEY_CHUNK < (size_t)k0 + nkeys) {
-    DevBuf b;
-    CBFT_HIP(b.reserve(cbft_key_chunk_bytes(wpk)));
-    const size_t ci = kt->chunks.size();
-    kt->chunks.push_back(b);
-    CBFT_HIP(hipMemcpyAsync(kt->chunk_ptrs.as<void*>() + ci, &kt->chunks.back().p, sizeof(void*),
-                            hipMemcpyHostToDevice, s));
-    CBFT_HIP(hipStreamSynchronize(s));  // the source is a host variable
+  const uint32_t total = k0 + nkeys;
+  const double budget = comb_budget_bytes();
+  auto fits = [&](int r) { return (double)total * cbft_comb_geom(r).words_per_unit() * 4.0 <= budget; };
+  if (fits(kt->geo.w)) {
+    const int rc = fill_keys(c, *kt, pk, hipMemcpyHostToDevice, k0, nkeys);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> g(c->mu);
+    kt->nkeys = total;
+    return CBFT_OK;
   }
-  for (uint32_t a = k0; a < k0 + nkeys;) {
-    const uint32_t ci = a >> CBFT_KEY_CHUNK_SHIFT, slot = a & (CBFT_KEY_CHUNK - 1);
-    const uint32_t m = std::min<uint32_t>(k0 + nkeys - a, CBFT_KEY_CHUNK - slot);
-    uint8_t* base = kt->chunks[ci].as<uint8_t>();
-    uint8_t* dpk = base + (size_t)CBFT_KEY_CHUNK * wpk * 4 + (size_t)slot * 32;
-    uint8_t* daok = base + (size_t)CBFT_KEY_CHUNK * (wpk * 4 + 32) + slot;
-    uint32_t* dcomb = reinterpret_cast<uint32_t*>(base) + (size_t)slot * wpk;
-    hipError_t e = hipMemcpyAsync(dpk, pk + (size_t)(a - k0) * 32, (size_t)m * 32, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = build_comb(dpk, m, 1, kt->geo, dcomb, daok, s);
-    if (e != hipSuccess) return cbft_fail(e, "comb table build", __FILE__, __LINE__);
-    a += m;
+  int r2 = 0;
+  for (int r : {13, 11, 8})
+    if (r < kt->geo.w && fits(r)) {
+      r2 = r;
+      break;
+    }
+  if (!r2) return CBFT_ENOMEM;
+  auto nt = std::make_shared<KeyTable>();
+  nt->geo = cbft_comb_geom(r2);
+  CBFT_HIP(nt->chunk_ptrs.reserve(CBFT_MAX_KEY_CHUNKS * sizeof(void*)));
+  int rc = CBFT_OK;
+  for (uint32_t ci = 0; rc == CBFT_OK && (size_t)ci * CBFT_KEY_CHUNK < k0; ci++)
+    rc = fill_keys(c, *nt, chunk_raw_keys(*kt, ci), hipMemcpyDeviceToDevice, ci * CBFT_KEY_CHUNK,
+                   std::min<uint32_t>(CBFT_KEY_CHUNK, k0 - ci * CBFT_KEY_CHUNK));
+  if (rc == CBFT_OK) rc = fill_keys(c, *nt, pk, hipMemcpyHostToDevice, k0, nkeys);
+  if (rc) {
+    for (DevBuf& b : nt->chunks) b.release();
+    nt->chunk_ptrs.release();
+    return rc;
   }
-  std::lock_guard<std::mutex> g(c->mu);
-  kt->nkeys = k0 + nkeys;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    nt->nkeys = total;
+    c->tables[id] = nt;  // new batches use the rebuilt table from here on
+  }
+  (void)hipDeviceSynchronize();  // batches queued against the old table (any stream) finish
+  for (DevBuf& b : kt->chunks) b.release();
+  kt->chunk_ptrs.release();
+  return CBFT_OK;
+}
+
+// Rebuild key slots in place with new keys (a rotated key reusing a released slot).  The caller
+// guarantees no batch in flight names these slots; the device is synchronised first anyway.
+int cbft_ed25519_replace_keys(cbft_ctx* c, uint32_t id, const uint32_t* idx, const uint8_t* pk, uint32_t n) {
+  if (!c || (n && (!idx || !pk))) return CBFT_EINVAL;
+  if (!c->kids.empty()) {
+    for (cbft_ctx* k : c->kids) {
+      const int rc = cbft_ed25519_replace_keys(k, id, idx, pk, n);
+      if (rc) return rc;
+    }
+    return CBFT_OK;
+  }
+  std::shared_ptr<KeyTable> kt;
+  std::unique_lock<std::mutex> ag;
+  for (;;) {
+    kt = find_table(c, id);
+    if (!kt) return CBFT_EINVAL;
+    ag = std::unique_lock<std::mutex>(kt->append_mu);
+    if (find_table(c, id) == kt) break;
+    ag.unlock();
+  }
+  uint32_t have;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    have = kt->nkeys;
+  }
+  for (uint32_t i = 0; i < n; i++)
+    if (idx[i] >= have) return CBFT_EINVAL;
+  CBFT_HIP(hipSetDevice(c->device));
+  CBFT_HIP(hipDeviceSynchronize());
+  for (uint32_t i = 0; i < n; i++) {
+    const int rc = fill_keys(c, *kt, pk + (size_t)i * 32, hipMemcpyHostToDevice, idx[i], 1);
+    if (rc) return rc;
+  }
   return CBFT_OK;
 }
 
@@ -712,10 +812,13 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
       for (int k = 0; k < 5; k++) parts[k].bytes = 0;  // moved
     }
   }
+  bool pageable_queued = false;  // copies still reading the caller's pageable memory
   if (!pack) {
     for (int k = 0; k < 5; k++)
-      if (parts[k].bytes && !pinned[k])
+      if (parts[k].bytes && !pinned[k]) {
         CBFT_HIP(hipMemcpyAsync(din + parts[k].off, parts[k].src, parts[k].bytes, hipMemcpyHostToDevice, c->copy_stream));
+        pageable_queued = true;
+      }
   }
   if (phi) {
     CBFT_HIP(s.pack.reserve(in_bytes));
@@ -728,6 +831,10 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
     if (parts[k].bytes && pinned[k])
       CBFT_HIP(hipMemcpyAsync(din + parts[k].off, parts[k].src, parts[k].bytes, hipMemcpyHostToDevice, c->copy_stream));
   CBFT_HIP(hipEventRecord(s.copied, c->copy_stream));
+  // the header's contract: pageable inputs may be reused as soon as the call returns, so a
+  // batch whose pageable parts were not packed returns only after their copies completed (the
+  // runtime may still be staging from the caller's memory)
+  if (pageable_queued) CBFT_HIP(hipEventSynchronize(s.copied));
   hipStream_t cs = c->compute[t & 1];
   CBFT_HIP(hipStreamWaitEvent(cs, s.copied, 0));
   rc = launch_locked(c, table_id, kt ? nullptr : din + o_key, kt ? reinterpret_cast<const uint32_t*>(din + o_key) : nullptr,

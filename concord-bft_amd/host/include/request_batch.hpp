@@ -20,10 +20,13 @@
 //                                        replica signatures over SHA3-256(result || result code ||
 //                                        client id || seq num) (PreProcessResultHashCreator.hpp:19-35)
 //
-// Wire structs are packed little-endian mirrors of the reference's (ClientMsgs.hpp:23-50,
-// PrePrepareMsg.hpp:33-53, MessageBase.hpp:30-33).  Outcomes equal the serial reference loop's:
-// the same request fails first with the same kind of error, and SigManager's counters move for
-// exactly the signatures the serial loop would have verified.
+// Wire structs are packed little-endian restatements of the reference's (ClientMsgs.hpp:23-50,
+// PrePrepareMsg.hpp:33-53, MessageBase.hpp:30-33) in namespace concord::hip::wire (their layout is
+// checked against the reference's own structs by tests/test_reference_boundary.py).  Outcomes
+// equal the serial reference loop's: the same request fails first with the same kind of error,
+// and SigManager's counters move for exactly the signatures the serial loop would have verified.
+// The ReplicasInfo and SigManager types are the reference's (bftEngine::impl::ReplicasInfo and
+// HipSigManager, derived from bftEngine::impl::SigManager).
 #pragma once
 
 #include <cstdint>
@@ -33,9 +36,15 @@
 #include <utility>
 #include <vector>
 
-#include "sig_manager.hpp"
+#include "hip_sig_manager.hpp"
 
-namespace bftEngine::impl {
+namespace concord::hip {
+
+using bftEngine::impl::PrincipalId;
+using bftEngine::impl::ReplicaId;
+using bftEngine::impl::ReplicasInfo;
+
+namespace wire {
 
 #pragma pack(push, 1)
 struct MessageBaseHeader {  // MessageBase.hpp:30-33
@@ -92,6 +101,8 @@ enum : uint64_t {
   RECONFIG_FLAG = 0x20,
 };
 constexpr uint32_t kMaxClientBatchSize = 1024;  // MAX_BATCH_SIZE of ClientBatchRequestMsg::checkElements
+}  // namespace wire
+using wire::ClientRequestMsgHeader;
 
 // Total size of a packed ClientRequestMsg as the reference computes it (compRequestMsgSize,
 // ClientRequestMsg.cpp:26-29), from its header.
@@ -120,7 +131,7 @@ struct RequestValidation {
 // it are not validated and their signatures not counted.  Otherwise (PreProcessor's client batch
 // loop) every request is validated and counted.
 RequestValidation validateClientRequests(const std::vector<ClientRequestView>& reqs, const ReplicasInfo& repInfo,
-                                         const SigManager& sigManager, bool stopAtFirstFailure);
+                                         const HipSigManager& sigManager, bool stopAtFirstFailure);
 
 // PrePrepareMsg::validate's request loop (PrePrepareMsg.cpp:116-125) for the PrePrepare message
 // bytes [body, body + size): the requests between payloadShift() and endLocationOfLastRequest,
@@ -129,7 +140,7 @@ RequestValidation validateClientRequests(const std::vector<ClientRequestView>& r
 // request is validated as ClientRequestMsg::validate; throws std::runtime_error with the first
 // failing request's error, exactly where the serial loop would.  Returns the number of requests.
 size_t validatePrePrepareRequests(const char* body, uint64_t size, const ReplicasInfo& repInfo,
-                                  const SigManager& sigManager);
+                                  const HipSigManager& sigManager);
 
 // The requests of a ClientBatchRequestMsg [body, body + size) (ClientBatchRequestMsg.cpp:
 // checkElements, then getClientPreProcessRequestMsgs): throws std::runtime_error if the batch
@@ -137,7 +148,7 @@ size_t validatePrePrepareRequests(const char* body, uint64_t size, const Replica
 // PreProcessor::checkClientBatchMsgCorrectness does (all of them, in one signature batch) and
 // returns the per-element outcome.
 RequestValidation validateClientBatchRequestMsg(const char* body, uint64_t size, const ReplicasInfo& repInfo,
-                                                const SigManager& sigManager);
+                                                const HipSigManager& sigManager);
 
 // PreProcessResultMsg::validatePreProcessResultSignatures (PreProcessResultMsg.cpp:57-99) for the
 // ClientRequestMsg-format message [body, body + size) whose extra data holds the serialized result
@@ -146,7 +157,7 @@ RequestValidation validateClientBatchRequestMsg(const char* body, uint64_t size,
 // signature: recomputed and compared, as there).  Throws std::runtime_error on a malformed
 // signature buffer (deserializeResultSignatures).
 std::optional<std::string> validatePreProcessResultSignatures(const char* body, uint64_t size, ReplicaId myReplicaId,
-                                                              int16_t fVal, const SigManager& sigManager);
+                                                              int16_t fVal, const HipSigManager& sigManager);
 
 // SHA3-256(result bytes (only when resultCode == SUCCESS = 0) || resultCode u32 || clientId u16
 // || reqSeqNum u64), host byte order as the reference's update(&x, sizeof x)
@@ -154,4 +165,4 @@ std::optional<std::string> validatePreProcessResultSignatures(const char* body, 
 std::string preProcessResultHash(const char* result, uint32_t len, uint32_t resultCode, uint16_t clientId,
                                  uint64_t reqSeqNum);
 
-}  // namespace bftEngine::impl
+}  // namespace concord::hip

@@ -26,10 +26,10 @@
 #include <string>
 #include <vector>
 
-#include "IThresholdAccumulator.h"
-#include "IThresholdSigner.h"
-#include "IThresholdVerifier.h"
-#include "VectorOfShares.h"
+#include "threshsign/IThresholdAccumulator.h"
+#include "threshsign/IThresholdSigner.h"
+#include "threshsign/IThresholdVerifier.h"
+#include "threshsign/VectorOfShares.h"
 
 namespace BLS {
 namespace Hip {

@@ -1,5 +1,6 @@
-// Ed25519 IVerifier / ISigner implementations over libcbft_hipcrypto (see crypto_utils.hpp).
-#include "crypto_utils.hpp"
+// HipEdDSAVerifier / EdDSASigner over libcbft_hipcrypto, and the process-wide Ed25519 engine that
+// owns the device key table (see hip_crypto.hpp).
+#include "hip_crypto.hpp"
 
 #include <openssl/evp.h>
 
@@ -13,10 +14,11 @@
 #include <mutex>
 #include <shared_mutex>
 #include <stdexcept>
+#include <vector>
 
 #include "cbft_hipcrypto.h"
 
-namespace concord::util::crypto {
+namespace concord::hip {
 
 // ---------------------------------------------------------------------------------- encoding
 std::string toHex(const uint8_t* p, size_t n) {
@@ -118,10 +120,11 @@ std::string ed25519PublicKeyToPem(const uint8_t raw[32]) {
 static int g_device = -1;
 void setEd25519Device(int device) { g_device = device; }
 
-// Comb radix of the engine's key table, chosen once for the expected number of keys
-// ($CBFT_EXPECTED_KEYS, default 4,096) against a 64 GB budget of the 288 GB HBM (the library's
-// own rule for a table loaded in one go, cbft_hipcrypto.cpp key_radix): radix 13 (10.5 MB per
-// key) up to ~6,100 keys, 11 (3.0 MB) up to ~21,000, then 8 (0.53 MB).
+// Comb radix the engine's key table starts with, for the expected number of keys
+// ($CBFT_EXPECTED_KEYS, default 4,096) against the library's 64 GB budget: radix 13 (10.5 MB per
+// key) up to ~6,100 keys, 11 (3.0 MB) up to ~21,000, then 8 (0.53 MB).  More keys than expected is
+// safe: the library re-radixes the table once the budget would be exceeded
+// (cbft_ed25519_append_keys).
 static int engineRadix() {
   if (const char* e = std::getenv("CBFT_COMB_RADIX")) return std::atoi(e);
   double keys = 4096;
@@ -134,11 +137,12 @@ static int engineRadix() {
 
 // Per-process owner of the GPU context and of the device key table.
 //
-// Keys are registered when a verifier is constructed (deduplicated: equal keys share an index,
-// as SigManager shares one verifier object between principals with the same key,
-// SigManager.cpp:139-150).  A registered key is appended to the device table (its comb table
-// built alone; the keys already loaded are untouched) before the first batch that needs it;
-// batches that only name loaded keys never wait for an append.
+// Keys are registered when a verifier is constructed and reference-counted per slot (equal keys
+// share a slot, as SigManager shares one verifier object between principals with the same key,
+// SigManager.cpp:139-150).  A new key is appended to the device table (its comb table built
+// alone; loaded keys untouched) before the first batch that needs it; a slot whose last verifier
+// is gone is reused by the next new key (rebuilt in place, cbft_ed25519_replace_keys), so client
+// key rotation (SigManager::setClientPublicKey) does not grow the table.
 //
 // verifyOne() coalesces concurrent single verifies (the reference calls IVerifier::verify from
 // 40 + 24 pool threads, ReplicaConfig.hpp:202-212): callers queue their request; one of them
@@ -166,28 +170,62 @@ class Ed25519Engine {
   }
 
   uint32_t registerKey(const uint8_t raw[32]) {
+    std::lock_guard<std::mutex> ag(append_mu_);  // a slot rebuild is a device-table write
     std::lock_guard<std::mutex> g(keys_mu_);
     std::string k(reinterpret_cast<const char*>(raw), 32);
     auto it = index_.find(k);
-    if (it != index_.end()) return it->second;
-    uint32_t idx = (uint32_t)keys_.size() / 32;
-    keys_.insert(keys_.end(), raw, raw + 32);
+    if (it != index_.end()) {
+      refs_[it->second]++;
+      return it->second;
+    }
+    uint32_t idx;
+    if (!free_.empty()) {
+      idx = free_.back();
+      free_.pop_back();
+      std::memcpy(&keys_[(size_t)idx * 32], raw, 32);
+      if (idx < loaded_.load()) {  // on the device already: rebuild the slot in place
+        const int rc = cbft_ed25519_replace_keys(ctx_, table_, &idx, raw, 1);
+        if (rc != CBFT_OK) {
+          free_.push_back(idx);
+          throw std::runtime_error(std::string("cbft_ed25519_replace_keys: ") + cbft_strerror(rc) + " " +
+                                   cbft_last_error());
+        }
+      }
+      refs_[idx] = 1;
+    } else {
+      idx = (uint32_t)(keys_.size() / 32);
+      keys_.insert(keys_.end(), raw, raw + 32);
+      refs_.push_back(1);
+    }
     index_.emplace(std::move(k), idx);
     return idx;
   }
 
-  // One GPU batch; out[i] = verdict of reqs[i] (false for non-Ed25519 verifiers).
+  void addRef(uint32_t idx) {
+    std::lock_guard<std::mutex> g(keys_mu_);
+    refs_[idx]++;
+  }
+
+  void releaseKey(uint32_t idx) {
+    std::lock_guard<std::mutex> g(keys_mu_);
+    if (--refs_[idx]) return;
+    index_.erase(std::string(reinterpret_cast<const char*>(&keys_[(size_t)idx * 32]), 32));
+    free_.push_back(idx);
+  }
+
+  // One GPU batch; out[i] = verdict of reqs[i] (false for non-Ed25519 verifiers).  Throws on a
+  // GPU failure (callers turn it into false verdicts).
   void verify(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out) {
     out.assign(reqs.size(), false);
     // wrong-length signatures (EVP returns 0) and messages the kernel's 32-bit SHA-512 length
-    // cannot hold (> CBFT's 0xFFFFFF00 bytes) are rejected without a GPU round trip
+    // cannot hold are rejected without a GPU round trip
     std::vector<size_t> pos;
     pos.reserve(reqs.size());
     size_t blob = 0;
     uint32_t maxKey = 0;
-    std::vector<const EdDSAVerifier*> ver(reqs.size(), nullptr);
+    std::vector<const HipEdDSAVerifier*> ver(reqs.size(), nullptr);
     for (size_t i = 0; i < reqs.size(); i++) {
-      ver[i] = dynamic_cast<const EdDSAVerifier*>(reqs[i].verifier);
+      ver[i] = dynamic_cast<const HipEdDSAVerifier*>(reqs[i].verifier);
       if (reqs[i].sigLength == 64 && ver[i] && reqs[i].dataLength <= kMaxMsg) {
         pos.push_back(i);
         blob += reqs[i].dataLength;
@@ -210,6 +248,8 @@ class Ed25519Engine {
       o += r.dataLength;
     }
     ensureLoaded(maxKey);
+    batches_++;
+    items_ += n;
     int rc = cbft_ed25519_verify_batch(ctx_, table_, kidx.data(), sig.data(), msg.data(), off.data(), len.data(), n,
                                        bitmap.data());
     if (rc != CBFT_OK)
@@ -218,8 +258,20 @@ class Ed25519Engine {
     for (size_t j = 0; j < n; j++) out[pos[j]] = (bitmap[j >> 3] >> (j & 7)) & 1;
   }
 
-  bool verifyOne(const EdDSAVerifier* v, const char* data, size_t len, const char* sig, size_t sigLen) {
+  // verify() for a batch API caller: a GPU failure gives false verdicts (IVerifier's contract:
+  // verification never throws, openssl_crypto.cpp:247-253) and is counted.
+  void verifyNoThrow(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out) {
+    try {
+      verify(reqs, out);
+    } catch (...) {
+      gpu_errors_++;
+      out.assign(reqs.size(), false);
+    }
+  }
+
+  bool verifyOne(const HipEdDSAVerifier* v, const char* data, size_t len, const char* sig, size_t sigLen) {
     if (sigLen != 64 || len > kMaxMsg) return false;
+    LatencyHistogram::Scope timer(recorders().ed25519_verify);
     Pending p{v, data, len, sig, sigLen};
     std::unique_lock<std::mutex> lk(q_mu_);
     queue_.push_back(&p);
@@ -242,24 +294,25 @@ class Ed25519Engine {
         q_cv_.wait(lk);
       }
     }
-    lk.unlock();
-    if (p.err) std::rethrow_exception(p.err);
     return p.verdict;
   }
 
-  uint64_t batchesRun() const { return batches_.load(); }
+  EngineStats stats() {
+    std::lock_guard<std::mutex> g(keys_mu_);
+    return EngineStats{batches_.load(), items_.load(), gpu_errors_.load(),
+                       (uint32_t)(keys_.size() / 32 - free_.size()), (uint32_t)(keys_.size() / 32)};
+  }
 
  private:
   static constexpr size_t kMaxMsg = 0xFFFFFF00u;
   struct Pending {
-    const EdDSAVerifier* v;
+    const HipEdDSAVerifier* v;
     const char* data;
     size_t len;
     const char* sig;
     size_t sigLen;
     bool done = false;
     bool verdict = false;
-    std::exception_ptr err;
   };
 
   void runBatch(std::vector<Pending*>& batch) {
@@ -267,14 +320,8 @@ class Ed25519Engine {
     for (size_t i = 0; i < batch.size(); i++)
       reqs[i] = {batch[i]->v, batch[i]->data, batch[i]->len, batch[i]->sig, batch[i]->sigLen};
     std::vector<bool> out;
-    try {
-      verify(reqs, out);
-      for (size_t i = 0; i < batch.size(); i++) batch[i]->verdict = out[i];
-    } catch (...) {
-      auto e = std::current_exception();
-      for (Pending* q : batch) q->err = e;
-    }
-    batches_++;
+    verifyNoThrow(reqs, out);
+    for (size_t i = 0; i < batch.size(); i++) batch[i]->verdict = out[i];
   }
 
   Ed25519Engine() {
@@ -311,42 +358,51 @@ class Ed25519Engine {
 
   cbft_ctx* ctx_ = nullptr;
   uint32_t table_ = CBFT_NO_KEY_TABLE;
-  std::mutex keys_mu_;  // guards keys_, index_
+  std::mutex keys_mu_;  // guards keys_, index_, refs_, free_
   std::vector<uint8_t> keys_;
   std::map<std::string, uint32_t> index_;
-  std::mutex append_mu_;  // one append at a time
+  std::vector<uint32_t> refs_;
+  std::vector<uint32_t> free_;
+  std::mutex append_mu_;  // one device-table write (append / slot rebuild) at a time
   std::atomic<uint32_t> loaded_{0};
   std::mutex q_mu_;  // coalescing queue
   std::condition_variable q_cv_;
   std::vector<Pending*> queue_;
   bool leader_ = false;
   int inflight_ = 0;
-  std::atomic<uint64_t> batches_{0};
+  std::atomic<uint64_t> batches_{0}, items_{0}, gpu_errors_{0};
 };
 
-uint64_t ed25519EngineBatches() { return Ed25519Engine::get()->batchesRun(); }
+EngineStats ed25519EngineStats() { return Ed25519Engine::get()->stats(); }
+
+Ed25519KeyRef::Ed25519KeyRef(const Ed25519KeyRef& o) : engine_(o.engine_), index_(o.index_) { engine_->addRef(index_); }
+Ed25519KeyRef::~Ed25519KeyRef() { engine_->releaseKey(index_); }
 
 // ---------------------------------------------------------------------------------- verifier
-EdDSAVerifier::EdDSAVerifier(const std::string& str_pub_key, KeyFormat fmt) : key_str_(str_pub_key) {
-  if (!parseEd25519PublicKey(str_pub_key, fmt, raw_)) throw std::invalid_argument("EdDSAVerifier: bad public key");
-  engine_ = Ed25519Engine::get();
-  key_index_ = engine_->registerKey(raw_);
+static Ed25519KeyRef registerEd25519(const std::string& str_pub_key, KeyFormat fmt, uint8_t raw[32]) {
+  if (!parseEd25519PublicKey(str_pub_key, fmt, raw)) throw std::invalid_argument("HipEdDSAVerifier: bad public key");
+  auto engine = Ed25519Engine::get();
+  const uint32_t idx = engine->registerKey(raw);
+  return Ed25519KeyRef(std::move(engine), idx);
 }
 
-EdDSAVerifier::~EdDSAVerifier() = default;
+HipEdDSAVerifier::HipEdDSAVerifier(const std::string& str_pub_key, KeyFormat fmt)
+    : key_str_(str_pub_key), raw_{}, key_(registerEd25519(str_pub_key, fmt, raw_)) {}
 
-bool EdDSAVerifier::verify(const std::string& data, const std::string& sig) const {
-  return engine_->verifyOne(this, data.data(), data.size(), sig.data(), sig.size());
+HipEdDSAVerifier::~HipEdDSAVerifier() = default;
+
+bool HipEdDSAVerifier::verify(const std::string& data, const std::string& sig) const {
+  return key_.engine().verifyOne(this, data.data(), data.size(), sig.data(), sig.size());
 }
 
-void EdDSAVerifier::verifyBatch(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out) {
+void HipEdDSAVerifier::verifyBatch(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out) {
   out.assign(reqs.size(), false);
   if (reqs.empty()) return;
-  const EdDSAVerifier* any = nullptr;
+  const HipEdDSAVerifier* any = nullptr;
   for (auto& r : reqs)
-    if ((any = dynamic_cast<const EdDSAVerifier*>(r.verifier))) break;
+    if ((any = dynamic_cast<const HipEdDSAVerifier*>(r.verifier))) break;
   if (!any) return;
-  any->engine_->verify(reqs, out);
+  any->key_.engine().verifyNoThrow(reqs, out);
 }
 
 // ---------------------------------------------------------------------------------- signer
@@ -390,4 +446,4 @@ std::string EdDSASigner::getPubKeyHex() const {
   return toHex(pk, 32);
 }
 
-}  // namespace concord::util::crypto
+}  // namespace concord::hip

@@ -1,16 +1,16 @@
-// RSA IVerifier / ISigner over libcbft_hipcrypto (see crypto_utils.hpp), the mixed-batch
-// dispatcher and makeVerifier().
+// HipRSAVerifier over libcbft_hipcrypto (see hip_crypto.hpp), the mixed-batch dispatcher and
+// makeVerifier() / makeSigner().
 //
-// Reference: concord::util::crypto::RSAVerifier / RSASigner (util/src/crypto_utils.cpp:101-117,
-// 119-168): Crypto++ RSASS<PKCS1v15, SHA256> keyed from hex DER (X509PublicKey /
-// PKCS8PrivateKey) or PEM.  Key parsing here uses the host OpenSSL (d2i_PUBKEY /
-// PEM_read_bio_PUBKEY); every verification runs on the GPU.
+// Reference: concord::util::crypto::RSAVerifier (util/src/crypto_utils.cpp:101-117,155-168):
+// Crypto++ RSASS<PKCS1v15, SHA256> keyed from hex DER (X509PublicKey) or PEM.  Key parsing here
+// uses the host OpenSSL (d2i_PUBKEY / PEM_read_bio_PUBKEY); every verification runs on the GPU.
 #include <openssl/bio.h>
 #include <openssl/bn.h>
 #include <openssl/core_names.h>
 #include <openssl/evp.h>
 #include <openssl/pem.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -19,9 +19,9 @@
 #include <stdexcept>
 
 #include "cbft_hipcrypto.h"
-#include "crypto_utils.hpp"
+#include "hip_crypto.hpp"
 
-namespace concord::util::crypto {
+namespace concord::hip {
 
 namespace {
 
@@ -105,14 +105,24 @@ class RsaEngine {
     return idx;
   }
 
+  // GPU failures become false verdicts (IVerifier never throws for a signature) and are counted
+  void verifyNoThrow(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out) {
+    try {
+      verify(reqs, out);
+    } catch (...) {
+      gpu_errors_++;
+      out.assign(reqs.size(), false);
+    }
+  }
+
   void verify(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out) {
     out.assign(reqs.size(), false);
     std::vector<size_t> pos;
-    std::vector<const RSAVerifier*> ver(reqs.size(), nullptr);
+    std::vector<const HipRSAVerifier*> ver(reqs.size(), nullptr);
     std::vector<std::string> sigs;  // normalised to 256 bytes (Crypto++ reads any length)
     size_t blob = 0;
     for (size_t i = 0; i < reqs.size(); i++) {
-      ver[i] = dynamic_cast<const RSAVerifier*>(reqs[i].verifier);
+      ver[i] = dynamic_cast<const HipRSAVerifier*>(reqs[i].verifier);
       if (!ver[i]) continue;
       size_t lead = 0;
       while (lead < reqs[i].sigLength && reqs[i].sig[lead] == 0) lead++;
@@ -201,81 +211,92 @@ class RsaEngine {
   std::map<std::string, uint32_t> index_;
   uint32_t table_ = kNoTable;
   uint32_t loaded_ = 0;
+  std::atomic<uint64_t> gpu_errors_{0};
 };
 
 // ---------------------------------------------------------------------------------- verifier
-RSAVerifier::RSAVerifier(const std::string& str_pub_key, KeyFormat fmt) : key_str_(str_pub_key) {
+HipRSAVerifier::HipRSAVerifier(const std::string& str_pub_key, KeyFormat fmt) : key_str_(str_pub_key) {
   EVP_PKEY* k = parsePublicKey(str_pub_key, fmt);
   uint8_t mod[256];
   uint32_t e = 0;
   const bool ok = rsaPublicParts(k, mod, &e);
   EVP_PKEY_free(k);
-  if (!ok) throw std::invalid_argument("RSAVerifier: not a 2048-bit RSA public key with a 32-bit exponent");
+  if (!ok) throw std::invalid_argument("HipRSAVerifier: not a 2048-bit RSA public key with a 32-bit exponent");
   engine_ = RsaEngine::get();
   key_index_ = engine_->registerKey(mod, e);
 }
 
-RSAVerifier::~RSAVerifier() = default;
+HipRSAVerifier::~HipRSAVerifier() = default;
 
-bool RSAVerifier::verify(const std::string& data, const std::string& sig) const {
+bool HipRSAVerifier::verify(const std::string& data, const std::string& sig) const {
+  LatencyHistogram::Scope timer(recorders().rsa_verify);
   std::vector<VerifyRequest> r{{this, data.data(), data.size(), sig.data(), sig.size()}};
   std::vector<bool> out;
-  engine_->verify(r, out);
+  engine_->verifyNoThrow(r, out);
   return out[0];
 }
 
-void RSAVerifier::verifyBatch(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out) {
+void HipRSAVerifier::verifyBatch(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out) {
   out.assign(reqs.size(), false);
   for (auto& r : reqs)
-    if (auto v = dynamic_cast<const RSAVerifier*>(r.verifier)) {
-      v->engine_->verify(reqs, out);
+    if (auto v = dynamic_cast<const HipRSAVerifier*>(r.verifier)) {
+      v->engine_->verifyNoThrow(reqs, out);
       return;
     }
 }
 
-// ---------------------------------------------------------------------------------- signer
-RSASigner::RSASigner(const std::string& str_priv_key, KeyFormat fmt) : key_str_(str_priv_key), pkey_(nullptr) {
-  EVP_PKEY* k = parsePrivateKey(str_priv_key, fmt);
-  if (!k || EVP_PKEY_get_base_id(k) != EVP_PKEY_RSA) {
-    EVP_PKEY_free(k);
-    throw std::invalid_argument("RSASigner: not an RSA private key");
-  }
-  pkey_ = k;
-}
-
-RSASigner::~RSASigner() {
-  if (pkey_) EVP_PKEY_free(static_cast<EVP_PKEY*>(pkey_));
-}
-
-std::string RSASigner::sign(const std::string& data) {
-  EVP_MD_CTX* ctx = EVP_MD_CTX_new();
-  std::string sig(512, '\0');
-  size_t sl = sig.size();
-  const bool ok = ctx && EVP_DigestSignInit(ctx, nullptr, EVP_sha256(), nullptr, static_cast<EVP_PKEY*>(pkey_)) == 1 &&
-                  EVP_DigestSign(ctx, reinterpret_cast<unsigned char*>(&sig[0]), &sl,
-                                 reinterpret_cast<const unsigned char*>(data.data()), data.size()) == 1;
-  EVP_MD_CTX_free(ctx);
-  if (!ok) throw std::runtime_error("RSASigner::sign failed");
-  sig.resize(sl);
-  return sig;
-}
-
 // ---------------------------------------------------------------------------------- dispatch
-std::shared_ptr<IVerifier> makeVerifier(const std::string& str_pub_key, KeyFormat fmt) {
+KeyKind publicKeyKind(const std::string& str_pub_key, KeyFormat fmt) {
   uint8_t raw[32];
-  if (parseEd25519PublicKey(str_pub_key, fmt, raw)) return std::make_shared<EdDSAVerifier>(str_pub_key, fmt);
-  return std::make_shared<RSAVerifier>(str_pub_key, fmt);
+  if (parseEd25519PublicKey(str_pub_key, fmt, raw)) return KeyKind::Ed25519;
+  EVP_PKEY* k = parsePublicKey(str_pub_key, fmt);
+  const KeyKind kind = (k && EVP_PKEY_get_base_id(k) == EVP_PKEY_RSA) ? KeyKind::RSA : KeyKind::Unknown;
+  EVP_PKEY_free(k);
+  return kind;
+}
+
+KeyKind privateKeyKind(const std::string& str_priv_key, KeyFormat fmt) {
+  std::vector<uint8_t> seed;
+  if (fmt == KeyFormat::HexaDecimalStrippedFormat && fromHex(str_priv_key, seed) && seed.size() == 32)
+    return KeyKind::Ed25519;  // an RFC 8032 seed
+  EVP_PKEY* k = parsePrivateKey(str_priv_key, fmt);
+  const int id = k ? EVP_PKEY_get_base_id(k) : 0;
+  EVP_PKEY_free(k);
+  return id == EVP_PKEY_ED25519 ? KeyKind::Ed25519 : id == EVP_PKEY_RSA ? KeyKind::RSA : KeyKind::Unknown;
+}
+
+std::shared_ptr<IVerifier> makeVerifier(const std::string& str_pub_key, KeyFormat fmt) {
+  switch (publicKeyKind(str_pub_key, fmt)) {
+    case KeyKind::Ed25519:
+      return std::make_shared<HipEdDSAVerifier>(str_pub_key, fmt);
+    case KeyKind::RSA:
+      return std::make_shared<HipRSAVerifier>(str_pub_key, fmt);
+    default:
+      throw std::invalid_argument("makeVerifier: neither an Ed25519 nor an RSA public key");
+  }
+}
+
+std::unique_ptr<ISigner> makeSigner(const std::string& str_priv_key, KeyFormat fmt) {
+  switch (privateKeyKind(str_priv_key, fmt)) {
+    case KeyKind::Ed25519:
+      return std::make_unique<EdDSASigner>(str_priv_key, fmt);
+    case KeyKind::RSA:
+      return std::make_unique<concord::util::crypto::RSASigner>(str_priv_key, fmt);
+    default:
+      throw std::invalid_argument("makeSigner: neither an Ed25519 nor an RSA private key");
+  }
 }
 
 void verifyBatch(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out) {
+  LatencyHistogram::Scope timer(recorders().verify_batch);
   out.assign(reqs.size(), false);
   bool any_ed = false, any_rsa = false;
   for (size_t i = 0; i < reqs.size(); i++) {
     const IVerifier* v = reqs[i].verifier;
     if (!v) continue;
-    if (dynamic_cast<const EdDSAVerifier*>(v)) {
+    if (dynamic_cast<const HipEdDSAVerifier*>(v)) {
       any_ed = true;
-    } else if (dynamic_cast<const RSAVerifier*>(v)) {
+    } else if (dynamic_cast<const HipRSAVerifier*>(v)) {
       any_rsa = true;
     } else {
       out[i] = v->verify(std::string(reqs[i].data, reqs[i].dataLength), std::string(reqs[i].sig, reqs[i].sigLength));
@@ -283,15 +304,15 @@ void verifyBatch(const std::vector<VerifyRequest>& reqs, std::vector<bool>& out)
   }
   std::vector<bool> part;
   if (any_ed) {
-    EdDSAVerifier::verifyBatch(reqs, part);
+    HipEdDSAVerifier::verifyBatch(reqs, part);
     for (size_t i = 0; i < reqs.size(); i++)
-      if (dynamic_cast<const EdDSAVerifier*>(reqs[i].verifier)) out[i] = part[i];
+      if (dynamic_cast<const HipEdDSAVerifier*>(reqs[i].verifier)) out[i] = part[i];
   }
   if (any_rsa) {
-    RSAVerifier::verifyBatch(reqs, part);
+    HipRSAVerifier::verifyBatch(reqs, part);
     for (size_t i = 0; i < reqs.size(); i++)
-      if (dynamic_cast<const RSAVerifier*>(reqs[i].verifier)) out[i] = part[i];
+      if (dynamic_cast<const HipRSAVerifier*>(reqs[i].verifier)) out[i] = part[i];
   }
 }
 
-}  // namespace concord::util::crypto
+}  // namespace concord::hip

@@ -6,7 +6,9 @@
 #include <cstring>
 #include <set>
 
-namespace bftEngine::impl {
+namespace concord::hip {
+
+using namespace wire;
 
 uint64_t clientRequestMsgSize(const ClientRequestMsgHeader& h) {
   return sizeof(ClientRequestMsgHeader) + (uint64_t)h.spanContextSize + h.requestLength + h.cidLength +
@@ -25,7 +27,7 @@ enum class Check { Fail, Accept, Verify };
 
 // ClientRequestMsg::validateImp (ClientRequestMsg.cpp:99-214) without the signature itself:
 // Fail (with the reference's message), Accept (no signature to check) or Verify (item filled).
-Check checkRequest(const ClientRequestView& r, const ReplicasInfo& repInfo, const SigManager& sm, std::string& err,
+Check checkRequest(const ClientRequestView& r, const ReplicasInfo& repInfo, const HipSigManager& sm, std::string& err,
                    SigBatchItem& item) {
   const uint64_t msgSize = r.size;
   if (msgSize < sizeof(ClientRequestMsgHeader)) {
@@ -49,7 +51,7 @@ Check checkRequest(const ClientRequestView& r, const ReplicasInfo& repInfo, cons
     return Check::Fail;
   }
   uint16_t expectedSigLen = 0;
-  const bool signing = sm.isClientTransactionSigningEnabled();
+  const bool signing = sm.clientSigningEnabled();
   const bool external = repInfo.isIdOfExternalClient(clientId);
   bool doSigVerify = false;
   const bool emptyReq = h.requestLength == 0;
@@ -97,7 +99,7 @@ Check checkRequest(const ClientRequestView& r, const ReplicasInfo& repInfo, cons
 }  // namespace
 
 RequestValidation validateClientRequests(const std::vector<ClientRequestView>& reqs, const ReplicasInfo& repInfo,
-                                         const SigManager& sm, bool stopAtFirstFailure) {
+                                         const HipSigManager& sm, bool stopAtFirstFailure) {
   RequestValidation out;
   const size_t n = reqs.size();
   out.ok.assign(n, false);
@@ -140,7 +142,7 @@ RequestValidation validateClientRequests(const std::vector<ClientRequestView>& r
 }
 
 size_t validatePrePrepareRequests(const char* body, uint64_t size, const ReplicasInfo& repInfo,
-                                  const SigManager& sm) {
+                                  const HipSigManager& sm) {
   if (size < sizeof(PrePrepareMsgHeader)) throw std::runtime_error("PrePrepareMsg::validate: basic");
   PrePrepareMsgHeader h;
   std::memcpy(&h, body, sizeof h);
@@ -170,7 +172,7 @@ size_t validatePrePrepareRequests(const char* body, uint64_t size, const Replica
     }
   }
   if (!good) throw std::runtime_error("PrePrepareMsg::validate: advanced");
-  if (sm.isClientTransactionSigningEnabled()) {
+  if (sm.clientSigningEnabled()) {
     RequestValidation v = validateClientRequests(reqs, repInfo, sm, true);
     if (v.firstFailure < reqs.size()) throw std::runtime_error(v.error[v.firstFailure]);
   }
@@ -178,7 +180,7 @@ size_t validatePrePrepareRequests(const char* body, uint64_t size, const Replica
 }
 
 RequestValidation validateClientBatchRequestMsg(const char* body, uint64_t size, const ReplicasInfo& repInfo,
-                                                const SigManager& sm) {
+                                                const HipSigManager& sm) {
   // ClientBatchRequestMsg::validate + checkElements
   if (size < sizeof(ClientBatchRequestMsgHeader)) throw std::runtime_error("ClientBatchRequestMsg::validate");
   ClientBatchRequestMsgHeader h;
@@ -187,7 +189,7 @@ RequestValidation validateClientBatchRequestMsg(const char* body, uint64_t size,
     throw std::runtime_error("ClientBatchRequestMsg::validate");
   if (!h.numOfMessagesInBatch || h.numOfMessagesInBatch > kMaxClientBatchSize)
     throw std::runtime_error("ClientBatchRequestMsg::validate: checkElements");
-  const bool signing = sm.isClientTransactionSigningEnabled();
+  const bool signing = sm.clientSigningEnabled();
   uint64_t pos = sizeof(ClientBatchRequestMsgHeader) + h.cidSize;
   std::vector<ClientRequestView> reqs;
   for (uint32_t k = 0; k < h.numOfMessagesInBatch; k++) {
@@ -237,7 +239,7 @@ struct ResultSig {
 }  // namespace
 
 std::optional<std::string> validatePreProcessResultSignatures(const char* body, uint64_t size, ReplicaId myReplicaId,
-                                                              int16_t fVal, const SigManager& sm) {
+                                                              int16_t fVal, const HipSigManager& sm) {
   if (size < sizeof(ClientRequestMsgHeader)) throw std::runtime_error("PreProcessResultMsg: short message");
   const ClientRequestMsgHeader h = readHeader(body);
   if (clientRequestMsgSize(h) > size) throw std::runtime_error("PreProcessResultMsg: short message");
@@ -295,4 +297,4 @@ std::optional<std::string> validatePreProcessResultSignatures(const char* body, 
   return std::nullopt;
 }
 
-}  // namespace bftEngine::impl
+}  // namespace concord::hip

@@ -104,10 +104,21 @@ int cbft_ed25519_unload_keys(cbft_ctx* ctx, uint32_t key_table_id);
  * setClientPublicKey, SigManager.cpp:250-264; KeyExchangeManager.cpp:310-320).  The keys get
  * indices *out_first_index .. + nkeys - 1; the keys already loaded are neither moved nor rebuilt,
  * and batches against them keep running while the new keys' tables are built (only the new
- * indices are unusable until this call returns).  Up to 1,048,576 keys per table (CBFT_E2BIG);
- * the table keeps the comb radix it was loaded with.  A table loaded with nkeys = 0 starts empty. */
+ * indices are unusable until this call returns).  Up to 1,048,576 keys per table (CBFT_E2BIG).
+ * The table keeps its comb radix while the grown table fits $CBFT_COMB_BUDGET_GB (default 64);
+ * past it the whole table is rebuilt once at the widest radix that fits (13 -> 11 -> 8, key
+ * indices unchanged, batches against the old table finish first), and past the budget at radix 8
+ * the call fails with CBFT_ENOMEM leaving the table as it was.  A table loaded with nkeys = 0
+ * starts empty. */
 int cbft_ed25519_append_keys(cbft_ctx* ctx, uint32_t key_table_id, const uint8_t* pk, uint32_t nkeys,
                              uint32_t* out_first_index);
+/* Rebuild loaded key slots idx[0..n) in place with new keys pk (n x 32 B): a rotated key reusing
+ * the slot of a key nothing references any more (SigManager::setClientPublicKey replaces a
+ * client's verifier, SigManager.cpp:250-264), so key rotation does not grow the table.  The
+ * caller guarantees no batch names these slots while the call runs.  CBFT_EINVAL if a slot is
+ * not loaded. */
+int cbft_ed25519_replace_keys(cbft_ctx* ctx, uint32_t key_table_id, const uint32_t* idx, const uint8_t* pk,
+                              uint32_t n);
 /* Published key count and comb radix of a table. */
 int cbft_ed25519_table_size(cbft_ctx* ctx, uint32_t key_table_id, uint32_t* out_nkeys, int* out_radix);
 

@@ -362,6 +362,33 @@ void shim_g1_mul(const uint8_t* in33, const uint8_t* kbe, uint8_t* out33) {
   g1_compress(out33, o);
 }
 
+// the constant-sequence ladders (g1_mul_ct / g2_mul_ct, used for secret scalars on the GPU)
+void shim_g1_mul_ct(const uint8_t* in33, const uint8_t* kbe, uint8_t* out33) {
+  g1a a;
+  g1_decompress(a, in33);
+  g1j p, r;
+  g1_from_affine(p, a);
+  uint32_t k[8];
+  be32_to_words(k, kbe);
+  g1_mul_ct(r, p, k);
+  g1a o;
+  g1_to_affine(o, r);
+  g1_compress(out33, o);
+}
+
+void shim_g2_mul_gen_ct(const uint8_t* skbe, uint8_t* out65) {
+  uint32_t k[8];
+  be32_to_words(k, skbe);
+  g2j P, acc;
+  fp2_load(P.X, Bn254Consts::G2X);
+  fp2_load(P.Y, Bn254Consts::G2Y);
+  fp2_one(P.Z);
+  g2_mul_ct(acc, P, k);
+  g2a a;
+  g2_to_affine(a, acc);
+  g2_compress(out65, a);
+}
+
 int shim_g2_decompress(const uint8_t* in65, uint8_t* out65) {
   g2a q;
   if (!g2_decompress(q, in65)) return 0;

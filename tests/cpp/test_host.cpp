@@ -20,12 +20,20 @@
 #include <string>
 #include <vector>
 
-#include "crypto_utils.hpp"
+#include "Metrics.hpp"
+#include "ReplicaConfig.hpp"
+#include "hip_crypto.hpp"
+#include "hip_sig_manager.hpp"
 #include "request_batch.hpp"
-#include "sig_manager.hpp"
 
-using namespace concord::util::crypto;
-using namespace bftEngine::impl;
+using namespace concord::hip;
+using namespace concord::hip::wire;
+using bftEngine::impl::PrincipalId;
+using bftEngine::impl::ReplicaIdsConfig;
+using bftEngine::impl::ReplicasInfo;
+using concord::util::crypto::KeyFormat;
+using concord::util::crypto::RSASigner;
+using SigManager = concord::hip::HipSigManager;
 
 #define CHECK(c)                                                   \
   do {                                                             \
@@ -82,7 +90,7 @@ static int testRsa() {
   // --- RSAVerifier / RSASigner (crypto_utils.cpp:101-168): hex DER and PEM keys
   RsaKeys kc = genRsa(65537), kr = genRsa(17);
   RSASigner sc(kc.privHex, KeyFormat::HexaDecimalStrippedFormat);
-  RSAVerifier vc(kc.pubHex, KeyFormat::HexaDecimalStrippedFormat), vcp(kc.pubPem, KeyFormat::PemFormat);
+  HipRSAVerifier vc(kc.pubHex, KeyFormat::HexaDecimalStrippedFormat), vcp(kc.pubPem, KeyFormat::PemFormat);
   CHECK(vc.signatureLength() == 256 && sc.signatureLength() == 256);
   std::string msg = "client request signed with RSA-2048";
   std::string sig = sc.sign(msg);
@@ -98,7 +106,7 @@ static int testRsa() {
   CHECK(!vc.verify(msg, sig.substr(1)) || sig[0] == 0);
   bool threw = false;
   try {
-    RSAVerifier broken("3000", KeyFormat::HexaDecimalStrippedFormat);
+    HipRSAVerifier broken("3000", KeyFormat::HexaDecimalStrippedFormat);
   } catch (const std::invalid_argument&) {
     threw = true;
   }
@@ -154,10 +162,10 @@ static int testRsa() {
     const bool client = ri.isIdOfExternalClient(who[i]);
     (expect[i] ? (client ? okC : okR) : (client ? badC : badR))++;
   }
-  const auto& m = sm.metrics();
-  CHECK(m.external_client_request_signatures_verified == okC && m.peer_replicas_signatures_verified == okR);
-  CHECK(m.external_client_request_signature_verification_failed == badC);
-  CHECK(m.peer_replicas_signature_verification_failed == badR);
+  const auto m = sm.counterValues();
+  CHECK(m.externalVerified == okC && m.replicaVerified == okR);
+  CHECK(m.externalFailed == badC);
+  CHECK(m.replicaFailed == badR);
   for (size_t i = 0; i < 12; i++)
     CHECK(sm.verifySig(who[i], datas[i].data(), datas[i].size(), sigs[i].data(), (uint16_t)sigs[i].size()) ==
           expect[i]);
@@ -214,9 +222,8 @@ static std::string clientBatch(uint16_t sender, const std::vector<std::string>& 
 }
 
 static uint64_t verifiedTotal(const SigManager& sm) {
-  const auto& m = sm.metrics();
-  return m.external_client_request_signatures_verified + m.external_client_request_signature_verification_failed +
-         m.peer_replicas_signatures_verified + m.peer_replicas_signature_verification_failed;
+  const auto m = sm.counterValues();
+  return m.externalVerified + m.externalFailed + m.replicaVerified + m.replicaFailed;
 }
 
 // Message-level batch checks (request_batch.hpp) against what the reference's serial loops do.
@@ -251,7 +258,7 @@ static int testMessages(SigManager& sm, const ReplicasInfo& ri, std::vector<EdDS
     r2[23][sizeof(ClientRequestMsgHeader) + 5] ^= 1;  // a payload byte: the signature no longer matches
     std::string pp2 = prePrepare(r2);
     before = verifiedTotal(sm);
-    const uint64_t failBefore = sm.metrics().external_client_request_signature_verification_failed;
+    const uint64_t failBefore = sm.counterValues().externalFailed;
     bool threw = false;
     try {
       validatePrePrepareRequests(pp2.data(), pp2.size(), ri, sm);
@@ -260,7 +267,7 @@ static int testMessages(SigManager& sm, const ReplicasInfo& ri, std::vector<EdDS
     }
     CHECK(threw);
     CHECK(verifiedTotal(sm) - before == 24);
-    CHECK(sm.metrics().external_client_request_signature_verification_failed - failBefore == 1);
+    CHECK(sm.counterValues().externalFailed - failBefore == 1);
   }
   // (3) a wrong signature length at request 10 and a bad signature at 40: the length error wins
   // and no signature after request 9 is counted
@@ -368,15 +375,15 @@ static int testPreProcessResult(const SigManager& sm, std::vector<EdDSASigner>& 
   return 0;
 }
 
-// 64 threads call EdDSAVerifier::verify concurrently (the reference's pool threads) while new
+// 64 threads call HipEdDSAVerifier::verify concurrently (the reference's pool threads) while new
 // client keys are registered: verdicts exact, calls coalesced into fewer GPU batches.
 static int testConcurrent() {
   const int T = 64, K = 24;
   std::vector<std::unique_ptr<EdDSASigner>> sg;
-  std::vector<std::unique_ptr<EdDSAVerifier>> vf;
+  std::vector<std::unique_ptr<HipEdDSAVerifier>> vf;
   for (int k = 0; k < 8; k++) {
     sg.emplace_back(new EdDSASigner(seedHex(300 + k), KeyFormat::HexaDecimalStrippedFormat));
-    vf.emplace_back(new EdDSAVerifier(sg.back()->getPubKeyHex(), KeyFormat::HexaDecimalStrippedFormat));
+    vf.emplace_back(new HipEdDSAVerifier(sg.back()->getPubKeyHex(), KeyFormat::HexaDecimalStrippedFormat));
   }
   std::vector<std::vector<std::string>> msgs(T), sigs(T);
   std::vector<std::vector<bool>> expect(T);
@@ -394,7 +401,7 @@ static int testConcurrent() {
     }
   }
   std::atomic<int> bad{0};
-  const uint64_t b0 = ed25519EngineBatches();
+  const uint64_t b0 = ed25519EngineStats().batches;
   auto t0 = std::chrono::steady_clock::now();
   std::vector<std::thread> th;
   for (int t = 0; t < T; t++)
@@ -403,16 +410,16 @@ static int testConcurrent() {
         if (vf[(t + k) % 8]->verify(msgs[t][k], sigs[t][k]) != expect[t][k]) bad++;
     });
   // meanwhile: new clients join (keys appended to the live device table)
-  std::vector<std::unique_ptr<EdDSAVerifier>> late;
+  std::vector<std::unique_ptr<HipEdDSAVerifier>> late;
   for (int k = 0; k < 6; k++) {
     EdDSASigner s(seedHex(400 + k), KeyFormat::HexaDecimalStrippedFormat);
-    late.emplace_back(new EdDSAVerifier(s.getPubKeyHex(), KeyFormat::HexaDecimalStrippedFormat));
+    late.emplace_back(new HipEdDSAVerifier(s.getPubKeyHex(), KeyFormat::HexaDecimalStrippedFormat));
     std::string m = "late client " + std::to_string(k);
     if (!late.back()->verify(m, s.sign(m))) bad++;
   }
   for (auto& x : th) x.join();
   const double secs = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  const uint64_t batches = ed25519EngineBatches() - b0;
+  const uint64_t batches = ed25519EngineStats().batches - b0;
   CHECK(bad == 0);
   CHECK(batches < (uint64_t)(T * K + 6));
   std::printf("test_host: %d concurrent verify() calls in %llu GPU batches, %.0f verifies/s\n", T * K + 6,
@@ -420,15 +427,84 @@ static int testConcurrent() {
   return 0;
 }
 
+// Metrics idiom of the reference (SigManager.hpp:65-67,83; SigManager.cpp:208-236): counters on
+// a "signature_manager" component, pushed to the aggregator on every failure and on every
+// 1,000th success.  Then client key rotation reusing freed device key slots.
+static int testAggregatorAndKeySlots() {
+  ReplicaIdsConfig cfg;
+  cfg.replicaId = 0;
+  cfg.numOfExternalClients = 2;
+  ReplicasInfo ri(cfg);
+  std::vector<EdDSASigner> rs;
+  HipSigManager::ReplicaKeys replicaKeys;
+  for (int r = 0; r < 4; r++) {
+    rs.emplace_back(seedHex(600 + r), KeyFormat::HexaDecimalStrippedFormat);
+    replicaKeys.insert({(PrincipalId)r, rs.back().getPubKeyHex()});
+  }
+  EdDSASigner c4(seedHex(610), KeyFormat::HexaDecimalStrippedFormat), c5(seedHex(611), KeyFormat::HexaDecimalStrippedFormat);
+  HipSigManager::ClientKeys clientKeys = {{c4.getPubKeyHex(), {4}}, {c5.getPubKeyHex(), {5}}};
+  std::unique_ptr<HipSigManager> sm(HipSigManager::initInTesting(0, seedHex(600), replicaKeys,
+                                                                 KeyFormat::HexaDecimalStrippedFormat, &clientKeys,
+                                                                 KeyFormat::HexaDecimalStrippedFormat, ri));
+  auto agg = std::make_shared<concordMetrics::Aggregator>();
+  sm->SetAggregator(agg);
+  auto ctr = [&](const char* name) { return (uint64_t)agg->GetCounter("signature_manager", name).Get(); };
+  std::vector<std::string> d(1001), sg(1001);
+  std::vector<SigBatchItem> items;
+  for (int i = 0; i < 1001; i++) {
+    d[i] = "replica message " + std::to_string(i);
+    sg[i] = rs[1].sign(d[i]);
+  }
+  for (int i = 0; i < 999; i++) items.push_back({1, d[i].data(), d[i].size(), sg[i].data(), 64});
+  std::vector<bool> out;
+  CHECK(sm->verifySigBatch(items, out) == 999);
+  CHECK(ctr("peer_replicas_signatures_verified") == 0 && agg->Pushes("signature_manager") == 0);
+  CHECK(sm->verifySig(1, d[999].data(), d[999].size(), sg[999].data(), 64));  // the 1,000th success
+  CHECK(ctr("peer_replicas_signatures_verified") == 1000 && agg->Pushes("signature_manager") == 1);
+  std::string badsig = sg[1000];
+  badsig[9] ^= 1;
+  items.assign(1, {1, d[1000].data(), d[1000].size(), badsig.data(), 64});
+  CHECK(sm->verifySigBatch(items, out) == 0 && !out[0]);
+  CHECK(ctr("peer_replicas_signature_verification_failed") == 1 && agg->Pushes("signature_manager") == 2);
+  items.assign(1, {77, d[0].data(), d[0].size(), sg[0].data(), 64});  // unknown principal
+  sm->verifySigBatch(items, out);
+  CHECK(ctr("signature_verification_failed_on_unrecognized_participant_id") == 1);
+  CHECK(agg->Pushes("signature_manager") == 3);
+  std::string cpk = sm->getClientsPublicKeys();  // CMF-encoded; Ed25519 clients are not listed (see header)
+  CHECK(cpk.size() >= 6);
+
+  // key rotation: the first new key takes a fresh slot (the old one is still referenced while the
+  // replacement is built), the second rotation reuses the slot the first one freed
+  const std::string m = "rotated client request";
+  CHECK(sm->verifySig(4, m.data(), m.size(), c4.sign(m).data(), 64));
+  const auto s0 = ed25519EngineStats();
+  EdDSASigner k1(seedHex(620), KeyFormat::HexaDecimalStrippedFormat), k2(seedHex(621), KeyFormat::HexaDecimalStrippedFormat);
+  sm->setClientPublicKey(k1.getPubKeyHex(), 4, KeyFormat::HexaDecimalStrippedFormat);
+  CHECK(sm->verifySig(4, m.data(), m.size(), k1.sign(m).data(), 64));
+  const auto s1 = ed25519EngineStats();
+  CHECK(s1.table_keys == s0.table_keys + 1 && s1.live_keys == s0.live_keys);
+  sm->setClientPublicKey(k2.getPubKeyHex(), 4, KeyFormat::HexaDecimalStrippedFormat);
+  CHECK(sm->verifySig(4, m.data(), m.size(), k2.sign(m).data(), 64));
+  CHECK(!sm->verifySig(4, m.data(), m.size(), k1.sign(m).data(), 64));
+  CHECK(!sm->verifySig(4, m.data(), m.size(), c4.sign(m).data(), 64));
+  CHECK(sm->verifySig(5, m.data(), m.size(), c5.sign(m).data(), 64));  // the other slots are untouched
+  const auto s2 = ed25519EngineStats();
+  CHECK(s2.table_keys == s1.table_keys && s2.live_keys == s1.live_keys);
+  CHECK(s2.gpu_errors == 0);
+  std::printf("test_host: aggregator pushes and key-slot reuse passed (%u device key slots)\n", s2.table_keys);
+  return 0;
+}
+
 int main() {
+  bftEngine::ReplicaConfig::instance().clientTransactionSigningEnabled = true;
   if (testRsa() != 0) return 1;
   // --- IVerifier/ISigner round trip, hex and PEM key formats
   EdDSASigner signer(seedHex(0), KeyFormat::HexaDecimalStrippedFormat);
   std::string pkhex = signer.getPubKeyHex();
-  EdDSAVerifier vhex(pkhex, KeyFormat::HexaDecimalStrippedFormat);
+  HipEdDSAVerifier vhex(pkhex, KeyFormat::HexaDecimalStrippedFormat);
   std::vector<uint8_t> raw;
   fromHex(pkhex, raw);
-  EdDSAVerifier vpem(ed25519PublicKeyToPem(raw.data()), KeyFormat::PemFormat);
+  HipEdDSAVerifier vpem(ed25519PublicKeyToPem(raw.data()), KeyFormat::PemFormat);
   CHECK(vhex.signatureLength() == 64 && signer.signatureLength() == 64);
   std::string msg = "concord client request payload";
   std::string sig = signer.sign(msg);
@@ -441,7 +517,7 @@ int main() {
   CHECK(!vhex.verify(msg, sig.substr(0, 63)));  // length gate
   bool threw = false;
   try {
-    EdDSAVerifier broken("zz", KeyFormat::HexaDecimalStrippedFormat);
+    HipEdDSAVerifier broken("zz", KeyFormat::HexaDecimalStrippedFormat);
   } catch (const std::invalid_argument&) {
     threw = true;
   }
@@ -525,12 +601,12 @@ int main() {
     CHECK(client == (items[i].pid >= 4));
     (expect[i] ? (client ? okC : okR) : (client ? badC : badR))++;
   }
-  const auto& m = sm.metrics();
-  CHECK(m.external_client_request_signatures_verified == okC);
-  CHECK(m.peer_replicas_signatures_verified == okR);
-  CHECK(m.external_client_request_signature_verification_failed == badC);
-  CHECK(m.peer_replicas_signature_verification_failed == badR);
-  CHECK(m.signature_verification_failed_on_unrecognized_participant_id == 1);
+  const auto m = sm.counterValues();
+  CHECK(m.externalVerified == okC);
+  CHECK(m.replicaVerified == okR);
+  CHECK(m.externalFailed == badC);
+  CHECK(m.replicaFailed == badR);
+  CHECK(m.unrecognizedPid == 1);
 
   // single-item path agrees with the batch
   for (size_t i = 0; i < 40; i++)
@@ -556,6 +632,7 @@ int main() {
   if (testMessages(sm, ri, signers, signerOf) != 0) return 1;
   if (testPreProcessResult(sm, signers) != 0) return 1;
   if (testConcurrent() != 0) return 1;
+  if (testAggregatorAndKeySlots() != 0) return 1;
   std::printf("test_host: all checks passed (%zu batch items)\n", items.size());
   return 0;
 }

@@ -165,3 +165,25 @@ def test_fp_lin3_combinations(shim):
         a2 = 2 * a
         assert got == [3 * a2 % P, (a2 - 2 * b) % P, (2 * a2 - 2 * b - 2 * c) % P, (a2 - 4 * b) % P,
                        (a2 - b - c) % P]
+
+
+def test_secret_scalar_ladders_match_double_and_add(shim):
+    """g1_mul_ct / g2_mul_ct (Montgomery ladder over k + 2r, masked swaps: used for signing and
+    sk*g2) equal the double-and-add forms for edge and random scalars k < r."""
+    import random
+
+    r = 0x2523648240000001BA344D8000000007FF9F800000000010A10000000000000D
+    rng = random.Random(5)
+    ks = [0, 1, 2, 3, r - 1, r - 2, (r - 1) // 2, 1 << 252, (1 << 253) - 1] + [rng.randrange(r) for _ in range(24)]
+    h = ctypes.create_string_buffer(33)
+    shim.shim_g1_map(b"ladder", 6, h)
+    for k in ks:
+        kb = k.to_bytes(32, "big")
+        a, b = ctypes.create_string_buffer(33), ctypes.create_string_buffer(33)
+        shim.shim_g1_mul(h.raw, kb, a)
+        shim.shim_g1_mul_ct(h.raw, kb, b)
+        assert a.raw == b.raw, hex(k)
+        c, d = ctypes.create_string_buffer(65), ctypes.create_string_buffer(65)
+        shim.shim_g2_mul_gen(kb, c)
+        shim.shim_g2_mul_gen_ct(kb, d)
+        assert c.raw == d.raw, hex(k)

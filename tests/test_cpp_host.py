@@ -1,4 +1,5 @@
-"""Runs the C++ host-side test (IVerifier/ISigner/SigManager mirror over the C ABI)."""
+"""Runs the C++ host-side tests of the plugin layer (concord::hip verifiers, HipSigManager over the
+reference-restating SigManager base, request-batch walkers, BLS::Hip) and the per-request bench."""
 import os
 import subprocess
 
@@ -32,3 +33,21 @@ def test_cpp_threshsign_bls():
                        timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "all checks passed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_host_bench_per_request_path_exact():
+    """tools/host_bench (the per-request leg bench.py reports): threads calling verify() and
+    SigManager::verifySig() concurrently, every verdict checked against the planted corruptions
+    and against OpenSSL on the host."""
+    import json
+
+    exe = os.path.join(ROOT, "tools", "host_bench")
+    if not os.path.exists(exe):
+        pytest.fail("tools/host_bench not built (make host)")
+    r = subprocess.run([exe, "16", "150", "64", "4"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    res = json.loads(r.stdout)
+    for leg in ("verify_mt", "verifysig_mt", "single", "openssl_mt"):
+        assert res[leg]["mismatches"] == 0
+    assert res["verify_mt"]["gpu_batches"] < res["verify_mt"]["calls"]  # concurrent calls coalesce

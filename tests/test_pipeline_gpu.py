@@ -253,3 +253,73 @@ def test_append_to_empty_table_and_index_bounds(ctx):
         assert np.array_equal(got, ss.expected)
     finally:
         ctx.unload_keys(tid)
+
+
+def test_append_past_budget_rebuilds_at_lower_radix(monkeypatch):
+    """appends check the HBM budget.  With a 20 MB budget a radix-13 table holds one
+    key (10.5 MB), radix 11 six (3.0 MB each), radix 8 thirty-seven (0.53 MB); appending past each
+    limit rebuilds the whole table once at the next radix with the same key indices, and past
+    radix 8 the append fails with CBFT_ENOMEM leaving the table usable."""
+    monkeypatch.setenv("CBFT_COMB_BUDGET_GB", "0.02")
+    ss = sigsets.make_sigset(2000, nkeys=40, msg_len=(16, 300), seed=81, invalid_frac=0.1)
+    msgs = ss.msgs()
+    with cb.Context(device=0) as c:
+        tid = c.load_keys(ss.pk[:1], radix=13)
+        assert c.table_size(tid) == (1, 13)
+        seen = []
+        for a, b in ((1, 2), (2, 6), (6, 20), (20, 37)):
+            assert c.append_keys(tid, ss.pk[a:b]) == a
+            n, r = c.table_size(tid)
+            seen.append((n, r))
+            use = np.nonzero(ss.key_idx < b)[0]
+            got = cb.bitmap_to_bools(c.verify(tid, ss.key_idx[use], ss.sig[use], [msgs[i] for i in use]), use.size)
+            assert np.array_equal(got, ss.expected[use]), (a, b)
+        assert seen == [(2, 11), (6, 11), (20, 8), (37, 8)]
+        with pytest.raises(cb.CbftError) as e:
+            c.append_keys(tid, ss.pk[37:40])
+        assert e.value.code == -12  # CBFT_ENOMEM
+        assert c.table_size(tid) == (37, 8)
+        use = np.nonzero(ss.key_idx < 37)[0]
+        got = cb.bitmap_to_bools(c.verify(tid, ss.key_idx[use], ss.sig[use], [msgs[i] for i in use]), use.size)
+        assert np.array_equal(got, ss.expected[use])
+        c.unload_keys(tid)
+
+
+def test_replace_key_slot(ctx):
+    """cbft_ed25519_replace_keys: a slot rebuilt with another key verifies that key's signatures
+    and no longer the old key's; the other slots are untouched."""
+    ss = sigsets.make_sigset(512, nkeys=8, msg_len=64, seed=83)
+    msgs = ss.msgs()
+    tid = ctx.load_keys(ss.pk[:6], radix=8)
+    try:
+        use = np.nonzero(ss.key_idx < 6)[0]
+        ctx.replace_keys(tid, [2], ss.pk[7:8])  # slot 2 now holds key 7
+        kidx = ss.key_idx[use].copy()
+        got = cb.bitmap_to_bools(ctx.verify(tid, kidx, ss.sig[use], [msgs[i] for i in use]), use.size)
+        exp = ss.expected[use] & (kidx != 2)
+        assert np.array_equal(got, exp)
+        seven = np.nonzero(ss.key_idx == 7)[0]
+        got7 = cb.bitmap_to_bools(ctx.verify(tid, np.full(seven.size, 2, np.uint32), ss.sig[seven],
+                                             [msgs[i] for i in seven]), seven.size)
+        assert got7.all()
+        with pytest.raises(cb.CbftError):
+            ctx.replace_keys(tid, [6], ss.pk[7:8])  # not a loaded slot
+    finally:
+        ctx.unload_keys(tid)
+
+
+def test_async_pageable_inputs_reusable_on_return(ctx, base):
+    """a pageable batch too large for the pinned pack (64K x 256 B = 16 MB of
+    messages) is copied before the _async call returns, so the caller may overwrite its buffers
+    at once and the verdicts still belong to the original inputs."""
+    tid = ctx.load_keys(base.pk, radix=8)
+    try:
+        sig, blob = base.sig.copy(), base.blob.copy()
+        out = np.zeros(base.n // 8, dtype=np.uint8)
+        t = ctx.verify_async(tid, base.key_idx, sig, blob, out, offs=base.off, lens=base.len)
+        sig[:] = 0xA5
+        blob[:] = 0x5A
+        ctx.wait(t)
+        assert np.array_equal(cb.bitmap_to_bools(out.tobytes(), base.n), base.expected)
+    finally:
+        ctx.unload_keys(tid)
