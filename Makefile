@@ -17,11 +17,14 @@ $(CSRC)/ed25519_verify.o: $(CSRC)/ed25519_verify.hip $(CSRC)/*.h
 $(CSRC)/cbft_hipcrypto.o: $(CSRC)/cbft_hipcrypto.cpp include/cbft_hipcrypto.h $(CSRC)/ed25519_verify.h $(CSRC)/cbft_internal.h $(CSRC)/rsa_verify.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-BLS_DEPS := $(CSRC)/bls_kernels.h $(CSRC)/bls_common.h $(CSRC)/bn254_*.h $(CSRC)/bls_ops.h $(CSRC)/sha256.h
+BLS_DEPS := $(CSRC)/bls_kernels.h $(CSRC)/bls_common.h $(CSRC)/bn254_*.h $(CSRC)/bls_ops.h $(CSRC)/sha256.h $(CSRC)/bls_glv.h
 $(CSRC)/bls_kernels.o: $(CSRC)/bls_kernels.hip $(BLS_DEPS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/bls_pairing.o: $(CSRC)/bls_pairing.hip $(BLS_DEPS)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(CSRC)/bls_msm_row.o: $(CSRC)/bls_msm_row.hip $(BLS_DEPS) $(CSRC)/bls_glv.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/bls_keys.o: $(CSRC)/bls_keys.hip $(BLS_DEPS)
@@ -36,7 +39,7 @@ $(CSRC)/cbft_rsa.o: $(CSRC)/cbft_rsa.cpp $(CSRC)/cbft_internal.h include/cbft_hi
 $(CSRC)/cbft_bls.o: $(CSRC)/cbft_bls.cpp $(CSRC)/cbft_internal.h $(CSRC)/rsa_verify.h include/cbft_hipcrypto.h $(CSRC)/bls_kernels.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-$(LIB): $(CSRC)/ed25519_verify.o $(CSRC)/cbft_hipcrypto.o $(CSRC)/bls_kernels.o $(CSRC)/bls_pairing.o $(CSRC)/bls_keys.o $(CSRC)/cbft_bls.o $(CSRC)/rsa_verify.o $(CSRC)/cbft_rsa.o
+$(LIB): $(CSRC)/ed25519_verify.o $(CSRC)/cbft_hipcrypto.o $(CSRC)/bls_kernels.o $(CSRC)/bls_msm_row.o $(CSRC)/bls_pairing.o $(CSRC)/bls_keys.o $(CSRC)/cbft_bls.o $(CSRC)/rsa_verify.o $(CSRC)/cbft_rsa.o
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^
 
 oracle: $(ORACLE_LIB)

@@ -31,6 +31,10 @@ hipError_t cbft_bls_launch_combine(const uint32_t* d_sig, const uint32_t* d_ids,
                                    uint32_t lo, uint32_t hi, int multisig, const uint32_t* d_inv, uint32_t* d_lambda,
                                    uint32_t* d_partial, uint8_t* d_out33, uint32_t* d_sig_aff, uint32_t* d_out_jac,
                                    hipStream_t s);
+// row-parallel combine (bls_msm_row.hip): lambda_j sigma_j per share (or the shares themselves for
+// multisig) summed level by level in d_work ((2 m + 16) BLS_JAC_WORDS words); *d_final = the sum
+hipError_t cbft_bls_launch_msm_row(const uint32_t* d_sig, const uint32_t* d_lambda, const uint8_t* d_use, uint32_t m,
+                                   int multisig, uint32_t* d_work, uint32_t** d_final, hipStream_t s);
 #define BLS_INV_TABLE 2048  // d^-1 mod r for d = 1 .. 2048 (share ids are <= 2048, IThresholdVerifier.h:36)
 hipError_t cbft_bls_launch_inv_table(uint32_t* d_inv, hipStream_t s);
 hipError_t cbft_bls_launch_and(const uint8_t* d_a, const uint8_t* d_b, uint8_t* d_use, uint32_t k, hipStream_t s);

@@ -190,7 +190,7 @@ static int bls_combine_range(cbft_ctx* c, const uint8_t* shares37, uint32_t k, u
   int rc = bls_prep(c, nullptr, shares37, k, false, 0);
   if (rc) return rc;
   CBFT_HIP(c->bls_lambda.reserve((size_t)k * 8 * 4));
-  CBFT_HIP(c->bls_partial.reserve((size_t)((k + 15) / 16 + 1) * BLS_JAC_WORDS * 4));
+  CBFT_HIP(c->bls_partial.reserve((size_t)(2 * k + 16) * BLS_JAC_WORDS * 4));  // row MSM levels
   CBFT_HIP(c->bls_out.reserve(BLS_JAC_WORDS * 4));
   // every share decoded? (the parse kernel wrote valid = decodable && id in range)
   std::vector<uint8_t> v(k);
@@ -324,7 +324,7 @@ int cbft_bls_combine_threshold(cbft_ctx* c, uint32_t id, const uint8_t* msg, uin
   CBFT_HIP(c->bls_first.reserve(k ? k : 1));
   CBFT_HIP(c->bls_use.reserve(k ? k : 1));
   CBFT_HIP(c->bls_lambda.reserve((size_t)(k ? k : 1) * 8 * 4));
-  CBFT_HIP(c->bls_partial.reserve((size_t)((k + 15) / 16 + 1) * BLS_JAC_WORDS * 4));
+  CBFT_HIP(c->bls_partial.reserve((size_t)(2 * k + 16) * BLS_JAC_WORDS * 4));  // row MSM levels
   CBFT_HIP(c->bls_out.reserve(BLS_JAC_WORDS * 4));
   CBFT_HIP(c->bls_flag.reserve(1));
   if (!c->bls_inv.p) {

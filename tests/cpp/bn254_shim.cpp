@@ -2,6 +2,7 @@
 // Python tests through ctypes: the SAME source that runs on gfx950, checked on the CPU against
 // oracle/bn254_ref.py.  Test infrastructure; also the labelled "not RELIC" CPU baseline.
 #include <cstring>
+#include <random>
 #include <thread>
 #include <vector>
 
@@ -20,6 +21,10 @@ static void fp12_flat(uint8_t* out, const fp12& x) {  // 12 x 32-byte big-endian
     words_to_be32(out + 32 * (k + 6), w);
   }
 }
+
+#include "row_emu.h"
+#include "bn254_row.h"
+#include "bn254_g1row.h"
 
 extern "C" {
 
@@ -387,6 +392,178 @@ void shim_g2_mul_gen_ct(const uint8_t* skbe, uint8_t* out65) {
   g2a a;
   g2_to_affine(a, acc);
   g2_compress(out65, a);
+}
+
+// Row-parallel Fp (bn254_row.h) over the host SIMD emulation: random chains of rf_mul / rf_add /
+// rf_sub in the four rows of a wave against f_mul / f_add / f_sub on one-lane elements.  Returns
+// the number of mismatches (0 = pass); edge operands (0, 1, q-1, 2q-1 and limbs at 2^29 + 8)
+// included.
+static HU row_of4(const fp* x) {
+  HU r;
+  for (int row = 0; row < 4; row++)
+    for (int i = 0; i < BN_LIMBS; i++) r.x[16 * row + i] = x[row].v[i];
+  return r;
+}
+static void fe_of_row(fp& r, const HU& x, int row) {  // normalise row `row` into a one-lane element
+  uint64_t c = 0;
+  for (int i = 0; i < BN_LIMBS; i++) {
+    const uint64_t t = (uint64_t)x.x[16 * row + i] + c;
+    r.v[i] = i == BN_LIMBS - 1 ? (uint32_t)t : (uint32_t)(t & BN_MASK);
+    c = t >> 29;
+  }
+  for (int i = 9; i < 16; i++)
+    if (x.x[16 * row + i]) r.v[0] = 0xFFFFFFFFu;  // lanes 9..15 must stay zero
+}
+static bool fe_same(const fp& a, const fp& b) {  // equal mod q
+  uint32_t wa[8], wb[8];
+  f_to_words(wa, a);
+  f_to_words(wb, b);
+  for (int i = 0; i < 8; i++)
+    if (wa[i] != wb[i]) return false;
+  return true;
+}
+int shim_rf_check(uint64_t seed, int iters) {
+  std::mt19937_64 g(seed);
+  auto rnd = [&](fp& x) {
+    uint32_t w[8];
+    for (int i = 0; i < 8; i++) w[i] = (uint32_t)g();
+    w[7] &= 0x1FFFFFFF;
+    f_from_words(x, w);  // Montgomery form of a value < 2^253 (< q)
+  };
+  HU tag;
+  const HU qrow = rf_row_const(FpParams::Q, tag), q8r = rf_row_const(RfConsts::Q8R, tag);
+  fp a[4], b[4];
+  for (int r = 0; r < 4; r++) {
+    rnd(a[r]);
+    rnd(b[r]);
+  }
+  f_zero(a[1]);                                    // 0
+  f_one(b[2]);                                     // 1 (Montgomery)
+  for (int i = 0; i < BN_LIMBS; i++) a[3].v[i] = FpParams::Q[i];  // q (= 0), unreduced operand
+  HU ra = row_of4(a), rb = row_of4(b);
+  int bad = 0;
+  for (int it = 0; it < iters; it++) {
+    const int op = it % 4;
+    HU rr;
+    fp e[4];
+    if (op == 0 || op == 3) {
+      rr = rf_mul<HU, HW>(ra, rb, qrow);
+      for (int r = 0; r < 4; r++) f_mul(e[r], a[r], b[r]);
+    } else if (op == 1) {
+      // a + b with a, b < 2q: a row-normal value < 4q
+      rr = rf_add(ra, rb);
+      for (int r = 0; r < 4; r++) f_add(e[r], a[r], b[r]);
+    } else {
+      rr = rf_sub(ra, rb, q8r);
+      for (int r = 0; r < 4; r++) f_sub(e[r], a[r], b[r]);
+    }
+    for (int r = 0; r < 4; r++) {
+      fp got;
+      fe_of_row(got, rr, r);
+      if (!fe_same(got, e[r])) bad++;
+      for (int l = 0; l < 16; l++)
+        if (l < 9 ? rr.x[16 * r + l] > (1u << 29) + 8 : rr.x[16 * r + l] != 0) bad++;
+    }
+    // next operands: the row results (reduced below 2q by a multiplication so the bounds hold)
+    if (op == 0 || op == 3) {
+      ra = rb;
+      for (int r = 0; r < 4; r++) a[r] = b[r];
+      rb = rr;
+      for (int r = 0; r < 4; r++) b[r] = e[r];
+    } else {
+      const HU m = rf_mul<HU, HW>(rr, ra, qrow);
+      for (int r = 0; r < 4; r++) f_mul(a[r], e[r], a[r]);
+      ra = m;
+    }
+  }
+  return bad;
+}
+
+// G1 row-parallel dbl / add (bn254_g1row.h) over the host emulation against g1_dbl / g1_add:
+// random points (multiples of g1_map outputs) including p + p (the doubling branch) and
+// p + (-p) (infinity).  Returns the number of mismatches.
+static HU row_all(const fp& x) {
+  HU r;
+  for (int row = 0; row < 4; row++)
+    for (int i = 0; i < BN_LIMBS; i++) r.x[16 * row + i] = x.v[i];
+  return r;
+}
+static bool rows_consistent(const HU& x) {  // every row holds the same element, lanes 9..15 zero
+  for (int row = 1; row < 4; row++)
+    for (int i = 0; i < 16; i++)
+      if (x.x[16 * row + i] != x.x[i]) return false;
+  for (int i = 9; i < 16; i++)
+    if (x.x[i]) return false;
+  return true;
+}
+static void g1j_of_row(g1j& r, const G1R<HU>& p) {
+  fe_of_row(r.X, p.X, 0);
+  fe_of_row(r.Y, p.Y, 0);
+  fe_of_row(r.Z, p.Z, 0);
+  const fp one = [] { fp o; f_one(o); return o; }();
+  f_mul(r.X, r.X, one);  // values < 4q -> < 2q (reduced, as the one-lane code expects)
+  f_mul(r.Y, r.Y, one);
+  f_mul(r.Z, r.Z, one);
+}
+static bool same_point(const g1j& a, const g1j& b) {
+  g1a x, y;
+  g1_to_affine(x, a);
+  g1_to_affine(y, b);
+  uint8_t ba[33], bb[33];
+  g1_compress(ba, x);
+  g1_compress(bb, y);
+  return std::memcmp(ba, bb, 33) == 0;
+}
+int shim_g1r_check(uint64_t seed, int iters) {
+  std::mt19937_64 g(seed);
+  HU tag;
+  const RowCtx<HU, HW> c(tag);
+  int bad = 0;
+  for (int it = 0; it < iters; it++) {
+    uint8_t msg[8];
+    for (auto& m : msg) m = (uint8_t)g();
+    g1a h;
+    g1_map(h, msg, 8);
+    g1j P, Q;
+    g1_from_affine(P, h);
+    uint32_t k[8] = {(uint32_t)g(), (uint32_t)g(), (uint32_t)g(), 0, 0, 0, 0, 0};
+    g1_mul(Q, P, k);  // a Jacobian Z != 1
+    const int kind = it % 5;
+    if (kind == 3) Q = P;                      // doubling branch
+    if (kind == 4) {                           // -P: infinity
+      Q = P;
+      f_neg(Q.Y, P.Y);
+    }
+    G1R<HU> rp{row_all(P.X), row_all(P.Y), row_all(P.Z)}, rq{row_all(Q.X), row_all(Q.Y), row_all(Q.Z)}, rr;
+    // doubling
+    g1r_dbl(rr, rq, c);
+    g1j e, got;
+    g1_dbl(e, Q);
+    g1j_of_row(got, rr);
+    if (!same_point(got, e) || !rows_consistent(rr.X) || !rows_consistent(rr.Y) || !rows_consistent(rr.Z)) bad++;
+    // addition (and a chain: the doubled point added to p)
+    const G1rAddResult res = g1r_add(rr, rp, rq, c);
+    g1_add(e, P, Q);
+    if (kind == 4) {
+      if (res != G1R_INF || !g1_is_inf(e)) bad++;
+      continue;
+    }
+    g1j_of_row(got, rr);
+    if (res != G1R_SUM || !same_point(got, e) || !rows_consistent(rr.X)) bad++;
+    G1R<HU> r2;
+    g1r_add(r2, rr, rp, c);
+    g1j e2;
+    g1_add(e2, e, P);
+    g1j_of_row(got, r2);
+    if (!same_point(got, e2)) bad++;
+    G1R<HU> rn;
+    g1r_neg(rn, rp, c);
+    g1j n = P;
+    f_neg(n.Y, P.Y);
+    g1j_of_row(got, rn);
+    if (!same_point(got, n)) bad++;
+  }
+  return bad;
 }
 
 int shim_g2_decompress(const uint8_t* in65, uint8_t* out65) {

@@ -473,8 +473,8 @@ static int testAggregatorAndKeySlots() {
   std::string cpk = sm->getClientsPublicKeys();  // CMF-encoded; Ed25519 clients are not listed (see header)
   CHECK(cpk.size() >= 6);
 
-  // key rotation: the first new key takes a fresh slot (the old one is still referenced while the
-  // replacement is built), the second rotation reuses the slot the first one freed
+  // key rotation: the new key is registered while the old one is still referenced, then the old
+  // slot is freed; the second rotation therefore reuses a freed slot and the table does not grow
   const std::string m = "rotated client request";
   CHECK(sm->verifySig(4, m.data(), m.size(), c4.sign(m).data(), 64));
   const auto s0 = ed25519EngineStats();
@@ -482,7 +482,9 @@ static int testAggregatorAndKeySlots() {
   sm->setClientPublicKey(k1.getPubKeyHex(), 4, KeyFormat::HexaDecimalStrippedFormat);
   CHECK(sm->verifySig(4, m.data(), m.size(), k1.sign(m).data(), 64));
   const auto s1 = ed25519EngineStats();
-  CHECK(s1.table_keys == s0.table_keys + 1 && s1.live_keys == s0.live_keys);
+  // one key in, one out; the new key took a free slot or one new slot (the engine is process-wide:
+  // earlier tests may have left free slots)
+  CHECK(s1.table_keys <= s0.table_keys + 1 && s1.live_keys == s0.live_keys);
   sm->setClientPublicKey(k2.getPubKeyHex(), 4, KeyFormat::HexaDecimalStrippedFormat);
   CHECK(sm->verifySig(4, m.data(), m.size(), k2.sign(m).data(), 64));
   CHECK(!sm->verifySig(4, m.data(), m.size(), k1.sign(m).data(), 64));
