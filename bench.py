@@ -636,6 +636,8 @@ def bench_bls(ctx, args, cpu_threads):
     cert = workload.make_bls_cert(n, k, extra=77, bad_frac=0.10, seed=2024, threads=cpu_threads)
     kid = ctx.bls_load_keys(cert.pk, cert.vks)
     try:
+        if not all(ctx.bls_key_status(kid, n)):
+            raise SystemExit("BLS keyset: a verification key failed to decode on the GPU")
         h33 = ctx.bls_hash_to_g1(cert.msg)
         valid = ctx.bls_verify_shares(kid, cert.msg, cert.shares)
         exp = np.array([j not in cert.bad for j in range(len(cert.shares))])
@@ -692,6 +694,9 @@ def bench_bls(ctx, args, cpu_threads):
             sig, ok, badv = ctx.bls_combine_threshold(kid, cert.msg, cert.shares, optimistic=True)
             assert ok and sig == cert.expected_sig and np.array_equal(np.asarray(badv, dtype=bool), planted)
 
+        # a threshold keyset (re)load, as on a per-window key rotation (CryptoManager.hpp:116-141):
+        # 1,024 vks + the group key decoded, subgroup-checked and their Miller-loop lines built
+        t_load = _median_ms(lambda: ctx.bls_unload_keys(ctx.bls_load_keys(cert.pk, cert.vks)), 3)
         t_cert = _median_ms(certificate, runs)
         t_fused = _median_ms(fused, runs)
         t_policy = _median_ms(policy, runs)
@@ -712,6 +717,9 @@ def bench_bls(ctx, args, cpu_threads):
                                        "SignaturesProcessingJob order -- optimistic combine of all shares + verify "
                                        "(fails with 10 % bad), then the fallback",
            "combine_ms": t_comb, "verify_ms": t_ver, "optimistic_ms": t_opt, "multisig_ms": t_ms,
+           "keyset_load_ms": t_load,
+           "keyset_load_basis": f"cbft_bls_load_keys + unload of {n} vks + the group key (decode, subgroup check, "
+                                f"70 normalised Miller-loop lines per key)",
            "verdicts": "share verdicts == planted bad set; combined sig == sk*H(m) byte-exact",
            "parity": parity}
     out["roofline"] = _bls_roofline()

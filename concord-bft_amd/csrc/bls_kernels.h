@@ -44,7 +44,10 @@ hipError_t cbft_bls_launch_g1_parts(const uint32_t* d_parts, uint32_t count, uin
 // BLS_G2_PART_WORDS) or compressed (d_out65)
 hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok, uint32_t n, const uint8_t* d_bitmap,
                                   uint32_t lo_id, uint32_t hi_id, uint8_t* d_ok, uint8_t* d_out65, uint32_t* d_out_part,
+                                  uint32_t* d_tmp,
                                   hipStream_t s);
+// scratch words cbft_bls_launch_g2_sum needs for the wave form's intermediate partials
+size_t cbft_bls_g2_sum_tmp_words();
 // H = g1_map(msg) (-> d_H when non-null) and e(H, PK) e(-sigma, g2) == 1 in one launch
 // multisig verify in one launch: PK = sum of count key-sum partials, its lines streamed from one
 // wave to the Miller loop of another, sigma's pair on a third (d_pk_ok = PK usable)

@@ -21,6 +21,21 @@
 #include "bn254_g1row.h"
 
 using RCtx = RowCtx<uint32_t, uint64_t>;
+
+#ifndef CBFT_BLS_PHASES
+#define CBFT_BLS_PHASES 0
+#endif
+#if CBFT_BLS_PHASES  // probe builds: block 0's phase timestamps, printed at its end
+__device__ uint64_t g_msm_phase[4];
+#define MSM_STAMP(s)                                                                      \
+  do {                                                                                    \
+    if (blockIdx.x == 0 && threadIdx.x == 0) g_msm_phase[(s)] = wall_clock64();           \
+  } while (0)
+#else
+#define MSM_STAMP(s) \
+  do {               \
+  } while (0)
+#endif
 using RPt = G1R<uint32_t>;
 
 // row point <- 9-limb words (one-lane limbs at p[0..8]: lane i of every row takes p[i])
@@ -71,6 +86,7 @@ __global__ void __launch_bounds__(MSM_ROW_BLOCK) bls_msm_row_kernel(const uint32
   __shared__ int xinf;
   const uint32_t j = blockIdx.x;
   if (j >= k) return;
+  MSM_STAMP(0);
   const int wave = threadIdx.x >> 6;
   const uint32_t tag = 0;
   const RCtx c(tag);
@@ -101,6 +117,7 @@ __global__ void __launch_bounds__(MSM_ROW_BLOCK) bls_msm_row_kernel(const uint32
     g1r_dbl(T[5], T[2], c);
     g1r_add(T[6], T[5], T[0], c);
     g1r_dbl(T[7], T[3], c);
+    MSM_STAMP(1);
 #pragma nounroll
     for (int w = 32; w >= 0; w--) {
       if (!inf) {
@@ -130,6 +147,7 @@ __global__ void __launch_bounds__(MSM_ROW_BLOCK) bls_msm_row_kernel(const uint32
       acc.X = c.mul(acc.X, rf_from_fe(beta, tag));
     }
   }
+  MSM_STAMP(2);
   // wave 1 hands its half to wave 0
   if (wave == 1) {
     const uint32_t l = __lane_id();
@@ -149,6 +167,12 @@ __global__ void __launch_bounds__(MSM_ROW_BLOCK) bls_msm_row_kernel(const uint32
   h.Z = xch[32 + rl];
   rpt_accum(acc, inf, h, xinf != 0, c);
   rpt_store(out + BLS_JAC_WORDS * (size_t)j, acc, inf, c);
+#if CBFT_BLS_PHASES
+  if (j == 0 && threadIdx.x == 0)
+    printf("bls_msm_row block 0 (us): table %.1f chain %.1f joined+stored %.1f\n",
+           (g_msm_phase[1] - g_msm_phase[0]) * 0.01, (g_msm_phase[2] - g_msm_phase[1]) * 0.01,
+           (wall_clock64() - g_msm_phase[0]) * 0.01);
+#endif
 }
 
 // sum of m points -> one Jacobian partial per block of 16 waves.  affine: points are parsed shares

@@ -242,6 +242,7 @@ __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uin
   }
   __syncthreads();
   fp f;
+  BLS_PHASE(wave == 0 ? 0 : wave == 1 ? 4 : 6);
   if (wave == 0) {
     g2j acc;
     fp2_one(acc.X);
@@ -254,21 +255,26 @@ __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uin
       bad |= parts[55 * (size_t)b + 54] != 0;
       g2_add_j(acc, acc, o);
     }
+    BLS_PHASE(1);
     g2a s;
     g2_to_affine<true>(s, acc);  // public point: variable-time inversion
+    BLS_PHASE(2);
     const bool ok = !bad && !s.inf;
     if (g.lane == 0) {
       pk_ok[0] = ok ? 1 : 0;
       usable = ok ? 1 : 0;
     }
     if (ok) g2w_lines_abc(lines, s, &progress);
+    BLS_PHASE(3);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (g.lane == 0) progress = BN_ATE_LINES + 1;  // release the consumer whatever happened
   } else if (wave == 1) {
     g1a P;
     g1_map_wave(P, msg, len);
+    BLS_PHASE(5);
     const uint32_t* l[1] = {lines};
     p36_miller<1, true>(f, &P, l, g, &progress);
+    BLS_PHASE(12);
   } else {
     g1a s;
     const bool ok = g1_decompress(s, sig33);
@@ -276,10 +282,12 @@ __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uin
       g1a P = s;
       f_neg(P.y, s.y);
       const uint32_t* l[1] = {gen_lines};
+      BLS_PHASE(13);
       p36_miller<1>(f, &P, l, g);
     } else {
       p36_one(f, g);
     }
+    BLS_PHASE(7);
     xchg_put(xc, f, g);
     if (g.lane == 0) xc.ok = ok ? 1 : 0;
   }
@@ -292,7 +300,19 @@ __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uin
     p36_mul(f, f, f1, g);
     good = p36_is_one_after_final_exp(f, g);
   }
+  BLS_PHASE(11);
   if (g.lane == 0) result[0] = good ? 1 : 0;
+#if CBFT_BLS_PHASES
+  if (g.lane == 0) {
+    const uint64_t t0 = g_bls_phase[0];
+    printf("bls_verify_multisig phases (us from start): key sum %.1f affine %.1f lines %.1f | H %.1f miller %.1f | "
+           "sigma %.1f miller %.1f | fe_inv %.1f fe_easy %.1f fe_pow_u %.1f fe_done %.1f\n",
+           (g_bls_phase[1] - t0) * 0.01, (g_bls_phase[2] - t0) * 0.01, (g_bls_phase[3] - t0) * 0.01,
+           (g_bls_phase[5] - t0) * 0.01, (g_bls_phase[12] - t0) * 0.01, (g_bls_phase[13] - t0) * 0.01,
+           (g_bls_phase[7] - t0) * 0.01, (g_bls_phase[8] - t0) * 0.01, (g_bls_phase[9] - t0) * 0.01,
+           (g_bls_phase[10] - t0) * 0.01, (g_bls_phase[11] - t0) * 0.01);
+  }
+#endif
 }
 
 // H = g1_map(msg) (block 0, when H is non-null) beside the decoding of k shares, one lane per

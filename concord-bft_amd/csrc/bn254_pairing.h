@@ -505,8 +505,8 @@ BN_HDN bool g2_in_subgroup(const g2a& q) {  // r * Q == O
 }
 
 // RELIC ep2_read_bin(pack = 1) as restated: 65 bytes, prefix 2 | f_relic_bit(y.a), x0 || x1 < p,
-// on E', and (CHECK) in the order-r subgroup.
-BN_HDN bool g2_decompress(g2a& r, const uint8_t* b) {
+// on E' -- without the subgroup check (g2_decompress adds it; bls_keys.hip runs it wave-wide).
+BN_HDN bool g2_decode_on_curve(g2a& r, const uint8_t* b) {
   r.inf = false;
   if (b[0] == 0) {
     uint8_t o = 0;
@@ -527,7 +527,13 @@ BN_HDN bool g2_decompress(g2a& r, const uint8_t* b) {
   fp2_add(rhs, rhs, b2);
   if (!fp2_sqrt(r.y, rhs)) return false;
   if (f_relic_bit(r.y.a) != (uint32_t)(b[0] & 1)) fp2_neg(r.y, r.y);
-  return g2_in_subgroup(r);
+  return true;
+}
+
+// ... and (CHECK) in the order-r subgroup (r Q == O; infinity decodes, for the caller to judge)
+BN_HDN bool g2_decompress(g2a& r, const uint8_t* b) {
+  if (!g2_decode_on_curve(r, b)) return false;
+  return r.inf || g2_in_subgroup(r);
 }
 
 BN_HDN void g2_compress(uint8_t* out, const g2a& a) {

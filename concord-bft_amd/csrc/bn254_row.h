@@ -113,9 +113,14 @@ RF_HD U rf_carry32(U x) {
   return (x & rf_const(x, BN_MASK)) + rl_shr<1>(x >> 29);
 }
 
+#ifndef RF_MUL_CHECK
+#define RF_MUL_CHECK(a, b)  // host emulation builds check every product's bounds (tests/cpp/bn254_shim.cpp)
+#endif
+
 // r = a * b * 2^-261 mod q (row-normal in, row-normal out, value < 2q).  qrow = rf_row_const(Q).
 template <class U, class W>
 RF_HD U rf_mul(U a, U b, U qrow) {
+  RF_MUL_CHECK(a, b);
   const U rl = rl_index(a);
   W col = rf_const64(a, 0ull);
   // product columns 0..15 in lanes 0..15; column 16 (= a8 b8 + m8 q8) separately

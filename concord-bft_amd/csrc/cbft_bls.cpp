@@ -393,13 +393,14 @@ int cbft_bls_verify_multisig(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint3
   if (rc) return rc;
   CBFT_HIP(c->bls_bitmap.reserve(256));
   CBFT_HIP(c->bls_ms_ok.reserve(1));
+  CBFT_HIP(c->bls_g2tmp.reserve(cbft_bls_g2_sum_tmp_words() * 4));
   CBFT_HIP(c->bls_partial.reserve(CBFT_BLS_G2_PARTIAL_BYTES));
   CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
   // PK = sum vk_i (one Jacobian partial), then the fused 3-wave verify (lines streamed into the
   // Miller loop)
   CBFT_HIP(cbft_bls_launch_g2_sum(ks->aff.as<uint32_t>() + BLS_G2A_WORDS, ks->ok.as<uint8_t>() + 1, ks->n,
                                   c->bls_bitmap.as<uint8_t>(), 1, ks->n + 1, c->bls_ms_ok.as<uint8_t>(), nullptr,
-                                  c->bls_partial.as<uint32_t>(), c->stream));
+                                  c->bls_partial.as<uint32_t>(), c->bls_g2tmp.as<uint32_t>(), c->stream));
   return bls_verify_multisig_parts(c, len, sig33, 1, out_ok);
 }
 
@@ -412,11 +413,12 @@ int cbft_bls_sum_keys(cbft_ctx* c, uint32_t id, const uint8_t* signers256, uint8
   CBFT_HIP(hipSetDevice(c->device));
   CBFT_HIP(c->bls_bitmap.reserve(256));
   CBFT_HIP(c->bls_ms_ok.reserve(1));
+  CBFT_HIP(c->bls_g2tmp.reserve(cbft_bls_g2_sum_tmp_words() * 4));
   CBFT_HIP(c->bls_out.reserve(65));
   CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(cbft_bls_launch_g2_sum(ks->aff.as<uint32_t>() + BLS_G2A_WORDS, ks->ok.as<uint8_t>() + 1, ks->n,
                                   c->bls_bitmap.as<uint8_t>(), 1, ks->n + 1, c->bls_ms_ok.as<uint8_t>(),
-                                  c->bls_out.as<uint8_t>(), nullptr, c->stream));
+                                  c->bls_out.as<uint8_t>(), nullptr, c->bls_g2tmp.as<uint32_t>(), c->stream));
   CBFT_HIP(hipMemcpyAsync(out65, c->bls_out.p, 65, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipStreamSynchronize(c->stream));
   return CBFT_OK;
@@ -432,11 +434,12 @@ int cbft_bls_sum_keys_partial(cbft_ctx* c, uint32_t id, const uint8_t* signers25
   CBFT_HIP(hipSetDevice(c->device));
   CBFT_HIP(c->bls_bitmap.reserve(256));
   CBFT_HIP(c->bls_ms_ok.reserve(1));
+  CBFT_HIP(c->bls_g2tmp.reserve(cbft_bls_g2_sum_tmp_words() * 4));
   CBFT_HIP(c->bls_partial.reserve(CBFT_BLS_G2_PARTIAL_BYTES));
   CBFT_HIP(hipMemcpyAsync(c->bls_bitmap.p, signers256, 256, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(cbft_bls_launch_g2_sum(ks->aff.as<uint32_t>() + BLS_G2A_WORDS, ks->ok.as<uint8_t>() + 1, ks->n,
                                   c->bls_bitmap.as<uint8_t>(), lo_id, hi_id, c->bls_ms_ok.as<uint8_t>(), nullptr,
-                                  c->bls_partial.as<uint32_t>(), c->stream));
+                                  c->bls_partial.as<uint32_t>(), c->bls_g2tmp.as<uint32_t>(), c->stream));
   CBFT_HIP(hipMemcpyAsync(out_partial, c->bls_partial.p, CBFT_BLS_G2_PARTIAL_BYTES, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipStreamSynchronize(c->stream));
   return CBFT_OK;

@@ -267,7 +267,7 @@ void cbft_close(cbft_ctx* c) {
   }
   for (DevBuf* b : {&c->bls_gen_lines, &c->bls_msg, &c->bls_H, &c->bls_shares, &c->bls_valid, &c->bls_sig,
                     &c->bls_ids, &c->bls_use, &c->bls_lambda, &c->bls_partial, &c->bls_out,
-                    &c->bls_ms_ok, &c->bls_bitmap, &c->bls_inv, &c->bls_first, &c->bls_flag})
+                    &c->bls_ms_ok, &c->bls_bitmap, &c->bls_inv, &c->bls_first, &c->bls_flag, &c->bls_g2tmp})
     b->release();
   (void)hipDeviceSynchronize();  // device-path batches may still run on caller streams
   for (DevBuf* b : {&c->base_table, &c->base_comb, &c->verdicts, &c->sig, &c->msg, &c->off, &c->len, &c->kidx, &c->pk,

@@ -188,7 +188,7 @@ struct cbft_ctx {
   hipEvent_t rsa_ev[2] = {nullptr, nullptr};  // around the last RSA kernel when profiling
   bool rsa_ev_valid = false;
   DevBuf bls_gen_lines, bls_msg, bls_H, bls_shares, bls_valid, bls_sig, bls_ids, bls_use, bls_lambda,
-      bls_partial, bls_out, bls_ms_ok, bls_bitmap, bls_inv, bls_first, bls_flag;
+      bls_partial, bls_out, bls_ms_ok, bls_bitmap, bls_inv, bls_first, bls_flag, bls_g2tmp;
 };
 
 int cbft_fail(hipError_t e, const char* what, const char* file, int line);

@@ -23,8 +23,34 @@ static void fp12_flat(uint8_t* out, const fp12& x) {  // 12 x 32-byte big-endian
 }
 
 #include "row_emu.h"
+// every rf_mul's operands checked against its precondition: row-normal limbs and
+// (a / q)(b / q) < 221 in every row (counted in g_rf_bound_violations)
+static void rf_mul_check(const HU& a, const HU& b);
+#define RF_MUL_CHECK(a, b) rf_mul_check(a, b)
 #include "bn254_row.h"
 #include "bn254_g1row.h"
+#include "bn254_g2row.h"
+
+static long g_rf_bound_violations = 0;
+static long double rf_row_over_q(const HU& x, int row) {
+  static const long double q = [] {
+    long double v = 0;
+    for (int i = BN_LIMBS - 1; i >= 0; i--) v = v * 536870912.0L + FpParams::Q[i];
+    return v;
+  }();
+  long double v = 0;
+  for (int i = BN_LIMBS - 1; i >= 0; i--) v = v * 536870912.0L + x.x[16 * row + i];
+  return v / q;
+}
+static void rf_mul_check(const HU& a, const HU& b) {
+  for (int row = 0; row < 4; row++) {
+    for (int l = 0; l < 16; l++) {
+      const uint32_t lim = l < 9 ? (1u << 29) + 8 : 0u;
+      if (a.x[16 * row + l] > lim || b.x[16 * row + l] > lim) g_rf_bound_violations++;
+    }
+    if (rf_row_over_q(a, row) * rf_row_over_q(b, row) >= 221.0L) g_rf_bound_violations++;
+  }
+}
 
 extern "C" {
 
@@ -564,6 +590,157 @@ int shim_g1r_check(uint64_t seed, int iters) {
     if (!same_point(got, n)) bad++;
   }
   return bad;
+}
+
+// G2 row-parallel arithmetic (bn254_g2row.h) over the host emulation against the one-lane G2
+// code: g2r_dbl<LINE> vs line_dbl_j / g2_dbl_j, g2r_madd<LINE> vs line_add_j / g2_add_j_body,
+// g2r_add vs g2_add_j_body (incl. T + T and T + (-T)), g2r_accum chains, and g2r_in_subgroup
+// vs g2_in_subgroup on points of G2 and off it.  Lines compared as field values (A, B, C), points
+// projectively.  Returns the mismatches plus every rf_mul bound violation seen.
+static F2R<HU> f2r_of(const fp2& x) { return {row_all(x.a), row_all(x.b)}; }
+static void fp2_of_row(fp2& r, const F2R<HU>& x) {
+  const fp one = [] { fp o; f_one(o); return o; }();
+  fe_of_row(r.a, x.a, 0);
+  fe_of_row(r.b, x.b, 0);
+  f_mul(r.a, r.a, one);  // value < 4q -> < 2q
+  f_mul(r.b, r.b, one);
+}
+static G2R<HU> g2r_of(const g2j& p) { return {f2r_of(p.X), f2r_of(p.Y), f2r_of(p.Z)}; }
+static void g2j_of_row(g2j& r, const G2R<HU>& p) {
+  fp2_of_row(r.X, p.X);
+  fp2_of_row(r.Y, p.Y);
+  fp2_of_row(r.Z, p.Z);
+}
+static bool fp2_same(const fp2& a, const fp2& b) { return fe_same(a.a, b.a) && fe_same(a.b, b.b); }
+static bool f2r_consistent(const F2R<HU>& x) { return rows_consistent(x.a) && rows_consistent(x.b); }
+static bool g2_same(const g2j& a, const g2j& b) {
+  g2a x, y;
+  g2_to_affine(x, a);
+  g2_to_affine(y, b);
+  uint8_t ba[65], bb[65];
+  g2_compress(ba, x);
+  g2_compress(bb, y);
+  return std::memcmp(ba, bb, 65) == 0;
+}
+static bool line_same(const F2R<HU>* l, const uint32_t* ln, const uint32_t* sa) {
+  fp2 A, B, C, eA, eB, eC;
+  fp2_of_row(A, l[0]);
+  fp2_of_row(B, l[1]);
+  fp2_of_row(C, l[2]);
+  fp2_fetch(eA, sa);
+  fp2_fetch(eB, ln);
+  fp2_fetch(eC, ln + 18);
+  return fp2_same(A, eA) && fp2_same(B, eB) && fp2_same(C, eC) && f2r_consistent(l[0]) && f2r_consistent(l[1]) &&
+         f2r_consistent(l[2]);
+}
+int shim_g2r_check(uint64_t seed, int iters) {
+  std::mt19937_64 g(seed);
+  HU tag;
+  const G2RowCtx<HU, HW> c(tag);
+  g_rf_bound_violations = 0;
+  int bad = 0;
+  g2j G;
+  fp2_load(G.X, Bn254Consts::G2X);
+  fp2_load(G.Y, Bn254Consts::G2Y);
+  fp2_one(G.Z);
+  for (int it = 0; it < iters; it++) {
+    uint32_t k[8] = {(uint32_t)g(), (uint32_t)g(), (uint32_t)g(), (uint32_t)g(), 0, 0, 0, 0};
+    g2j P, Q;
+    g2_mul_ct(P, G, k);  // Jacobian, Z != 1
+    k[0] ^= 0x5a5a;
+    g2_mul_ct(Q, G, k);
+    g2a qa;
+    g2_to_affine(qa, Q);
+    // doubling with / without the line
+    {
+      g2j T = P, e = P;
+      uint32_t ln[36], sa[36];
+      line_dbl_j(ln, sa, e);
+      G2R<HU> rt = g2r_of(T);
+      F2R<HU> l[3];
+      g2r_dbl<true>(l, rt, c);
+      g2j got;
+      g2j_of_row(got, rt);
+      if (!g2_same(got, e) || !line_same(l, ln, sa) || !f2r_consistent(rt.X) || !f2r_consistent(rt.Y) ||
+          !f2r_consistent(rt.Z))
+        bad++;
+      G2R<HU> r2 = g2r_of(T);
+      g2r_dbl<false>((F2R<HU>*)nullptr, r2, c);
+      g2j_of_row(got, r2);
+      g2j e2;
+      g2_dbl_j(e2, T);
+      if (!g2_same(got, e2)) bad++;
+    }
+    // mixed addition with / without the line
+    {
+      g2j e = P;
+      uint32_t ln[36], sa[36];
+      line_add_j(ln, sa, e, qa.x, qa.y);
+      G2R<HU> rt = g2r_of(P);
+      F2R<HU> l[3];
+      bool same = false;
+      g2r_madd<true>(l, rt, f2r_of(qa.x), f2r_of(qa.y), c, same);
+      g2j got;
+      g2j_of_row(got, rt);
+      if (!g2_same(got, e) || !line_same(l, ln, sa)) bad++;
+      G2R<HU> r2 = g2r_of(P);
+      if (!g2r_madd<false>((F2R<HU>*)nullptr, r2, f2r_of(qa.x), f2r_of(qa.y), c, same)) bad++;
+      g2j_of_row(got, r2);
+      if (!g2_same(got, e)) bad++;
+    }
+    // full addition, and its exceptional cases
+    {
+      G2R<HU> rt = g2r_of(P);
+      bool same = false;
+      if (!g2r_add(rt, g2r_of(Q), c, same)) bad++;
+      g2j e, got;
+      g2_add_j(e, P, Q);
+      g2j_of_row(got, rt);
+      if (!g2_same(got, e)) bad++;
+      g2j P2;  // P in another Jacobian representation
+      g2_add_j(P2, P, G);
+      g2j nG = G;
+      fp2_neg(nG.Y, G.Y);
+      g2_add_j(P2, P2, nG);
+      G2R<HU> a = g2r_of(P);
+      if (g2r_add(a, g2r_of(P2), c, same) || !same) bad++;  // P + P: the doubling case
+      g2j nP = P2;
+      fp2_neg(nP.Y, P2.Y);
+      G2R<HU> b = g2r_of(P);
+      if (g2r_add(b, g2r_of(nP), c, same) || same) bad++;  // P + (-P): infinity
+      // accumulate chains with the flags: P + P + (-2P) + Q == Q
+      G2R<HU> acc{};
+      bool inf = true;
+      g2r_accum(acc, inf, g2r_of(P), false, c);
+      g2r_accum(acc, inf, g2r_of(P2), false, c);
+      g2j m2;
+      g2_dbl_j(m2, P);
+      fp2_neg(m2.Y, m2.Y);
+      g2r_accum(acc, inf, g2r_of(m2), false, c);
+      if (!inf) bad++;
+      g2r_accum_aff(acc, inf, f2r_of(qa.x), f2r_of(qa.y), c);
+      g2j_of_row(got, acc);
+      if (inf || !g2_same(got, Q)) bad++;
+    }
+    // subgroup membership: a point of G2, and (every 4th iteration) a twist point off it
+    if (it % 4 == 0) {
+      g2a pa;
+      g2_to_affine(pa, P);
+      if (!g2r_in_subgroup(f2r_of(pa.x), f2r_of(pa.y), c)) bad++;
+      uint8_t enc[65] = {0x02};
+      for (uint32_t x = 1 + (uint32_t)(g() & 0xffff);; x++) {
+        enc[64] = (uint8_t)x;
+        enc[63] = (uint8_t)(x >> 8);
+        enc[62] = (uint8_t)(x >> 16);
+        enc[32] = 1;
+        g2a t;
+        if (!g2_decode_on_curve(t, enc)) continue;
+        if (g2r_in_subgroup(f2r_of(t.x), f2r_of(t.y), c) != g2_in_subgroup(t)) bad++;
+        break;
+      }
+    }
+  }
+  return bad + (int)g_rf_bound_violations;
 }
 
 int shim_g2_decompress(const uint8_t* in65, uint8_t* out65) {

@@ -228,3 +228,100 @@ def test_sharded_multisig_key_sum(ctx, world):
         assert not ctx.bls_verify_multisig_partials(msg, sig, parts2)
     finally:
         ctx.bls_unload_keys(kid)
+
+
+def _bad_g2_keys():
+    """Encodings bls_keys_wave_kernel must reject exactly as g2_decompress does (the one-lane
+    kernel and the oracle): bad prefix, x >= p, an x off E', a point of E'(Fp2) outside the
+    order-r subgroup, and infinity (decodes, but a threshold key of infinity is unusable)."""
+    x = 1
+    while B.f2_sqrt(B.F2(x, 1) * B.F2(x, 1) * B.F2(x, 1) + B.B2) is not None:  # x^3 + b' a non-square: off the curve
+        x += 1
+    off_curve = b"\x02" + x.to_bytes(32, "big") + (1).to_bytes(32, "big")
+    x = 1
+    while True:  # a twist point: E'(Fp2) has order r * h2, so [r]Q != O for this x
+        y = B.f2_sqrt(B.F2(x, 2) * B.F2(x, 2) * B.F2(x, 2) + B.B2)
+        if y is not None:
+            pt = (B.F2(x, 2), y)
+            if B.ec_mul(B.R, pt) is not None:
+                break
+        x += 1
+    return {"prefix": b"\x05" + bytes(64), "x_ge_p": b"\x02" + B.P.to_bytes(32, "big") + bytes(32),
+            "off_curve": off_curve, "not_in_g2": B.g2_to_bytes(pt), "infinity": bytes(65)}
+
+
+def test_key_decoding_edge_cases_and_lines(ctx):
+    """Key status of a set mixing valid and invalid verification keys equals the oracle's decode
+    (infinity excepted: unusable), and the lines built for the valid ones verify their shares
+    while every share under an invalid key is rejected."""
+    n, k = 12, 8
+    sk, sks, pk, vks = blsgen.keyset(n, k, seed=29)
+    bad = _bad_g2_keys()
+    slots = {2: "prefix", 5: "x_ge_p", 7: "off_curve", 9: "not_in_g2", 11: "infinity"}
+    vks = list(vks)
+    for i, name in slots.items():
+        vks[i - 1] = bad[name]
+    for name, enc in bad.items():
+        if name == "infinity":
+            assert B.g2_from_bytes(enc) is None
+        else:
+            with pytest.raises(ValueError):
+                B.g2_from_bytes(enc)
+    msg = bytes(range(7, 39))
+    good = blsgen.shares(sks, range(1, n + 1), msg)
+    kid = ctx.bls_load_keys(pk, vks)
+    try:
+        status = ctx.bls_key_status(kid, n)
+        got = ctx.bls_verify_shares(kid, msg, good)
+    finally:
+        ctx.bls_unload_keys(kid)
+    assert status[0] == 1  # the group key
+    assert [bool(s) for s in status[1:]] == [i not in slots for i in range(1, n + 1)]
+    assert got.tolist() == [i not in slots for i in range(1, n + 1)]
+
+
+def test_generator_and_key_lines_verify_full_keyset(ctx):
+    """A 1,024-key set (the config #4 size, one wave pair per key): all keys decode, and a share
+    of every 64th signer verifies while a doubled one does not."""
+    n, k = 1024, 683
+    sk, sks, pk, vks = blsgen.keyset(n, k, seed=31)
+    msg = bytes(32)
+    ids = list(range(1, n + 1, 64)) + [n]
+    good = blsgen.shares(sks, ids, msg)
+    cases = good + [blsgen.doubled(good[0]), blsgen.doubled(good[-1])]
+    kid = ctx.bls_load_keys(pk, vks)
+    try:
+        assert all(ctx.bls_key_status(kid, n))
+        got = ctx.bls_verify_shares(kid, msg, cases)
+    finally:
+        ctx.bls_unload_keys(kid)
+    assert got.tolist() == [True] * len(good) + [False, False]
+
+
+def test_sum_keys_exceptional_cases(ctx):
+    """The wave key sum's exact group law: a key repeated (the addition turns into a doubling),
+    a key and its negation (the partial sum hits infinity, then continues), a sum that ends at
+    infinity, a selected key that did not decode (sum unusable), over 1,024 keys so the sum
+    runs over several blocks and levels."""
+    n = 1024
+    sk, sks, pk, vks = blsgen.keyset(n, 2, seed=37)
+    vks = list(vks)
+    neg = lambda e: bytes([e[0] ^ 1]) + e[1:]  # noqa: E731  (-P: the y sign bit flipped)
+    vks[3] = vks[2]            # id 4 = id 3
+    vks[5] = neg(vks[4])       # id 6 = -id 5
+    vks[700] = neg(vks[699])   # id 701 = -id 700, in another block
+    vks[900] = b"\x05" + bytes(64)  # id 901 does not decode
+    pts = [B.g2_from_bytes(v) if i != 900 else None for i, v in enumerate(vks)]
+    kid = ctx.bls_load_keys(pk, vks)
+    try:
+        cases = [[3, 4], [5, 6], [3, 4, 5, 6, 7], [700, 701], list(range(1, 17)), list(range(1, 901)),
+                 [i for i in range(1, n + 1) if i % 3 and i != 901], list(range(2, 700, 7))]
+        for ids in cases:
+            acc = None
+            for i in ids:
+                acc = B.ec_add(acc, pts[i - 1], None)
+            assert ctx.bls_sum_keys(kid, B.signers_bitmap(ids)) == B.g2_to_bytes(acc), ids[:8]
+        bm = B.signers_bitmap([1, 2, 901])
+        assert ctx.bls_sum_keys(kid, bm) == bytes(65)  # a selected key that did not decode
+    finally:
+        ctx.bls_unload_keys(kid)

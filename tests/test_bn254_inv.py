@@ -187,3 +187,23 @@ def test_secret_scalar_ladders_match_double_and_add(shim):
         shim.shim_g2_mul_gen(kb, c)
         shim.shim_g2_mul_gen_ct(kb, d)
         assert c.raw == d.raw, hex(k)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_row_fp_and_g1_emulation(shim, seed):
+    """Row-parallel Fp (bn254_row.h) and G1 (bn254_g1row.h) over the host SIMD emulation of the
+    gfx950 DPP / ds_bpermute moves, against the one-lane field and group code (0 = no mismatch)."""
+    for fn, iters in ((shim.shim_rf_check, 4000), (shim.shim_g1r_check, 60)):
+        fn.argtypes = [ctypes.c_uint64, ctypes.c_int]
+        assert fn(seed, iters) == 0, fn.__name__
+
+
+@pytest.mark.parametrize("seed", [11, 12, 13, 14])
+def test_row_g2_emulation(shim, seed):
+    """Row-parallel G2 (bn254_g2row.h) against the one-lane G2 code: doubling and mixed addition
+    with their Miller-loop lines (line_dbl_j / line_add_j values), full Jacobian addition incl.
+    T + T and T + (-T), flag-carrying accumulation chains, and the NAF subgroup check against
+    r Q == O on points of G2 and twist points off it; every row product's operands are checked
+    against rf_mul's bounds (row-normal limbs, (a/q)(b/q) < 221)."""
+    shim.shim_g2r_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
+    assert shim.shim_g2r_check(seed, 24) == 0

@@ -1,5 +1,6 @@
-"""Phase timing of bls_verify_kernel (needs a library built with -DCBFT_BLS_PHASES=1, selected by
-$CBFT_LIB): one verify of a config #4 combined signature; the kernel's printf lines go to stdout."""
+"""Phase timing of the BLS kernels that print them (needs a library built with
+-DCBFT_BLS_PHASES=1, selected by $CBFT_LIB): bls_verify_kernel, bls_verify_multisig_kernel and
+block 0 of bls_msm_row_kernel on a config #4 certificate; the kernels' printf lines go to stdout."""
 import os
 import sys
 
@@ -15,3 +16,15 @@ with cb.Context(device=0) as ctx:
     for _ in range(3):
         ok = ctx.bls_verify(kid, cert.msg, comb)
     print("verify ok", ok, flush=True)
+    use = cert.shares[:683]
+    for _ in range(2):
+        c = ctx.bls_combine(use)
+    print("combine ok", c == comb, flush=True)
+    bitmap = bytearray(256)
+    for s in use:
+        i = int.from_bytes(s[:4], "big")
+        bitmap[(i - 1) // 8] |= 1 << ((i - 1) % 8)
+    msig = ctx.bls_combine(use, multisig=True)
+    for _ in range(3):
+        ok = ctx.bls_verify_multisig(kid, cert.msg, msig, bytes(bitmap))
+    print("multisig ok", ok, flush=True)
