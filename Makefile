@@ -5,6 +5,12 @@ CSRC    := concord-bft_amd/csrc
 LIB     := concord-bft_amd/libcbft_hipcrypto.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall -Wno-unused-function
 ORACLE_LIB := oracle/libcbft_oracle.so
+# The row-parallel BN-P254 code (bn254_row.h: row_shr / row_shl moves with zero fill) is built
+# without LLVM's DPP combiner: on this toolchain (ROCm 7.2 LLVM, gfx950) folding those moves into
+# their consumers left non-zero values in lanes that must read 0 (a G2 addition came out wrong in
+# one inlined copy and right in another; tools/microbench/g2r_dbg2.hip reproduces it, and the
+# host SIMD emulation of the same source is exact).  Costs one v_mov_dpp per move.
+ROWFLAGS := -mllvm -amdgpu-dpp-combine=false
 
 .PHONY: all lib oracle clean shim sanitize
 all: lib oracle cpu host shim
@@ -22,13 +28,13 @@ $(CSRC)/bls_kernels.o: $(CSRC)/bls_kernels.hip $(BLS_DEPS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(CSRC)/bls_pairing.o: $(CSRC)/bls_pairing.hip $(BLS_DEPS)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(ROWFLAGS) -c $< -o $@
 
 $(CSRC)/bls_msm_row.o: $(CSRC)/bls_msm_row.hip $(BLS_DEPS) $(CSRC)/bls_glv.h
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(ROWFLAGS) -c $< -o $@
 
 $(CSRC)/bls_keys.o: $(CSRC)/bls_keys.hip $(BLS_DEPS)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(ROWFLAGS) -c $< -o $@
 
 $(CSRC)/rsa_verify.o: $(CSRC)/rsa_verify.hip $(CSRC)/rsa_verify.h $(CSRC)/sha256.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@

@@ -1,10 +1,10 @@
 // BLS BN-P254 G2 kernels for gfx950: key decoding + Miller-loop line precomputation, the multisig
 // key sum, the signer's public key (threshsign path).
 //
-//   bls_keys_wave_kernel     per G2 key, one block of two waves: decompress + subgroup check
-//                            (wave 0) beside the 70 Miller-loop lines (wave 1), every step's Fp
-//                            products on separate lanes (bn254_g2wave.h); also the generator's
-//                            lines (BlsThresholdVerifier ctor; lines make per-share work G2-free)
+//   bls_keys_row_kernel      per G2 key, one block of two waves: decompress + subgroup check
+//                            (wave 0) beside the 70 Miller-loop lines (wave 1), on row-parallel
+//                            Fp (bn254_g2row.h: limbs across 16-lane rows, four products per
+//                            pass); also the generator's lines (BlsThresholdVerifier ctor; lines make per-share work G2-free)
 //   bls_keys_kernel          the same on one lane per key (kept for A/B: $CBFT_BLS_KEYS=lane)
 //   bls_g2_sum_kernel        multisig PK = sum vk_i over the signer bitmap (Jacobian partial, or
 //                            compressed for cbft_bls_sum_keys)
@@ -30,63 +30,65 @@ __global__ void __launch_bounds__(64) bls_keys_kernel(const uint8_t* keys65, uin
   if (good) g2_precompute_lines_batch(lines + (size_t)k * LINES_PER_KEY, q, scratch + (size_t)k * LINE_SCRATCH_WORDS);
 }
 
-// Normalised lines (lambda, mu: BN_LINE_WORDS words each, g2_precompute_lines_batch's output) from
-// the wave's unnormalised (A, B, C) records in LDS: lambda_k = -B_k / A_k, mu_k = C_k / A_k with
-// Montgomery's trick over the A_k -- prefix products (one Fp2 product per step, its three Fp
-// products on three lanes), one variable-time Fp2 inversion (public key material), the
-// back-substitution (two Fp2 products per step on six lanes), then the 140 lambda / mu products
-// one Fp2 product per lane.  pre: BN_ATE_LINES x 18 words of LDS.  Every lane calls it.
-__device__ __noinline__ void g2w_normalise_lines(uint32_t* out, const uint32_t* abc, uint32_t* pre) {
-  const int lane = threadIdx.x & 63;
-  fp U[6], V[6], p[6];
-  fp2 acc, a;
-  fp2_fetch(acc, abc);
-  if (lane < 18) pre[lane] = lane < 9 ? acc.a.v[lane] : acc.b.v[lane - 9];
+// Normalised lines (lambda, mu: BN_LINE_WORDS words each, g2_precompute_lines_batch's values)
+// from the wave's unnormalised (A, B, C) records in LDS, lambda_k = -B_k / A_k, mu_k = C_k / A_k,
+// by Montgomery's trick over the A_k on row-parallel Fp: prefix products (one Fp2 product per
+// step: one pass), one variable-time Fp2 inversion on every lane (public key material), the
+// back-substitution (two Fp2 products per step: two passes), then the 140 lambda / mu products
+// row-locally, four lines' coefficients at a time.  pre: BN_ATE_LINES x 18 words of LDS.
+__device__ __noinline__ void g2r_normalise_lines(uint32_t* out, const uint32_t* abc, uint32_t* pre) {
+  using R2 = F2R<uint32_t>;
+  const G2RowCtx<uint32_t, uint64_t> c(0u);
+  uint32_t A[6], B[6], P[6];
+  R2 acc = f2r_ld(abc);
+  f2r_st_row0(pre, acc);
 #pragma nounroll
   for (int k = 1; k < BN_ATE_LINES; k++) {
-    fp2_fetch(a, abc + k * BN_ABC_WORDS);
-    g2w_mul_ops(U, V, 0, acc, a);
-    g2w_round<3>(p, U, V, lane);
-    g2w_mul_res(acc, p, 0);
-    if (lane < 18) pre[18 * k + lane] = lane < 9 ? acc.a.v[lane] : acc.b.v[lane - 9];
+    const R2 a = f2r_ld(abc + k * BN_ABC_WORDS);
+    f2r_mul_ops(A, B, 0, acc, a);
+    r_prods<3>(P, A, B, c);
+    f2r_mul_res(acc, P, 0, c);
+    f2r_st_row0(pre + 18 * k, acc);
   }
-  fp2 inv;
-  fp2_inv<true>(inv, acc);
+  fp2 n;
+  rf_to_fe(n.a, acc.a);
+  rf_to_fe(n.b, acc.b);
+  fp2_inv<true>(n, n);
+  R2 inv = f2r_from(n);
 #pragma nounroll
   for (int k = BN_ATE_LINES - 1; k >= 1; k--) {
-    fp2 pk;
-    fp2_fetch(pk, pre + 18 * (k - 1));
-    fp2_fetch(a, abc + k * BN_ABC_WORDS);
-    g2w_mul_ops(U, V, 0, inv, pk);  // 1 / A_k
-    g2w_mul_ops(U, V, 3, inv, a);   // 1 / (A_0 .. A_{k-1})
-    g2w_round<6>(p, U, V, lane);
-    fp2 ai;
-    g2w_mul_res(ai, p, 0);
-    g2w_mul_res(inv, p, 3);
-    if (lane < 18) pre[18 * k + lane] = lane < 9 ? ai.a.v[lane] : ai.b.v[lane - 9];
+    const R2 pk = f2r_ld(pre + 18 * (k - 1)), a = f2r_ld(abc + k * BN_ABC_WORDS);
+    f2r_mul_ops(A, B, 0, inv, pk);  // 1 / A_k
+    f2r_mul_ops(A, B, 3, inv, a);   // 1 / (A_0 .. A_{k-1})
+    r_prods<6>(P, A, B, c);
+    R2 ai;
+    f2r_mul_res(ai, P, 0, c);
+    f2r_mul_res(inv, P, 3, c);
+    f2r_st_row0(pre + 18 * k, ai);
   }
-  if (lane < 18) pre[lane] = lane < 9 ? inv.a.v[lane] : inv.b.v[lane - 9];
-#pragma unroll 1
-  for (int base = 0; base < 2 * BN_ATE_LINES; base += 64) {
-    const int i = base + lane;
-    if (i < 2 * BN_ATE_LINES) {
-      const int k = i >> 1, mu = i & 1;
-      fp2 x, ai, r;
-      fp2_fetch(x, abc + k * BN_ABC_WORDS + (mu ? 36 : 18));
-      fp2_fetch(ai, pre + 18 * k);
-      fp2_mul(r, x, ai);
-      if (!mu) fp2_neg(r, r);
-      fp2_store(out + (size_t)k * BN_LINE_WORDS + 18 * mu, r);
-    }
+  f2r_st_row0(pre, inv);
+  const int row = (threadIdx.x & 63) >> 4;
+#pragma nounroll
+  for (int base = 0; base < 2 * BN_ATE_LINES; base += 4) {  // 140 = 35 x 4
+    const int i = base + row, k = i >> 1, mu = i & 1;
+    const R2 x = f2r_ld(abc + k * BN_ABC_WORDS + (mu ? 36 : 18)), y = f2r_ld(pre + 18 * k);
+    const uint32_t p0 = c.mul(x.a, y.a), p1 = c.mul(x.b, y.b), p2 = c.mul(rf_add(x.a, x.b), rf_add(y.a, y.b));
+    R2 r{c.red(c.sub(p0, p1)), c.red(c.sub(c.sub(p2, p0), p1))};
+    const R2 nr = f2r_red(f2r_sub(R2{c.zero, c.zero}, r, c), c);
+    r.a = mu ? r.a : nr.a;  // lambda = -B / A
+    r.b = mu ? r.b : nr.b;
+    f2r_st(out + (size_t)k * BN_LINE_WORDS + 18 * mu, r);
   }
 }
 
-// keys65 = nullptr: the generator g2's lines only (gen_lines).  Else key k = blockIdx.x: ok[k] =
-// decodes && not infinity && r Q == O (g2_decompress's verdict), aff[k], lines[k] (written for
-// every decodable key; only ok keys are ever read).
-#define KEYS_WAVE_BLOCK 128
-__global__ void __launch_bounds__(KEYS_WAVE_BLOCK) bls_keys_wave_kernel(const uint8_t* keys65, uint32_t nkeys,
-                                                                        uint32_t* lines, uint8_t* ok, uint32_t* aff) {
+// keys65 = nullptr: the generator g2's lines only (gen_lines).  Else key k = blockIdx.x, one block
+// of two waves: both decode it (one lane's work), then wave 0 checks r Q == O on rows
+// (g2r_in_subgroup) and writes ok[k] (decodes && not infinity && in G2, g2_decompress's verdict)
+// and aff[k], while wave 1 builds the 70 lines (g2r_lines_abc into LDS) and normalises them into
+// lines[k] (written for every decodable key; only ok keys are ever read).
+#define KEYS_ROW_BLOCK 128
+__global__ void __launch_bounds__(KEYS_ROW_BLOCK) bls_keys_row_kernel(const uint8_t* keys65, uint32_t nkeys,
+                                                                      uint32_t* lines, uint8_t* ok, uint32_t* aff) {
   __shared__ uint32_t abc[BN_ATE_LINES * BN_ABC_WORDS];
   __shared__ uint32_t pre[BN_ATE_LINES * 18];
   const uint32_t k = blockIdx.x;
@@ -104,7 +106,8 @@ __global__ void __launch_bounds__(KEYS_WAVE_BLOCK) bls_keys_wave_kernel(const ui
   }
   if (wave == 0) {
     if (!keys65) return;
-    const bool good = dec && g2w_in_subgroup(q);
+    const G2RowCtx<uint32_t, uint64_t> c(0u);
+    const bool good = dec && g2r_in_subgroup(f2r_from(q.x), f2r_from(q.y), c);
     if (lane == 0) {
       ok[k] = good ? 1 : 0;
       if (!good) q.inf = true;
@@ -113,8 +116,8 @@ __global__ void __launch_bounds__(KEYS_WAVE_BLOCK) bls_keys_wave_kernel(const ui
     return;
   }
   if (!dec) return;
-  g2w_lines_abc(abc, q);
-  g2w_normalise_lines(lines + (size_t)k * LINES_PER_KEY, abc, pre);
+  g2r_lines_abc(abc, q);
+  g2r_normalise_lines(lines + (size_t)k * LINES_PER_KEY, abc, pre);
 }
 
 __global__ void bls_gen_lines_kernel(uint32_t* lines) {
@@ -197,45 +200,50 @@ __global__ void __launch_bounds__(SUM_THREADS, 1) bls_g2_sum_kernel(const uint32
   g2_sum_tail(acc, bad != 0, ok, out65);
 }
 
-// The multisig key sum on waves, every addition's Fp products on separate lanes
-// (bn254_g2wave.h): a block of G2S_WAVES waves.  Level 0 (parts == nullptr): wave w of block b
-// adds the selected keys among ids [lo + G2S_IDS (b G2S_WAVES + w), +G2S_IDS) within [lo, hi) by
-// mixed additions (a selected key that did not decode marks the sum bad); level > 0: partials
-// [G2S_PARTS (b G2S_WAVES + w), +G2S_PARTS) of count.  The block's waves then meet in an LDS
-// tree and wave 0 writes the block's partial (54 words + bad flag) to out_parts[b], or, with
-// out65 (a one-block launch), the compressed sum and ok (g2_sum_tail).  Group law exact in every
-// case (g2w_accum), so the sum is the bls_g2_sum_kernel's point.
-#define G2S_WAVES 4
-#define G2S_IDS 16
-#define G2S_PARTS 4
+// The multisig key sum on row-parallel Fp (bn254_g2row.h): a block of G2S_WAVES waves.  Level 0
+// (parts == nullptr): wave w of block b adds the selected keys among ids
+// [lo + G2S_IDS (b G2S_WAVES + w), +G2S_IDS) within [lo, hi) by mixed additions (a selected key
+// that did not decode marks the sum bad); level > 0: partials [G2S_PARTS (b G2S_WAVES + w),
+// +G2S_PARTS) of count.  The block's waves then meet in an LDS tree and wave 0 writes the block's
+// partial (54 words < 2q + bad flag: g2j_load form) to out_parts[b], or, with out65 (a one-block
+// launch), the compressed sum and ok (g2_sum_tail).  The group law is exact in every case
+// (g2r_accum), so the sum is bls_g2_sum_kernel's point.
+#ifndef G2S_WAVES
+#define G2S_WAVES 8
+#endif
+#ifndef G2S_IDS
+#define G2S_IDS 8
+#endif
+#ifndef G2S_PARTS
+#define G2S_PARTS 2
+#endif
 #define G2S_MAX_PARTS 64  // level-0 blocks for ids up to 4,096
-__device__ __forceinline__ void g2w_part_store(uint32_t* o, const g2j& acc, bool inf, bool bad, int lane) {
-  g2j a = acc;
-  if (inf) {
-    fp2_one(a.X);
-    fp2_one(a.Y);
-    fp2_zero(a.Z);
-  }
-  uint32_t wv[BLS_G2_PART_WORDS];
-  g2j_store(wv, a);
-  wv[54] = bad ? 1u : 0u;
-  uint32_t w = wv[0];
-#pragma unroll
-  for (int i = 1; i < BLS_G2_PART_WORDS; i++) w = lane == i ? wv[i] : w;
-  if (lane < BLS_G2_PART_WORDS) o[lane] = w;
+using G2RCtx = G2RowCtx<uint32_t, uint64_t>;
+// rows -> 54 one-lane words (< 2q: each coordinate through one Montgomery product with 1) + bad
+__device__ __forceinline__ void g2r_part_store(uint32_t* o, const G2R<uint32_t>& p, bool inf, bool bad,
+                                               const G2RCtx& c) {
+  uint32_t A[6] = {p.X.a, p.X.b, p.Y.a, p.Y.b, p.Z.a, p.Z.b}, B[6], P[6];
+  for (int i = 0; i < 6; i++) B[i] = c.one;
+  r_prods<6>(P, A, B, c);
+  for (int i = 0; i < 6; i++) rf_st9_row0(o + 9 * i, inf ? (i < 4 ? c.one : c.zero) : P[i]);
+  if (__lane_id() == 0) o[54] = bad ? 1u : 0u;
 }
-__global__ void __launch_bounds__(64 * G2S_WAVES) bls_g2_sum_wave_kernel(const uint32_t* aff, const uint8_t* key_ok,
-                                                                       const uint8_t* bitmap, uint32_t lo, uint32_t hi,
-                                                                       const uint32_t* parts, uint32_t count,
-                                                                       uint32_t* out_parts, uint8_t* ok,
-                                                                       uint8_t* out65) {
+__device__ __forceinline__ bool g2r_part_load(G2R<uint32_t>& p, const uint32_t* o, const G2RCtx& c) {
+  p.X = f2r_ld(o);
+  p.Y = f2r_ld(o + 18);
+  p.Z = f2r_ld(o + 36);
+  return c.zero4(p.Z);  // infinity
+}
+__global__ void __launch_bounds__(64 * G2S_WAVES) bls_g2_sum_row_kernel(const uint32_t* aff, const uint8_t* key_ok,
+                                                                      const uint8_t* bitmap, uint32_t lo, uint32_t hi,
+                                                                      const uint32_t* parts, uint32_t count,
+                                                                      uint32_t* out_parts, uint8_t* ok,
+                                                                      uint8_t* out65) {
   __shared__ uint32_t xp[G2S_WAVES][BLS_G2_PART_WORDS + 1];
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
   const uint32_t wid = blockIdx.x * G2S_WAVES + wave;
-  g2j acc;
-  fp2_one(acc.X);
-  fp2_one(acc.Y);
-  fp2_zero(acc.Z);
+  const G2RCtx c(0u);
+  G2R<uint32_t> acc{{c.one, c.zero}, {c.one, c.zero}, {c.zero, c.zero}};
   bool inf = true, bad = false;
   if (!parts) {
     const uint32_t s0 = lo + wid * G2S_IDS;
@@ -246,44 +254,49 @@ __global__ void __launch_bounds__(64 * G2S_WAVES) bls_g2_sum_wave_kernel(const u
         bad = true;
         continue;
       }
-      g2a q;
-      g2a_load(q, aff + (size_t)(id - 1) * BLS_G2A_WORDS);
-      g2w_accum_aff(acc, inf, q.x, q.y, lane);
+      const uint32_t* a = aff + (size_t)(id - 1) * BLS_G2A_WORDS;  // x.a x.b y.a y.b (g2a_store)
+      g2r_accum_aff(acc, inf, f2r_ld(a), f2r_ld(a + 18), c);
     }
   } else {
 #pragma nounroll
     for (uint32_t i = wid * G2S_PARTS; i < (wid + 1) * G2S_PARTS && i < count; i++) {
-      g2j o;
-      g2j_load(o, parts + (size_t)BLS_G2_PART_WORDS * i);
-      bad |= parts[(size_t)BLS_G2_PART_WORDS * i + 54] != 0;
-      g2w_accum(acc, inf, o, fp2_is_zero(o.Z), lane);
+      const uint32_t* o = parts + (size_t)BLS_G2_PART_WORDS * i;
+      G2R<uint32_t> q;
+      const bool qinf = g2r_part_load(q, o, c);
+      bad |= o[54] != 0;
+      g2r_accum(acc, inf, q, qinf, c);
     }
   }
 #pragma unroll 1
   for (int stride = G2S_WAVES / 2; stride >= 1; stride >>= 1) {
-    if (wave >= stride && wave < 2 * stride) g2w_part_store(xp[wave - stride], acc, inf, bad, lane);
+    if (wave >= stride && wave < 2 * stride) {
+      uint32_t* o = xp[wave - stride];
+      f2r_st_row0(o, acc.X);
+      f2r_st_row0(o + 18, acc.Y);
+      f2r_st_row0(o + 36, inf ? F2R<uint32_t>{c.zero, c.zero} : acc.Z);
+      if (__lane_id() == 0) o[54] = bad ? 1u : 0u;
+    }
     __syncthreads();
     if (wave < stride) {
-      g2j o;
-      g2j_load(o, xp[wave]);
+      G2R<uint32_t> q;
+      const bool qinf = g2r_part_load(q, xp[wave], c);
       bad |= xp[wave][54] != 0;
-      g2w_accum(acc, inf, o, fp2_is_zero(o.Z), lane);
+      g2r_accum(acc, inf, q, qinf, c);
     }
     __syncthreads();
   }
   if (wave != 0) return;
   if (out65) {
-    if (lane == 0) {
-      if (inf) {
-        fp2_one(acc.X);
-        fp2_one(acc.Y);
-        fp2_zero(acc.Z);
-      }
-      g2_sum_tail(acc, bad, ok, out65);
+    __shared__ uint32_t fin[BLS_G2_PART_WORDS];
+    g2r_part_store(fin, acc, inf, bad, c);
+    if (__lane_id() == 0) {
+      g2j s;
+      g2j_load(s, fin);
+      g2_sum_tail(s, bad, ok, out65);
     }
     return;
   }
-  g2w_part_store(out_parts + (size_t)BLS_G2_PART_WORDS * blockIdx.x, acc, inf, bad, lane);
+  g2r_part_store(out_parts + (size_t)BLS_G2_PART_WORDS * blockIdx.x, acc, inf, bad, c);
 }
 
 // vk = sk * g2 as 65 compressed bytes: the signer's public key (BlsThresholdSigner's
@@ -322,7 +335,7 @@ hipError_t cbft_bls_launch_keys(const uint8_t* d_keys65, uint32_t nkeys, uint32_
     hipLaunchKernelGGL(bls_keys_kernel, dim3((nkeys + 63) / 64), dim3(64), 0, s, d_keys65, nkeys, d_lines, d_ok,
                        d_aff, d_scratch);
   else
-    hipLaunchKernelGGL(bls_keys_wave_kernel, dim3(nkeys), dim3(KEYS_WAVE_BLOCK), 0, s, d_keys65, nkeys, d_lines,
+    hipLaunchKernelGGL(bls_keys_row_kernel, dim3(nkeys), dim3(KEYS_ROW_BLOCK), 0, s, d_keys65, nkeys, d_lines,
                        d_ok, d_aff);
   return hipGetLastError();
 }
@@ -330,7 +343,7 @@ hipError_t cbft_bls_launch_gen_lines(uint32_t* d_lines, hipStream_t s) {
   if (keys_lane_form())
     hipLaunchKernelGGL(bls_gen_lines_kernel, dim3(1), dim3(64), 0, s, d_lines);
   else
-    hipLaunchKernelGGL(bls_keys_wave_kernel, dim3(1), dim3(KEYS_WAVE_BLOCK), 0, s, nullptr, 1u, d_lines, nullptr,
+    hipLaunchKernelGGL(bls_keys_row_kernel, dim3(1), dim3(KEYS_ROW_BLOCK), 0, s, nullptr, 1u, d_lines, nullptr,
                        nullptr);
   return hipGetLastError();
 }
@@ -350,13 +363,13 @@ hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok
   uint32_t* cur = d_tmp;
   uint32_t* nxt = d_tmp + (size_t)BLS_G2_PART_WORDS * G2S_MAX_PARTS;
   const bool one = nb == 1;
-  hipLaunchKernelGGL(bls_g2_sum_wave_kernel, dim3(nb), dim3(64 * G2S_WAVES), 0, s, d_aff, d_key_ok, d_bitmap, lo, hi,
+  hipLaunchKernelGGL(bls_g2_sum_row_kernel, dim3(nb), dim3(64 * G2S_WAVES), 0, s, d_aff, d_key_ok, d_bitmap, lo, hi,
                      (const uint32_t*)nullptr, 0u, one && d_out_part ? d_out_part : cur, d_ok,
                      one ? d_out65 : (uint8_t*)nullptr);
   while (nb > 1) {
     const uint32_t nb2 = (nb + G2S_WAVES * G2S_PARTS - 1) / (G2S_WAVES * G2S_PARTS);
     const bool last = nb2 == 1;
-    hipLaunchKernelGGL(bls_g2_sum_wave_kernel, dim3(nb2), dim3(64 * G2S_WAVES), 0, s, d_aff, d_key_ok, d_bitmap, lo,
+    hipLaunchKernelGGL(bls_g2_sum_row_kernel, dim3(nb2), dim3(64 * G2S_WAVES), 0, s, d_aff, d_key_ok, d_bitmap, lo,
                        hi, (const uint32_t*)cur, nb, last && d_out_part ? d_out_part : nxt, d_ok,
                        last ? d_out65 : (uint8_t*)nullptr);
     uint32_t* t = cur;

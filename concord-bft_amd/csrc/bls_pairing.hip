@@ -264,7 +264,7 @@ __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uin
       pk_ok[0] = ok ? 1 : 0;
       usable = ok ? 1 : 0;
     }
-    if (ok) g2w_lines_abc(lines, s, &progress);
+    if (ok) g2r_lines_abc(lines, s, &progress);
     BLS_PHASE(3);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (g.lane == 0) progress = BN_ATE_LINES + 1;  // release the consumer whatever happened

@@ -18,6 +18,7 @@
 // product is (8q)(24q) = 192 q^2 (E (D - X3), r (V - X3)); every bound is noted where it is used.
 #pragma once
 #include "bn254_g1row.h"
+#include "bn254_tower.h"
 
 template <class U>
 struct F2R {

@@ -15,6 +15,7 @@
 // needed.  bn254_pair36.h evaluates them at the same cost as normalised lines.
 #pragma once
 #include "bn254_cycsq.h"
+#include "bn254_g2row.h"
 #include "bn254_pairing.h"
 
 #define BN_ABC_WORDS 54  // A | B | C (fp2 each)
@@ -201,261 +202,6 @@ __device__ __forceinline__ void g2w_add(uint32_t* ln, g2j& T, const fp2& qx, con
   T.X = X3;
 }
 
-// T <- 2T (dbl-2009-l, the products of g2w_dbl without the tangent's A, B, C): 7, 6 and 3
-// products in three rounds.  The subgroup check's chain (bls_keys.hip).
-__device__ __forceinline__ void g2w_dbl_only(g2j& T, int lane) {
-  fp U[7], V[7], p[7];
-  g2w_sqr_ops(U, V, 0, T.X);
-  g2w_sqr_ops(U, V, 2, T.Y);
-  g2w_mul_ops(U, V, 4, T.Y, T.Z);
-  g2w_round<7>(p, U, V, lane);
-  fp2 XX, YY, t, E, D0;
-  g2w_sqr_res(XX, p, 0);
-  g2w_sqr_res(YY, p, 2);
-  g2w_mul_res(t, p, 4);
-  fp2_dbl(t, t);  // 2YZ = Z3
-  fp_lin3<3, 0, 0, 0>(E.a, XX.a, XX.a, XX.a);
-  fp_lin3<3, 0, 0, 0>(E.b, XX.b, XX.b, XX.b);
-  fp2_add(D0, T.X, YY);
-  g2w_sqr_ops(U, V, 0, YY);  // YYYY
-  g2w_sqr_ops(U, V, 2, D0);  // (X + YY)^2
-  g2w_sqr_ops(U, V, 4, E);   // F = E^2
-  g2w_round<6>(p, U, V, lane);
-  fp2 YYYY, D, F, X3, w;
-  g2w_sqr_res(YYYY, p, 0);
-  g2w_sqr_res(D, p, 2);
-  g2w_sqr_res(F, p, 4);
-  fp_lin3<2, -2, -2, 8>(D.a, D.a, XX.a, YYYY.a);
-  fp_lin3<2, -2, -2, 8>(D.b, D.b, XX.b, YYYY.b);
-  fp_lin3<1, -2, 0, 4>(X3.a, F.a, D.a, D.a);
-  fp_lin3<1, -2, 0, 4>(X3.b, F.b, D.b, D.b);
-  fp2_sub(w, D, X3);
-  g2w_mul_ops(U, V, 0, E, w);
-  g2w_round<3>(p, U, V, lane);
-  fp2 Y3;
-  g2w_mul_res(Y3, p, 0);
-  fp u;
-  fp_lin3<1, -4, 0, 8>(u, Y3.a, YYYY.a, YYYY.a);
-  fp_lin3<1, -4, 0, 8>(T.Y.a, u, YYYY.a, YYYY.a);
-  fp_lin3<1, -4, 0, 8>(u, Y3.b, YYYY.b, YYYY.b);
-  fp_lin3<1, -4, 0, 8>(T.Y.b, u, YYYY.b, YYYY.b);
-  T.X = X3;
-  T.Z = t;
-}
-
-// T <- T + (qx, qy) (madd-2007-bl, the products of g2w_add without the line), T finite.  When
-// x(T) = qx (H = 0: T = Q or T = -Q) nothing is computed and the function returns false with
-// same_y = (T == Q); the caller doubles or takes infinity, as g2_add_j does.  Wave-uniform.
-__device__ __forceinline__ bool g2w_madd_only(g2j& T, const fp2& qx, const fp2& qy, int lane, bool& same_y) {
-  fp U[6], V[6], p[6];
-  g2w_sqr_ops(U, V, 0, T.Z);
-  g2w_mul_ops(U, V, 2, qy, T.Z);
-  g2w_round<5>(p, U, V, lane);
-  fp2 ZZ, QZ;
-  g2w_sqr_res(ZZ, p, 0);
-  g2w_mul_res(QZ, p, 2);
-  g2w_mul_ops(U, V, 0, qx, ZZ);  // U2
-  g2w_mul_ops(U, V, 3, QZ, ZZ);  // S2
-  g2w_round<6>(p, U, V, lane);
-  fp2 U2, S2, H, R, r, ZH;
-  g2w_mul_res(U2, p, 0);
-  g2w_mul_res(S2, p, 3);
-  fp2_sub(H, U2, T.X);
-  fp2_sub(R, S2, T.Y);
-  if (fp2_is_zero(H)) {
-    same_y = fp2_is_zero(R);
-    return false;
-  }
-  fp2_dbl(r, R);
-  fp2_add(ZH, T.Z, H);
-  g2w_sqr_ops(U, V, 0, H);   // HH
-  g2w_sqr_ops(U, V, 2, r);   // r^2
-  g2w_sqr_ops(U, V, 4, ZH);  // (Z + H)^2
-  g2w_round<6>(p, U, V, lane);
-  fp2 HH, rr, I;
-  g2w_sqr_res(HH, p, 0);
-  g2w_sqr_res(rr, p, 2);
-  g2w_sqr_res(ZH, p, 4);
-  fp2_dbl(I, HH);
-  fp2_dbl(I, I);
-  g2w_mul_ops(U, V, 0, H, I);    // J
-  g2w_mul_ops(U, V, 3, T.X, I);  // V
-  g2w_round<6>(p, U, V, lane);
-  fp2 J, Vv, X3, w;
-  g2w_mul_res(J, p, 0);
-  g2w_mul_res(Vv, p, 3);
-  fp2_sub(X3, rr, J);
-  fp2_sub(X3, X3, Vv);
-  fp2_sub(X3, X3, Vv);
-  fp2_sub(w, Vv, X3);
-  g2w_mul_ops(U, V, 0, r, w);
-  g2w_mul_ops(U, V, 3, T.Y, J);
-  g2w_round<6>(p, U, V, lane);
-  fp2 Y3, YJ;
-  g2w_mul_res(Y3, p, 0);
-  g2w_mul_res(YJ, p, 3);
-  fp2_dbl(YJ, YJ);
-  fp2_sub(T.Y, Y3, YJ);
-  fp2_sub(ZH, ZH, ZZ);
-  fp2_sub(T.Z, ZH, HH);
-  T.X = X3;
-  return true;
-}
-
-// T <- T + Q for Jacobian T, Q, both finite (add-2007-bl, g2_add_j_body's formulas): 4, 10, 11
-// and 6 products in four rounds (the H-dependent squares ride in the third).  When U1 = U2
-// (T = +-Q) nothing is written and the function returns false with same_y = (T == Q).
-__device__ __forceinline__ bool g2w_add_full(g2j& T, const g2j& Q, int lane, bool& same_y) {
-  fp U[12], V[12], p[12];
-  g2w_sqr_ops(U, V, 0, T.Z);
-  g2w_sqr_ops(U, V, 2, Q.Z);
-  g2w_round<4>(p, U, V, lane);
-  fp2 Z1Z1, Z2Z2;
-  g2w_sqr_res(Z1Z1, p, 0);
-  g2w_sqr_res(Z2Z2, p, 2);
-  g2w_mul_ops(U, V, 0, T.X, Z2Z2);  // U1
-  g2w_mul_ops(U, V, 3, Q.X, Z1Z1);  // U2
-  g2w_mul_ops(U, V, 6, T.Y, Q.Z);
-  g2w_mul_ops(U, V, 9, Q.Y, T.Z);
-  g2w_round<12>(p, U, V, lane);
-  fp2 U1, U2, Y1Z2, Y2Z1, H, H2, ZS;
-  g2w_mul_res(U1, p, 0);
-  g2w_mul_res(U2, p, 3);
-  g2w_mul_res(Y1Z2, p, 6);
-  g2w_mul_res(Y2Z1, p, 9);
-  fp2_sub(H, U2, U1);
-  fp2_dbl(H2, H);
-  fp2_add(ZS, T.Z, Q.Z);
-  g2w_mul_ops(U, V, 0, Y1Z2, Z2Z2);  // S1
-  g2w_mul_ops(U, V, 3, Y2Z1, Z1Z1);  // S2
-  g2w_sqr_ops(U, V, 6, H2);          // I = (2H)^2
-  g2w_sqr_ops(U, V, 8, ZS);          // (Z1 + Z2)^2
-  g2w_round<10>(p, U, V, lane);
-  fp2 S1, S2, R, I, ZZ;
-  g2w_mul_res(S1, p, 0);
-  g2w_mul_res(S2, p, 3);
-  fp2_sub(R, S2, S1);
-  if (fp2_is_zero(H)) {
-    same_y = fp2_is_zero(R);
-    return false;
-  }
-  g2w_sqr_res(I, p, 6);
-  g2w_sqr_res(ZZ, p, 8);
-  fp2_sub(ZZ, ZZ, Z1Z1);
-  fp2_sub(ZZ, ZZ, Z2Z2);
-  fp2 r;
-  fp2_dbl(r, R);
-  g2w_mul_ops(U, V, 0, H, I);    // J
-  g2w_mul_ops(U, V, 3, U1, I);   // V
-  g2w_mul_ops(U, V, 6, ZZ, H);   // Z3
-  g2w_sqr_ops(U, V, 9, r);       // r^2
-  g2w_round<11>(p, U, V, lane);
-  fp2 J, Vv, rr, X3, w;
-  g2w_mul_res(J, p, 0);
-  g2w_mul_res(Vv, p, 3);
-  g2w_mul_res(T.Z, p, 6);
-  g2w_sqr_res(rr, p, 9);
-  fp2_sub(X3, rr, J);
-  fp2_sub(X3, X3, Vv);
-  fp2_sub(X3, X3, Vv);
-  fp2_sub(w, Vv, X3);
-  g2w_mul_ops(U, V, 0, r, w);
-  g2w_mul_ops(U, V, 3, S1, J);
-  g2w_round<6>(p, U, V, lane);
-  fp2 Y3, SJ;
-  g2w_mul_res(Y3, p, 0);
-  g2w_mul_res(SJ, p, 3);
-  fp2_dbl(SJ, SJ);
-  fp2_sub(T.Y, Y3, SJ);
-  T.X = X3;
-  return true;
-}
-
-// acc += o with wave-uniform infinity flags, every case of g2_add_j_body (O + o, acc + O,
-// acc = o -> doubling, acc = -o -> O); a doubling that lands on O (2-torsion) sets the flag
-__device__ __forceinline__ void g2w_accum(g2j& acc, bool& inf, const g2j& o, bool oinf, int lane) {
-  if (oinf) return;
-  if (inf) {
-    acc = o;
-    inf = false;
-    return;
-  }
-  bool same_y = false;
-  if (!g2w_add_full(acc, o, lane, same_y)) {
-    if (same_y) {
-      g2w_dbl_only(acc, lane);
-      inf = fp2_is_zero(acc.Z);
-    } else {
-      inf = true;
-    }
-  }
-}
-// acc += (qx, qy), an affine point (not infinity)
-__device__ __forceinline__ void g2w_accum_aff(g2j& acc, bool& inf, const fp2& qx, const fp2& qy, int lane) {
-  if (inf) {
-    acc.X = qx;
-    acc.Y = qy;
-    fp2_one(acc.Z);
-    inf = false;
-    return;
-  }
-  bool same_y = false;
-  if (!g2w_madd_only(acc, qx, qy, lane, same_y)) {
-    if (same_y) {
-      g2w_dbl_only(acc, lane);
-      inf = fp2_is_zero(acc.Z);
-    } else {
-      inf = true;
-    }
-  }
-}
-
-// r Q == O for affine Q (not infinity), by the NAF of r (254 digits, 33 non-zero: 253 doublings
-// and 32 mixed additions of +-Q) with every step's products on separate lanes; exceptional
-// sums (T = +-Q, a doubling to infinity) are resolved exactly as g2_in_subgroup's g2_add_j /
-// g2_dbl_j chain would, so the verdict equals g2_in_subgroup's.  Every lane returns it.
-__device__ __noinline__ bool g2w_in_subgroup(const g2a& q) {
-  const uint32_t pos[8] = {0x00000011u, 0xa1000000u, 0x00000010u, 0x00200000u,
-                           0x00000008u, 0x02445000u, 0x40000002u, 0x25240482u};
-  const uint32_t neg[8] = {0x00000004u, 0x00000000u, 0x00000000u, 0x00808000u,
-                           0x00000000u, 0x48100280u, 0x00000000u, 0x0000a000u};
-  const int lane = threadIdx.x & 63;
-  fp2 nqy;
-  fp2_neg(nqy, q.y);
-  g2j T;
-  T.X = q.x;
-  T.Y = q.y;
-  fp2_one(T.Z);
-  bool inf = false;
-#pragma nounroll
-  for (int i = 252; i >= 0; i--) {
-    if (!inf) {
-      g2w_dbl_only(T, lane);
-      inf = fp2_is_zero(T.Z);  // 2T = O (a point of order 2)
-    }
-    const bool dp = (pos[i >> 5] >> (i & 31)) & 1, dn = (neg[i >> 5] >> (i & 31)) & 1;
-    if (!dp && !dn) continue;
-    const fp2& qy = dp ? q.y : nqy;
-    if (inf) {
-      T.X = q.x;
-      T.Y = qy;
-      fp2_one(T.Z);
-      inf = false;
-      continue;
-    }
-    bool same_y = false;
-    if (!g2w_madd_only(T, q.x, qy, lane, same_y)) {
-      if (same_y) {
-        g2w_dbl_only(T, lane);
-        inf = fp2_is_zero(T.Z);
-      } else {
-        inf = true;
-      }
-    }
-  }
-  return inf || fp2_is_zero(T.Z);
-}
-
 // Streaming hand-over of lines to a consumer wave of the same block (progress in LDS): after
 // line k is stored, progress = k + 1 (release at workgroup scope).
 __device__ __forceinline__ void g2w_publish(volatile int* progress, int k, int lane) {
@@ -499,5 +245,54 @@ __device__ __noinline__ void g2w_lines_abc(uint32_t* out, const g2a& q, volatile
   fp2_mul(q2y, q.y, c);
   fp2_neg(q2y, q2y);
   g2w_add(out + (k++) * BN_ABC_WORDS, T, q2x, q2y, lane);
+  g2w_publish(progress, k, lane);
+}
+
+// ---- the same lines on row-parallel Fp (bn254_g2row.h): T in rows, each step's Fp products four
+// per pass; each (A, B, C) record is written from row 0 as normalised limbs (values < 4q, which
+// p36_line_abc's products take).  Same records as g2w_lines_abc (field values; host emulation:
+// tests/cpp/bn254_shim.cpp against line_dbl_j / line_add_j).
+__device__ __forceinline__ void g2r_store_abc(uint32_t* ln, const F2R<uint32_t>* l) {
+  f2r_st_row0(ln, l[0]);
+  f2r_st_row0(ln + 18, l[1]);
+  f2r_st_row0(ln + 36, l[2]);
+}
+__device__ __noinline__ void g2r_lines_abc(uint32_t* out, const g2a& q, volatile int* progress = nullptr) {
+  const int lane = threadIdx.x & 63;
+  const G2RowCtx<uint32_t, uint64_t> c(0u);
+  const F2R<uint32_t> qx = f2r_from(q.x), qy = f2r_from(q.y);
+  G2R<uint32_t> T{qx, qy, F2R<uint32_t>{c.one, c.zero}};
+  F2R<uint32_t> l[3];
+  bool same_y;
+  int k = 0;
+#pragma nounroll
+  for (int i = BN_ATE_DBL - 1; i >= 0; i--) {
+    g2r_dbl<true>(l, T, c);
+    g2r_store_abc(out + (k++) * BN_ABC_WORDS, l);
+    g2w_publish(progress, k, lane);
+    if (bn_ate_bit(i)) {
+      g2r_madd<true>(l, T, qx, qy, c, same_y);
+      g2r_store_abc(out + (k++) * BN_ABC_WORDS, l);
+      g2w_publish(progress, k, lane);
+    }
+  }
+  T.Y = f2r_red(f2r_sub(F2R<uint32_t>{c.zero, c.zero}, T.Y, c), c);  // 6u + 2 < 0
+  fp2 q1x, q1y, q2x, q2y, cc;
+  fp2_conj(q1x, q.x);
+  fp2_load(cc, Bn254Consts::TWX1);
+  fp2_mul(q1x, q1x, cc);
+  fp2_conj(q1y, q.y);
+  fp2_load(cc, Bn254Consts::TWY1);
+  fp2_mul(q1y, q1y, cc);
+  fp2_load(cc, Bn254Consts::TWX2);
+  fp2_mul(q2x, q.x, cc);
+  fp2_load(cc, Bn254Consts::TWY2);
+  fp2_mul(q2y, q.y, cc);
+  fp2_neg(q2y, q2y);
+  g2r_madd<true>(l, T, f2r_from(q1x), f2r_from(q1y), c, same_y);
+  g2r_store_abc(out + (k++) * BN_ABC_WORDS, l);
+  g2w_publish(progress, k, lane);
+  g2r_madd<true>(l, T, f2r_from(q2x), f2r_from(q2y), c, same_y);
+  g2r_store_abc(out + (k++) * BN_ABC_WORDS, l);
   g2w_publish(progress, k, lane);
 }

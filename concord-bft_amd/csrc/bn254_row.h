@@ -83,7 +83,15 @@ RF_HD uint32_t rf_sel(bool c, uint32_t a, uint32_t b) { return c ? a : b; }
 RF_HD uint64_t rf_sel(bool c, uint64_t a, uint64_t b) { return c ? a : b; }
 RF_HD uint32_t rf_const(uint32_t, uint32_t v) { return v; }
 RF_HD uint64_t rf_const64(uint32_t, uint64_t v) { return v; }
-RF_HD uint64_t rf_sra29(uint64_t w) { return (uint64_t)((int64_t)w >> 29); }
+// 64-bit lane shifts by 29 as 32-bit funnel shifts (v_alignbit_b32) of the register halves
+RF_HD uint64_t rf_shr29(uint64_t w) {
+  const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+  return (uint64_t)__builtin_amdgcn_alignbit(hi, lo, 29) | ((uint64_t)(hi >> 29) << 32);
+}
+RF_HD uint64_t rf_sra29(uint64_t w) {
+  const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
+  return (uint64_t)__builtin_amdgcn_alignbit(hi, lo, 29) | ((uint64_t)(uint32_t)((int32_t)hi >> 29) << 32);
+}
 RF_HD uint64_t rf_ballot(bool c) { return __ballot(c); }
 RF_HD uint32_t rl_lane(uint32_t) { return __lane_id(); }
 RF_HD uint64_t rf_widen(uint32_t x) { return x; }
@@ -105,7 +113,8 @@ RF_HD U rf_row_const(const uint32_t* c, U tag) {
 // carry pass on 64-bit lanes: x = (x & mask) + carry of the lane below
 template <class U, class W>
 RF_HD W rf_carry64(W x) {
-  const U c_lo = rl_shr<1>(rf_lo(x >> 29)), c_hi = rl_shr<1>(rf_hi(x >> 29));
+  const W x29 = rf_shr29(x);
+  const U c_lo = rl_shr<1>(rf_lo(x29)), c_hi = rl_shr<1>(rf_hi(x29));
   return (x & rf_const64(c_lo, (uint64_t)BN_MASK)) + rf_w(c_lo, c_hi);
 }
 template <class U>
@@ -135,7 +144,7 @@ RF_HD U rf_mul(U a, U b, U qrow) {
     const U m = rl_bcast<I>((rf_lo(col) * rf_const(a, FpParams::NPRIME)) & rf_const(a, BN_MASK)); \
     col = rf_mad(m, rl_shr<I>(qrow), col);                                                 \
     if (I == 8) c16 = rf_mad(m, rl_bcast<8>(qrow), c16);                                   \
-    const W c = col >> 29;                                                                 \
+    const W c = rf_shr29(col);                                                             \
     const U c_lo = rl_shr<1>(rf_lo(c)), c_hi = rl_shr<1>(rf_hi(c));                        \
     col = col + rf_sel(rl == rf_const(a, (uint32_t)(I + 1)), rf_w(c_lo, c_hi), rf_const64(a, 0ull)); \
   }

@@ -2,6 +2,7 @@
 // Python tests through ctypes: the SAME source that runs on gfx950, checked on the CPU against
 // oracle/bn254_ref.py.  Test infrastructure; also the labelled "not RELIC" CPU baseline.
 #include <cstring>
+#include <memory>
 #include <random>
 #include <thread>
 #include <vector>
@@ -697,6 +698,14 @@ int shim_g2r_check(uint64_t seed, int iters) {
       g2_add_j(e, P, Q);
       g2j_of_row(got, rt);
       if (!g2_same(got, e)) bad++;
+      // both affine (Z = 1): the key sum's first additions
+      g2a pa;
+      g2_to_affine(pa, P);
+      g2j Pa{pa.x, pa.y, G.Z}, Qa{qa.x, qa.y, G.Z};
+      G2R<HU> ra = g2r_of(Pa);
+      if (!g2r_add(ra, g2r_of(Qa), c, same)) bad++;
+      g2j_of_row(got, ra);
+      if (!g2_same(got, e)) bad++;
       g2j P2;  // P in another Jacobian representation
       g2_add_j(P2, P, G);
       g2j nG = G;
@@ -741,6 +750,83 @@ int shim_g2r_check(uint64_t seed, int iters) {
     }
   }
   return bad + (int)g_rf_bound_violations;
+}
+
+// the key-sum kernel's flow (bls_g2_sum_row_kernel) on the host emulation: waves of 8 ids each
+// (mixed additions from affine keys), then a pairwise tree through one-lane words (the LDS
+// exchange) -> compressed; 1 iff equal to the one-lane g2_add_j sum of the same keys
+int shim_g2r_sum_check(uint64_t seed, int nkeys, int stride) {
+  std::mt19937_64 g(seed);
+  HU tag;
+  const G2RowCtx<HU, HW> c(tag);
+  g2j G;
+  fp2_load(G.X, Bn254Consts::G2X);
+  fp2_load(G.Y, Bn254Consts::G2Y);
+  fp2_one(G.Z);
+  std::vector<g2a> keys(nkeys);
+  g2j ref;
+  fp2_one(ref.X);
+  fp2_one(ref.Y);
+  fp2_zero(ref.Z);
+  for (int i = 0; i < nkeys; i++) {
+    uint32_t k[8] = {(uint32_t)g(), (uint32_t)g(), 0, 0, 0, 0, 0, 0};
+    g2j P;
+    g2_mul_ct(P, G, k);
+    g2_to_affine(keys[i], P);
+    if (i % stride == 0) {
+      g2j t;
+      t.X = keys[i].x;
+      t.Y = keys[i].y;
+      fp2_one(t.Z);
+      g2_add_j(ref, ref, t);
+    }
+  }
+  const int W = (nkeys + 7) / 8;
+  std::vector<G2R<HU>> acc(W);
+  std::unique_ptr<bool[]> inf(new bool[W]);
+  for (int w = 0; w < W; w++) inf[w] = true;
+  for (int w = 0; w < W; w++)
+    for (int i = 8 * w; i < 8 * w + 8 && i < nkeys; i++)
+      if (i % stride == 0) g2r_accum_aff(acc[w], inf[w], f2r_of(keys[i].x), f2r_of(keys[i].y), c);
+  for (int st = 1; st < W; st *= 2)
+    for (int w = 0; w + st < W; w += 2 * st) {
+      // the LDS round trip: normalised one-lane words back into rows
+      g2j o;
+      g2j_of_row(o, acc[w + st]);
+      g2r_accum(acc[w], inf[w], g2r_of(o), inf[w + st], c);
+    }
+  g2j got;
+  g2j_of_row(got, acc[0]);
+  if (inf[0]) fp2_zero(got.Z);
+  g2a a, b;
+  g2_to_affine(a, got);
+  g2_to_affine(b, ref);
+  uint8_t ea[65], eb[65];
+  g2_compress(ea, a);
+  g2_compress(eb, b);
+  return std::memcmp(ea, eb, 65) == 0 && g_rf_bound_violations == 0;
+}
+
+// G + 2G through g2r_add on the host emulation, compressed (debug aid)
+void shim_g2r_3g(uint8_t* out65) {
+  HU tag;
+  const G2RowCtx<HU, HW> c(tag);
+  g2j G, Q2;
+  fp2_load(G.X, Bn254Consts::G2X);
+  fp2_load(G.Y, Bn254Consts::G2Y);
+  fp2_one(G.Z);
+  g2_dbl_j(Q2, G);
+  g2a qa;
+  g2_to_affine(qa, Q2);
+  g2j Qa{qa.x, qa.y, G.Z};
+  G2R<HU> t = g2r_of(G);
+  bool sy = false;
+  g2r_add(t, g2r_of(Qa), c, sy);
+  g2j r;
+  g2j_of_row(r, t);
+  g2a a;
+  g2_to_affine(a, r);
+  g2_compress(out65, a);
 }
 
 int shim_g2_decompress(const uint8_t* in65, uint8_t* out65) {

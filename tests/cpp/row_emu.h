@@ -140,6 +140,11 @@ inline HW operator-(const HW& a, const HW& b) {
   for (int l = 0; l < 64; l++) r.x[l] = a.x[l] - b.x[l];
   return r;
 }
+inline HW rf_shr29(const HW& w) {
+  HW r;
+  for (int l = 0; l < 64; l++) r.x[l] = w.x[l] >> 29;
+  return r;
+}
 inline HW rf_sra29(const HW& w) {
   HW r;
   for (int l = 0; l < 64; l++) r.x[l] = (uint64_t)((int64_t)w.x[l] >> 29);

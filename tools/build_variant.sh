@@ -7,7 +7,9 @@ out=$1; shift
 tmp=$(mktemp -d)
 pids=()
 for src in ed25519_verify.hip cbft_hipcrypto.cpp bls_kernels.hip bls_msm_row.hip bls_pairing.hip bls_keys.hip cbft_bls.cpp rsa_verify.hip cbft_rsa.cpp; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Iconcord-bft_amd/csrc -Wno-unused-function "$@" \
+  extra=()
+  case $src in bls_keys.hip|bls_msm_row.hip|bls_pairing.hip) extra=(-mllvm -amdgpu-dpp-combine=false);; esac  # see Makefile ROWFLAGS
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Iconcord-bft_amd/csrc -Wno-unused-function "${extra[@]}" "$@" \
     -c concord-bft_amd/csrc/$src -o "$tmp/${src%.*}.o" &
   pids+=($!)
 done
