@@ -40,11 +40,11 @@ __device__ __noinline__ void g2r_normalise_lines(uint32_t* out, const uint32_t* 
   using R2 = F2R<uint32_t>;
   const G2RowCtx<uint32_t, uint64_t> c(0u);
   uint32_t A[6], B[6], P[6];
-  R2 acc = f2r_ld(abc);
+  R2 acc = f2r_red(f2r_ld(abc), c);  // the records' coefficients are unreduced (< 50q)
   f2r_st_row0(pre, acc);
 #pragma nounroll
   for (int k = 1; k < BN_ATE_LINES; k++) {
-    const R2 a = f2r_ld(abc + k * BN_ABC_WORDS);
+    const R2 a = f2r_red(f2r_ld(abc + k * BN_ABC_WORDS), c);
     f2r_mul_ops(A, B, 0, acc, a);
     r_prods<3>(P, A, B, c);
     f2r_mul_res(acc, P, 0, c);
@@ -57,7 +57,7 @@ __device__ __noinline__ void g2r_normalise_lines(uint32_t* out, const uint32_t* 
   R2 inv = f2r_from(n);
 #pragma nounroll
   for (int k = BN_ATE_LINES - 1; k >= 1; k--) {
-    const R2 pk = f2r_ld(pre + 18 * (k - 1)), a = f2r_ld(abc + k * BN_ABC_WORDS);
+    const R2 pk = f2r_ld(pre + 18 * (k - 1)), a = f2r_red(f2r_ld(abc + k * BN_ABC_WORDS), c);
     f2r_mul_ops(A, B, 0, inv, pk);  // 1 / A_k
     f2r_mul_ops(A, B, 3, inv, a);   // 1 / (A_0 .. A_{k-1})
     r_prods<6>(P, A, B, c);
@@ -71,7 +71,7 @@ __device__ __noinline__ void g2r_normalise_lines(uint32_t* out, const uint32_t* 
 #pragma nounroll
   for (int base = 0; base < 2 * BN_ATE_LINES; base += 4) {  // 140 = 35 x 4
     const int i = base + row, k = i >> 1, mu = i & 1;
-    const R2 x = f2r_ld(abc + k * BN_ABC_WORDS + (mu ? 36 : 18)), y = f2r_ld(pre + 18 * k);
+    const R2 x = f2r_red(f2r_ld(abc + k * BN_ABC_WORDS + (mu ? 36 : 18)), c), y = f2r_ld(pre + 18 * k);
     const uint32_t p0 = c.mul(x.a, y.a), p1 = c.mul(x.b, y.b), p2 = c.mul(rf_add(x.a, x.b), rf_add(y.a, y.b));
     R2 r{c.red(c.sub(p0, p1)), c.red(c.sub(c.sub(p2, p0), p1))};
     const R2 nr = f2r_red(f2r_sub(R2{c.zero, c.zero}, r, c), c);
@@ -81,19 +81,33 @@ __device__ __noinline__ void g2r_normalise_lines(uint32_t* out, const uint32_t* 
   }
 }
 
-// keys65 = nullptr: the generator g2's lines only (gen_lines).  Else key k = blockIdx.x, one block
-// of two waves: both decode it (one lane's work), then wave 0 checks r Q == O on rows
-// (g2r_in_subgroup) and writes ok[k] (decodes && not infinity && in G2, g2_decompress's verdict)
-// and aff[k], while wave 1 builds the 70 lines (g2r_lines_abc into LDS) and normalises them into
-// lines[k] (written for every decodable key; only ok keys are ever read).
-#define KEYS_ROW_BLOCK 128
+// keys65 = nullptr: the generator g2's lines only (gen_lines, one block).  Else two one-wave blocks
+// per key k: block k checks r Q == O on rows (g2r_in_subgroup) and writes ok[k] (decodes && not
+// infinity && in G2, g2_decompress's verdict) and aff[k]; block nkeys + k builds the 70 lines
+// (g2r_lines_abc into LDS) and normalises them into lines[k] (written for every decodable key;
+// only ok keys are ever read); both decode the key (one lane's work).  The chip holds 2 x 1,024
+// of these waves at once (VGPR-bound), so of the n + 1 = 1,025 keys' 2,050 blocks the last two
+// start when the first finish: they are lines blocks (~0.6 ms), not subgroup checks (~1 ms).
+// (Two-wave blocks put the group key's whole block in a second round.)
+#define KEYS_ROW_BLOCK 64
 __global__ void __launch_bounds__(KEYS_ROW_BLOCK) bls_keys_row_kernel(const uint8_t* keys65, uint32_t nkeys,
                                                                       uint32_t* lines, uint8_t* ok, uint32_t* aff) {
   __shared__ uint32_t abc[BN_ATE_LINES * BN_ABC_WORDS];
   __shared__ uint32_t pre[BN_ATE_LINES * 18];
-  const uint32_t k = blockIdx.x;
+#if defined(KEYS_FORCE_TASK)  // A/B probes only: every block runs one task
+  const int task = keys65 ? KEYS_FORCE_TASK : 1;
+#elif defined(KEYS_ONE_WAVE)  // A/B: one wave per key, subgroup check then lines
+  const int task = keys65 ? 2 : 1;
+#else
+  const int task = keys65 ? (blockIdx.x >= nkeys) : 1;
+#endif
+#if defined(KEYS_ONE_WAVE)
+  const uint32_t k = keys65 ? blockIdx.x : 0;
+#else
+  const uint32_t k = keys65 ? blockIdx.x - (task ? nkeys : 0) : 0;
+#endif
   if (k >= nkeys) return;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63;
   g2a q;
   bool dec;
   if (keys65) {
@@ -104,16 +118,16 @@ __global__ void __launch_bounds__(KEYS_ROW_BLOCK) bls_keys_row_kernel(const uint
     q.inf = false;
     dec = true;
   }
-  if (wave == 0) {
-    if (!keys65) return;
+  if (task != 1) {
     const G2RowCtx<uint32_t, uint64_t> c(0u);
     const bool good = dec && g2r_in_subgroup(f2r_from(q.x), f2r_from(q.y), c);
     if (lane == 0) {
       ok[k] = good ? 1 : 0;
-      if (!good) q.inf = true;
-      g2a_store(aff + (size_t)k * BLS_G2A_WORDS, q);
+      g2a qs = q;
+      if (!good) qs.inf = true;
+      g2a_store(aff + (size_t)k * BLS_G2A_WORDS, qs);
     }
-    return;
+    if (task == 0) return;
   }
   if (!dec) return;
   g2r_lines_abc(abc, q);
@@ -335,8 +349,13 @@ hipError_t cbft_bls_launch_keys(const uint8_t* d_keys65, uint32_t nkeys, uint32_
     hipLaunchKernelGGL(bls_keys_kernel, dim3((nkeys + 63) / 64), dim3(64), 0, s, d_keys65, nkeys, d_lines, d_ok,
                        d_aff, d_scratch);
   else
+#if defined(KEYS_ONE_WAVE)
     hipLaunchKernelGGL(bls_keys_row_kernel, dim3(nkeys), dim3(KEYS_ROW_BLOCK), 0, s, d_keys65, nkeys, d_lines,
                        d_ok, d_aff);
+#else
+    hipLaunchKernelGGL(bls_keys_row_kernel, dim3(2 * nkeys), dim3(KEYS_ROW_BLOCK), 0, s, d_keys65, nkeys, d_lines,
+                       d_ok, d_aff);
+#endif
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_gen_lines(uint32_t* d_lines, hipStream_t s) {

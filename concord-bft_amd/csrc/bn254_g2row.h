@@ -13,8 +13,9 @@
 // pass, a multiply ~110 instructions -- a G2 doubling with its line is 8 passes.
 //
 // Value bounds (bn254_row.h: products need (a/q)(b/q) < 221; rf_sub needs b < 4q, rf_sub32
-// b < 16q; rf_reduce x < 2^261 -> < 4q): point coordinates and line coefficients leave every
-// function below 4q (R4); Karatsuba operand sums are formed from R4 values (< 8q), the worst
+// b < 16q; rf_reduce x < 2^261 -> < 4q): point coordinates leave every function below 4q (R4);
+// line coefficients are left unreduced (< 50q: a one-lane f_mul against a value < 2q still
+// returns < 2q, and the key-table normalisation reduces them as it loads them); Karatsuba operand sums are formed from R4 values (< 8q), the worst
 // product is (8q)(24q) = 192 q^2 (E (D - X3), r (V - X3)); every bound is noted where it is used.
 #pragma once
 #include "bn254_g1row.h"
@@ -88,6 +89,13 @@ RF_HD void f2r_mul_res(F2R<U>& r, const U* p, int o, const RowCtx<U, W>& c) {
   r.a = c.red(c.sub(p[o], p[o + 1]));
   r.b = c.red(c.sub(c.sub(p[o + 2], p[o]), p[o + 1]));
 }
+// x * y unreduced: a < 10q, b < 18q (for a subtrahend-free use: the minuend of a subtraction, a
+// line coefficient, or one more reduction after further sums)
+template <class U, class W>
+RF_HD void f2r_mul_raw(F2R<U>& r, const U* p, int o, const RowCtx<U, W>& c) {
+  r.a = c.sub(p[o], p[o + 1]);
+  r.b = c.sub(c.sub(p[o + 2], p[o]), p[o + 1]);
+}
 // x^2: a < 2q (a product), b = 2 x0 x1 < 4q
 template <class U>
 RF_HD void f2r_sqr_res(F2R<U>& r, const U* p, int o) {
@@ -125,7 +133,7 @@ RF_HD void g2r_dbl(F2R<U>* line, G2R<U>& T, const G2RowCtx<U, W>& c) {
     f2r_mul_ops(A, B, 6, T.Y, T.Z);
     r_prods<9>(P, A, B, c);
     f2r_sqr_res(ZZ, P, 4);
-    f2r_mul_res(YZ, P, 6, c);
+    f2r_mul_raw(YZ, P, 6, c);  // < 18q: only 2YZ is used, reduced
   } else {
     r_prods<4>(P, A, B, c);
   }
@@ -149,11 +157,11 @@ RF_HD void g2r_dbl(F2R<U>* line, G2R<U>& T, const G2RowCtx<U, W>& c) {
   U yz2 = {};
   if constexpr (LINE) {
     r_prods<15>(P, A, B, c);
-    f2r_mul_res(line[0], P, 0, c);
-    f2r_mul_res(line[1], P, 3, c);
+    f2r_mul_raw(line[0], P, 0, c);  // line coefficients stay unreduced: < 18q, < 18q, < 50q
+    f2r_mul_raw(line[1], P, 3, c);
     F2R<U> X3E;
-    f2r_mul_res(X3E, P, 6, c);
-    line[2] = f2r_red(f2r_sub32(X3E, f2r_add(YY, YY), c), c);  // 3X^3 - 2Y^2 (2YY < 8q)
+    f2r_mul_raw(X3E, P, 6, c);
+    line[2] = f2r_sub32(X3E, f2r_add(YY, YY), c);  // 3X^3 - 2Y^2 (2YY < 8q)
   } else {
     f2r_mul_ops(A, B, 6, T.Y, T.Z);  // Y Z: two of its products here, the third in the last pass
     yz2 = A[8];
@@ -181,13 +189,13 @@ RF_HD void g2r_dbl(F2R<U>* line, G2R<U>& T, const G2RowCtx<U, W>& c) {
     B[3] = B[8];
     r_prods<4>(P, A, B, c);
     const U yzp[3] = {yz01[0], yz01[1], P[3]};
-    f2r_mul_res(YZ, yzp, 0, c);
-    t = f2r_red(f2r_add(YZ, YZ), c);  // Z3 = 2YZ
+    f2r_mul_raw(YZ, yzp, 0, c);
+    t = f2r_red(f2r_add(YZ, YZ), c);  // Z3 = 2YZ (< 36q before the reduction)
   }
   (void)yz2;
-  f2r_mul_res(Y3, P, 0, c);
+  f2r_mul_raw(Y3, P, 0, c);
   const F2R<U> Y4 = f2r_add(f2r_add(YYYY, YYYY), f2r_add(YYYY, YYYY));  // 4 YYYY < 16q
-  T.Y = f2r_red(f2r_sub32(f2r_sub32(Y3, Y4, c), Y4, c), c);              // E (D - X3) - 8 YYYY
+  T.Y = f2r_red(f2r_sub32(f2r_sub32(Y3, Y4, c), Y4, c), c);              // E (D - X3) - 8 YYYY < 82q
   T.X = X3;
   T.Z = t;
 }
@@ -219,13 +227,13 @@ RF_HD bool g2r_madd(F2R<U>* line, G2R<U>& T, const F2R<U>& qx, const F2R<U>& qy,
     f2r_mul_ops(A, B, 6, QZ, T.X);  // qy Z X
     r_prods<9>(P, A, B, c);
     F2R<U> QZX;
-    f2r_mul_res(QZX, P, 6, c);
-    line[2] = f2r_red(f2r_sub(QZX, QXY, c), c);
+    f2r_mul_raw(QZX, P, 6, c);
+    line[2] = f2r_sub(QZX, QXY, c);  // < 26q, unreduced
   } else {
     r_prods<6>(P, A, B, c);
   }
-  f2r_mul_res(U2, P, 0, c);
-  f2r_mul_res(S2, P, 3, c);
+  f2r_mul_raw(U2, P, 0, c);  // minuends: reduced after the subtraction
+  f2r_mul_raw(S2, P, 3, c);
   const F2R<U> H = f2r_red(f2r_sub(U2, T.X, c), c);
   const F2R<U> R = f2r_red(f2r_sub(S2, T.Y, c), c);
   if constexpr (!LINE) {
@@ -234,7 +242,7 @@ RF_HD bool g2r_madd(F2R<U>* line, G2R<U>& T, const F2R<U>& qx, const F2R<U>& qy,
       return false;
     }
   } else {
-    line[1] = f2r_red(f2r_sub(F2R<U>{c.zero, c.zero}, R, c), c);
+    line[1] = f2r_sub(F2R<U>{c.zero, c.zero}, R, c);  // -R + 8q < 8q, unreduced
   }
   const F2R<U> r = f2r_red(f2r_add(R, R), c);
   const F2R<U> ZH = f2r_red(f2r_add(T.Z, H), c);
@@ -247,7 +255,7 @@ RF_HD bool g2r_madd(F2R<U>* line, G2R<U>& T, const F2R<U>& qx, const F2R<U>& qy,
   f2r_sqr_ops(A, B, o + 2, r, c);
   f2r_sqr_ops(A, B, o + 4, ZH, c);
   r_prods<LINE ? 9 : 6>(P, A, B, c);
-  if constexpr (LINE) f2r_mul_res(line[0], P, 0, c);
+  if constexpr (LINE) f2r_mul_raw(line[0], P, 0, c);
   F2R<U> HH, rr, ZH2;
   f2r_sqr_res(HH, P, o);
   f2r_sqr_res(rr, P, o + 2);
@@ -265,9 +273,9 @@ RF_HD bool g2r_madd(F2R<U>* line, G2R<U>& T, const F2R<U>& qx, const F2R<U>& qy,
   f2r_mul_ops(A, B, 3, T.Y, J);
   r_prods<6>(P, A, B, c);
   F2R<U> Y3, YJ;
-  f2r_mul_res(Y3, P, 0, c);
+  f2r_mul_raw(Y3, P, 0, c);
   f2r_mul_res(YJ, P, 3, c);
-  T.Y = f2r_red(f2r_sub32(Y3, f2r_add(YJ, YJ), c), c);
+  T.Y = f2r_red(f2r_sub32(Y3, f2r_add(YJ, YJ), c), c);    // < 18q + 32q
   T.Z = f2r_red(f2r_sub(f2r_sub(ZH2, ZZ, c), HH, c), c);  // (Z + H)^2 - ZZ - HH < 20q
   T.X = X3;
   return true;

@@ -7,7 +7,9 @@
 // the multi-scalar multiplication, the combined-signature check.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
+#include <thread>
 
 #include "bls_kernels.h"
 #include "cbft_internal.h"
@@ -43,10 +45,35 @@ static BlsKeySet* find_set(cbft_ctx* c, uint32_t id) {
   return it == c->bls_sets.end() ? nullptr : &it->second;
 }
 
+// Run f(kid index) for every device of a multi-GPU context, one host thread per device (each
+// device's calls take its own context mutex, so the devices work concurrently); the first
+// failure's code is returned.
+template <class F>
+static int for_each_kid(cbft_ctx* c, F f) {
+  const size_t G = c->kids.size();
+  std::vector<int> rc(G, CBFT_OK);
+  std::vector<std::thread> th;
+  th.reserve(G);
+  for (size_t g = 0; g < G; g++) th.emplace_back([&, g] { rc[g] = f(g); });
+  for (auto& t : th) t.join();
+  for (int r : rc)
+    if (r) return r;
+  return CBFT_OK;
+}
+
 extern "C" {
 
 int cbft_bls_load_keys(cbft_ctx* c, const uint8_t* pk65, const uint8_t* vks65, uint32_t n, uint32_t* out_id) {
-  c = cbft_dev0(c);
+  if (c && !c->kids.empty()) {  // multi-GPU: the key set on every device, the ids kept in step
+    if (!pk65 || !out_id || (n && !vks65) || n > BLS_MAX_SHARES) return CBFT_EINVAL;
+    std::vector<uint32_t> ids(c->kids.size(), 0);
+    const int rc = for_each_kid(c, [&](size_t g) { return cbft_bls_load_keys(c->kids[g], pk65, vks65, n, &ids[g]); });
+    if (rc) return rc;
+    for (uint32_t id : ids)
+      if (id != ids[0]) return CBFT_EIO;
+    *out_id = ids[0];
+    return CBFT_OK;
+  }
   if (!c || !pk65 || !out_id || (n && !vks65) || n > BLS_MAX_SHARES) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
@@ -76,7 +103,14 @@ int cbft_bls_load_keys(cbft_ctx* c, const uint8_t* pk65, const uint8_t* vks65, u
 }
 
 int cbft_bls_unload_keys(cbft_ctx* c, uint32_t id) {
-  c = cbft_dev0(c);
+  if (c && !c->kids.empty()) {
+    int rc = CBFT_OK;
+    for (cbft_ctx* k : c->kids) {
+      const int r = cbft_bls_unload_keys(k, id);
+      if (r && !rc) rc = r;
+    }
+    return rc;
+  }
   if (!c) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   BlsKeySet* ks = find_set(c, id);
@@ -152,7 +186,28 @@ static int bls_verify_parsed(cbft_ctx* c, BlsKeySet* ks, uint32_t k) {
 
 int cbft_bls_verify_shares(cbft_ctx* c, uint32_t id, const uint8_t* msg, uint32_t len, const uint8_t* shares37,
                            uint32_t k, uint8_t* valid_bitmap) {
-  c = cbft_dev0(c);
+  if (c && !c->kids.empty()) {
+    // multi-GPU: contiguous share slices, one per device, verified
+    // concurrently against the device's copy of the key set; the slice bitmaps are merged
+    if ((k && (!shares37 || !valid_bitmap)) || (len && !msg) || k > BLS_MAX_SHARES) return CBFT_EINVAL;
+    if (!k) return CBFT_OK;
+    const size_t G = c->kids.size(), per = (k + G - 1) / G;
+    std::vector<std::vector<uint8_t>> part(G);
+    const int rc = for_each_kid(c, [&](size_t g) {
+      const size_t lo = std::min<size_t>(k, g * per), hi = std::min<size_t>(k, lo + per);
+      part[g].assign((hi - lo + 7) / 8 + 1, 0);
+      if (hi == lo) return (int)CBFT_OK;
+      return cbft_bls_verify_shares(c->kids[g], id, msg, len, shares37 + 37 * lo, (uint32_t)(hi - lo), part[g].data());
+    });
+    if (rc) return rc;
+    std::memset(valid_bitmap, 0, (k + 7) / 8);
+    for (size_t g = 0; g < G; g++) {
+      const size_t lo = std::min<size_t>(k, g * per), hi = std::min<size_t>(k, lo + per);
+      for (size_t j = lo; j < hi; j++)
+        if ((part[g][(j - lo) >> 3] >> ((j - lo) & 7)) & 1) valid_bitmap[j >> 3] |= (uint8_t)(1u << (j & 7));
+    }
+    return CBFT_OK;
+  }
   if (!c || (k && (!shares37 || !valid_bitmap)) || (len && !msg) || k > BLS_MAX_SHARES) return CBFT_EINVAL;
   std::lock_guard<std::mutex> g(c->mu);
   BlsKeySet* ks = find_set(c, id);

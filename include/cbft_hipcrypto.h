@@ -62,7 +62,9 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch);
 /* Open one context over every GPU whose bit is set in device_mask (bit d = device d; SURVEY.md
  * §8(b)).  Ed25519 key tables are replicated on each device; an Ed25519 host-buffer batch is cut
  * into contiguous shards of whole 64-signature words, one per device, verified concurrently, and
- * the verdicts land in the caller's one bitmap.  BLS, RSA and the profiling calls run on the
+ * the verdicts land in the caller's one bitmap.  BLS key sets are loaded on every device and
+ * cbft_bls_verify_shares cuts the shares into contiguous slices, one per device, verified
+ * concurrently (bitmaps merged); the other BLS calls, RSA and the profiling calls run on the
  * lowest device of the mask; the _device entry points need a single-GPU context (CBFT_EINVAL).
  * A one-bit mask is exactly cbft_open. */
 int cbft_open_mask(cbft_ctx** out, uint32_t device_mask, size_t max_batch);

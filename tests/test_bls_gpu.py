@@ -325,3 +325,34 @@ def test_sum_keys_exceptional_cases(ctx):
         assert ctx.bls_sum_keys(kid, bm) == bytes(65)  # a selected key that did not decode
     finally:
         ctx.bls_unload_keys(kid)
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0] * 4])
+def test_multi_device_share_verification(ctx, devices):
+    """cbft_open_devices: the key set on every device, the shares cut into one contiguous slice
+    per device and verified concurrently -- the merged bitmap equals the single-device one
+    (on one GPU the devices repeat, each child with its own streams)."""
+    n, k = 40, 27
+    sk, sks, pk, vks = blsgen.keyset(n, k, seed=41)
+    msg = bytes(range(3, 35))
+    good = blsgen.shares(sks, range(1, n + 1), msg)
+    cases = list(good)
+    for j in (0, 7, 13, 21, 39):
+        cases[j] = blsgen.doubled(good[j])  # bad shares spread over the slices
+    cases.append((n + 1).to_bytes(4, "big") + good[1][4:])  # id out of range
+    kid = ctx.bls_load_keys(pk, vks)
+    try:
+        want = ctx.bls_verify_shares(kid, msg, cases)
+    finally:
+        ctx.bls_unload_keys(kid)
+    with cb.Context(devices=devices) as g:
+        gk = g.bls_load_keys(pk, vks)
+        try:
+            assert all(g.bls_key_status(gk, n))
+            got = g.bls_verify_shares(gk, msg, cases)
+            assert got.tolist() == want.tolist()
+            assert sum(want) == n - 5
+            sig, ok, bad = g.bls_combine_threshold(gk, msg, cases, optimistic=True)
+            assert ok and sig == blsgen.sign_point(sk, msg)
+        finally:
+            g.bls_unload_keys(gk)

@@ -34,6 +34,7 @@ msig = ctx.bls_combine(use, multisig=True)
 assert ctx.bls_verify_multisig(kid, cert.msg, msig, bytes(bitmap))
 out = {}
 for name, fn in (("keyset_load", lambda: ctx.bls_unload_keys(ctx.bls_load_keys(cert.pk, cert.vks))),
+                 ("keyset_load_1key", lambda: ctx.bls_unload_keys(ctx.bls_load_keys(cert.pk, []))),
                  ("share_verify", lambda: ctx.bls_verify_shares(kid, cert.msg, cert.shares)),
                  ("combine", lambda: ctx.bls_combine(use)),
                  ("verify", lambda: ctx.bls_verify(kid, cert.msg, comb)),
