@@ -76,6 +76,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-runs", type=int, default=200)
     ap.add_argument("--inflight", type=int, default=4, help="host-path batches in flight")
+    ap.add_argument("--single-process-devices", default="",
+                    help="also time one process over these devices (comma list, repeats allowed: cbft_open_devices); "
+                         "with --gpus N > 1 rank 0 does this over all N GPUs (cbft_open_mask) by default")
     ap.add_argument("--no-extras", dest="extras", action="store_false",
                     help="skip the config #3 (mixed), config #4 (BLS) and RSA-2048 side measurements")
     return ap.parse_args()
@@ -332,6 +335,18 @@ def main():
                          "note": "the step's binding resource: host->device bytes of the batch over PCIe Gen5 x16"},
                 "device_resident_ceiling": dev_value}
 
+    # ---- the replica's own multi-GPU form: ONE process over all N devices (cbft_open_mask), the
+    # same per-device batch as a shard of one N x batch call, verdicts gated as above
+    single = None
+    sp_devices = [int(x) for x in args.single_process_devices.split(",") if x] or \
+        (list(range(world)) if world > 1 else [])
+    if world > 1:
+        dist.barrier()
+    if rank == 0 and sp_devices:
+        single = bench_single_process(args, ss, sp_devices, mask=(world > 1 and not args.single_process_devices))
+    if world > 1:
+        dist.barrier()
+
     out = None
     if rank == 0:
         cpu = None
@@ -419,6 +434,7 @@ def main():
             "bls_config4": bls,
             "rsa_2048": rsa,
             "per_request_path": per_request,
+            "single_process_multi_gpu": single,
             "verdicts": "bit-exact vs host OpenSSL (checked before and after timing)",
             "parity": parity,
         }
@@ -427,6 +443,55 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_single_process(args, ss, devices, mask):
+    """One process over several GPUs (cbft_open_mask / cbft_open_devices): each step is ONE
+    len(devices) x batch signature call, cut by the library into per-device shards of whole
+    64-signature words that run concurrently, verdicts landing in one bitmap (the
+    in-process form a replica would use).  Key table replicated per device; same pinned-host
+    pipeline as the headline; every slot's verdicts checked against OpenSSL's."""
+    G, n, L = len(devices), args.batch, args.msg_len
+    N = G * n
+    g = cb.Context(device_mask=sum(1 << d for d in devices), max_batch=N) if mask else \
+        cb.Context(devices=devices, max_batch=N)
+    try:
+        tid = g.load_keys(ss.pk, radix=args.comb_radix)
+        blk, h_kidx, h_sig, b_raw = g.batch_views(N, L)
+        h_kidx[:] = np.tile(ss.key_idx, G)
+        h_sig[:] = np.tile(ss.sig, (G, 1))
+        b_raw[:] = np.tile(ss.blob[: n * L], G)
+        expected = np.tile(ss.expected, G)
+        depth = max(1, args.inflight)
+        outs = [np.zeros(N // 8 + 1, dtype=np.uint8) for _ in range(depth)]
+
+        def run(steps):
+            tk = []
+            for st in range(steps):
+                tk.append(g.verify_async(tid, h_kidx, h_sig, b_raw, outs[st % depth], msg_len=L, n=N))
+                if st >= depth - 1:
+                    g.wait(tk[st - depth + 1])
+            for st in range(max(0, steps - depth), steps):
+                g.wait(tk[st])
+
+        run(1)
+        if not np.array_equal(cb.bitmap_to_bools(outs[0][: (N + 7) // 8].tobytes(), N), expected):
+            raise SystemExit("single-process multi-GPU: verdicts differ from OpenSSL")
+        run(args.warmup)
+        t0 = time.perf_counter()
+        run(args.steps)
+        dt = time.perf_counter() - t0
+        for j in range(min(depth, args.steps)):
+            if not np.array_equal(cb.bitmap_to_bools(outs[j][: (N + 7) // 8].tobytes(), N), expected):
+                raise SystemExit("single-process multi-GPU: pipelined verdicts differ from OpenSSL")
+        g.host_free(blk)
+        return {"value": N * args.steps / dt, "unit": "verifies/s", "devices": devices,
+                "open": "cbft_open_mask" if mask else "cbft_open_devices", "batch_per_call": N,
+                "ms_per_step": dt / args.steps * 1e3, "verdicts_exact": True,
+                "basis": f"{args.steps} steps of one {N}-signature call (per-device shards of {n}), "
+                         f"{depth} in flight, pinned host inputs, H2D included"}
+    finally:
+        g.close()
 
 
 def bench_per_request(cpu_threads):

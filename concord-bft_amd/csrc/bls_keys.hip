@@ -87,25 +87,16 @@ __device__ __noinline__ void g2r_normalise_lines(uint32_t* out, const uint32_t* 
 // (g2r_lines_abc into LDS) and normalises them into lines[k] (written for every decodable key;
 // only ok keys are ever read); both decode the key (one lane's work).  The chip holds 2 x 1,024
 // of these waves at once (VGPR-bound), so of the n + 1 = 1,025 keys' 2,050 blocks the last two
-// start when the first finish: they are lines blocks (~0.6 ms), not subgroup checks (~1 ms).
-// (Two-wave blocks put the group key's whole block in a second round.)
+// start when the first finish: they are lines blocks (0.63 ms alone), not subgroup checks
+// (1.7 ms alone).  Measured on 1,025 keys: 4.0 ms; two-wave blocks 4.5 ms (the group key's block
+// ran in a second round); one wave per key doing both tasks 4.2 ms.
 #define KEYS_ROW_BLOCK 64
 __global__ void __launch_bounds__(KEYS_ROW_BLOCK) bls_keys_row_kernel(const uint8_t* keys65, uint32_t nkeys,
                                                                       uint32_t* lines, uint8_t* ok, uint32_t* aff) {
   __shared__ uint32_t abc[BN_ATE_LINES * BN_ABC_WORDS];
   __shared__ uint32_t pre[BN_ATE_LINES * 18];
-#if defined(KEYS_FORCE_TASK)  // A/B probes only: every block runs one task
-  const int task = keys65 ? KEYS_FORCE_TASK : 1;
-#elif defined(KEYS_ONE_WAVE)  // A/B: one wave per key, subgroup check then lines
-  const int task = keys65 ? 2 : 1;
-#else
   const int task = keys65 ? (blockIdx.x >= nkeys) : 1;
-#endif
-#if defined(KEYS_ONE_WAVE)
-  const uint32_t k = keys65 ? blockIdx.x : 0;
-#else
   const uint32_t k = keys65 ? blockIdx.x - (task ? nkeys : 0) : 0;
-#endif
   if (k >= nkeys) return;
   const int lane = threadIdx.x & 63;
   g2a q;
@@ -118,7 +109,7 @@ __global__ void __launch_bounds__(KEYS_ROW_BLOCK) bls_keys_row_kernel(const uint
     q.inf = false;
     dec = true;
   }
-  if (task != 1) {
+  if (task == 0) {
     const G2RowCtx<uint32_t, uint64_t> c(0u);
     const bool good = dec && g2r_in_subgroup(f2r_from(q.x), f2r_from(q.y), c);
     if (lane == 0) {
@@ -127,7 +118,7 @@ __global__ void __launch_bounds__(KEYS_ROW_BLOCK) bls_keys_row_kernel(const uint
       if (!good) qs.inf = true;
       g2a_store(aff + (size_t)k * BLS_G2A_WORDS, qs);
     }
-    if (task == 0) return;
+    return;
   }
   if (!dec) return;
   g2r_lines_abc(abc, q);
@@ -349,13 +340,8 @@ hipError_t cbft_bls_launch_keys(const uint8_t* d_keys65, uint32_t nkeys, uint32_
     hipLaunchKernelGGL(bls_keys_kernel, dim3((nkeys + 63) / 64), dim3(64), 0, s, d_keys65, nkeys, d_lines, d_ok,
                        d_aff, d_scratch);
   else
-#if defined(KEYS_ONE_WAVE)
-    hipLaunchKernelGGL(bls_keys_row_kernel, dim3(nkeys), dim3(KEYS_ROW_BLOCK), 0, s, d_keys65, nkeys, d_lines,
-                       d_ok, d_aff);
-#else
     hipLaunchKernelGGL(bls_keys_row_kernel, dim3(2 * nkeys), dim3(KEYS_ROW_BLOCK), 0, s, d_keys65, nkeys, d_lines,
                        d_ok, d_aff);
-#endif
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_gen_lines(uint32_t* d_lines, hipStream_t s) {
