@@ -135,6 +135,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   c->device = device;
   if (const char* e = getenv("CBFT_FINISH_BATCH")) c->finish_batch = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e);
+  if (const char* e = getenv("CBFT_STAGE_ORDER_MIN")) c->stage_order_min = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_LADDER_LANES")) {
     const int l = atoi(e);
     if (l == 2 || l == 4) c->ladder_lanes = l;
@@ -651,8 +652,13 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     // the quad ladder (half the additions per lane) for the latency of small batches
     w.comb_lanes = c->ladder_lanes ? c->ladder_lanes : (n >= 32768 ? 2 : 4);
   }
+  // Stage order pays for big batches (their stages fill the chip; see cbft_ctx::stage_order).
+  // Small batches are latency-bound single waves per stage: ordering them only serialises
+  // concurrent callers' batches (the per-request coalescer keeps several in flight), so they run
+  // unordered ($CBFT_STAGE_ORDER_MIN, default 4,096 signatures).
+  const bool ordered = c->stage_order && n >= c->stage_order_min;
   StageOrder order{};
-  if (c->stage_order) {
+  if (ordered) {
     for (hipEvent_t& e : c->stage_done)
       if (!e) CBFT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     order.wait = c->stage_used;
@@ -662,8 +668,8 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   }
   hipEvent_t* evp = nullptr;
   if (c->profiling) evp = c->prof_mode == 2 ? &c->ring[(c->ring_n++ % CBFT_PROF_RING) * 4] : c->ev;
-  CBFT_HIP(cbft_ed25519_launch_verify(b, w, s, evp, c->stage_order ? &order : nullptr));
-  c->stage_used = c->stage_order != 0;
+  CBFT_HIP(cbft_ed25519_launch_verify(b, w, s, evp, ordered ? &order : nullptr));
+  if (ordered) c->stage_used = true;
   CBFT_HIP(hipEventRecord(slot.done, s));
   slot.used = true;
   c->ev_valid = c->profiling;

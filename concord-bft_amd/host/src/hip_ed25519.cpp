@@ -146,9 +146,10 @@ static int engineRadix() {
 //
 // verifyOne() coalesces concurrent single verifies (the reference calls IVerifier::verify from
 // 40 + 24 pool threads, ReplicaConfig.hpp:202-212): callers queue their request; one of them
-// leads a batch as soon as fewer than kMaxInflight batches are on the GPU, taking everything
+// leads a batch as soon as fewer than maxInflight_ batches are on the GPU, taking everything
 // queued by then.  A lone caller goes straight to the GPU; under load, requests that arrive
-// while batches run are verified together in the next one.
+// while batches run are verified together in the next one.  Each request waits on its own
+// condition variable (woken for its verdict or to lead), never on a shared one.
 class Ed25519Engine {
  public:
   static constexpr int kMaxInflight = 2;
@@ -275,24 +276,36 @@ class Ed25519Engine {
     Pending p{v, data, len, sig, sigLen};
     std::unique_lock<std::mutex> lk(q_mu_);
     queue_.push_back(&p);
+    if (!leader_ && inflight_ < maxInflight_) {  // a GPU slot is free: go now, with whatever is queued
+      p.lead = true;
+      leader_ = true;
+    }
     while (!p.done) {
-      if (!leader_ && !queue_.empty()) {
-        leader_ = true;
-        q_cv_.wait(lk, [&] { return inflight_ < kMaxInflight || queue_.size() >= kMaxBatch; });
-        std::vector<Pending*> batch;
-        batch.swap(queue_);
-        leader_ = false;
-        inflight_++;
-        q_cv_.notify_all();  // the next arrival (or a waiter) may lead the next batch
-        lk.unlock();
-        runBatch(batch);
-        lk.lock();
-        inflight_--;
-        for (Pending* q : batch) q->done = true;
-        q_cv_.notify_all();
-      } else {
-        q_cv_.wait(lk);
+      if (!p.lead) {
+        p.cv.wait(lk);  // woken only for this request: its verdict, or its turn to lead
+        continue;
       }
+      // lead one batch: everything queued so far (up to kMaxBatch)
+      p.lead = false;
+      std::vector<Pending*> batch;
+      if (queue_.size() <= kMaxBatch) {
+        batch.swap(queue_);
+      } else {
+        batch.assign(queue_.begin(), queue_.begin() + kMaxBatch);
+        queue_.erase(queue_.begin(), queue_.begin() + kMaxBatch);
+      }
+      leader_ = false;
+      inflight_++;
+      appointLocked();  // requests that queued meanwhile may lead the next batch if a slot is free
+      lk.unlock();
+      runBatch(batch);
+      lk.lock();
+      inflight_--;
+      for (Pending* q : batch) {
+        q->done = true;
+        if (q != &p) q->cv.notify_one();
+      }
+      appointLocked();
     }
     return p.verdict;
   }
@@ -313,7 +326,20 @@ class Ed25519Engine {
     size_t sigLen;
     bool done = false;
     bool verdict = false;
+    bool lead = false;
+    std::condition_variable cv;
   };
+
+  // With no leader and a free GPU slot, the oldest queued request leads the next batch (q_mu_
+  // held).  Waking only that one request, and each finished request only once, keeps 64 pool
+  // threads from stampeding on one condition variable at every batch boundary.
+  void appointLocked() {
+    if (leader_ || queue_.empty() || inflight_ >= maxInflight_) return;
+    Pending* h = queue_.front();
+    h->lead = true;
+    leader_ = true;
+    h->cv.notify_one();
+  }
 
   void runBatch(std::vector<Pending*>& batch) {
     std::vector<VerifyRequest> reqs(batch.size());
@@ -366,8 +392,12 @@ class Ed25519Engine {
   std::mutex append_mu_;  // one device-table write (append / slot rebuild) at a time
   std::atomic<uint32_t> loaded_{0};
   std::mutex q_mu_;  // coalescing queue
-  std::condition_variable q_cv_;
   std::vector<Pending*> queue_;
+  int maxInflight_ = [] {  // GPU batches in flight ($CBFT_ENGINE_INFLIGHT, default kMaxInflight)
+    const char* e = std::getenv("CBFT_ENGINE_INFLIGHT");
+    const int v = e ? std::atoi(e) : kMaxInflight;
+    return v < 1 ? 1 : (v > 8 ? 8 : v);
+  }();
   bool leader_ = false;
   int inflight_ = 0;
   std::atomic<uint64_t> batches_{0}, items_{0}, gpu_errors_{0};
