@@ -136,6 +136,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   if (const char* e = getenv("CBFT_FINISH_BATCH")) c->finish_batch = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER_MIN")) c->stage_order_min = (size_t)atoll(e);
+  if (const char* e = getenv("CBFT_SMALL_MAX")) c->small_max = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_LADDER_LANES")) {
     const int l = atoi(e);
     if (l == 2 || l == 4) c->ladder_lanes = l;
@@ -651,12 +652,13 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     // pair ladder (fewer additions in total, 2 waves/SIMD) once a batch fills the chip with it;
     // the quad ladder (half the additions per lane) for the latency of small batches
     w.comb_lanes = c->ladder_lanes ? c->ladder_lanes : (n >= 32768 ? 2 : 4);
+    w.small = n <= c->small_max && !c->ladder_lanes;
   }
   // Stage order pays for big batches (their stages fill the chip; see cbft_ctx::stage_order).
   // Small batches are latency-bound single waves per stage: ordering them only serialises
   // concurrent callers' batches (the per-request coalescer keeps several in flight), so they run
   // unordered ($CBFT_STAGE_ORDER_MIN, default 4,096 signatures).
-  const bool ordered = c->stage_order && n >= c->stage_order_min;
+  const bool ordered = c->stage_order && n >= c->stage_order_min && !w.small;
   StageOrder order{};
   if (ordered) {
     for (hipEvent_t& e : c->stage_done)
@@ -798,6 +800,11 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
       phi = std::max(phi, parts[k].off + parts[k].bytes);
     }
   uint8_t* din = s.in.as<uint8_t>();
+  // a small packed batch (the per-request path) copies on its compute stream: no copy-stream
+  // event to record and wait for; bigger batches overlap their copies with earlier batches' kernels
+  hipStream_t cs = c->compute[t & 1];
+  const bool one_stream = pack && n <= c->small_max;
+  hipStream_t cps = one_stream ? cs : c->copy_stream;
   // every part pinned and laid out in one host block exactly as in the device image
   // (cbft_ed25519_batch_layout): the whole batch is one DMA
   {
@@ -814,7 +821,7 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
       hi = std::max(hi, parts[k].off + parts[k].bytes);
     }
     if (same && base && is_pinned(base + lo, hi - lo)) {
-      CBFT_HIP(hipMemcpyAsync(din + lo, base + lo, hi - lo, hipMemcpyHostToDevice, c->copy_stream));
+      CBFT_HIP(hipMemcpyAsync(din + lo, base + lo, hi - lo, hipMemcpyHostToDevice, cps));
       for (int k = 0; k < 5; k++) parts[k].bytes = 0;  // moved
     }
   }
@@ -822,7 +829,7 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
   if (!pack) {
     for (int k = 0; k < 5; k++)
       if (parts[k].bytes && !pinned[k]) {
-        CBFT_HIP(hipMemcpyAsync(din + parts[k].off, parts[k].src, parts[k].bytes, hipMemcpyHostToDevice, c->copy_stream));
+        CBFT_HIP(hipMemcpyAsync(din + parts[k].off, parts[k].src, parts[k].bytes, hipMemcpyHostToDevice, cps));
         pageable_queued = true;
       }
   }
@@ -830,19 +837,20 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
     CBFT_HIP(s.pack.reserve(in_bytes));
     for (int k = 0; k < 5; k++)
       if (parts[k].bytes && !pinned[k]) std::memcpy(s.pack.as<uint8_t>(parts[k].off), parts[k].src, parts[k].bytes);
-    CBFT_HIP(hipMemcpyAsync(din + plo, s.pack.as<uint8_t>(plo), phi - plo, hipMemcpyHostToDevice, c->copy_stream));
+    CBFT_HIP(hipMemcpyAsync(din + plo, s.pack.as<uint8_t>(plo), phi - plo, hipMemcpyHostToDevice, cps));
   }
   // pinned parts after the packed run (stream order: they win where the run spans them)
   for (int k = 0; k < 5; k++)
     if (parts[k].bytes && pinned[k])
-      CBFT_HIP(hipMemcpyAsync(din + parts[k].off, parts[k].src, parts[k].bytes, hipMemcpyHostToDevice, c->copy_stream));
-  CBFT_HIP(hipEventRecord(s.copied, c->copy_stream));
-  // the header's contract: pageable inputs may be reused as soon as the call returns, so a
-  // batch whose pageable parts were not packed returns only after their copies completed (the
-  // runtime may still be staging from the caller's memory)
-  if (pageable_queued) CBFT_HIP(hipEventSynchronize(s.copied));
-  hipStream_t cs = c->compute[t & 1];
-  CBFT_HIP(hipStreamWaitEvent(cs, s.copied, 0));
+      CBFT_HIP(hipMemcpyAsync(din + parts[k].off, parts[k].src, parts[k].bytes, hipMemcpyHostToDevice, cps));
+  if (!one_stream) {
+    CBFT_HIP(hipEventRecord(s.copied, cps));
+    // the header's contract: pageable inputs may be reused as soon as the call returns, so a
+    // batch whose pageable parts were not packed returns only after their copies completed (the
+    // runtime may still be staging from the caller's memory)
+    if (pageable_queued) CBFT_HIP(hipEventSynchronize(s.copied));
+    CBFT_HIP(hipStreamWaitEvent(cs, s.copied, 0));
+  }
   rc = launch_locked(c, table_id, kt ? nullptr : din + o_key, kt ? reinterpret_cast<const uint32_t*>(din + o_key) : nullptr,
                      din + o_sig, din + o_msg - blo, fixed ? nullptr : reinterpret_cast<const uint64_t*>(din + o_off),
                      fixed ? nullptr : reinterpret_cast<const uint32_t*>(din + o_len), fixed_len, n,

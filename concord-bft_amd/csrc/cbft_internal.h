@@ -159,6 +159,9 @@ struct cbft_ctx {
   // the SIMDs idle).  $CBFT_STAGE_ORDER: 0 off, 1 hash + ladder, 2 ladder only.
   int stage_order = 1;
   size_t stage_order_min = 4096;  // smaller batches run unordered ($CBFT_STAGE_ORDER_MIN)
+  // key-table batches up to this size run as one fused launch (ed25519_small_kernel;
+  // $CBFT_SMALL_MAX, 0 = never): the per-request coalescer's batches
+  size_t small_max = 1024;
   int b_radix = CBFT_COMB_B_RADIX;  // radix of B's comb table ($CBFT_B_RADIX, 16..22)
   int ladder_lanes = 0;             // comb ladder lanes per signature ($CBFT_LADDER_LANES 2 | 4; 0 = by batch)
   hipEvent_t stage_done[2] = {nullptr, nullptr};  // last hash, last ladder

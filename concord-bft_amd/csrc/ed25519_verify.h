@@ -123,6 +123,7 @@ struct Ed25519Work {
   uint8_t* flags;              // n bytes
   uint32_t* xyz_soa;           // 27 x n words
   uint64_t* verdict_words;     // ceil(n/64) words; bit (i % 64) of word i/64 = accept
+  int small;                   // key-table batch in ONE launch (ed25519_small_kernel): small batches
 };
 
 size_t cbft_ed25519_table_words_per_unit();

@@ -215,10 +215,9 @@ __device__ __forceinline__ bool unit_aok(const Ed25519Batch& b, const uint8_t* a
   return b.key_idx ? b.keys.aok(unit) : aok[unit] != 0;
 }
 
-__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const Ed25519Batch b, uint32_t* h_soa,
-                                                                          uint8_t* flags) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= b.n) return;
+// h = SHA-512(R||A||M) mod L of signature i (hw, 8 LE words) and its flag (S < L, key index in
+// range, length supported): K1's per-signature work, also run by the fused small-batch kernel.
+__device__ __forceinline__ void ed25519_hash_sig(const Ed25519Batch& b, size_t i, uint32_t* hw, bool& flag) {
   const uint32_t key = batch_unit(b, i);
   const bool key_ok = !b.key_idx || b.key_idx[i] < b.nkeys;
   uint32_t Aw[8], Rw[8], Sw[8];
@@ -251,16 +250,26 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const E
     }
     sha512_compress(H, W);
   }
-  uint32_t dig[16], hw[8];
+  uint32_t dig[16];
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     dig[2 * k] = bswap32((uint32_t)(H[k] >> 32));
     dig[2 * k + 1] = bswap32((uint32_t)H[k]);
   }
   sc_reduce512(hw, dig);
+  flag = sc_is_canonical(Sw) && key_ok && len_ok;
+}
+
+__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const Ed25519Batch b, uint32_t* h_soa,
+                                                                          uint8_t* flags) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= b.n) return;
+  uint32_t hw[8];
+  bool flag;
+  ed25519_hash_sig(b, i, hw, flag);
 #pragma unroll
   for (int k = 0; k < 8; k++) h_soa[k * b.n + i] = hw[k];
-  flags[i] = (sc_is_canonical(Sw) && key_ok && len_ok) ? 1 : 0;
+  flags[i] = flag ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -645,23 +654,22 @@ __device__ __forceinline__ void add256(uint32_t* s, const uint32_t* off) {
 #define CBFT_COMB_MIN_WAVES 4
 #endif
 
-__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
-    ed25519_comb_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* btbl,
-                               const CombLadder cl, uint32_t* xyz_soa) {
-  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const uint32_t q = threadIdx.x & 3u;
-  size_t i = g >> 2;
-  const bool live = i < b.n;
-  if (!live) i = b.n - 1;  // tail quads compute a copy (all lanes stay active for the DPP)
+// Lane q's quarter of the comb sum [h](-A) + [S]B of signature i (h = h_in, 8 LE words): its
+// nper mixed additions from the key's and B's comb tables, entries staged through LDS one
+// addition ahead (sdig: COMB_MAX_STEPS x BLOCK ints, stage: BLOCK / 64 x 7 x 64 uint4 of LDS).
+// The caller combines the quad's four partial sums.
+template <int BLOCK>
+__device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, uint32_t q, const uint32_t* h_in,
+                                              const uint32_t* btbl, const CombLadder& cl, int32_t* sdig, uint4* stage,
+                                              ge_p3& P) {
   const uint32_t ntot = cl.a.npos + cl.b.npos;
   const uint32_t first = q * cl.nper;
   // Digits of this lane's additions (signed, up to +-2^21), kept in LDS ([step][thread]:
   // conflict-free) so the addition loop holds no digit registers.
-  __shared__ int32_t sdig[COMB_MAX_STEPS][CBFT_VERIFY_BLOCK];
   {
     uint32_t hs[8], ss[8];
 #pragma unroll
-    for (int k = 0; k < 8; k++) hs[k] = h_soa[k * b.n + i];
+    for (int k = 0; k < 8; k++) hs[k] = h_in[k];
     load_words8(ss, b.sig + i * 64 + 32);
     add256(hs, cl.offA);
     add256(ss, cl.offB);
@@ -680,7 +688,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
       // top digit in [0, 2^(w-1)]; only S >= L (flagged, rejected in K4) can exceed it
       int d = pos == top ? (int)(ch < half ? ch : half) : (int)ch - (int)half;
       if (jj >= cl.nper || k >= ntot) d = 0;
-      sdig[jj][threadIdx.x] = d;
+      sdig[jj * BLOCK + threadIdx.x] = d;
     }
   }
   const uint32_t* akey = b.keys.comb(batch_unit(b, i));
@@ -691,15 +699,13 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
     const uint32_t pos = k < ntot ? k - cl.a.npos : 0u;  // past the last position: identity
     return btbl + ((size_t)pos * cl.b.entries() + ad) * COMB_STRIDE;
   };
-  auto digit = [&](int jj) { return sdig[jj][threadIdx.x]; };
-  ge_p3 P;
+  auto digit = [&](int jj) { return sdig[jj * BLOCK + threadIdx.x]; };
   ge_p3_0(P);
   // Table entries are staged through LDS with global_load_lds (no VGPR destination): entry
   // jj+1's 7 x 16 B are requested as soon as entry jj has been read out of LDS, so its HBM /
   // Infinity-Cache latency overlaps the rest of addition jj.  LDS image per wave:
   // [chunk 0..6][lane][16 B] (lane-linear, as one global_load_lds_dwordx4 writes it), 7 KB.
-  __shared__ uint4 stage[CBFT_VERIFY_BLOCK / 64][7][64];
-  uint4(*st)[64] = stage[threadIdx.x >> 6];
+  uint4(*st)[64] = reinterpret_cast<uint4(*)[64]>(stage + (threadIdx.x >> 6) * 7 * 64);
   const uint32_t ln = threadIdx.x & 63u;
   auto request = [&](const uint32_t* e) {
 #pragma unroll
@@ -760,6 +766,29 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
     fe_mul(P.Y, t.Y, t.Z);
     fe_mul(P.Z, t.Z, t.T);
   }
+}
+
+__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
+    ed25519_comb_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* btbl,
+                               const CombLadder cl, uint32_t* xyz_soa) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t q = threadIdx.x & 3u;
+  size_t i = g >> 2;
+  const bool live = i < b.n;
+  if (!live) i = b.n - 1;  // tail quads compute a copy (all lanes stay active for the DPP)
+  // Digits of this lane's additions (signed, up to +-2^21), kept in LDS ([step][thread]:
+  // conflict-free) so the addition loop holds no digit registers.
+  __shared__ int32_t sdig[COMB_MAX_STEPS * CBFT_VERIFY_BLOCK];
+  // Table entries are staged through LDS with global_load_lds (no VGPR destination): entry
+  // jj+1's 7 x 16 B are requested as soon as entry jj has been read out of LDS, so its HBM /
+  // Infinity-Cache latency overlaps the rest of addition jj.  LDS image per wave:
+  // [chunk 0..6][lane][16 B] (lane-linear, as one global_load_lds_dwordx4 writes it), 7 KB.
+  __shared__ uint4 stage[CBFT_VERIFY_BLOCK / 64 * 7 * 64];
+  uint32_t hs[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) hs[k] = h_soa[k * b.n + i];
+  ge_p3 P;
+  comb_quad_sum<CBFT_VERIFY_BLOCK>(b, i, q, hs, btbl, cl, sdig, stage, P);
   quad_combine<0xB1>(P, true);
   quad_combine<0x4E>(P, false);
   if (live && q == 0) {
@@ -767,6 +796,51 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
     fe_store_soa(xyz_soa + 9 * b.n, b.n, i, P.Y);
     fe_store_soa(xyz_soa + 18 * b.n, b.n, i, P.Z);
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Small batches in ONE launch (the per-request path: a few coalesced verify() calls): one wave
+// per 16 signatures, a lane quad per signature -- every lane of the quad hashes (the same
+// digest, so no exchange), the quad runs the comb sum as K3q and combines it by DPP, and every
+// lane encodes and compares; the verdicts of the wave's 16 signatures go out as one 16-bit
+// word.  Three launches (hash, ladder, finish) and their inter-kernel gaps become one, and no
+// per-signature state goes through HBM.
+// ---------------------------------------------------------------------------------------
+#define SMALL_SIGS 16
+__global__ void __launch_bounds__(64) ed25519_small_kernel(const Ed25519Batch b, const uint32_t* btbl,
+                                                           const CombLadder cl, uint16_t* verdict16) {
+  __shared__ int32_t sdig[COMB_MAX_STEPS * 64];
+  __shared__ uint4 stage[7 * 64];
+  const uint32_t ln = threadIdx.x, q = ln & 3u;
+  size_t i = (size_t)blockIdx.x * SMALL_SIGS + (ln >> 2);
+  const bool live = i < b.n;
+  if (!live) i = b.n - 1;
+  uint32_t hs[8];
+  bool flag;
+  ed25519_hash_sig(b, i, hs, flag);
+  ge_p3 P;
+  comb_quad_sum<64>(b, i, q, hs, btbl, cl, sdig, stage, P);
+  quad_combine<0xB1>(P, true);
+  quad_combine<0x4E>(P, false);
+  uint32_t Rp[8], Rw[8];
+  {  // encode R' (public: variable-time inversion)
+    fe zi, x, y;
+    fe_invert_var(zi, P.Z);
+    fe_mul<false>(x, P.X, zi);
+    fe_mul<false>(y, P.Y, zi);
+    fe_to_words(Rp, y);
+    Rp[7] ^= fe_isnegative(x) << 31;
+  }
+  load_words8(Rw, b.sig + i * 64);
+  uint32_t diff = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) diff |= Rp[k] ^ Rw[k];
+  const bool verdict = live && diff == 0 && flag && b.keys.aok(batch_unit(b, i));
+  const uint64_t bal = __ballot(verdict);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int s = 0; s < SMALL_SIGS; s++) bits |= (uint32_t)((bal >> (4 * s)) & 1u) << s;
+  if (ln == 0) verdict16[blockIdx.x] = (uint16_t)bits;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -969,6 +1043,15 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   if (comb && w.comb_lanes == 2 && w.comb.a.npos + w.comb.b.npos > 2 * COMB2_MAX_STEPS) return hipErrorInvalidValue;
   const dim3 grid(grid_for(b.n)), block(CBFT_VERIFY_BLOCK);
   hipError_t e;
+  if (comb && w.small) {  // the per-request path: hash + quad comb + finish in one launch, unordered
+    if (w.comb.nper > COMB_MAX_STEPS) return hipErrorInvalidValue;
+    if (ev)
+      for (int k = 0; k < 3; k++) (void)hipEventRecord(ev[k], stream);
+    hipLaunchKernelGGL(ed25519_small_kernel, dim3((unsigned)((b.n + SMALL_SIGS - 1) / SMALL_SIGS)), dim3(64), 0, stream,
+                       b, w.base_comb, w.comb, reinterpret_cast<uint16_t*>(w.verdict_words));
+    if (ev) (void)hipEventRecord(ev[3], stream);
+    return hipGetLastError();
+  }
   if (order && order->wait && order->hash && (e = hipStreamWaitEvent(stream, order->done[0], 0)) != hipSuccess)
     return e;
   if (ev) (void)hipEventRecord(ev[0], stream);

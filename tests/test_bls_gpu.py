@@ -356,3 +356,86 @@ def test_multi_device_share_verification(ctx, devices):
             assert ok and sig == blsgen.sign_point(sk, msg)
         finally:
             g.bls_unload_keys(gk)
+
+
+def test_keyset_rotation_per_checkpoint_window(ctx):
+    """Per-checkpoint-window threshold systems (CryptoManager.hpp:62-78,116-141): get(sn) picks the
+    system of the last checkpoint <= (sn-1)/W.  Window w+1's key set is loaded while window w's
+    certificates are being verified and combined on another thread, and window w-1's is unloaded
+    once its certificates are done.  Every certificate must verify, report exactly its doubled
+    shares and combine to sk_w * H(m) under its own window's keys, and fail under the next one."""
+    import hashlib
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+
+    W, n, k, windows = 150, 64, 43, 4
+    systems = [blsgen.keyset(n, k, seed=900 + w) for w in range(windows)]
+    certs = []
+    for w, (sk, sks, pk, vks) in enumerate(systems):
+        rng = random.Random(w)
+        cw = []
+        for j in range(5):
+            sn = w * W + 1 + 30 * j
+            msg = hashlib.sha256(b"cert %d" % sn).digest()
+            sh = blsgen.shares(sks, sorted(rng.sample(range(1, n + 1), k + 4)), msg)
+            bad = set(rng.sample(range(len(sh)), 2))
+            sh = [blsgen.doubled(s) if i in bad else s for i, s in enumerate(sh)]
+            cw.append((sn, msg, sh, bad, blsgen.sign_point(sk, msg)))
+        certs.append(cw)
+
+    lock = threading.Lock()
+    loaded = {0: ctx.bls_load_keys(systems[0][2], systems[0][3])}
+    ready = [threading.Event() for _ in range(windows)]
+    started = [threading.Event() for _ in range(windows)]
+    done = [threading.Event() for _ in range(windows)]
+    ready[0].set()
+
+    def get(sn):
+        chk = (sn - 1) // W
+        with lock:
+            c = max(c for c in loaded if c <= chk)
+            return c, loaded[c]
+
+    def loader():
+        for w in range(1, windows):
+            assert started[w - 1].wait(120)  # window w-1's certificates are in flight
+            kid = ctx.bls_load_keys(systems[w][2], systems[w][3])
+            assert all(ctx.bls_key_status(kid, n))
+            with lock:
+                loaded[w] = kid
+            ready[w].set()
+            if w >= 2:
+                assert done[w - 2].wait(120)
+                with lock:
+                    old = loaded.pop(w - 2)
+                ctx.bls_unload_keys(old)
+
+    def certify(w):
+        assert ready[w].wait(120)
+        for j, (sn, msg, sh, bad, want) in enumerate(certs[w]):
+            c, kid = get(sn)
+            assert c == w
+            valid = ctx.bls_verify_shares(kid, msg, sh)
+            assert valid.tolist() == [i not in bad for i in range(len(sh))]
+            sig, ok, badmask = ctx.bls_combine_threshold(kid, msg, sh, optimistic=j % 2 == 0)
+            assert ok and sig == want and set(np.flatnonzero(badmask).tolist()) == bad
+            assert ctx.bls_verify(kid, msg, sig)
+            started[w].set()
+        if w + 1 < windows:  # the next window's keys reject this window's shares and signature
+            assert ready[w + 1].wait(120)
+            with lock:
+                nxt = loaded[w + 1]
+            sn, msg, sh, bad, want = certs[w][0]
+            assert not ctx.bls_verify_shares(nxt, msg, sh).any()
+            assert not ctx.bls_verify(nxt, msg, want)
+        done[w].set()
+
+    try:
+        with ThreadPoolExecutor(max_workers=windows + 1) as ex:
+            futs = [ex.submit(loader)] + [ex.submit(certify, w) for w in range(windows)]
+            for f in futs:
+                f.result(timeout=300)
+        assert sorted(loaded) == [windows - 2, windows - 1]
+    finally:
+        for kid in loaded.values():
+            ctx.bls_unload_keys(kid)

@@ -343,3 +343,32 @@ def test_config3_full_shape(ctx):
         ctx.unload_keys(tid)
     assert np.array_equal(got, ss.expected)
     assert 0.05 < (~ss.expected).mean() < 0.15
+
+
+@pytest.mark.parametrize("chunk", [1, 15, 16, 17, 64, 65, 300, 1024])
+def test_golden_small_batches_fused_kernel(ctx, golden, chunk):
+    """Key-table batches up to 1,024 signatures run as ONE fused launch (ed25519_small_kernel:
+    hash + quad comb + finish, 16 signatures per wave, 16-bit verdict words): the golden set in
+    batches of `chunk` gives the golden verdicts, equal to the three-kernel path
+    ($CBFT_SMALL_MAX=0) batch for batch, including partial words and tail quads."""
+    keys = sorted({v.pk for v in golden})
+    index = {k: i for i, k in enumerate(keys)}
+    exp = np.array([bool(v.verdict) for v in golden])
+    os.environ["CBFT_SMALL_MAX"] = "0"
+    try:
+        three = cb.Context(device=0)
+    finally:
+        del os.environ["CBFT_SMALL_MAX"]
+    tid, tid3 = ctx.load_keys(keys), three.load_keys(keys)
+    try:
+        for lo in range(0, len(golden), chunk):
+            part = golden[lo:lo + chunk]
+            args = ([index[v.pk] for v in part], [v.sig for v in part], [v.msg for v in part])
+            got = _bools(ctx.verify(tid, *args), len(part))
+            ref = _bools(three.verify(tid3, *args), len(part))
+            assert np.array_equal(got, exp[lo:lo + chunk]), f"fused kernel, batch at {lo}"
+            assert np.array_equal(ref, got), f"three-kernel path disagrees at {lo}"
+    finally:
+        ctx.unload_keys(tid)
+        three.unload_keys(tid3)
+        three.close()
