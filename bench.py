@@ -162,7 +162,9 @@ def main():
     # parity first: every golden verdict class (Ed25519 edge cases through both key modes, the
     # RELIC key fixture, RSA accepts and rejects); any mismatch exits non-zero before timing
     parity = parity_gate.run(ctx, rsa=args.extras, relic=args.extras)
+    t_keys = time.perf_counter()
     tid = ctx.load_keys(ss.pk, radix=args.comb_radix)  # key tables resident, like SigManager's verifiers
+    key_load_ms = (time.perf_counter() - t_keys) * 1e3
 
     # the batch as a caller builds it: in one pinned host block (cbft_host_alloc) laid out as
     # cbft_ed25519_batch_layout says, so each step's host -> device transfer is one DMA
@@ -428,6 +430,9 @@ def main():
             "p50_latency_ms_batch1k": lat,
             "p50_latency_ms_batch1k_python_lists": lat_py,
             "device_resident_value": dev_value,
+            "key_table_load_ms": key_load_ms,
+            "key_table_load_basis": f"one cbft_ed25519_load_keys of {args.nkeys} client keys before timing: decode, "
+                                    "per-key position points, radix comb tables (HBM-resident, reused by every step)",
             "pageable_host_value": pageable,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
             "mixed_config3": mixed,

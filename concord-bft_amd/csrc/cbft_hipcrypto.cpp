@@ -32,7 +32,7 @@ int cbft_fail(hipError_t e, const char* what, const char* file, int line) {
 }
 
 // table-build lanes per launch (bounds the projective staging buffer: 18 KB per lane)
-static const size_t kCombBuildLanes = 131072;
+static const size_t kCombBuildLanes = 262144;  // 4 waves per SIMD; 4.7 GB of staging
 
 // comb radix of a key table: explicit (8..13), else $CBFT_COMB_RADIX, else the widest radix
 // whose tables for nkeys keys fit the per-table budget ($CBFT_COMB_BUDGET_GB, default 64 GB of
@@ -53,18 +53,22 @@ static int key_radix(int requested, uint32_t nkeys) {
 }
 
 // Build comb tables for nunits encoded points (d_pk, 32 B each) into d_tbl, in launches of at
-// most kCombBuildLanes lanes (B's radix-2^22 table alone is 196,608 lanes); synchronous.
+// most kCombBuildLanes lanes (B's radix-2^22 table is 196,608 lanes, 4,096 radix-2^13 keys
+// 2.6 M); synchronous.
 static hipError_t build_comb(const uint8_t* d_pk, size_t nunits, int negate, const CombGeom& g, uint32_t* d_tbl,
                              uint8_t* d_aok, hipStream_t s) {
   const size_t lanes = nunits * (size_t)g.npos * g.chunks();
   const size_t step = std::min(lanes, kCombBuildLanes);
-  DevBuf tmp;
+  DevBuf tmp, pos;
   hipError_t e = tmp.reserve(cbft_ed25519_comb_tmp_words(step) * sizeof(uint32_t));
+  if (e == hipSuccess) e = pos.reserve(cbft_ed25519_comb_pos_words(nunits, g) * sizeof(uint32_t));
+  if (e == hipSuccess) e = cbft_ed25519_launch_comb_pos(d_pk, nunits, negate, g, pos.as<uint32_t>(), d_aok, s);
   for (size_t l0 = 0; e == hipSuccess && l0 < lanes; l0 += step)
-    e = cbft_ed25519_launch_comb_tables(d_pk, nunits, negate, g, d_tbl, tmp.as<uint32_t>(), d_aok, l0,
+    e = cbft_ed25519_launch_comb_tables(pos.as<uint32_t>(), nunits, g, d_tbl, tmp.as<uint32_t>(), l0,
                                         std::min(step, lanes - l0), s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   tmp.release();
+  pos.release();
   return e;
 }
 

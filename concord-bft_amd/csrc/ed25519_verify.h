@@ -129,12 +129,16 @@ struct Ed25519Work {
 size_t cbft_ed25519_table_words_per_unit();
 // staging words for `lanes` table-build lanes (18 KB each)
 size_t cbft_ed25519_comb_tmp_words(size_t lanes);
-// Comb tables of nunits encoded points (32 B each at d_pk): build lanes [lane0, lane0 + nlanes) of
-// the nunits * npos * chunks() lanes (lane = (unit, position, chunk of 128 multiples)); d_tmp holds
+// Comb tables of nunits encoded points (32 B each at d_pk), in two steps: the position points
+// 2^(w j) (+-P) of every unit into d_pos (cbft_ed25519_comb_pos_words words; decode verdicts to
+// d_aok when non-null), then build lanes [lane0, lane0 + nlanes) of the nunits * npos * chunks()
+// lanes (lane = (unit, position, chunk of 128 multiples)); d_tmp holds
 // cbft_ed25519_comb_tmp_words(nlanes) words.
-hipError_t cbft_ed25519_launch_comb_tables(const uint8_t* d_pk, size_t nunits, int negate, const CombGeom& g,
-                                           uint32_t* d_tbl, uint32_t* d_tmp, uint8_t* d_aok, size_t lane0,
-                                           size_t nlanes, hipStream_t stream);
+size_t cbft_ed25519_comb_pos_words(size_t nunits, const CombGeom& g);
+hipError_t cbft_ed25519_launch_comb_pos(const uint8_t* d_pk, size_t nunits, int negate, const CombGeom& g,
+                                        uint32_t* d_pos, uint8_t* d_aok, hipStream_t stream);
+hipError_t cbft_ed25519_launch_comb_tables(const uint32_t* d_pos, size_t nunits, const CombGeom& g, uint32_t* d_tbl,
+                                           uint32_t* d_tmp, size_t lane0, size_t nlanes, hipStream_t stream);
 size_t cbft_ed25519_base_table_words();
 hipError_t cbft_ed25519_build_base_table(uint32_t* d_tbl, hipStream_t stream);
 hipError_t cbft_ed25519_launch_prep(const uint8_t* d_pk, size_t nunits, uint32_t* d_tbl, uint8_t* d_aok,

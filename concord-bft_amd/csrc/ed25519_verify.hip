@@ -490,12 +490,51 @@ __global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519B
 #define COMB_TABLE_BLOCK 64
 #define COMB_MAX_STEPS 12  // additions per lane (nper) the ladder supports
 
-// One lane per (unit, position j, chunk c): P_j = 2^(w j) P (w j doublings), then the multiples
-// 128c+1 .. 128c+128 of P_j projectively into tmp, Montgomery batch inversion, affine niels into
+// One lane per unit: decode (aok), negate, then P_j = 2^(w j) P for every position j along ONE
+// doubling chain (w (npos - 1) doublings), each stored in the cached form (YpX | YmX | Z | T2d)
+// to pos[unit][j].  The table lanes of a position then start from P_j instead of each redoing
+// its w j doublings (32 chunk lanes per position shared the same chain: ~30 % of the build).
+__global__ void __launch_bounds__(COMB_TABLE_BLOCK) ed25519_comb_pos_kernel(const uint8_t* pk, size_t nunits,
+                                                                           int negate, CombGeom geo, uint32_t* pos,
+                                                                           uint8_t* aok) {
+  const size_t u = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= nunits) return;
+  uint32_t Aw[8];
+  load_words8(Aw, pk + u * 32);
+  ge_p3 P;
+  const bool ok = ge_frombytes(P, Aw);
+  if (aok) aok[u] = ok ? 1 : 0;
+  if (negate) {
+    fe_neg(P.X, P.X);
+    fe_neg(P.T, P.T);
+  }
+  uint32_t* o = pos + u * (size_t)geo.npos * CACHED_WORDS;
+#pragma nounroll
+  for (int j = 0; j < geo.npos; j++) {
+    if (j > 0) {
+#pragma nounroll
+      for (int d = 0; d < geo.w; d++) {
+        ge_p1p1 r;
+        ge_dbl(r, P.X, P.Y, P.Z);
+        ge_p1p1_to_p3(P, r);
+      }
+    }
+    ge_cached cj;
+    ge_p3_to_cached(cj, P);
+    uint32_t* e = o + (size_t)j * CACHED_WORDS;
+    fe_store(e, cj.YpX);
+    fe_store(e + 9, cj.YmX);
+    fe_store(e + 18, cj.Z);
+    fe_store(e + 27, cj.T2d);
+  }
+}
+
+// One lane per (unit, position j, chunk c): the multiples 128c+1 .. 128c+128 of P_j (from
+// ed25519_comb_pos_kernel) projectively into tmp, Montgomery batch inversion, affine niels into
 // tbl[unit][j][128c+1 .. 128c+128]; the c = 0 lane also writes the identity entry 0.
-__global__ void __launch_bounds__(COMB_TABLE_BLOCK) ed25519_comb_table_kernel(const uint8_t* pk, size_t nunits,
-                                                                             int negate, CombGeom geo, uint32_t* tbl,
-                                                                             uint32_t* tmp, uint8_t* aok, size_t lane0,
+__global__ void __launch_bounds__(COMB_TABLE_BLOCK) ed25519_comb_table_kernel(const uint32_t* pos, size_t nunits,
+                                                                             CombGeom geo, uint32_t* tbl,
+                                                                             uint32_t* tmp, size_t lane0,
                                                                              size_t nlanes) {
   const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // lane of this launch (tmp slot)
   if (gl >= nlanes) return;
@@ -505,23 +544,14 @@ __global__ void __launch_bounds__(COMB_TABLE_BLOCK) ed25519_comb_table_kernel(co
   const int j = (int)((g / chunks) % geo.npos);
   const int c = (int)(g % chunks);
   if (u >= nunits) return;
-  uint32_t Aw[8];
-  load_words8(Aw, pk + u * 32);
-  ge_p3 Pj;
-  const bool ok = ge_frombytes(Pj, Aw);
-  if (aok && j == 0 && c == 0) aok[u] = ok ? 1 : 0;
-  if (negate) {
-    fe_neg(Pj.X, Pj.X);
-    fe_neg(Pj.T, Pj.T);
-  }
-#pragma nounroll
-  for (int d = 0; d < geo.w * j; d++) {
-    ge_p1p1 r;
-    ge_dbl(r, Pj.X, Pj.Y, Pj.Z);
-    ge_p1p1_to_p3(Pj, r);
-  }
   ge_cached cj;
-  ge_p3_to_cached(cj, Pj);
+  {
+    const uint32_t* e = pos + (u * (size_t)geo.npos + j) * CACHED_WORDS;
+    fe_load(cj.YpX, e);
+    fe_load(cj.YmX, e + 9);
+    fe_load(cj.Z, e + 18);
+    fe_load(cj.T2d, e + 27);
+  }
   // Q = (128c + 1) P_j, MSB first over the w - 1 bits a multiple index can have
   ge_p3 Q;
   ge_p3_0(Q);
@@ -1006,14 +1036,26 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
 // ---------------------------------------------------------------------------------------
 size_t cbft_ed25519_comb_tmp_words(size_t lanes) { return lanes * COMB_TMP_WORDS_PER_LANE; }
 
-hipError_t cbft_ed25519_launch_comb_tables(const uint8_t* d_pk, size_t nunits, int negate, const CombGeom& g,
-                                           uint32_t* d_tbl, uint32_t* d_tmp, uint8_t* d_aok, size_t lane0,
-                                           size_t nlanes, hipStream_t stream) {
+size_t cbft_ed25519_comb_pos_words(size_t nunits, const CombGeom& g) {
+  return nunits * (size_t)g.npos * CACHED_WORDS;
+}
+
+hipError_t cbft_ed25519_launch_comb_pos(const uint8_t* d_pk, size_t nunits, int negate, const CombGeom& g,
+                                        uint32_t* d_pos, uint8_t* d_aok, hipStream_t stream) {
+  if (nunits == 0) return hipSuccess;
+  if (g.w < 8 || g.w > CBFT_COMB_MAX_RADIX || g.npos < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ed25519_comb_pos_kernel, dim3((unsigned)((nunits + COMB_TABLE_BLOCK - 1) / COMB_TABLE_BLOCK)),
+                     dim3(COMB_TABLE_BLOCK), 0, stream, d_pk, nunits, negate, g, d_pos, d_aok);
+  return hipGetLastError();
+}
+
+hipError_t cbft_ed25519_launch_comb_tables(const uint32_t* d_pos, size_t nunits, const CombGeom& g, uint32_t* d_tbl,
+                                           uint32_t* d_tmp, size_t lane0, size_t nlanes, hipStream_t stream) {
   if (nunits == 0 || nlanes == 0) return hipSuccess;
   if (g.w < 8 || g.w > CBFT_COMB_MAX_RADIX || g.npos < 1) return hipErrorInvalidValue;
   if (lane0 + nlanes > nunits * g.npos * g.chunks()) return hipErrorInvalidValue;
   hipLaunchKernelGGL(ed25519_comb_table_kernel, dim3((unsigned)((nlanes + COMB_TABLE_BLOCK - 1) / COMB_TABLE_BLOCK)),
-                     dim3(COMB_TABLE_BLOCK), 0, stream, d_pk, nunits, negate, g, d_tbl, d_tmp, d_aok, lane0, nlanes);
+                     dim3(COMB_TABLE_BLOCK), 0, stream, d_pos, nunits, g, d_tbl, d_tmp, lane0, nlanes);
   return hipGetLastError();
 }
 size_t cbft_ed25519_table_words_per_unit() { return (size_t)Shape::TA * CACHED_WORDS; }

@@ -152,7 +152,7 @@ static int engineRadix() {
 // condition variable (woken for its verdict or to lead), never on a shared one.
 class Ed25519Engine {
  public:
-  static constexpr int kMaxInflight = 2;
+  static constexpr int kMaxInflight = 3;  // profiles/r03_host_bench_inflight*.json: 3 > 2, 4 at 64 threads
   static constexpr size_t kMaxBatch = 65536;
 
   static std::shared_ptr<Ed25519Engine> get() {
