@@ -45,22 +45,6 @@ static BlsKeySet* find_set(cbft_ctx* c, uint32_t id) {
   return it == c->bls_sets.end() ? nullptr : &it->second;
 }
 
-// Run f(kid index) for every device of a multi-GPU context, one host thread per device (each
-// device's calls take its own context mutex, so the devices work concurrently); the first
-// failure's code is returned.
-template <class F>
-static int for_each_kid(cbft_ctx* c, F f) {
-  const size_t G = c->kids.size();
-  std::vector<int> rc(G, CBFT_OK);
-  std::vector<std::thread> th;
-  th.reserve(G);
-  for (size_t g = 0; g < G; g++) th.emplace_back([&, g] { rc[g] = f(g); });
-  for (auto& t : th) t.join();
-  for (int r : rc)
-    if (r) return r;
-  return CBFT_OK;
-}
-
 extern "C" {
 
 int cbft_bls_load_keys(cbft_ctx* c, const uint8_t* pk65, const uint8_t* vks65, uint32_t n, uint32_t* out_id) {

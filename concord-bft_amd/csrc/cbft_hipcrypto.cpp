@@ -64,7 +64,7 @@ static hipError_t build_comb(const uint8_t* d_pk, size_t nunits, int negate, con
   if (e == hipSuccess) e = pos.reserve(cbft_ed25519_comb_pos_words(nunits, g) * sizeof(uint32_t));
   if (e == hipSuccess) e = cbft_ed25519_launch_comb_pos(d_pk, nunits, negate, g, pos.as<uint32_t>(), d_aok, s);
   for (size_t l0 = 0; e == hipSuccess && l0 < lanes; l0 += step)
-    e = cbft_ed25519_launch_comb_tables(pos.as<uint32_t>(), nunits, g, d_tbl, tmp.as<uint32_t>(), l0,
+    e = cbft_ed25519_launch_comb_tables(pos.as<uint32_t>(), nunits, g, d_tbl, nullptr, 0, tmp.as<uint32_t>(), l0,
                                         std::min(step, lanes - l0), s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   tmp.release();
@@ -373,16 +373,15 @@ int cbft_sync(cbft_ctx* c) {
 int cbft_ed25519_load_keys_ex(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, int comb_radix, uint32_t* out_id) {
   if (!c || !out_id || (nkeys && !pk)) return CBFT_EINVAL;
   if (comb_radix && (comb_radix < 8 || comb_radix > 13)) return CBFT_EINVAL;
-  if (!c->kids.empty()) {  // replicate the table on every device (the children's ids stay in step)
-    uint32_t id0 = 0;
-    for (size_t k = 0; k < c->kids.size(); k++) {
-      uint32_t id = 0;
-      const int rc = cbft_ed25519_load_keys_ex(c->kids[k], pk, nkeys, comb_radix, &id);
-      if (rc) return rc;
-      if (k == 0) id0 = id;
-      if (id != id0) return CBFT_EIO;
-    }
-    *out_id = id0;
+  if (!c->kids.empty()) {  // replicate the table on every device, concurrently (ids stay in step)
+    std::vector<uint32_t> ids(c->kids.size(), 0);
+    const int rc = for_each_kid(c, [&](size_t g) {
+      return cbft_ed25519_load_keys_ex(c->kids[g], pk, nkeys, comb_radix, &ids[g]);
+    });
+    if (rc) return rc;
+    for (uint32_t id : ids)
+      if (id != ids[0]) return CBFT_EIO;
+    *out_id = ids[0];
     return CBFT_OK;
   }
   CBFT_HIP(hipSetDevice(c->device));
@@ -426,8 +425,11 @@ static double comb_budget_bytes() {
 }
 
 // Write keys [k0, k0 + n) of a table (their raw encodings from pk, host or device memory): new
-// chunks as needed (their pointers appended to the device chunk array), the keys copied into
-// their chunk slots and their comb tables built, all on the build stream; synchronous.
+// chunks as needed (their pointers appended to the device chunk array), then on the build stream
+// one staging copy of the n keys, ONE position-point launch for all of them (decode verdicts,
+// 2^(w j) (-A)), the raw keys and verdicts into their chunk slots, and the table lanes in
+// launches that span chunks (through the device chunk-pointer array); one synchronisation at
+// the end, staging allocated once per call.
 static int fill_keys(cbft_ctx* c, KeyTable& kt, const uint8_t* pk, hipMemcpyKind kind, uint32_t k0, uint32_t n) {
   const size_t wpk = kt.geo.words_per_unit();
   hipStream_t s = c->build_stream;
@@ -440,18 +442,36 @@ static int fill_keys(cbft_ctx* c, KeyTable& kt, const uint8_t* pk, hipMemcpyKind
                             hipMemcpyHostToDevice, s));
     CBFT_HIP(hipStreamSynchronize(s));  // the source is a host variable
   }
-  for (uint32_t a = k0; a < k0 + n;) {
+  if (n == 0) return CBFT_OK;
+  const size_t lanes = (size_t)n * kt.geo.npos * kt.geo.chunks();
+  const size_t step = std::min(lanes, kCombBuildLanes);
+  DevBuf raw, pos, aok, tmp;
+  hipError_t e = raw.reserve((size_t)n * 32);
+  if (e == hipSuccess) e = pos.reserve(cbft_ed25519_comb_pos_words(n, kt.geo) * sizeof(uint32_t));
+  if (e == hipSuccess) e = aok.reserve(n);
+  if (e == hipSuccess) e = tmp.reserve(cbft_ed25519_comb_tmp_words(step) * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemcpyAsync(raw.p, pk, (size_t)n * 32, kind, s);
+  if (e == hipSuccess)
+    e = cbft_ed25519_launch_comb_pos(raw.as<uint8_t>(), n, 1, kt.geo, pos.as<uint32_t>(), aok.as<uint8_t>(), s);
+  for (uint32_t a = k0; e == hipSuccess && a < k0 + n;) {  // raw keys and verdicts into the chunk slots
     const uint32_t ci = a >> CBFT_KEY_CHUNK_SHIFT, slot = a & (CBFT_KEY_CHUNK - 1);
     const uint32_t m = std::min<uint32_t>(k0 + n - a, CBFT_KEY_CHUNK - slot);
     uint8_t* base = kt.chunks[ci].as<uint8_t>();
     uint8_t* dpk = base + (size_t)CBFT_KEY_CHUNK * wpk * 4 + (size_t)slot * 32;
     uint8_t* daok = base + (size_t)CBFT_KEY_CHUNK * (wpk * 4 + 32) + slot;
-    uint32_t* dcomb = reinterpret_cast<uint32_t*>(base) + (size_t)slot * wpk;
-    hipError_t e = hipMemcpyAsync(dpk, pk + (size_t)(a - k0) * 32, (size_t)m * 32, kind, s);
-    if (e == hipSuccess) e = build_comb(dpk, m, 1, kt.geo, dcomb, daok, s);
-    if (e != hipSuccess) return cbft_fail(e, "comb table build", __FILE__, __LINE__);
+    e = hipMemcpyAsync(dpk, raw.as<uint8_t>() + (size_t)(a - k0) * 32, (size_t)m * 32, hipMemcpyDeviceToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(daok, aok.as<uint8_t>() + (a - k0), m, hipMemcpyDeviceToDevice, s);
     a += m;
   }
+  for (size_t l0 = 0; e == hipSuccess && l0 < lanes; l0 += step)  // table lanes across chunks
+    e = cbft_ed25519_launch_comb_tables(pos.as<uint32_t>(), n, kt.geo, nullptr, kt.chunk_ptrs.as<void*>(), k0,
+                                        tmp.as<uint32_t>(), l0, std::min(step, lanes - l0), s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  raw.release();
+  pos.release();
+  aok.release();
+  tmp.release();
+  if (e != hipSuccess) return cbft_fail(e, "comb table build", __FILE__, __LINE__);
   return CBFT_OK;
 }
 
@@ -469,14 +489,15 @@ static const uint8_t* chunk_raw_keys(const KeyTable& kt, uint32_t ci) {
 // 8 the append fails with CBFT_ENOMEM and the table is unchanged.
 int cbft_ed25519_append_keys(cbft_ctx* c, uint32_t id, const uint8_t* pk, uint32_t nkeys, uint32_t* out_first) {
   if (!c || !out_first || (nkeys && !pk)) return CBFT_EINVAL;
-  if (!c->kids.empty()) {
-    for (size_t k = 0; k < c->kids.size(); k++) {
-      uint32_t first = 0;
-      const int rc = cbft_ed25519_append_keys(c->kids[k], id, pk, nkeys, &first);
-      if (rc) return rc;
-      if (k == 0) *out_first = first;
-      if (first != *out_first) return CBFT_EIO;
-    }
+  if (!c->kids.empty()) {  // every device concurrently
+    std::vector<uint32_t> firsts(c->kids.size(), 0);
+    const int rc = for_each_kid(c, [&](size_t g) {
+      return cbft_ed25519_append_keys(c->kids[g], id, pk, nkeys, &firsts[g]);
+    });
+    if (rc) return rc;
+    for (uint32_t f : firsts)
+      if (f != firsts[0]) return CBFT_EIO;
+    *out_first = firsts[0];
     return CBFT_OK;
   }
   std::shared_ptr<KeyTable> kt;

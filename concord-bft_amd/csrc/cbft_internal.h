@@ -8,6 +8,7 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -204,3 +205,19 @@ cbft_ctx* cbft_dev0(cbft_ctx* c);
     hipError_t _e = (expr);                                                     \
     if (_e != hipSuccess) return cbft_fail(_e, #expr, __FILE__, __LINE__);      \
   } while (0)
+
+// Run f(kid index) for every device of a multi-GPU context, one host thread per device (each
+// device's calls take its own context mutex, so the devices work concurrently); the first
+// failure's code is returned.
+template <class F>
+static int for_each_kid(cbft_ctx* c, F f) {
+  const size_t G = c->kids.size();
+  std::vector<int> rc(G, CBFT_OK);
+  std::vector<std::thread> th;
+  th.reserve(G);
+  for (size_t g = 0; g < G; g++) th.emplace_back([&, g] { rc[g] = f(g); });
+  for (auto& t : th) t.join();
+  for (int r : rc)
+    if (r) return r;
+  return CBFT_OK;
+}

@@ -132,13 +132,15 @@ size_t cbft_ed25519_comb_tmp_words(size_t lanes);
 // Comb tables of nunits encoded points (32 B each at d_pk), in two steps: the position points
 // 2^(w j) (+-P) of every unit into d_pos (cbft_ed25519_comb_pos_words words; decode verdicts to
 // d_aok when non-null), then build lanes [lane0, lane0 + nlanes) of the nunits * npos * chunks()
-// lanes (lane = (unit, position, chunk of 128 multiples)); d_tmp holds
-// cbft_ed25519_comb_tmp_words(nlanes) words.
+// lanes (lane = (unit, position, chunk of 128 multiples)) into d_tbl (units contiguous) or, with
+// d_tbl null, into keys a0 .. a0 + nunits - 1 of the chunked key table whose device chunk-pointer
+// array is d_chunks; d_tmp holds cbft_ed25519_comb_tmp_words(nlanes) words.
 size_t cbft_ed25519_comb_pos_words(size_t nunits, const CombGeom& g);
 hipError_t cbft_ed25519_launch_comb_pos(const uint8_t* d_pk, size_t nunits, int negate, const CombGeom& g,
                                         uint32_t* d_pos, uint8_t* d_aok, hipStream_t stream);
 hipError_t cbft_ed25519_launch_comb_tables(const uint32_t* d_pos, size_t nunits, const CombGeom& g, uint32_t* d_tbl,
-                                           uint32_t* d_tmp, size_t lane0, size_t nlanes, hipStream_t stream);
+                                           void* const* d_chunks, uint32_t a0, uint32_t* d_tmp, size_t lane0,
+                                           size_t nlanes, hipStream_t stream);
 size_t cbft_ed25519_base_table_words();
 hipError_t cbft_ed25519_build_base_table(uint32_t* d_tbl, hipStream_t stream);
 hipError_t cbft_ed25519_launch_prep(const uint8_t* d_pk, size_t nunits, uint32_t* d_tbl, uint8_t* d_aok,

@@ -490,10 +490,26 @@ __global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519B
 #define COMB_TABLE_BLOCK 64
 #define COMB_MAX_STEPS 12  // additions per lane (nper) the ladder supports
 
-// One lane per unit: decode (aok), negate, then P_j = 2^(w j) P for every position j along ONE
-// doubling chain (w (npos - 1) doublings), each stored in the cached form (YpX | YmX | Z | T2d)
-// to pos[unit][j].  The table lanes of a position then start from P_j instead of each redoing
-// its w j doublings (32 chunk lanes per position shared the same chain: ~30 % of the build).
+// One lane per unit: decode (aok), negate, then along ONE doubling chain P_j = 2^(w j) P and
+// S_j = 2^(w - 8) P_j (the stride of a build lane's multiples, on the way to P_(j+1)) for every
+// position j, stored in the cached form (YpX | YmX | Z | T2d) to pos[unit][j][P_j, S_j].  The
+// table lanes of a position start from these instead of each redoing its w j doublings.
+#define COMB_POS_WORDS (2 * CACHED_WORDS)
+__device__ __forceinline__ void cached_store(uint32_t* e, const ge_p3& P) {
+  ge_cached cj;
+  ge_p3_to_cached(cj, P);
+  fe_store(e, cj.YpX);
+  fe_store(e + 9, cj.YmX);
+  fe_store(e + 18, cj.Z);
+  fe_store(e + 27, cj.T2d);
+}
+__device__ __forceinline__ void cached_load(ge_cached& cj, const uint32_t* e) {
+  fe_load(cj.YpX, e);
+  fe_load(cj.YmX, e + 9);
+  fe_load(cj.Z, e + 18);
+  fe_load(cj.T2d, e + 27);
+}
+
 __global__ void __launch_bounds__(COMB_TABLE_BLOCK) ed25519_comb_pos_kernel(const uint8_t* pk, size_t nunits,
                                                                            int negate, CombGeom geo, uint32_t* pos,
                                                                            uint8_t* aok) {
@@ -508,118 +524,143 @@ __global__ void __launch_bounds__(COMB_TABLE_BLOCK) ed25519_comb_pos_kernel(cons
     fe_neg(P.X, P.X);
     fe_neg(P.T, P.T);
   }
-  uint32_t* o = pos + u * (size_t)geo.npos * CACHED_WORDS;
+  const int cb = geo.w - 8;  // build lanes per position = 2^cb
+  uint32_t* o = pos + u * (size_t)geo.npos * COMB_POS_WORDS;
 #pragma nounroll
   for (int j = 0; j < geo.npos; j++) {
-    if (j > 0) {
+    uint32_t* e = o + (size_t)j * COMB_POS_WORDS;
+    cached_store(e, P);
 #pragma nounroll
-      for (int d = 0; d < geo.w; d++) {
-        ge_p1p1 r;
-        ge_dbl(r, P.X, P.Y, P.Z);
-        ge_p1p1_to_p3(P, r);
-      }
+    for (int d = 0; d < geo.w; d++) {
+      if (d == cb) cached_store(e + CACHED_WORDS, P);
+      if (j + 1 == geo.npos && d == cb) break;
+      ge_p1p1 r;
+      ge_dbl(r, P.X, P.Y, P.Z);
+      ge_p1p1_to_p3(P, r);
     }
-    ge_cached cj;
-    ge_p3_to_cached(cj, P);
-    uint32_t* e = o + (size_t)j * CACHED_WORDS;
-    fe_store(e, cj.YpX);
-    fe_store(e + 9, cj.YmX);
-    fe_store(e + 18, cj.Z);
-    fe_store(e + 27, cj.T2d);
   }
 }
 
-// One lane per (unit, position j, chunk c): the multiples 128c+1 .. 128c+128 of P_j (from
-// ed25519_comb_pos_kernel) projectively into tmp, Montgomery batch inversion, affine niels into
-// tbl[unit][j][128c+1 .. 128c+128]; the c = 0 lane also writes the identity entry 0.
+// One lane per (unit, position j, chunk c) builds the multiples e = c + 1 + 2^cb k, k = 0..127,
+// of P_j (cb = w - 8: 2^cb lanes per position, stride S_j = 2^cb P_j from
+// ed25519_comb_pos_kernel): projective points and prefix Z products into tmp (lane-interleaved,
+// so every tmp access is one contiguous 256-B wave access), Montgomery batch inversion, affine
+// niels entries (y+x | y-x | 2dxy, 128-B lines) staged through LDS and written by the whole wave
+// in 16-B pieces: the lanes of a position hold consecutive entries, so each store instruction
+// writes 1 KB runs.  The c = 0 lane also writes the identity entry 0.  Units are contiguous from
+// tbl, or (key_chunks != nullptr) keys a0 + u of a chunked key table, so one launch spans key
+// chunks.
 __global__ void __launch_bounds__(COMB_TABLE_BLOCK) ed25519_comb_table_kernel(const uint32_t* pos, size_t nunits,
                                                                              CombGeom geo, uint32_t* tbl,
+                                                                             void* const* key_chunks, uint32_t a0,
                                                                              uint32_t* tmp, size_t lane0,
                                                                              size_t nlanes) {
-  const size_t gl = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // lane of this launch (tmp slot)
-  if (gl >= nlanes) return;
+  static_assert(COMB_TABLE_BLOCK == 64, "one wave per block: the LDS staging is per wave");
+  __shared__ uint4 ent[64][COMB_STRIDE / 4];
+  __shared__ uint32_t* dst[64];
+  const int ln = threadIdx.x;
+  const size_t gl = (size_t)blockIdx.x * blockDim.x + ln;  // lane of this launch (tmp column)
   const size_t g = lane0 + gl;
-  const int chunks = geo.chunks();
+  const int cb = geo.w - 8;
+  const int chunks = 1 << cb;
   const size_t u = g / ((size_t)geo.npos * chunks);
   const int j = (int)((g / chunks) % geo.npos);
   const int c = (int)(g % chunks);
-  if (u >= nunits) return;
-  ge_cached cj;
-  {
-    const uint32_t* e = pos + (u * (size_t)geo.npos + j) * CACHED_WORDS;
-    fe_load(cj.YpX, e);
-    fe_load(cj.YmX, e + 9);
-    fe_load(cj.Z, e + 18);
-    fe_load(cj.T2d, e + 27);
-  }
-  // Q = (128c + 1) P_j, MSB first over the w - 1 bits a multiple index can have
-  ge_p3 Q;
-  ge_p3_0(Q);
-  const uint32_t k0 = (uint32_t)c * COMB_CHUNK + 1u;
-#pragma nounroll
-  for (int bit = geo.w - 2; bit >= 0; bit--) {
-    ge_p1p1 r;
-    ge_dbl(r, Q.X, Q.Y, Q.Z);
-    ge_p1p1_to_p3(Q, r);
-    if ((k0 >> bit) & 1u) {
-      ge_add(r, Q, cj, false);
-      ge_p1p1_to_p3(Q, r);
-    }
-  }
-  uint32_t* t = tmp + gl * (size_t)COMB_TMP_WORDS_PER_LANE;
-  uint32_t* out = tbl + (u * geo.npos + j) * (size_t)geo.entries() * COMB_STRIDE;
-  fe acc;
-  fe_1(acc);
-#pragma nounroll
-  for (int k = 1; k <= COMB_CHUNK; k++) {
-    uint32_t* e = t + (size_t)(k - 1) * CACHED_WORDS;
-    fe_store(e, Q.X);
-    fe_store(e + 9, Q.Y);
-    fe_store(e + 18, Q.Z);
-    fe_mul(acc, acc, Q.Z);
-    fe_store(e + 27, acc);  // prefix product Z_1 .. Z_k
-    if (k < COMB_CHUNK) {
-      ge_p1p1 r;
-      ge_add(r, Q, cj, false);
-      ge_p1p1_to_p3(Q, r);
-    }
-  }
+  const bool live = gl < nlanes && u < nunits;
+  const size_t nl = nlanes;  // tmp row stride
+  const size_t estride = (size_t)chunks * COMB_STRIDE;  // words between a lane's consecutive entries
   fe inv;
-  fe_invert(inv, acc);
+  if (live) {
+    const size_t wpk = geo.words_per_unit();
+    uint32_t* unit_tbl = tbl + u * wpk;
+    if (key_chunks) {
+      const uint32_t ka = a0 + (uint32_t)u;
+      unit_tbl = static_cast<uint32_t*>(key_chunks[ka >> CBFT_KEY_CHUNK_SHIFT]) + (size_t)(ka & (CBFT_KEY_CHUNK - 1)) * wpk;
+    }
+    uint32_t* out = unit_tbl + (size_t)j * geo.entries() * COMB_STRIDE;
+    dst[ln] = out + (size_t)(c + 1) * COMB_STRIDE;
+    if (c == 0) {
+#pragma unroll
+      for (int w = 0; w < COMB_STRIDE; w++) out[w] = (w == 0 || w == 9) ? 1u : 0u;  // identity (1, 1, 0)
+    }
+    ge_cached cj, cs;
+    const uint32_t* pe = pos + (u * (size_t)geo.npos + j) * COMB_POS_WORDS;
+    cached_load(cj, pe);
+    cached_load(cs, pe + CACHED_WORDS);
+    // Q = (c + 1) P_j, MSB first over the cb + 1 bits c + 1 can have
+    ge_p3 Q;
+    ge_p3_0(Q);
+    const uint32_t k0 = (uint32_t)c + 1u;
+#pragma nounroll
+    for (int bit = cb; bit >= 0; bit--) {
+      ge_p1p1 r;
+      ge_dbl(r, Q.X, Q.Y, Q.Z);
+      ge_p1p1_to_p3(Q, r);
+      if ((k0 >> bit) & 1u) {
+        ge_add(r, Q, cj, false);
+        ge_p1p1_to_p3(Q, r);
+      }
+    }
+    fe acc;
+    fe_1(acc);
+#pragma nounroll
+    for (int k = 0; k < COMB_CHUNK; k++) {
+      uint32_t* e = tmp + (size_t)k * CACHED_WORDS * nl;
+      fe_store_soa(e, nl, gl, Q.X);
+      fe_store_soa(e + 9 * nl, nl, gl, Q.Y);
+      fe_store_soa(e + 18 * nl, nl, gl, Q.Z);
+      fe_mul(acc, acc, Q.Z);
+      fe_store_soa(e + 27 * nl, nl, gl, acc);  // prefix product Z_0 .. Z_k
+      if (k + 1 < COMB_CHUNK) {
+        ge_p1p1 r;
+        ge_add(r, Q, cs, false);
+        ge_p1p1_to_p3(Q, r);
+      }
+    }
+    fe_invert(inv, acc);
+  } else {
+    dst[ln] = nullptr;
+  }
   fe d2;
   fe_load_const(d2, kFeD2);
 #pragma nounroll
-  for (int k = COMB_CHUNK; k >= 1; k--) {
-    uint32_t* e = t + (size_t)(k - 1) * CACHED_WORDS;
-    fe zi, x, y, z, xy, ypx, ymx, t2d;
-    if (k > 1) {
-      fe pre;
-      fe_load(pre, e - CACHED_WORDS + 27);
-      fe_mul(zi, inv, pre);
-    } else {
-      fe_copy(zi, inv);
+  for (int k = COMB_CHUNK - 1; k >= 0; k--) {
+    if (live) {
+      const uint32_t* e = tmp + (size_t)k * CACHED_WORDS * nl;
+      fe zi, x, y, z, xy, ypx, ymx, t2d;
+      if (k > 0) {
+        fe pre;
+        fe_load_soa(pre, e - CACHED_WORDS * nl + 27 * nl, nl, gl);
+        fe_mul(zi, inv, pre);
+      } else {
+        fe_copy(zi, inv);
+      }
+      fe_load_soa(z, e + 18 * nl, nl, gl);
+      fe_mul(inv, inv, z);
+      fe_load_soa(x, e, nl, gl);
+      fe_load_soa(y, e + 9 * nl, nl, gl);
+      fe_mul(x, x, zi);
+      fe_mul(y, y, zi);
+      fe_mul(xy, x, y);
+      fe_add(ypx, y, x);
+      fe_carry(ypx);
+      fe_sub(ymx, y, x);
+      fe_mul(t2d, xy, d2);
+      uint32_t* o = reinterpret_cast<uint32_t*>(&ent[ln][0]);
+      fe_store(o, ypx);
+      fe_store(o + 9, ymx);
+      fe_store(o + 18, t2d);
+#pragma unroll
+      for (int w = 27; w < COMB_STRIDE; w++) o[w] = 0;
     }
-    fe_load(z, e + 18);
-    fe_mul(inv, inv, z);
-    fe_load(x, e);
-    fe_load(y, e + 9);
-    fe_mul(x, x, zi);
-    fe_mul(y, y, zi);
-    fe_mul(xy, x, y);
-    fe_add(ypx, y, x);
-    fe_carry(ypx);
-    fe_sub(ymx, y, x);
-    fe_mul(t2d, xy, d2);
-    uint32_t* o = out + ((size_t)c * COMB_CHUNK + k) * COMB_STRIDE;
-    fe_store(o, ypx);
-    fe_store(o + 9, ymx);
-    fe_store(o + 18, t2d);
+    __syncthreads();
 #pragma unroll
-    for (int w = 27; w < COMB_STRIDE; w++) o[w] = 0;
-  }
-  if (c == 0) {
-#pragma unroll
-    for (int w = 0; w < COMB_STRIDE; w++) out[w] = (w == 0 || w == 9) ? 1u : 0u;  // identity (1, 1, 0)
+    for (int it = 0; it < COMB_STRIDE / 4; it++) {  // 64 entries x 8 pieces, 64 pieces per instruction
+      const int p = it * 64 + ln, L = p >> 3, piece = p & 7;
+      uint32_t* d = dst[L];
+      if (d) reinterpret_cast<uint4*>(d + (size_t)k * estride)[piece] = ent[L][piece];
+    }
+    __syncthreads();
   }
 }
 
@@ -1037,7 +1078,7 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
 size_t cbft_ed25519_comb_tmp_words(size_t lanes) { return lanes * COMB_TMP_WORDS_PER_LANE; }
 
 size_t cbft_ed25519_comb_pos_words(size_t nunits, const CombGeom& g) {
-  return nunits * (size_t)g.npos * CACHED_WORDS;
+  return nunits * (size_t)g.npos * COMB_POS_WORDS;
 }
 
 hipError_t cbft_ed25519_launch_comb_pos(const uint8_t* d_pk, size_t nunits, int negate, const CombGeom& g,
@@ -1050,12 +1091,14 @@ hipError_t cbft_ed25519_launch_comb_pos(const uint8_t* d_pk, size_t nunits, int 
 }
 
 hipError_t cbft_ed25519_launch_comb_tables(const uint32_t* d_pos, size_t nunits, const CombGeom& g, uint32_t* d_tbl,
-                                           uint32_t* d_tmp, size_t lane0, size_t nlanes, hipStream_t stream) {
+                                           void* const* d_chunks, uint32_t a0, uint32_t* d_tmp, size_t lane0,
+                                           size_t nlanes, hipStream_t stream) {
   if (nunits == 0 || nlanes == 0) return hipSuccess;
   if (g.w < 8 || g.w > CBFT_COMB_MAX_RADIX || g.npos < 1) return hipErrorInvalidValue;
   if (lane0 + nlanes > nunits * g.npos * g.chunks()) return hipErrorInvalidValue;
+  if (!d_chunks == !d_tbl) return hipErrorInvalidValue;  // exactly one destination form
   hipLaunchKernelGGL(ed25519_comb_table_kernel, dim3((unsigned)((nlanes + COMB_TABLE_BLOCK - 1) / COMB_TABLE_BLOCK)),
-                     dim3(COMB_TABLE_BLOCK), 0, stream, d_pos, nunits, g, d_tbl, d_tmp, lane0, nlanes);
+                     dim3(COMB_TABLE_BLOCK), 0, stream, d_pos, nunits, g, d_tbl, d_chunks, a0, d_tmp, lane0, nlanes);
   return hipGetLastError();
 }
 size_t cbft_ed25519_table_words_per_unit() { return (size_t)Shape::TA * CACHED_WORDS; }
