@@ -141,6 +141,9 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER_MIN")) c->stage_order_min = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_SMALL_MAX")) c->small_max = (size_t)atoll(e);
+  if (const char* e = getenv("CBFT_ZERO_COPY")) c->zero_copy = atoi(e);
+  if (const char* e = getenv("CBFT_BLOCKING_SYNC")) c->blocking_sync = atoi(e);
+  if (const char* e = getenv("CBFT_SMALL_STREAMS")) c->nsmall = std::max(1, std::min(CBFT_SMALL_STREAMS, atoi(e)));
   if (const char* e = getenv("CBFT_LADDER_LANES")) {
     const int l = atoi(e);
     if (l == 2 || l == 4) c->ladder_lanes = l;
@@ -259,6 +262,8 @@ void cbft_close(cbft_ctx* c) {
   }
   for (hipStream_t st : {c->stream, c->copy_stream, c->compute[0], c->compute[1]})
     if (st) (void)hipStreamSynchronize(st);
+  for (hipStream_t st : c->small_streams)
+    if (st) (void)hipStreamSynchronize(st);
   if (c->build_stream) (void)hipStreamSynchronize(c->build_stream);
   for (auto& kv : c->tables) {
     std::lock_guard<std::mutex> ag(kv.second->append_mu);
@@ -298,10 +303,12 @@ void cbft_close(cbft_ctx* c) {
     for (DevBuf* b : {&hs.in, &hs.verd}) b->release();
     hs.pack.release();
     hs.hverd.release();
-    for (hipEvent_t e : {hs.copied, hs.done})
+    for (hipEvent_t e : {hs.copied, hs.done, hs.done_blk})
       if (e) (void)hipEventDestroy(e);
   }
   for (hipStream_t st : {c->stream, c->copy_stream, c->compute[0], c->compute[1], c->build_stream})
+    if (st) (void)hipStreamDestroy(st);
+  for (hipStream_t st : c->small_streams)
     if (st) (void)hipStreamDestroy(st);
   delete c;
 }
@@ -367,6 +374,8 @@ int cbft_sync(cbft_ctx* c) {
   if (!c->kids.empty()) return CBFT_OK;
   (void)hipSetDevice(c->device);
   for (hipStream_t st : {c->stream, c->copy_stream, c->compute[0], c->compute[1]}) CBFT_HIP(hipStreamSynchronize(st));
+  for (hipStream_t st : c->small_streams)
+    if (st) CBFT_HIP(hipStreamSynchronize(st));
   return CBFT_OK;
 }
 
@@ -643,13 +652,17 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     if (it == c->tables.end() || !d_kidx) return CBFT_EINVAL;
     kt = it->second.get();
   }
-  WorkSlot& slot = c->slots[c->next_slot++ % CBFT_WORK_SLOTS];
-  if (table_id == CBFT_NO_KEY_TABLE) {
-    CBFT_HIP(slot.ps_tbl.reserve(n * cbft_ed25519_table_words_per_unit() * sizeof(uint32_t)));
-    CBFT_HIP(slot.ps_aok.reserve(n));
+  // the fused small-batch kernel keeps everything in registers: no work slot to order against
+  const bool small = kt && n <= c->small_max && !c->ladder_lanes;
+  WorkSlot& slot = c->slots[small ? 0 : c->next_slot++ % CBFT_WORK_SLOTS];
+  if (!small) {
+    if (table_id == CBFT_NO_KEY_TABLE) {
+      CBFT_HIP(slot.ps_tbl.reserve(n * cbft_ed25519_table_words_per_unit() * sizeof(uint32_t)));
+      CBFT_HIP(slot.ps_aok.reserve(n));
+    }
+    // the slot's previous batch (maybe on another stream) must be done with its buffers
+    if (slot.used) CBFT_HIP(hipStreamWaitEvent(s, slot.done, 0));
   }
-  // the slot's previous batch (maybe on another stream) must be done with its buffers
-  if (slot.used) CBFT_HIP(hipStreamWaitEvent(s, slot.done, 0));
 
   Ed25519Batch b{n, d_pk, d_kidx, KeyChunks{nullptr, 0}, d_sig, d_msg, d_off, d_len,
                  kt ? kt->nkeys : (uint32_t)n, fixed_len};
@@ -677,7 +690,7 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     // pair ladder (fewer additions in total, 2 waves/SIMD) once a batch fills the chip with it;
     // the quad ladder (half the additions per lane) for the latency of small batches
     w.comb_lanes = c->ladder_lanes ? c->ladder_lanes : (n >= 32768 ? 2 : 4);
-    w.small = n <= c->small_max && !c->ladder_lanes;
+    w.small = small;
   }
   // Stage order pays for big batches (their stages fill the chip; see cbft_ctx::stage_order).
   // Small batches are latency-bound single waves per stage: ordering them only serialises
@@ -697,8 +710,10 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   if (c->profiling) evp = c->prof_mode == 2 ? &c->ring[(c->ring_n++ % CBFT_PROF_RING) * 4] : c->ev;
   CBFT_HIP(cbft_ed25519_launch_verify(b, w, s, evp, ordered ? &order : nullptr));
   if (ordered) c->stage_used = true;
-  CBFT_HIP(hipEventRecord(slot.done, s));
-  slot.used = true;
+  if (!small) {
+    CBFT_HIP(hipEventRecord(slot.done, s));
+    slot.used = true;
+  }
   c->ev_valid = c->profiling;
   return CBFT_OK;
 }
@@ -740,7 +755,7 @@ static void batch_layout(size_t n, bool key_table, bool fixed, BatchLayout& l) {
 static int collect_locked(HostSlot& s) {
   if (!s.pending) return s.status;
   s.pending = false;
-  hipError_t e = hipEventSynchronize(s.done);
+  hipError_t e = hipEventSynchronize(s.wait_ev ? s.wait_ev : s.done);
   if (e != hipSuccess) return s.status = cbft_fail(e, "hipEventSynchronize(batch done)", __FILE__, __LINE__);
   const size_t nbytes = (s.n + 7) / 8;
   std::memcpy(s.bitmap, s.hverd.p, nbytes);  // little-endian host: verdict words == bitmap bytes
@@ -799,6 +814,8 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
   CBFT_HIP(s.hverd.reserve(nw * 8));
   if (!s.copied) CBFT_HIP(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
   if (!s.done) CBFT_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+  if (!s.done_blk) CBFT_HIP(hipEventCreateWithFlags(&s.done_blk, hipEventDisableTiming | hipEventBlockingSync));
+  s.wait_ev = s.done;
   struct Part {
     const void* src;
     size_t bytes, off;
@@ -827,9 +844,42 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
   uint8_t* din = s.in.as<uint8_t>();
   // a small packed batch (the per-request path) copies on its compute stream: no copy-stream
   // event to record and wait for; bigger batches overlap their copies with earlier batches' kernels
-  hipStream_t cs = c->compute[t & 1];
   const bool one_stream = pack && n <= c->small_max;
+  hipStream_t cs = c->compute[t & 1];
+  if (one_stream) {
+    hipStream_t& ss = c->small_streams[t % c->nsmall];
+    if (!ss) CBFT_HIP(hipStreamCreateWithFlags(&ss, hipStreamNonBlocking));
+    cs = ss;
+  }
   hipStream_t cps = one_stream ? cs : c->copy_stream;
+  // zero-copy: a fused small batch whose parts are all pageable (the per-request coalescer's
+  // case) is packed into the slot's pinned image and the kernel reads it there over PCIe and
+  // writes its verdict words straight into pinned memory: one launch and one event per batch
+  // instead of two DMAs around the launch (the host API time of the copies bounded the
+  // coalescer's batch rate)
+  bool zc = one_stream && kt && c->zero_copy && !c->ladder_lanes;
+  for (int k = 0; k < 5 && zc; k++)
+    if (parts[k].bytes && pinned[k]) zc = false;
+  if (zc) {
+    CBFT_HIP(s.pack.reserve(in_bytes));
+    for (int k = 0; k < 5; k++)
+      if (parts[k].bytes) std::memcpy(s.pack.as<uint8_t>(parts[k].off), parts[k].src, parts[k].bytes);
+    const uint8_t* zin = static_cast<const uint8_t*>(s.pack.dev);
+    rc = launch_locked(c, table_id, nullptr, reinterpret_cast<const uint32_t*>(zin + o_key), zin + o_sig,
+                       zin + o_msg - blo, fixed ? nullptr : reinterpret_cast<const uint64_t*>(zin + o_off),
+                       fixed ? nullptr : reinterpret_cast<const uint32_t*>(zin + o_len), fixed_len, n,
+                       static_cast<uint64_t*>(s.hverd.dev), cs);
+    if (rc) return rc;
+    s.wait_ev = c->blocking_sync ? s.done_blk : s.done;
+    CBFT_HIP(hipEventRecord(s.wait_ev, cs));
+    s.ticket = t;
+    s.pending = true;
+    s.status = CBFT_OK;
+    s.n = n;
+    s.bitmap = bitmap;
+    *ticket = t;
+    return CBFT_OK;
+  }
   // every part pinned and laid out in one host block exactly as in the device image
   // (cbft_ed25519_batch_layout): the whole batch is one DMA
   {

@@ -20,16 +20,19 @@
 // into it and move them with one DMA copy instead of one pageable copy per array.
 struct HostBuf {
   void* p = nullptr;
+  void* dev = nullptr;  // the same memory as kernels address it (zero-copy reads and writes)
   size_t cap = 0;
   hipError_t reserve(size_t bytes) {
     if (bytes <= cap) return hipSuccess;
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = dev = nullptr;
     cap = 0;
     size_t want = std::max<size_t>(bytes, 1 << 16);
     hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostGetDevicePointer(&dev, p, 0);
     if (e != hipSuccess) {
-      p = nullptr;
+      if (p) (void)hipHostFree(p);
+      p = dev = nullptr;
       return e;
     }
     cap = want;
@@ -37,7 +40,7 @@ struct HostBuf {
   }
   void release() {
     if (p) (void)hipHostFree(p);
-    p = nullptr;
+    p = dev = nullptr;
     cap = 0;
   }
   template <class T>
@@ -113,11 +116,15 @@ struct WorkSlot {
 // or packed into `pack` first when they are pageable; the copy runs on the context's copy stream
 // while earlier batches' kernels run on the compute streams.  A slot is reused only after its
 // previous batch was collected (verdict words copied to that batch's bitmap).
-#define CBFT_HOST_SLOTS 4
+#define CBFT_HOST_SLOTS 16
 struct HostSlot {
   DevBuf in, verd;      // packed device inputs, device verdict words
   HostBuf pack, hverd;  // pinned packing image for pageable inputs, pinned verdict words
   hipEvent_t copied = nullptr, done = nullptr;
+  // fused small batches complete on a blocking-sync event: their waiters sleep instead of
+  // spinning, so dozens of concurrent per-request callers do not burn the host's cores
+  hipEvent_t done_blk = nullptr;
+  hipEvent_t wait_ev = nullptr;  // the event the pending batch completes on
   std::mutex m;         // guards the fields below (collect vs. reuse)
   uint64_t ticket = 0;  // batch currently owning the slot
   bool pending = false; // submitted, verdicts not yet delivered
@@ -144,6 +151,12 @@ struct cbft_ctx {
   // host-buffer pipeline
   hipStream_t copy_stream = nullptr;
   hipStream_t compute[2] = {nullptr, nullptr};
+  // fused small batches (the per-request path) rotate over their own streams, created on first
+  // use, so that concurrent callers' batches run side by side instead of queueing on compute[]
+#define CBFT_SMALL_STREAMS 16
+  hipStream_t small_streams[CBFT_SMALL_STREAMS] = {};
+  int nsmall = 4;  // streams in use ($CBFT_SMALL_STREAMS, 1..16; kernels of different streams
+                   // overlap only as far as the process has hardware queues: GPU_MAX_HW_QUEUES)
   HostSlot hslots[CBFT_HOST_SLOTS];
   uint64_t next_ticket = 0;
   DevBuf base_table, base_comb;
@@ -163,6 +176,8 @@ struct cbft_ctx {
   // key-table batches up to this size run as one fused launch (ed25519_small_kernel;
   // $CBFT_SMALL_MAX, 0 = never): the per-request coalescer's batches
   size_t small_max = 1024;
+  int blocking_sync = 1;  // small batches' waiters sleep ($CBFT_BLOCKING_SYNC)
+  int zero_copy = 1;  // fused small batches read pinned inputs and write verdicts in place ($CBFT_ZERO_COPY)
   int b_radix = CBFT_COMB_B_RADIX;  // radix of B's comb table ($CBFT_B_RADIX, 16..22)
   int ladder_lanes = 0;             // comb ladder lanes per signature ($CBFT_LADDER_LANES 2 | 4; 0 = by batch)
   hipEvent_t stage_done[2] = {nullptr, nullptr};  // last hash, last ladder

@@ -152,7 +152,7 @@ static int engineRadix() {
 // condition variable (woken for its verdict or to lead), never on a shared one.
 class Ed25519Engine {
  public:
-  static constexpr int kMaxInflight = 3;  // profiles/r03_host_bench_inflight*.json: 3 > 2, 4 at 64 threads
+  static constexpr int kMaxInflight = 4;  // profiles/r03_host_bench_sweep.txt (zero-copy, blocking-sync small batches)
   static constexpr size_t kMaxBatch = 65536;
 
   static std::shared_ptr<Ed25519Engine> get() {
@@ -396,7 +396,7 @@ class Ed25519Engine {
   int maxInflight_ = [] {  // GPU batches in flight ($CBFT_ENGINE_INFLIGHT, default kMaxInflight)
     const char* e = std::getenv("CBFT_ENGINE_INFLIGHT");
     const int v = e ? std::atoi(e) : kMaxInflight;
-    return v < 1 ? 1 : (v > 8 ? 8 : v);
+    return v < 1 ? 1 : (v > 16 ? 16 : v);
   }();
   bool leader_ = false;
   int inflight_ = 0;
