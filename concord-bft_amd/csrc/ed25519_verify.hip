@@ -870,47 +870,97 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
 }
 
 // ---------------------------------------------------------------------------------------
-// Small batches in ONE launch (the per-request path: a few coalesced verify() calls): one wave
-// per 16 signatures, a lane quad per signature -- every lane of the quad hashes (the same
-// digest, so no exchange), the quad runs the comb sum as K3q and combines it by DPP, and every
-// lane encodes and compares; the verdicts of the wave's 16 signatures go out as one 16-bit
-// word.  Three launches (hash, ladder, finish) and their inter-kernel gaps become one, and no
-// per-signature state goes through HBM.
+// Small batches in ONE launch (the per-request path: a few coalesced verify() calls): one block
+// of two waves per 16 signatures.  Wave 0: a lane quad per signature -- every lane of the quad
+// hashes (the same digest, so no exchange), the quad runs the comb sum as K3q and combines it by
+// DPP.  Wave 1, meanwhile on another SIMD: decodes each signature's R.  The verdict then needs
+// no inversion: encode(R') == R (OpenSSL's memcmp of the encodings) holds exactly when R's y is
+// canonical, R decodes, R is not "x = 0 with the sign bit set", and R' = (X : Y : Z) equals
+// (x_R, y_R) projectively (X = x_R Z, Y = y_R Z): the encoding is a bijection between points and
+// canonical encodings, and the decoder picks x by the sign bit.  The R decode (a square-root
+// chain) runs under the hash and the comb instead of an inversion after them.  The verdicts of
+// the block's 16 signatures go out as one 16-bit word; no per-signature state goes through HBM.
 // ---------------------------------------------------------------------------------------
 #define SMALL_SIGS 16
-__global__ void __launch_bounds__(64) ed25519_small_kernel(const Ed25519Batch b, const uint32_t* btbl,
-                                                           const CombLadder cl, uint16_t* verdict16) {
+#define SMALL_BLOCK 128
+__global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed25519Batch b, const uint32_t* btbl,
+                                                                    const CombLadder cl, uint16_t* verdict16) {
   __shared__ int32_t sdig[COMB_MAX_STEPS * 64];
   __shared__ uint4 stage[7 * 64];
-  const uint32_t ln = threadIdx.x, q = ln & 3u;
-  size_t i = (size_t)blockIdx.x * SMALL_SIGS + (ln >> 2);
+  __shared__ uint32_t rdec[SMALL_SIGS][2 * FE_LIMBS + 1];  // x_R | y_R | decodes
+  const uint32_t ln = threadIdx.x & 63u, wave = threadIdx.x >> 6, q = ln & 3u, sl = ln >> 2;
+  size_t i = (size_t)blockIdx.x * SMALL_SIGS + sl;
   const bool live = i < b.n;
   if (!live) i = b.n - 1;
+#if CBFT_ED_PHASES  // probe builds: block 0's phase times (10 ns ticks), printed by lane 0
+  uint64_t ph[6];
+#define ED_STAMP(k) ph[k] = wall_clock64()
+#else
+#define ED_STAMP(k)
+#endif
+  if (wave == 1) {
+#if CBFT_ED_PHASES
+    const uint64_t d0 = wall_clock64();
+#endif
+    uint32_t Rw[8];
+    load_words8(Rw, b.sig + i * 64);
+    ge_p3 R;
+    bool ok = ge_frombytes(R, Rw);
+#if CBFT_ED_PHASES
+    if (blockIdx.x == 0 && ln == 0) printf("ed25519_small block 0: R decode %.1f us\n", (wall_clock64() - d0) * 0.01);
+#endif
+    // y < p: the 255-bit y is not one of 2^255 - 19 .. 2^255 - 1
+    bool top = (Rw[7] & 0x7fffffffu) == 0x7fffffffu && Rw[0] >= 0xffffffedu;
+#pragma unroll
+    for (int k = 1; k < 7; k++) top = top && Rw[k] == 0xffffffffu;
+    ok = ok && !top && !(fe_iszero(R.X) && (Rw[7] >> 31));
+    if (q == 0) {
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        rdec[sl][k] = R.X.v[k];
+        rdec[sl][FE_LIMBS + k] = R.Y.v[k];
+      }
+      rdec[sl][2 * FE_LIMBS] = ok ? 1u : 0u;
+    }
+    __syncthreads();
+    return;
+  }
+  ED_STAMP(0);
   uint32_t hs[8];
   bool flag;
   ed25519_hash_sig(b, i, hs, flag);
+  ED_STAMP(1);
   ge_p3 P;
   comb_quad_sum<64>(b, i, q, hs, btbl, cl, sdig, stage, P);
+  ED_STAMP(2);
   quad_combine<0xB1>(P, true);
   quad_combine<0x4E>(P, false);
-  uint32_t Rp[8], Rw[8];
-  {  // encode R' (public: variable-time inversion)
-    fe zi, x, y;
-    fe_invert_var(zi, P.Z);
-    fe_mul<false>(x, P.X, zi);
-    fe_mul<false>(y, P.Y, zi);
-    fe_to_words(Rp, y);
-    Rp[7] ^= fe_isnegative(x) << 31;
-  }
-  load_words8(Rw, b.sig + i * 64);
-  uint32_t diff = 0;
+  ED_STAMP(3);
+  __syncthreads();  // wave 1's R decodes
+  fe xr, yr, t;
 #pragma unroll
-  for (int k = 0; k < 8; k++) diff |= Rp[k] ^ Rw[k];
-  const bool verdict = live && diff == 0 && flag && b.keys.aok(batch_unit(b, i));
+  for (int k = 0; k < FE_LIMBS; k++) {
+    xr.v[k] = rdec[sl][k];
+    yr.v[k] = rdec[sl][FE_LIMBS + k];
+  }
+  bool same = rdec[sl][2 * FE_LIMBS] != 0;
+  fe_mul<false>(t, xr, P.Z);
+  fe_sub(t, P.X, t);
+  same = same && fe_iszero(t);
+  fe_mul<false>(t, yr, P.Z);
+  fe_sub(t, P.Y, t);
+  same = same && fe_iszero(t);
+  ED_STAMP(4);
+#if CBFT_ED_PHASES
+  if (blockIdx.x == 0 && ln == 0)
+    printf("ed25519_small block 0 (us): hash %.1f comb %.1f combine %.1f check %.1f\n", (ph[1] - ph[0]) * 0.01,
+           (ph[2] - ph[1]) * 0.01, (ph[3] - ph[2]) * 0.01, (ph[4] - ph[3]) * 0.01);
+#endif
+  const bool verdict = live && same && flag && b.keys.aok(batch_unit(b, i));
   const uint64_t bal = __ballot(verdict);
   uint32_t bits = 0;
 #pragma unroll
-  for (int s = 0; s < SMALL_SIGS; s++) bits |= (uint32_t)((bal >> (4 * s)) & 1u) << s;
+  for (int s2 = 0; s2 < SMALL_SIGS; s2++) bits |= (uint32_t)((bal >> (4 * s2)) & 1u) << s2;
   if (ln == 0) verdict16[blockIdx.x] = (uint16_t)bits;
 }
 
@@ -1132,7 +1182,7 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
     if (w.comb.nper > COMB_MAX_STEPS) return hipErrorInvalidValue;
     if (ev)
       for (int k = 0; k < 3; k++) (void)hipEventRecord(ev[k], stream);
-    hipLaunchKernelGGL(ed25519_small_kernel, dim3((unsigned)((b.n + SMALL_SIGS - 1) / SMALL_SIGS)), dim3(64), 0, stream,
+    hipLaunchKernelGGL(ed25519_small_kernel, dim3((unsigned)((b.n + SMALL_SIGS - 1) / SMALL_SIGS)), dim3(SMALL_BLOCK), 0, stream,
                        b, w.base_comb, w.comb, reinterpret_cast<uint16_t*>(w.verdict_words));
     if (ev) (void)hipEventRecord(ev[3], stream);
     return hipGetLastError();

@@ -1,0 +1,19 @@
+"""Phase probe of the fused small-batch Ed25519 kernel (variant library built with
+-DCBFT_ED_PHASES=1, selected by $CBFT_LIB): a few key-table batches of 1 and 16 signatures."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(HERE, ".."), os.path.join(HERE, "..", "concord-bft_amd"), HERE]
+import numpy as np  # noqa: E402
+import cbft_hipcrypto as cb  # noqa: E402
+import workload  # noqa: E402
+
+ss = workload.make_sigset(64, nkeys=16, msg_len=256, seed=5)
+ctx = cb.Context(device=0)
+tid = ctx.load_keys(ss.pk)
+for n in (1, 16, 16, 16):
+    msgs = [bytes(ss.blob[256 * i: 256 * i + 256]) for i in range(n)]
+    bm = ctx.verify(tid, ss.key_idx[:n], ss.sig[:n], msgs)
+    print("n", n, "verdicts", np.unpackbits(np.frombuffer(bm, dtype=np.uint8), bitorder="little")[:n].sum(), flush=True)
+ctx.close()
