@@ -385,28 +385,51 @@ RF_HD void g2r_accum_aff(G2R<U>& acc, bool& inf, const F2R<U>& qx, const F2R<U>&
   }
 }
 
-// r Q == O for affine Q (qx, qy; R4, not infinity) by the NAF of r (254 digits, 33 non-zero:
-// 253 doublings and 32 mixed additions of +-Q), exact in every case (g2r_accum_aff), so the
-// verdict equals g2_in_subgroup's.  Wave-uniform.
+// Q in G2 (Q a decoded point of E'(Fp2), not infinity) by the endomorphism psi = twist^-1 o
+// Frobenius o twist: psi(Q) = [6u^2] Q.  psi satisfies psi^2 - t psi + p = 0 with t = 6u^2 + 1
+// (the trace of E over Fp, #E(Fp) = r), so psi(Q) = [6u^2] Q gives [(6u^2)^2 - t 6u^2 + p] Q =
+// [r] Q = O; conversely G2 is psi's eigenspace for p = r + 6u^2 on E'[r].  So the verdict is
+// r Q == O's (g2_in_subgroup), for half the doublings: [6u^2] Q is 126 doublings and 11 mixed
+// additions of Q (exact in every case, g2r_accum_aff), then psi(Q) = (conj(x) g_x, conj(y) g_y)
+// against T = (X : Y : Z): X = x' Z^2, Y = y' Z^3.  Wave-uniform.
 template <class U, class W>
 RF_HD bool g2r_in_subgroup(const F2R<U>& qx, const F2R<U>& qy, const G2RowCtx<U, W>& c) {
-  const uint32_t pos[8] = {0x00000011u, 0xa1000000u, 0x00000010u, 0x00200000u,
-                           0x00000008u, 0x02445000u, 0x40000002u, 0x25240482u};
-  const uint32_t neg[8] = {0x00000004u, 0x00000000u, 0x00000000u, 0x00808000u,
-                           0x00000000u, 0x48100280u, 0x00000000u, 0x0000a000u};
-  const F2R<U> nqy = f2r_red(f2r_sub(F2R<U>{c.zero, c.zero}, qy, c), c);
+  const uint32_t k[4] = {0x00000006u, 0x06000000u, 0x00000003u, 0x61818000u};  // 6u^2, bit 126 on top
   G2R<U> T{qx, qy, F2R<U>{c.one, c.zero}};
   bool inf = false;
 #pragma nounroll
-  for (int i = 252; i >= 0; i--) {
+  for (int i = 125; i >= 0; i--) {
     if (!inf) {
       g2r_dbl<false>((F2R<U>*)nullptr, T, c);
       inf = c.zero4(T.Z);
     }
-    const bool dp = (pos[i >> 5] >> (i & 31)) & 1, dn = (neg[i >> 5] >> (i & 31)) & 1;
-    if (dp || dn) g2r_accum_aff(T, inf, qx, dp ? qy : nqy, c);
+    if ((k[i >> 5] >> (i & 31)) & 1u) g2r_accum_aff(T, inf, qx, qy, c);
   }
-  return inf || c.zero4(T.Z);
+  if (inf) return false;  // [6u^2] Q = O but psi(Q) is not O
+  fp2 g;
+  fp2_load(g, Bn254Consts::TWX1);
+  const F2R<U> gx{rf_from_fe(g.a, c.zero), rf_from_fe(g.b, c.zero)};
+  fp2_load(g, Bn254Consts::TWY1);
+  const F2R<U> gy{rf_from_fe(g.a, c.zero), rf_from_fe(g.b, c.zero)};
+  const F2R<U> cx{qx.a, c.sub(c.zero, qx.b)}, cy{qy.a, c.sub(c.zero, qy.b)};  // conjugates, b < 8q
+  U A[8], B[8], P[8];
+  F2R<U> ZZ, xs, ys, ZZZ, xz, yz;
+  f2r_sqr_ops(A, B, 0, T.Z, c);  // Z R4: (8q)(12q)
+  f2r_mul_ops(A, B, 2, cx, gx);  // (12q)(4q)
+  f2r_mul_ops(A, B, 5, cy, gy);
+  r_prods<8>(P, A, B, c);
+  f2r_sqr_res(ZZ, P, 0);  // a < 2q, b < 4q
+  f2r_mul_res(xs, P, 2, c);
+  f2r_mul_res(ys, P, 5, c);
+  f2r_mul_ops(A, B, 0, ZZ, T.Z);  // (6q)(8q)
+  f2r_mul_ops(A, B, 3, xs, ZZ);   // (8q)(6q)
+  r_prods<6>(P, A, B, c);
+  f2r_mul_res(ZZZ, P, 0, c);
+  f2r_mul_res(xz, P, 3, c);
+  f2r_mul_ops(A, B, 0, ys, ZZZ);  // (8q)(8q)
+  r_prods<3>(P, A, B, c);
+  f2r_mul_res(yz, P, 0, c);
+  return c.zero4(f2r_red(f2r_sub(T.X, xz, c), c)) && c.zero4(f2r_red(f2r_sub(T.Y, yz, c), c));
 }
 
 #if defined(__HIPCC__)

@@ -82,3 +82,43 @@ def test_host_build_matches_oracle():
     o2 = ctypes.create_string_buffer(65)
     lib.shim_g2_mul_gen((77).to_bytes(32, "big"), o2)
     assert o2.raw == B.g2_to_bytes(B.ec_mul(77, B.G2_GEN))
+
+
+def test_g2_membership_by_psi():
+    """The key load's subgroup test (bn254_g2row.h g2r_in_subgroup): Q in G2 iff psi(Q) = [6u^2]Q.
+    psi (twist^-1 o Frobenius o twist) satisfies psi^2 - t psi + p = 0 with t = 6u^2 + 1, so
+    psi(Q) = [6u^2]Q forces [(6u^2)^2 - t 6u^2 + p]Q = [r]Q = O; G2 is psi's p-eigenspace and
+    p = r + 6u^2.  Checked here on points of G2, random twist points and points of the cofactor's
+    small prime-order subgroups (13, 96757), against r Q == O."""
+    import random as _r
+    k = 6 * B.U * B.U
+    t = B.P + 1 - B.R
+    assert t == k + 1 and k * k - t * k + B.P == B.R
+    h2 = 2 * B.P - B.R
+    assert h2 % 13 == 0 and h2 % 96757 == 0
+
+    def psi(q):
+        return (q[0].conj() * B.GX1, q[1].conj() * B.GY1)
+
+    def member(q):
+        return psi(q) == B.ec_mul(k, q, None)
+
+    rng = _r.Random(3)
+
+    def twist_point():
+        while True:
+            x = B.F2(rng.randrange(B.P), rng.randrange(B.P))
+            y = B.f2_sqrt(x * x * x + B.B2)
+            if y is not None:
+                return (x, y)
+
+    assert member(B.G2_GEN)
+    assert member(B.ec_mul(h2, twist_point(), None))
+    for _ in range(2):
+        q = twist_point()
+        assert not member(q) and B.ec_mul(B.R, q, None) is not None
+    for ell in (13, 96757):
+        q = None
+        while q is None:  # a random point has an order-ell component with probability 1 - 1/ell
+            q = B.ec_mul(B.R * h2 // ell, twist_point(), None)
+        assert B.ec_mul(ell, q, None) is None and not member(q)
