@@ -752,6 +752,42 @@ int shim_g2r_check(uint64_t seed, int iters) {
   return bad + (int)g_rf_bound_violations;
 }
 
+// g2r_in_subgroup (the psi(Q) = [6u^2]Q test) against r Q == O on twist points multiplied by
+// k1 then k2 (8 LE words each; e.g. r and h2 / ell land in the cofactor's order-ell subgroup, h2
+// and 1 in G2): returns mismatches, *tested = points that were not infinity.
+int shim_g2r_subgroup_scaled(uint64_t seed, int n, const uint32_t* k1, const uint32_t* k2, int* tested) {
+  std::mt19937_64 g(seed);
+  HU tag;
+  const G2RowCtx<HU, HW> c(tag);
+  int bad = 0;
+  *tested = 0;
+  for (int it = 0; it < n; it++) {
+    uint8_t enc[65] = {0x02};
+    for (uint32_t x = 1 + (uint32_t)(g() & 0xffffff);; x++) {
+      enc[64] = (uint8_t)x;
+      enc[63] = (uint8_t)(x >> 8);
+      enc[62] = (uint8_t)(x >> 16);
+      enc[32] = (uint8_t)(1 + (g() & 7));
+      g2a t;
+      if (!g2_decode_on_curve(t, enc)) continue;
+      g2j p, q;
+      p.X = t.x;
+      p.Y = t.y;
+      fp2_one(p.Z);
+      g2_mul_ct(q, p, k1);
+      g2_mul_ct(p, q, k2);
+      g2a a;
+      g2_to_affine(a, p);
+      if (!a.inf) {
+        ++*tested;
+        if (g2r_in_subgroup(f2r_of(a.x), f2r_of(a.y), c) != g2_in_subgroup(a)) bad++;
+      }
+      break;
+    }
+  }
+  return bad + (int)g_rf_bound_violations;
+}
+
 // the key-sum kernel's flow (bls_g2_sum_row_kernel) on the host emulation: waves of 8 ids each
 // (mixed additions from affine keys), then a pairwise tree through one-lane words (the LDS
 // exchange) -> compressed; 1 iff equal to the one-lane g2_add_j sum of the same keys

@@ -207,3 +207,23 @@ def test_row_g2_emulation(shim, seed):
     against rf_mul's bounds (row-normal limbs, (a/q)(b/q) < 221)."""
     shim.shim_g2r_check.argtypes = [ctypes.c_uint64, ctypes.c_int]
     assert shim.shim_g2r_check(seed, 24) == 0
+
+
+def test_row_g2_subgroup_on_cofactor_torsion():
+    """bls_keys_row_kernel's subgroup test (g2r_in_subgroup: psi(Q) = [6u^2]Q) == r Q == O
+    (g2_in_subgroup) on points of G2 ([h2] T) and of the cofactor's order-13 and order-96757
+    subgroups ([r][h2 / ell] T), T random twist points; host emulation of the row code."""
+    import bn254_ref as B
+    lib = ctypes.CDLL(SHIM)
+    lib.shim_g2r_subgroup_scaled.argtypes = [ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                             ctypes.POINTER(ctypes.c_int)]
+    h2 = 2 * B.P - B.R
+
+    def words(x):
+        return (ctypes.c_uint32 * 8)(*[(x >> (32 * i)) & 0xFFFFFFFF for i in range(8)])
+
+    for k1, k2, want in ((h2, 1, 8), (B.R, h2 // 13, 6), (B.R, h2 // 96757, 7), (1, 1, 8)):
+        tested = ctypes.c_int(0)
+        bad = lib.shim_g2r_subgroup_scaled(k1 * 7 + k2, 8, words(k1), words(k2), ctypes.byref(tested))
+        assert bad == 0
+        assert tested.value >= want - 1  # a point may have no component in the target subgroup
