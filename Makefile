@@ -69,7 +69,7 @@ HOST_LIB := concord-bft_amd/libcbft_host.so
 HOST_DIR := concord-bft_amd/host
 HOST_SRC := $(HOST_DIR)/src/hip_ed25519.cpp $(HOST_DIR)/src/hip_rsa.cpp $(HOST_DIR)/src/bls_hip.cpp $(HOST_DIR)/src/request_batch.cpp
 MIRROR_SRC := $(wildcard $(HOST_DIR)/ref_mirror/src/*.cpp)
-HOST_INC := -Iinclude -I$(HOST_DIR)/include -I$(HOST_DIR)/ref_mirror/include
+HOST_INC := -Iinclude -I$(HOST_DIR)/include -I$(HOST_DIR)/ref_mirror/include -DCBFT_WITH_CLIENT_KEYS_MAP
 HOST_HDRS := $(wildcard $(HOST_DIR)/include/*.hpp $(HOST_DIR)/include/threshsign/*.hpp $(HOST_DIR)/ref_mirror/include/*.hpp $(HOST_DIR)/ref_mirror/include/threshsign/*.h)
 host: $(HOST_LIB) tests/cpp/test_host tests/cpp/test_bls_host tools/host_bench
 $(HOST_LIB): $(HOST_SRC) $(MIRROR_SRC) $(HOST_HDRS) $(LIB)
@@ -94,11 +94,11 @@ $(SHIM): tests/cpp/bn254_shim.cpp $(CSRC)/bn254_*.h $(CSRC)/bls_ops.h $(CSRC)/sh
 # ASan+UBSan and TSan variants of the C++ host library and its tests; run on a GPU box with
 # tools/sanitize.sh.
 SAN_DIR := tests/cpp/san
-sanitize: $(LIB)
+sanitize: $(LIB) $(MIRROR_SRC) $(HOST_SRC)
 	mkdir -p $(SAN_DIR)
 	for s in address,undefined thread; do \
 	  t=$$(echo $$s | cut -d, -f1); \
-	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 -fPIC -shared $(HOST_INC) -o $(SAN_DIR)/libcbft_host_$$t.so $(HOST_SRC) -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' && \
-	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 -DCONCORD_BFT_TESTING $(HOST_INC) -o $(SAN_DIR)/test_host_$$t tests/cpp/test_host.cpp -L$(SAN_DIR) -lcbft_host_$$t -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' && \
-	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 $(HOST_INC) -o $(SAN_DIR)/test_bls_host_$$t tests/cpp/test_bls_host.cpp -L$(SAN_DIR) -lcbft_host_$$t -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' || exit 1; \
+	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 -fPIC -shared $(HOST_INC) -o $(SAN_DIR)/libcbft_host_$$t.so $(HOST_SRC) $(MIRROR_SRC) -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -lpthread -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' && \
+	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 -DCONCORD_BFT_TESTING $(HOST_INC) -o $(SAN_DIR)/test_host_$$t tests/cpp/test_host.cpp -L$(SAN_DIR) -lcbft_host_$$t -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -lpthread -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' && \
+	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 $(HOST_INC) -o $(SAN_DIR)/test_bls_host_$$t tests/cpp/test_bls_host.cpp -L$(SAN_DIR) -lcbft_host_$$t -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -lpthread -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' || exit 1; \
 	done

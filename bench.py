@@ -42,6 +42,7 @@ for p in (os.path.join(ROOT, "concord-bft_amd"), os.path.join(ROOT, "tools")):
 
 import cbft_hipcrypto as cb  # noqa: E402  (ctypes binding; the library loads at the first Context)
 import parity_gate  # noqa: E402  (golden-data verdict gate, run before anything is timed)
+import tree_hash  # noqa: E402  (csrc stamp: PMC records are attached only to the tree they describe)
 import workload  # noqa: E402
 
 METRIC = "Ed25519 verifies/sec at batch 64K on 1–8 MI355X; p50 latency @ batch 1K"
@@ -292,18 +293,14 @@ def main():
     lanes = int(os.environ.get("CBFT_LADDER_LANES", "0")) or (2 if n >= 32768 else 4)
     b_radix = int(os.environ.get("CBFT_B_RADIX", "22"))
     kname = "ed25519_comb2_ladder_kernel" if lanes == 2 else "ed25519_comb_ladder_kernel"
+    # PMC record of the headline workload (tools/ed_pmc_probe.py --mode headline under
+    # tools/pmc_passes.sh): attached only while it was collected on this csrc tree
     traffic = slot_ops = None
-    pmc = os.path.join(ROOT, "profiles", "pmc_ladder.json")
-    if os.path.exists(pmc):
-        try:
-            rec = json.load(open(pmc))
-            if rec.get("kernel") == kname and rec.get("batch") == n and rec.get("comb_radix") == args.comb_radix \
-                    and rec.get("b_radix", 16) == b_radix:
-                traffic = rec.get("hbm_bytes_per_launch")
-                k = rec["counters"][kname]
-                slot_ops = (k["SQ_INSTS_VALU"] + k["SQ_INSTS_VALU_INT64"]) * 64
-        except Exception:  # noqa: BLE001
-            traffic = slot_ops = None
+    lrec, lstat = _pmc_record("pmc_ed25519_headline.json", kname)
+    if lrec:
+        traffic = lrec.get("hbm_bytes")
+        slot_ops = (lrec["SQ_INSTS_VALU"] + lrec["SQ_INSTS_VALU_INT64"]) * 64 \
+            if "SQ_INSTS_VALU" in lrec and "SQ_INSTS_VALU_INT64" in lrec else None
     # Algorithmic work of the comb ladder: one mixed addition per comb position (radix-2^w_A key
     # table + radix-2^w_B B table), 7 field multiplications each, 81 + 9 v_mad_u64_u32 per
     # multiplication (9 x 29-bit limbs, fe25519.h); the pair / quad combines are parallelisation
@@ -317,25 +314,18 @@ def main():
                 "frac": achieved / MAD64_PEAK, "traffic": traffic,
                 "kernel": kname, "kernel_ms": ladder_ms, "units_per_launch": n,
                 "ops_per_unit": mads_per_unit,
-                "achieved_basis": f"{npos} comb additions x 7 field multiplications x 90 v_mad_u64_u32 (81 products "
-                                  f"+ 9 folds) per verify x units / ladder launch duration",
-                "work_equiv_frac": OPS_DSM * n / (ladder_ms * 1e-3) / INT32_PEAK,
-                "work_equiv_basis": "SURVEY.md 8(d) ref10 model (1020 S + 1460 M, M = 72, S = 44 INT32 ops = 150,000 "
-                                    "per verify) / INT32 peak: over-credits the comb, which does no doublings",
-                "kernel_ms_basis": f"mean of {pipe_batches} launches inside the timed host pipeline (HIP events "
-                                   f"on the launch streams)",
+                "achieved_basis": f"{npos} comb additions x 7 field mults x 90 v_mad_u64_u32 per verify x units / "
+                                  f"mean ladder launch ({pipe_batches} launches, HIP events on the launch streams, "
+                                  f"inside the timed pipeline)",
                 "issue_frac": (slot_ops / (ladder_ms * 1e-3) / INT32_PEAK) if slot_ops else None,
-                "issue_frac_basis": "executed VALU issue slots per launch (PMC, profiles/pmc_ladder.json; "
-                                    "INT64-class x2) / kernel time",
-                "stage_ms_pipelined": pipe_stage,
-                "stage_ms_isolated": {k: statistics.median(v) for k, v in iso.items()},
+                "pmc": _pmc_brief(lrec, lstat),
+                "stage_ms_pipelined": {k: round(v, 4) for k, v in pipe_stage.items()},
+                "stage_ms_isolated": {k: round(statistics.median(v), 4) for k, v in iso.items()},
                 "pcie": {"bound": "pcie_h2d", "achieved": value / world * h2d_bytes / 1e9, "peak": PCIE_PEAK / 1e9,
                          "measured_copy_rate": h2d_rate / 1e9, "unit": "GB/s",
                          "frac": value / world * h2d_bytes / PCIE_PEAK,
                          "frac_of_measured": value / world * h2d_bytes / h2d_rate,
-                         "bytes_per_unit": h2d_bytes,
-                         "note": "the step's binding resource: host->device bytes of the batch over PCIe Gen5 x16"},
-                "device_resident_ceiling": dev_value}
+                         "bytes_per_unit": h2d_bytes}}
 
     # ---- the replica's own multi-GPU form: ONE process over all N devices (cbft_open_mask), the
     # same per-device batch as a shard of one N x batch call, verdicts gated as above
@@ -413,6 +403,12 @@ def main():
             parity["config4_bls"] = bls.pop("parity")
         if rsa:
             parity["rsa_2048_bench_sets"] = {"n": 2 * args.batch, "mismatch": 0}
+        detail = _write_detail({"parity": parity, "roofline": roofline, "mixed_config3": mixed, "bls_config4": bls,
+                                "rsa_2048": rsa, "per_request_path": per_request, "single_process_multi_gpu": single})
+        small_k, small_stat = _pmc_record("pmc_ed25519_small.json", "ed25519_small_kernel")
+        # The line: the contract's keys first, then side measurements, and LAST what the driver's
+        # stdout tail must keep: the second half of the metric (p50 @ 1K), the
+        # device-resident ceiling, the per-request path, the key-table load and the BLS timings.
         out = {
             "metric": METRIC, "value": value, "unit": "verifies/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
@@ -427,27 +423,128 @@ def main():
                                                                   if world > 1 else ""),
                        "rank0_numa_node": numa},
             "roofline": roofline, "cpu_baseline": cpu,
-            "p50_latency_ms_batch1k": lat,
-            "p50_latency_ms_batch1k_python_lists": lat_py,
-            "device_resident_value": dev_value,
-            "key_table_load_ms": key_load_ms,
-            "key_table_load_basis": f"one cbft_ed25519_load_keys of {args.nkeys} client keys before timing: decode, "
-                                    "per-key position points, radix comb tables (HBM-resident, reused by every step)",
-            "pageable_host_value": pageable,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
-            "mixed_config3": mixed,
-            "bls_config4": bls,
-            "rsa_2048": rsa,
-            "per_request_path": per_request,
-            "single_process_multi_gpu": single,
             "verdicts": "bit-exact vs host OpenSSL (checked before and after timing)",
-            "parity": parity,
+            "parity": {"all_exact": True, "blocks": _parity_counts(parity), "detail": detail},
+            "pageable_host_value": pageable,
+            "single_process_multi_gpu": _brief(single, ("value", "devices", "open", "ms_per_step")),
+            "rsa_2048": _rsa_brief(rsa),
+            "mixed_config3": _brief(mixed, ("value", "pipelined_pinned_value", "device_resident_value",
+                                            "hash_kernel_ms", "hash_pmc", "exact_match", "n")),
+            "bls_config4": _bls_brief(bls),
+            "per_request_path": _per_request_brief(per_request),
+            "key_table_load_ms": key_load_ms,
+            "device_resident_value": dev_value,
+            "p50_small_kernel_pmc": _pmc_brief(small_k, small_stat),
+            "p50_latency_ms_batch1k_python_lists": lat_py,
+            "p50_latency_ms_batch1k": lat,
         }
         print(json.dumps(out), flush=True)
     ctx.host_free(blk)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def _pmc_record(fname: str, kernel: str):
+    """(counters of `kernel`, status) from profiles/<fname> (tools/pmc_record.py), or (None, why):
+    a record collected on another csrc tree (tools/tree_hash.py) is stale and dropped."""
+    path = os.path.join(ROOT, "profiles", fname)
+    if not os.path.exists(path):
+        return None, f"profiles/{fname} absent"
+    try:
+        rec = json.load(open(path))
+    except Exception as e:  # noqa: BLE001
+        return None, f"profiles/{fname} unreadable: {e}"
+    if rec.get("csrc_tree") != tree_hash.csrc_tree_hash():
+        return None, f"profiles/{fname} stale (csrc tree {rec.get('csrc_tree')} != {tree_hash.csrc_tree_hash()}): dropped"
+    k = rec.get("kernels", {}).get(kernel)
+    if k is None:
+        return None, f"profiles/{fname} has no {kernel}"
+    return k, f"profiles/{fname} (csrc tree {rec['csrc_tree']})"
+
+
+def _pmc_brief(k, status):
+    """The per-kernel PMC fields the bench line carries."""
+    out = {"source": status}
+    if k:
+        for key in ("duration_ms", "waves_per_simd", "valu_insts_per_wave", "valu_active_frac", "issue_stall_frac",
+                    "waitcnt_frac", "wave_cycles_per_valu", "mad_frac_of_peak", "hbm_bytes"):
+            if k.get(key) is not None:
+                out[key] = round(k[key], 4) if isinstance(k[key], float) else k[key]
+    return out
+
+
+def _write_detail(rec: dict) -> str:
+    """The full per-class parity record and every side measurement, as a file beside the run
+    (gpurun_out/ when it exists, which gpurun brings back; the builder copies it under profiles/)."""
+    d = os.path.join(ROOT, "gpurun_out")
+    path = os.path.join(d if os.path.isdir(d) else os.path.join(ROOT, "profiles"), "bench_detail_last.json")
+    try:
+        with open(path, "w") as f:
+            json.dump(rec, f, indent=1, default=str)
+    except OSError:
+        return "unwritten"
+    return os.path.relpath(path, ROOT)
+
+
+def _brief(rec, keys):
+    if not rec:
+        return None
+    return {k: (round(rec[k], 5) if isinstance(rec[k], float) else rec[k]) for k in keys if k in rec}
+
+
+def _per_request_brief(pr):
+    if not pr:
+        return None
+    v, o, one = pr["verify_mt"], pr["openssl_mt"], pr["single"]
+    return {"verify_mt_per_s": v["verifies_per_s"], "verify_mt_p50_us": v["p50_us"], "verify_mt_p99_us": v["p99_us"],
+            "threads": v["threads"], "calls_per_batch": v["calls_per_batch"], "single_call_p50_us": one["p50_us"],
+            "verifysig_mt_per_s": pr["verifysig_mt"]["verifies_per_s"], "openssl_mt_per_s": o["verifies_per_s"],
+            "openssl_threads": o["threads"], "gpu_vs_openssl_mt": pr["gpu_vs_openssl_mt"]}
+
+
+def _rsa_brief(rsa):
+    if not rsa:
+        return None
+    out = {}
+    for label in ("client_e65537", "replica_e17"):
+        r = rsa.get(label)
+        if r:
+            out[label] = {"value": r["value"], "kernel_ms": round(r["kernel_ms"], 4),
+                          "frac": round(r["roofline"]["frac"], 4), "cpu_value": r["cpu_baseline"]["value"]}
+    return out
+
+
+def _bls_brief(bls):
+    if not bls:
+        return None
+    out = {k: (round(bls[k], 4) if isinstance(bls[k], float) else bls[k])
+           for k in ("certificate_ms", "certificate_fused_ms", "certificate_policy_ms", "share_verify_ms",
+                     "combine_ms", "verify_ms", "optimistic_ms", "multisig_ms", "sign_ms", "public_key_ms",
+                     "keyset_load_ms") if k in bls}
+    rf = bls.get("roofline") or {}
+    out["kernels_pmc"] = rf.get("kernels")
+    out["pmc_source"] = rf.get("source")
+    if bls.get("cpu_baseline"):
+        out["cpu_baseline_shares_per_s"] = bls["cpu_baseline"]["value"]
+    return out
+
+
+def _parity_counts(parity: dict) -> dict:
+    """Counts per gate block for the bench line (the per-class detail goes to a file)."""
+    out = {}
+    for name, blk in parity.items():
+        if not isinstance(blk, dict):
+            continue
+        if "vectors" in blk:
+            out[name] = {"n": blk["vectors"], "mismatch": blk.get("mismatch", 0)}
+        elif "n" in blk or "shares" in blk:
+            out[name] = {"n": blk.get("n", blk.get("shares")),
+                         "mismatch": blk.get("mismatch", blk.get("share_verdict_mismatch", 0))}
+        else:
+            out[name] = {"checks": sum(v for v in blk.values() if isinstance(v, int)), "mismatch": 0}
+    return out
 
 
 def bench_single_process(args, ss, devices, mask):
@@ -578,9 +675,12 @@ def bench_mixed(ctx, args, cpu_threads):
         finally:
             for v in views:
                 ctx.host_free(v)
+        dres, hash_ms = _mixed_device_resident(ctx, tid, ss, args)
     finally:
         ctx.unload_keys(tid)
+    hk, hstat = _pmc_record("pmc_ed25519_mixed.json", "ed25519_hash_kernel")
     return {"config": f"config #3: {n} sigs, 4096 keys, msg 64-4096 B log-uniform, 10% invalid",
+            "device_resident_value": dres, "hash_kernel_ms": hash_ms, "hash_pmc": _pmc_brief(hk, hstat),
             "value": n / (ms * 1e-3), "unit": "verifies/s (pageable host buffers, blocking call, PCIe included)",
             "pipelined_pinned_value": pipe,
             "pipelined_pinned_basis": "pinned host arrays (cbft_host_alloc), cbft_ed25519_verify_batch_async, "
@@ -588,6 +688,47 @@ def bench_mixed(ctx, args, cpu_threads):
             "pipelined_verdicts_exact": bool(pipe_match),
             "exact_match": match, "n": n, "invalid": int((~ss.expected).sum()),
             "msg_bytes_total": int(ss.len.sum())}
+
+
+def _mixed_device_resident(ctx, tid, ss, args):
+    """Config #3 with its inputs already in HBM (cbft_ed25519_verify_batch_device, two streams):
+    the GPU's own rate on the variable-length batch, and the hash kernel's isolated duration."""
+    import torch
+
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n = ss.n
+
+    def to_dev(a, dtype):
+        return torch.from_numpy(np.ascontiguousarray(a).view(dtype).copy()).to(dev)
+
+    d_sig, d_blob = to_dev(ss.sig.reshape(-1), np.uint8), to_dev(ss.blob, np.uint8)
+    d_off, d_len, d_k = to_dev(ss.off, np.int64), to_dev(ss.len, np.int32), to_dev(ss.key_idx, np.int32)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    outs = [torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev) for _ in range(2)]
+
+    def dstep(j):
+        ctx.verify_device(tid, 0, d_k.data_ptr(), d_sig.data_ptr(), d_blob.data_ptr(), d_off.data_ptr(),
+                          d_len.data_ptr(), n, outs[j % 2].data_ptr(), streams[j % 2].cuda_stream)
+
+    for j in range(4):
+        dstep(j)
+    torch.cuda.synchronize()
+    steps = max(10, args.steps // 2)
+    c0 = time.perf_counter()
+    for j in range(steps):
+        dstep(j)
+    torch.cuda.synchronize()
+    value = n * steps / (time.perf_counter() - c0)
+    for o in outs:
+        if not np.array_equal(cb.bitmap_to_bools(o.cpu().numpy().view(np.uint8).tobytes(), n), ss.expected):
+            raise SystemExit("config #3: device-path verdicts differ from OpenSSL")
+    ctx.set_profiling(True)
+    hs = []
+    for _ in range(3):
+        dstep(0)
+        hs.append(ctx.stage_times_ms()["hash"])
+    ctx.set_profiling(False)
+    return value, statistics.median(hs)
 
 
 # MAD64_PEAK (top): v_mad_u64_u32 issues at half the INT32 rate (MI355X_MICROARCH.md): 256 CU x 4
@@ -772,6 +913,15 @@ def bench_bls(ctx, args, cpu_threads):
         t_policy = _median_ms(policy, runs)
         t_opt = _median_ms(optimistic, runs)
         t_ms = _median_ms(multisig, runs)
+        # replica-side signing (IThresholdSigner::signData, BlsThresholdSigner.cpp:32-47) and the
+        # signer's verification key (sk * g2), checked against the host build's bytes
+        sid, sk, share = cert.sign_probe
+        if ctx.bls_sign(sk, sid, cert.msg) != share:
+            raise SystemExit("BLS signData: GPU share differs from the expected bytes")
+        if ctx.bls_public_key(sk) != cert.vks[sid - 1]:
+            raise SystemExit("BLS public key: GPU sk*g2 differs from the key set's vk")
+        t_sign = _median_ms(lambda: ctx.bls_sign(sk, sid, cert.msg), runs)
+        t_pub = _median_ms(lambda: ctx.bls_public_key(sk), 3)
     finally:
         ctx.bls_unload_keys(kid)
     nsh = len(cert.shares)
@@ -787,7 +937,7 @@ def bench_bls(ctx, args, cpu_threads):
                                        "SignaturesProcessingJob order -- optimistic combine of all shares + verify "
                                        "(fails with 10 % bad), then the fallback",
            "combine_ms": t_comb, "verify_ms": t_ver, "optimistic_ms": t_opt, "multisig_ms": t_ms,
-           "keyset_load_ms": t_load,
+           "keyset_load_ms": t_load, "sign_ms": t_sign, "public_key_ms": t_pub,
            "keyset_load_basis": f"cbft_bls_load_keys + unload of {n} vks + the group key (decode, subgroup check, "
                                 f"70 normalised Miller-loop lines per key)",
            "verdicts": "share verdicts == planted bad set; combined sig == sk*H(m) byte-exact",
@@ -809,25 +959,25 @@ def bench_bls(ctx, args, cpu_threads):
 
 def _bls_roofline():
     """BLS kernels are latency-bound, not throughput-bound: a pairing check is one dependent
-    instruction stream per wave (36 of 64 lanes carry the Fp12 state, bn254_pair36.h), 760
-    checks fill 760 of 1,024 SIMDs once, and a certificate is a chain of such kernels.  Their
-    roofline is therefore the per-wave issue rate, with the MAD64 fraction alongside to show how
-    far from the throughput peak the latency form sits.  Numbers from one rocprofv3 --pmc pass
-    (tools/bls_prof.sh -> tools/pmc_bls.py -> profiles/pmc_bls.json)."""
+    instruction stream per wave, 760 checks fill 760 of 1,024 SIMDs once, and a certificate is a
+    chain of such kernels.  Their roofline is therefore the per-wave issue rate, with the MAD64
+    fraction alongside to show how far from the throughput peak the latency form sits.  From
+    profiles/pmc_bls.json (tools/pmc_passes.sh over tools/bls_probe.py -> tools/pmc_record.py),
+    attached only while its csrc stamp matches this tree."""
     path = os.path.join(ROOT, "profiles", "pmc_bls.json")
     if not os.path.exists(path):
-        return None
+        return {"source": "profiles/pmc_bls.json absent"}
     rec = json.load(open(path))
+    if rec.get("csrc_tree") != tree_hash.csrc_tree_hash():
+        return {"source": f"profiles/pmc_bls.json stale (csrc tree {rec.get('csrc_tree')} != "
+                          f"{tree_hash.csrc_tree_hash()}): dropped"}
     ks = {}
     for name, k in rec["kernels"].items():
-        ks[name] = {key: k.get(key) for key in ("duration_ms", "waves", "mad_frac_of_peak", "wave_cycles_per_valu",
-                                                "valu_insts_per_wave")}
+        ks[name] = {key: (round(k[key], 4) if isinstance(k.get(key), float) else k.get(key))
+                    for key in ("duration_ms", "waves_per_simd", "mad_frac_of_peak", "wave_cycles_per_valu",
+                                "valu_active_frac")}
     return {"bound": "latency: one wave per pairing check / point chain (per-wave VALU issue)",
-            "peak_mad64_lane_ops_per_s": rec.get("mad64_peak_lane_ops_per_s"),
-            "per_wave_issue_floor_cycles_per_valu": 4.8,
-            "per_wave_issue_floor_basis": "v_mad_u64_u32 at saturation, 13.3 lanes/clk/SIMD "
-                                          "(profiles/r01_intrate_microbench.txt): a wave64 mad every 4.8 cycles",
-            "kernels": ks, "source": "profiles/pmc_bls.json"}
+            "kernels": ks, "source": f"profiles/pmc_bls.json (csrc tree {rec['csrc_tree']})"}
 
 
 def _openssl_version():

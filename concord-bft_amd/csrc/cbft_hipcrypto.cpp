@@ -38,6 +38,13 @@ static const size_t kCombBuildLanes = 262144;  // 4 waves per SIMD; 4.7 GB of st
 // whose tables for nkeys keys fit the per-table budget ($CBFT_COMB_BUDGET_GB, default 64 GB of
 // the 288 GB HBM): 13 (10.5 MB/key, 9 additions per lane) up to ~6,100 keys, 11 (3.0 MB/key,
 // 10) up to ~21,000, then 8 (0.53 MB/key, 12).
+// HBM a table of nkeys keys takes at radix r: keys live in whole CBFT_KEY_CHUNK-key chunks (comb
+// tables + raw keys + decode status), so even one key costs a whole chunk.
+static double table_bytes(uint64_t nkeys, int r) {
+  const uint64_t chunks = (nkeys + CBFT_KEY_CHUNK - 1) / CBFT_KEY_CHUNK;
+  return (double)chunks * (double)cbft_key_chunk_bytes(cbft_comb_geom(r).words_per_unit());
+}
+
 static int key_radix(int requested, uint32_t nkeys) {
   if (requested) return requested;
   if (const char* e = getenv("CBFT_COMB_RADIX")) {
@@ -47,7 +54,7 @@ static int key_radix(int requested, uint32_t nkeys) {
   double budget = 64.0;
   if (const char* e = getenv("CBFT_COMB_BUDGET_GB")) budget = atof(e);
   for (int r : {13, 11}) {
-    if ((double)nkeys * cbft_comb_geom(r).words_per_unit() * 4.0 <= budget * 1e9) return r;
+    if (table_bytes(nkeys, r) <= budget * 1e9) return r;
   }
   return 8;
 }
@@ -379,6 +386,9 @@ int cbft_sync(cbft_ctx* c) {
   return CBFT_OK;
 }
 
+static int append_keys(cbft_ctx* c, uint32_t id, const uint8_t* pk, uint32_t nkeys, uint32_t* out_first,
+                       bool check_budget);
+
 int cbft_ed25519_load_keys_ex(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, int comb_radix, uint32_t* out_id) {
   if (!c || !out_id || (nkeys && !pk)) return CBFT_EINVAL;
   if (comb_radix && (comb_radix < 8 || comb_radix > 13)) return CBFT_EINVAL;
@@ -406,7 +416,7 @@ int cbft_ed25519_load_keys_ex(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, in
   }
   if (nkeys) {
     uint32_t first = 0;
-    const int rc = cbft_ed25519_append_keys(c, id, pk, nkeys, &first);
+    const int rc = append_keys(c, id, pk, nkeys, &first, comb_radix == 0);
     if (rc) {
       (void)cbft_ed25519_unload_keys(c, id);
       return rc;
@@ -497,11 +507,18 @@ static const uint8_t* chunk_raw_keys(const KeyTable& kt, uint32_t ci) {
 // already queued against the old table finish before it is released.  Past the budget at radix
 // 8 the append fails with CBFT_ENOMEM and the table is unchanged.
 int cbft_ed25519_append_keys(cbft_ctx* c, uint32_t id, const uint8_t* pk, uint32_t nkeys, uint32_t* out_first) {
+  return append_keys(c, id, pk, nkeys, out_first, true);
+}
+
+// check_budget = false: the initial fill of a table whose radix the caller chose explicitly
+// (cbft_ed25519_load_keys_ex with comb_radix != 0) is built at that radix whatever the budget.
+static int append_keys(cbft_ctx* c, uint32_t id, const uint8_t* pk, uint32_t nkeys, uint32_t* out_first,
+                       bool check_budget) {
   if (!c || !out_first || (nkeys && !pk)) return CBFT_EINVAL;
   if (!c->kids.empty()) {  // every device concurrently
     std::vector<uint32_t> firsts(c->kids.size(), 0);
     const int rc = for_each_kid(c, [&](size_t g) {
-      return cbft_ed25519_append_keys(c->kids[g], id, pk, nkeys, &firsts[g]);
+      return append_keys(c->kids[g], id, pk, nkeys, &firsts[g], check_budget);
     });
     if (rc) return rc;
     for (uint32_t f : firsts)
@@ -529,8 +546,8 @@ int cbft_ed25519_append_keys(cbft_ctx* c, uint32_t id, const uint8_t* pk, uint32
   if ((uint64_t)k0 + nkeys > (uint64_t)CBFT_MAX_KEY_CHUNKS * CBFT_KEY_CHUNK) return CBFT_E2BIG;
   const uint32_t total = k0 + nkeys;
   const double budget = comb_budget_bytes();
-  auto fits = [&](int r) { return (double)total * cbft_comb_geom(r).words_per_unit() * 4.0 <= budget; };
-  if (fits(kt->geo.w)) {
+  auto fits = [&](int r) { return table_bytes(total, r) <= budget; };
+  if (!check_budget || fits(kt->geo.w)) {
     const int rc = fill_keys(c, *kt, pk, hipMemcpyHostToDevice, k0, nkeys);
     if (rc) return rc;
     std::lock_guard<std::mutex> g(c->mu);
@@ -544,6 +561,14 @@ int cbft_ed25519_append_keys(cbft_ctx* c, uint32_t id, const uint8_t* pk, uint32
       break;
     }
   if (!r2) return CBFT_ENOMEM;
+  // A rebuild holds the old and the new table at once (plus the build staging) until the swap:
+  // refuse it up front, table unchanged, when the device cannot hold the new one beside the old.
+  {
+    size_t free_b = 0, total_b = 0;
+    CBFT_HIP(hipMemGetInfo(&free_b, &total_b));
+    const double staging = (double)cbft_ed25519_comb_tmp_words(kCombBuildLanes) * 4.0;
+    if (table_bytes(total, r2) + staging > (double)free_b) return CBFT_ENOMEM;
+  }
   auto nt = std::make_shared<KeyTable>();
   nt->geo = cbft_comb_geom(r2);
   CBFT_HIP(nt->chunk_ptrs.reserve(CBFT_MAX_KEY_CHUNKS * sizeof(void*)));

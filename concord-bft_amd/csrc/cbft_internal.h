@@ -185,6 +185,7 @@ struct cbft_ctx {
   DevBuf verdicts;
   DevBuf sig, msg, off, len, kidx, pk;
   std::vector<uint64_t> host_verdicts;
+  std::vector<uint64_t> host_off;  // rebased message offsets of a host RSA batch
   HostBuf hstage;  // packed host inputs + verdict words of the host-buffer path
   DevBuf dstage;   // the same packing on the device
   // profiling: events around K1 (hash), K3 (ladder), K4 (finish) of the last verify

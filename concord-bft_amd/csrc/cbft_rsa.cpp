@@ -3,10 +3,18 @@
 // Replaces concord::util::crypto::RSAVerifier (util/src/crypto_utils.cpp:101-117,155-168):
 // SigManager builds one verifier per replica / client key (SigManager.cpp:138,146,255); here a
 // key table is loaded once (records built on the GPU) and every verify is a batch on the GPU.
+//
+// Multi-GPU contexts (cbft_open_mask / cbft_open_devices): key tables are loaded on every device
+// (concurrently, table ids in step) and a host-buffer batch is cut into contiguous shards of whole
+// 64-signature verdict words, one per device, verified concurrently (one host thread per device),
+// each shard's verdicts landing in place in the caller's bitmap -- as for Ed25519 (SURVEY.md
+// §8(e)).  The _device entry point needs a single-GPU context (CBFT_EINVAL otherwise).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "cbft_internal.h"
 
@@ -41,8 +49,16 @@ extern "C" {
 
 int cbft_rsa_load_keys(cbft_ctx* c, const uint8_t* moduli, const uint32_t* exponents, uint32_t nkeys,
                        uint32_t* out_id) {
-  c = cbft_dev0(c);
   if (!c || !out_id || (nkeys && (!moduli || !exponents))) return CBFT_EINVAL;
+  if (!c->kids.empty()) {  // every device, concurrently; the ids stay in step
+    std::vector<uint32_t> ids(c->kids.size(), 0);
+    const int rc = for_each_kid(c, [&](size_t g) { return cbft_rsa_load_keys(c->kids[g], moduli, exponents, nkeys, &ids[g]); });
+    if (rc) return rc;
+    for (uint32_t i : ids)
+      if (i != ids[0]) return CBFT_EIO;
+    *out_id = ids[0];
+    return CBFT_OK;
+  }
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
   RsaKeyTable kt;
@@ -71,8 +87,15 @@ int cbft_rsa_load_keys(cbft_ctx* c, const uint8_t* moduli, const uint32_t* expon
 }
 
 int cbft_rsa_unload_keys(cbft_ctx* c, uint32_t id) {
-  c = cbft_dev0(c);
   if (!c) return CBFT_EINVAL;
+  if (!c->kids.empty()) {
+    int rc = CBFT_OK;
+    for (cbft_ctx* k : c->kids) {
+      const int r = cbft_rsa_unload_keys(k, id);
+      if (r && !rc) rc = r;
+    }
+    return rc;
+  }
   std::lock_guard<std::mutex> g(c->mu);
   auto it = c->rsa_tables.find(id);
   if (it == c->rsa_tables.end()) return CBFT_EINVAL;
@@ -100,17 +123,35 @@ int cbft_rsa_key_status(cbft_ctx* c, uint32_t id, uint8_t* out_ok) {
 int cbft_rsa_verify_batch(cbft_ctx* c, uint32_t id, const uint32_t* key_idx, const uint8_t* sig,
                           const uint8_t* msg_blob, const uint64_t* msg_off, const uint32_t* msg_len, size_t n,
                           uint8_t* bitmap) {
-  c = cbft_dev0(c);
   if (!c || (n && (!key_idx || !sig || !msg_off || !msg_len || !bitmap))) return CBFT_EINVAL;
   if (n == 0) return CBFT_OK;
+  if (!c->kids.empty()) {  // contiguous shards of whole 64-signature words, one per device
+    const size_t G = c->kids.size();
+    const size_t per = (((n + G - 1) / G) + 63) / 64 * 64;
+    return for_each_kid(c, [&](size_t g) {
+      const size_t lo = g * per;
+      if (lo >= n) return (int)CBFT_OK;
+      const size_t m = std::min(n, lo + per) - lo;
+      return cbft_rsa_verify_batch(c->kids[g], id, key_idx + lo, sig + lo * RSA_MOD_BYTES, msg_blob, msg_off + lo,
+                                   msg_len + lo, m, bitmap + lo / 8);
+    });
+  }
   std::lock_guard<std::mutex> g(c->mu);
   auto it = c->rsa_tables.find(id);
   if (it == c->rsa_tables.end()) return CBFT_EINVAL;
   for (size_t i = 0; i < n; i++)
     if (key_idx[i] >= it->second.nkeys) return CBFT_EINVAL;
-  uint64_t blob = 0;
-  for (size_t i = 0; i < n; i++) blob = std::max<uint64_t>(blob, msg_off[i] + msg_len[i]);
-  if (blob && !msg_blob) return CBFT_EINVAL;
+  // the batch's messages are the blob range [lo, hi) its offsets span: only that range moves
+  // (a shard of a multi-GPU batch carries its own part of the caller's blob), offsets rebased
+  uint64_t lo = UINT64_MAX, hi = 0;
+  for (size_t i = 0; i < n; i++) {
+    lo = std::min<uint64_t>(lo, msg_off[i]);
+    hi = std::max<uint64_t>(hi, msg_off[i] + msg_len[i]);
+  }
+  if (hi > lo && !msg_blob) return CBFT_EINVAL;
+  const uint64_t blob = hi > lo ? hi - lo : 0;
+  c->host_off.resize(n);
+  for (size_t i = 0; i < n; i++) c->host_off[i] = msg_off[i] - lo;
   CBFT_HIP(hipSetDevice(c->device));
   CBFT_HIP(c->rsa_kidx.reserve(n * 4));
   CBFT_HIP(c->rsa_sig.reserve(n * RSA_MOD_BYTES));
@@ -120,8 +161,8 @@ int cbft_rsa_verify_batch(cbft_ctx* c, uint32_t id, const uint32_t* key_idx, con
   CBFT_HIP(c->verdicts.reserve(((n + 63) / 64) * 8));
   CBFT_HIP(hipMemcpyAsync(c->rsa_kidx.p, key_idx, n * 4, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(hipMemcpyAsync(c->rsa_sig.p, sig, n * RSA_MOD_BYTES, hipMemcpyHostToDevice, c->stream));
-  if (blob) CBFT_HIP(hipMemcpyAsync(c->msg.p, msg_blob, blob, hipMemcpyHostToDevice, c->stream));
-  CBFT_HIP(hipMemcpyAsync(c->off.p, msg_off, n * 8, hipMemcpyHostToDevice, c->stream));
+  if (blob) CBFT_HIP(hipMemcpyAsync(c->msg.p, msg_blob + lo, blob, hipMemcpyHostToDevice, c->stream));
+  CBFT_HIP(hipMemcpyAsync(c->off.p, c->host_off.data(), n * 8, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(hipMemcpyAsync(c->len.p, msg_len, n * 4, hipMemcpyHostToDevice, c->stream));
   int rc = rsa_launch_locked(c, it->second, c->rsa_kidx.as<uint32_t>(), c->rsa_sig.as<uint8_t>(),
                              c->msg.as<uint8_t>(), c->off.as<uint64_t>(), c->len.as<uint32_t>(), n,
@@ -140,7 +181,7 @@ int cbft_rsa_verify_batch(cbft_ctx* c, uint32_t id, const uint32_t* key_idx, con
 int cbft_rsa_verify_batch_device(cbft_ctx* c, uint32_t id, const uint32_t* d_key_idx, const uint8_t* d_sig,
                                  const uint8_t* d_msg, const uint64_t* d_off, const uint32_t* d_len, size_t n,
                                  uint64_t* d_verdicts, void* stream) {
-  c = cbft_dev0(c);
+  if (c && !c->kids.empty()) return CBFT_EINVAL;  // device pointers belong to one GPU: use its own context
   if (!c || (n && (!d_key_idx || !d_sig || !d_off || !d_len || !d_verdicts))) return CBFT_EINVAL;
   if (reinterpret_cast<uintptr_t>(d_sig) & 3) return CBFT_EINVAL;  // signatures are read as words
   if (n == 0) return CBFT_OK;

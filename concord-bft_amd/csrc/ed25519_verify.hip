@@ -961,7 +961,13 @@ __global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed2551
   uint32_t bits = 0;
 #pragma unroll
   for (int s2 = 0; s2 < SMALL_SIGS; s2++) bits |= (uint32_t)((bal >> (4 * s2)) & 1u) << s2;
-  if (ln == 0) verdict16[blockIdx.x] = (uint16_t)bits;
+  if (ln == 0) {
+    verdict16[blockIdx.x] = (uint16_t)bits;
+    // the last block also zeroes the 16-bit pieces of its 64-bit verdict word that no block
+    // covers, so the call writes whole ceil(n/64) words (bits past n = 0) like the ballot kernels
+    if (blockIdx.x == gridDim.x - 1)
+      for (uint32_t p = blockIdx.x + 1; (p & 3u) != 0u; p++) verdict16[p] = 0;
+  }
 }
 
 // ---------------------------------------------------------------------------------------

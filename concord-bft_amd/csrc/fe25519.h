@@ -131,8 +131,167 @@ FE_INLINE void mac1216(uint64_t& acc, uint32_t a) {
   }
 }
 
+// CBFT_FE_ASMCOL: each column's whole mad chain is ONE inline-asm block.  The compiler puts an
+// s_nop after every inline-asm statement (it cannot see the hazard state inside the text), so
+// the one-asm-per-mad chain paid ~90 s_nop per multiply (480 per comb addition, ISA of the pair
+// ladder); with one block per column it is 17.  Same instructions otherwise, same order.
+#ifndef CBFT_FE_ASMCOL
+#define CBFT_FE_ASMCOL 1
+#endif
+#define CBFT_MC_LINE(p) "v_mad_u64_u32 %[acc], %[cc], %[x" #p "], %[y" #p "], %[acc]\n\t"
+#define CBFT_MC_IN(p) [x##p] "v"(x[p]), [y##p] "v"(y[p])
+// acc += sum_{p < N} x[p] * y[p] as one dependent v_mad_u64_u32 chain (one asm statement)
+template <int N>
+FE_INLINE void mad_chain(uint64_t& acc, const uint32_t* x, const uint32_t* y) {
+  uint64_t cc;
+  if constexpr (N == 1) {
+    asm(CBFT_MC_LINE(0) : [acc] "+v"(acc), [cc] "=s"(cc) : CBFT_MC_IN(0));
+  } else if constexpr (N == 2) {
+    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) : [acc] "+v"(acc), [cc] "=s"(cc) : CBFT_MC_IN(0), CBFT_MC_IN(1));
+  } else if constexpr (N == 3) {
+    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2)
+        : [acc] "+v"(acc), [cc] "=s"(cc) : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2));
+  } else if constexpr (N == 4) {
+    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3)
+        : [acc] "+v"(acc), [cc] "=s"(cc) : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3));
+  } else if constexpr (N == 5) {
+    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3) CBFT_MC_LINE(4)
+        : [acc] "+v"(acc), [cc] "=s"(cc)
+        : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3), CBFT_MC_IN(4));
+  } else if constexpr (N == 6) {
+    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3) CBFT_MC_LINE(4) CBFT_MC_LINE(5)
+        : [acc] "+v"(acc), [cc] "=s"(cc)
+        : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3), CBFT_MC_IN(4), CBFT_MC_IN(5));
+  } else if constexpr (N == 7) {
+    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3) CBFT_MC_LINE(4) CBFT_MC_LINE(5)
+            CBFT_MC_LINE(6)
+        : [acc] "+v"(acc), [cc] "=s"(cc)
+        : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3), CBFT_MC_IN(4), CBFT_MC_IN(5), CBFT_MC_IN(6));
+  } else if constexpr (N == 8) {
+    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3) CBFT_MC_LINE(4) CBFT_MC_LINE(5)
+            CBFT_MC_LINE(6) CBFT_MC_LINE(7)
+        : [acc] "+v"(acc), [cc] "=s"(cc)
+        : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3), CBFT_MC_IN(4), CBFT_MC_IN(5), CBFT_MC_IN(6),
+          CBFT_MC_IN(7));
+  } else if constexpr (N == 9) {
+    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3) CBFT_MC_LINE(4) CBFT_MC_LINE(5)
+            CBFT_MC_LINE(6) CBFT_MC_LINE(7) CBFT_MC_LINE(8)
+        : [acc] "+v"(acc), [cc] "=s"(cc)
+        : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3), CBFT_MC_IN(4), CBFT_MC_IN(5), CBFT_MC_IN(6),
+          CBFT_MC_IN(7), CBFT_MC_IN(8));
+  } else if constexpr (N == 10) {
+    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3) CBFT_MC_LINE(4) CBFT_MC_LINE(5)
+            CBFT_MC_LINE(6) CBFT_MC_LINE(7) CBFT_MC_LINE(8) CBFT_MC_LINE(9)
+        : [acc] "+v"(acc), [cc] "=s"(cc)
+        : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3), CBFT_MC_IN(4), CBFT_MC_IN(5), CBFT_MC_IN(6),
+          CBFT_MC_IN(7), CBFT_MC_IN(8), CBFT_MC_IN(9));
+  } else {
+    static_assert(N >= 1 && N <= 10, "mad_chain: 1..10 products");
+  }
+}
+
+// Column k of a x b (products a_i b_{k-i}) plus, when F, a leading fold term f * 1216, as one chain
+template <int K, bool F>
+FE_INLINE void fe_column(uint64_t& acc, const fe& a, const fe& b, uint32_t f) {
+  constexpr int LO = K < FE_LIMBS ? 0 : K - FE_LIMBS + 1;
+  constexpr int HI = K < FE_LIMBS ? K : FE_LIMBS - 1;
+  constexpr int N = HI - LO + 1 + (F ? 1 : 0);
+  uint32_t x[N], y[N];
+  int p = 0;
+  if (F) {
+    x[0] = f;
+    y[0] = 1216u;
+    p = 1;
+  }
+#pragma unroll
+  for (int i = LO; i <= HI; i++, p++) {
+    x[p] = a.v[i];
+    y[p] = b.v[K - i];
+  }
+  mad_chain<N>(acc, x, y);
+}
+// Column k of a^2 (a2 = 2a): a2_i a_j for i < j plus a_{k/2}^2, and the optional fold term
+template <int K, bool F>
+FE_INLINE void fe_sq_column(uint64_t& acc, const fe& a, const uint32_t* a2, uint32_t f) {
+  constexpr int LO = K < FE_LIMBS ? 0 : K - FE_LIMBS + 1;
+  constexpr int NP = (K - LO + 1) / 2 - ((K - LO + 1) % 2 == 0 ? 0 : 0);  // pairs i < j with i >= LO
+  constexpr int NPAIRS = ((K & 1) ? (K + 1) / 2 : K / 2) - LO;
+  constexpr int N = NPAIRS + ((K & 1) ? 0 : 1) + (F ? 1 : 0);
+  (void)NP;
+  uint32_t x[N], y[N];
+  int p = 0;
+  if (F) {
+    x[0] = f;
+    y[0] = 1216u;
+    p = 1;
+  }
+#pragma unroll
+  for (int i = LO; 2 * i < K; i++, p++) {
+    x[p] = a2[i];
+    y[p] = a.v[K - i];
+  }
+  if ((K & 1) == 0) {
+    x[p] = a.v[K >> 1];
+    y[p] = a.v[K >> 1];
+  }
+  mad_chain<N>(acc, x, y);
+}
+
+template <int K>
+FE_INLINE void fe_mul_hi_cols(uint64_t& t, uint32_t* h, const fe& a, const fe& b) {
+  if constexpr (K < 17) {
+    fe_column<K, false>(t, a, b, 0u);
+    h[K - 9] = (uint32_t)t & FE_MASK;
+    t >>= 29;
+    fe_mul_hi_cols<K + 1>(t, h, a, b);
+  }
+}
+template <int K>
+FE_INLINE void fe_mul_lo_cols(uint64_t& acc, uint32_t* o, const uint32_t* h, const fe& a, const fe& b) {
+  if constexpr (K < 9) {
+    fe_column<K, true>(acc, a, b, h[K]);
+    o[K] = (uint32_t)acc & FE_MASK;
+    acc >>= 29;
+    fe_mul_lo_cols<K + 1>(acc, o, h, a, b);
+  }
+}
+template <int K>
+FE_INLINE void fe_sq_hi_cols(uint64_t& t, uint32_t* h, const fe& a, const uint32_t* a2) {
+  if constexpr (K < 17) {
+    fe_sq_column<K, false>(t, a, a2, 0u);
+    h[K - 9] = (uint32_t)t & FE_MASK;
+    t >>= 29;
+    fe_sq_hi_cols<K + 1>(t, h, a, a2);
+  }
+}
+template <int K>
+FE_INLINE void fe_sq_lo_cols(uint64_t& acc, uint32_t* o, const uint32_t* h, const fe& a, const uint32_t* a2) {
+  if constexpr (K < 9) {
+    fe_sq_column<K, true>(acc, a, a2, h[K]);
+    o[K] = (uint32_t)acc & FE_MASK;
+    acc >>= 29;
+    fe_sq_lo_cols<K + 1>(acc, o, h, a, a2);
+  }
+}
+
 template <bool C = CBFT_FE_CHAIN>
 FE_INLINE void fe_mul(fe& r, const fe& a, const fe& b) {
+#if CBFT_FE_ASMCOL
+  if (C) {
+    fe o;
+    uint32_t h[9];
+    uint64_t t = 0;
+    fe_mul_hi_cols<9>(t, h, a, b);
+    h[8] = (uint32_t)t;
+    uint64_t acc = 0;
+    fe_mul_lo_cols<0>(acc, o.v, h, a, b);
+    uint64_t w = acc * 1216ull + (uint64_t)o.v[0];
+    o.v[0] = (uint32_t)w & FE_MASK;
+    o.v[1] += (uint32_t)(w >> 29);
+    r = o;
+    return;
+  }
+#endif
   fe o;  // r may alias a or b
   uint32_t h[9];
   uint64_t t = 0;
@@ -164,6 +323,21 @@ FE_INLINE void fe_sq(fe& r, const fe& a) {
   uint32_t a2[FE_LIMBS];
 #pragma unroll
   for (int i = 0; i < FE_LIMBS; i++) a2[i] = a.v[i] << 1;
+#if CBFT_FE_ASMCOL
+  if (C) {
+    uint32_t h[9];
+    uint64_t t = 0;
+    fe_sq_hi_cols<9>(t, h, a, a2);
+    h[8] = (uint32_t)t;
+    uint64_t acc = 0;
+    fe_sq_lo_cols<0>(acc, o.v, h, a, a2);
+    uint64_t w = acc * 1216ull + (uint64_t)o.v[0];
+    o.v[0] = (uint32_t)w & FE_MASK;
+    o.v[1] += (uint32_t)(w >> 29);
+    r = o;
+    return;
+  }
+#endif
   uint32_t h[9];
   uint64_t t = 0;
 #pragma unroll

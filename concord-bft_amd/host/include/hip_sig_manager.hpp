@@ -24,11 +24,18 @@
 //                      every 1,000th success of each counter); with stopAtFirstFailure only the
 //                      items up to the first failure are counted (the serial loops throw there).
 //   setClientPublicKey SigManager.cpp:250-264 with a GPU verifier of the key's type (the base's
-//                      version builds an RSAVerifier); callers that hold a HipSigManager* get it.
+//                      version builds an RSAVerifier), and the key recorded in the CMF
+//                      ClientsPublicKeys map exactly as the reference records it (:260).  The
+//                      base method is NOT virtual: through a SigManager* the base's runs.  Key
+//                      exchange therefore calls setClientPublicKeyOf(SigManager::instance(), ...)
+//                      (the KeyExchangeManager.cpp:310-320 patch in INTEGRATION.md), which routes
+//                      to this version when the instance is the HipSigManager that init() made.
 //
-// Not covered: an Ed25519 client key is not entered into the reference's CMF ClientsPublicKeys
-// map (getClientsPublicKeys, SigManager.cpp:27-32; its key-type tag only knows "1 = RSAVerifier",
-// :156) — publishing Ed25519 client keys needs that tag extended upstream.
+// The CMF map: clientsPublicKeys_ is a namespace-scope global of the reference's SigManager.cpp
+// (:25) whose type comes from the generated keys_and_signatures.cmf.hpp; builds that have that
+// header (corebft, and the standalone build's restatement in ref_mirror/) define
+// CBFT_WITH_CLIENT_KEYS_MAP.  Its version tag stays the reference's "1 = RSAVerifier" (:156): a
+// reader of an Ed25519 entry must tell the key type from the key itself (32 raw bytes / 64 hex).
 #pragma once
 
 #include <chrono>
@@ -46,6 +53,13 @@
 #include "ReplicasInfo.hpp"
 #include "SigManager.hpp"
 #include "hip_crypto.hpp"
+
+#if defined(CBFT_WITH_CLIENT_KEYS_MAP)
+#include "keys_and_signatures.cmf.hpp"
+namespace bftEngine::impl {
+extern concord::messages::keys_and_signatures::ClientsPublicKeys clientsPublicKeys_;  // SigManager.cpp:25
+}
+#endif
 
 namespace concord::hip {
 
@@ -79,7 +93,21 @@ class HipSigManager : public bftEngine::impl::SigManager {
     HipSigManager* sm = initInTesting(myId, mySigPrivateKey, publicKeysOfReplicas, replicasKeysFormat,
                                       publicKeysOfClients, clientsKeysFormat, replicasInfo);
     Base::instance(sm);
+    registered() = sm;
     return sm;
+  }
+  ~HipSigManager() {
+    if (registered() == this) registered() = nullptr;
+  }
+
+  // Key exchange's entry (KeyExchangeManager::loadClientPublicKey, KeyExchangeManager.cpp:316-322):
+  // `sm` is SigManager::instance().  When it is the HipSigManager init() registered, the rotation
+  // gets a GPU verifier of the key's type; otherwise the reference's own method runs.
+  static void setClientPublicKeyOf(Base* sm, const std::string& key, PrincipalId id, Fmt format) {
+    if (sm != nullptr && sm == static_cast<Base*>(registered()))
+      registered()->setClientPublicKey(key, id, format);
+    else if (sm != nullptr)
+      sm->setClientPublicKey(key, id, format);
   }
   // the same without touching the instance (SigManager::initInTesting)
   static HipSigManager* initInTesting(ReplicaId myId, const std::string& mySigPrivateKey,
@@ -159,6 +187,17 @@ class HipSigManager : public bftEngine::impl::SigManager {
     auto v = makeVerifier(key, format);  // throws on a bad key, like the reference (:258)
     std::unique_lock lock(mutex_);
     verifiers_.insert_or_assign(id, std::move(v));
+#if defined(CBFT_WITH_CLIENT_KEYS_MAP)
+    bftEngine::impl::clientsPublicKeys_.ids_to_keys[id] =
+        concord::messages::keys_and_signatures::PublicKey{key, (uint8_t)format};  // SigManager.cpp:260
+#endif
+  }
+
+  // The verifier object a principal's signatures go to (nullptr: unknown principal).
+  std::shared_ptr<concord::util::crypto::IVerifier> verifierOf(PrincipalId id) const {
+    std::shared_lock lock(mutex_);
+    auto it = verifiers_.find(id);
+    return it == verifiers_.end() ? nullptr : it->second;
   }
 
   // isClientTransactionSigningEnabled() is non-const in the reference
@@ -175,6 +214,10 @@ class HipSigManager : public bftEngine::impl::SigManager {
   }
 
  private:
+  static HipSigManager*& registered() {
+    static HipSigManager* sm = nullptr;
+    return sm;
+  }
   struct RsaSubset {  // what the base constructor may see: RSA keys only
     std::pair<std::string, Fmt> myKey;
     KeyList keys;

@@ -12,21 +12,19 @@
 
 #include "ReplicaConfig.hpp"
 #include "ReplicasInfo.hpp"
+#include "keys_and_signatures.cmf.hpp"
 
 namespace bftEngine {
 namespace impl {
 
 using concord::util::crypto::KeyFormat;
 
-namespace {
-// keys_and_signatures.cmf: ClientsPublicKeys { map uint16 PublicKey{string key, uint8 format}
-// ids_to_keys; uint16 version }.  CMF: integers big-endian, strings and maps u32-length prefixed
-// (messages/compiler/cpp/serialize.cpp).
-struct ClientsPublicKeys {
-  std::map<uint16_t, std::pair<std::string, uint8_t>> ids_to_keys;
-  uint16_t version = 0;
-} clientsPublicKeys_;
+// keys_and_signatures.cmf's ClientsPublicKeys, a namespace-scope global as in the reference
+// (SigManager.cpp:25): HipSigManager::setClientPublicKey updates it too.  CMF encoding: integers
+// big-endian, strings and maps u32-length prefixed (messages/compiler/cpp/serialize.cpp).
+concord::messages::keys_and_signatures::ClientsPublicKeys clientsPublicKeys_;
 
+namespace {
 void putBE(std::vector<uint8_t>& o, uint64_t v, int bytes) {
   for (int i = bytes - 1; i >= 0; i--) o.push_back((uint8_t)(v >> (8 * i)));
 }
@@ -38,9 +36,9 @@ std::string SigManager::getClientsPublicKeys() {
   putBE(out, clientsPublicKeys_.ids_to_keys.size(), 4);
   for (const auto& [id, k] : clientsPublicKeys_.ids_to_keys) {
     putBE(out, id, 2);
-    putBE(out, k.first.size(), 4);
-    out.insert(out.end(), k.first.begin(), k.first.end());
-    out.push_back(k.second);
+    putBE(out, k.key.size(), 4);
+    out.insert(out.end(), k.key.begin(), k.key.end());
+    out.push_back(k.format);
   }
   putBE(out, clientsPublicKeys_.version, 2);
   return std::string(out.begin(), out.end());

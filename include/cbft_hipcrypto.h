@@ -64,8 +64,10 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch);
  * into contiguous shards of whole 64-signature words, one per device, verified concurrently, and
  * the verdicts land in the caller's one bitmap.  BLS key sets are loaded on every device and
  * cbft_bls_verify_shares cuts the shares into contiguous slices, one per device, verified
- * concurrently (bitmaps merged); the other BLS calls, RSA and the profiling calls run on the
- * lowest device of the mask; the _device entry points need a single-GPU context (CBFT_EINVAL).
+ * concurrently (bitmaps merged).  RSA key tables are loaded on every device and an RSA
+ * host-buffer batch is sharded like an Ed25519 one.  The other BLS calls and the profiling calls
+ * run on the lowest device of the mask; the _device entry points need a single-GPU context
+ * (CBFT_EINVAL).
  * A one-bit mask is exactly cbft_open. */
 int cbft_open_mask(cbft_ctx** out, uint32_t device_mask, size_t max_batch);
 /* The same over an explicit device list, in shard order; a device may repeat (several shards,

@@ -61,6 +61,10 @@ bool useThroughReferenceTypes(bftEngine::impl::ReplicasInfo& ri, const std::stri
   std::vector<bool> out;
   hip->verifySigBatch({{0, msg, len, sig, 64}}, out);
   validatePrePrepareRequests(msg, len, ri, *hip);
+  // KeyExchangeManager::loadClientPublicKey (KeyExchangeManager.cpp:316-322), patched as in
+  // the rotation reaches the GPU verifiers through SigManager::instance()
+  HipSigManager::setClientPublicKeyOf(bftEngine::impl::SigManager::instance(), key, 5,
+                                      concord::util::crypto::KeyFormat::PemFormat);
   return v->verify(std::string(msg, len), std::string(sig, 64)) && sm->verifySig(0, msg, len, sig, 64);
 }
 }  // namespace concord::hip::boundary

@@ -176,6 +176,66 @@ static int testRsa() {
   return 0;
 }
 
+// Key exchange (KeyExchangeManager::loadClientPublicKey, KeyExchangeManager.cpp:316-322) calls
+// SigManager::instance()->setClientPublicKey, a NON-virtual method: with the INTEGRATION.md patch
+// it goes through HipSigManager::setClientPublicKeyOf(SigManager::instance(), ...).  A rotation
+// must stay on the GPU (RSA -> HipRSAVerifier, Ed25519 -> HipEdDSAVerifier), verify signatures
+// of the new key only, and enter the key into the CMF ClientsPublicKeys map (SigManager.cpp:260).
+static int testKeyRotation() {
+  using Base = bftEngine::impl::SigManager;
+  RsaKeys k0 = genRsa(65537), k1 = genRsa(65537), kr = genRsa(17);
+  EdDSASigner e0(seedHex(60), KeyFormat::HexaDecimalStrippedFormat), e1(seedHex(61), KeyFormat::HexaDecimalStrippedFormat);
+  ReplicaIdsConfig cfg;
+  cfg.replicaId = 0;
+  cfg.numOfExternalClients = 4;
+  ReplicasInfo ri(cfg);
+  std::set<std::pair<PrincipalId, const std::string>> replicaKeys;
+  for (PrincipalId r = 0; r < 4; r++) replicaKeys.insert({r, kr.pubHex});
+  std::set<std::pair<const std::string, std::set<uint16_t>>> clientKeys = {{k0.pubHex, {4}}, {e0.getPubKeyHex(), {5}}};
+  std::unique_ptr<SigManager> smp(SigManager::init(0, kr.privHex, replicaKeys, KeyFormat::HexaDecimalStrippedFormat,
+                                                   &clientKeys, KeyFormat::HexaDecimalStrippedFormat, ri));
+  Base* base = Base::instance();
+  CHECK(base == static_cast<Base*>(smp.get()));
+  const std::string m = "request after key exchange";
+  RSASigner s0(k0.privHex, KeyFormat::HexaDecimalStrippedFormat), s1(k1.privHex, KeyFormat::HexaDecimalStrippedFormat);
+  const std::string rs0 = s0.sign(m), rs1 = s1.sign(m), es0 = e0.sign(m), es1 = e1.sign(m);
+  CHECK(base->verifySig(4, m.data(), m.size(), rs0.data(), (uint16_t)rs0.size()));
+  CHECK(!base->verifySig(4, m.data(), m.size(), rs1.data(), (uint16_t)rs1.size()));
+  // RSA rotation through the base pointer: the new verifier is a GPU one, the new key verifies
+  SigManager::setClientPublicKeyOf(base, k1.pubHex, 4, KeyFormat::HexaDecimalStrippedFormat);
+  CHECK(dynamic_cast<HipRSAVerifier*>(smp->verifierOf(4).get()) != nullptr);
+  CHECK(base->verifySig(4, m.data(), m.size(), rs1.data(), (uint16_t)rs1.size()));
+  CHECK(!base->verifySig(4, m.data(), m.size(), rs0.data(), (uint16_t)rs0.size()));
+  // Ed25519 rotation (the base's method would throw: it builds an RSAVerifier)
+  SigManager::setClientPublicKeyOf(base, e1.getPubKeyHex(), 5, KeyFormat::HexaDecimalStrippedFormat);
+  CHECK(dynamic_cast<HipEdDSAVerifier*>(smp->verifierOf(5).get()) != nullptr);
+  CHECK(base->verifySig(5, m.data(), m.size(), es1.data(), (uint16_t)es1.size()));
+  CHECK(!base->verifySig(5, m.data(), m.size(), es0.data(), (uint16_t)es0.size()));
+  // an RSA client rotated to Ed25519, and a replica id refused ("Illegal id": unchanged)
+  SigManager::setClientPublicKeyOf(base, e0.getPubKeyHex(), 4, KeyFormat::HexaDecimalStrippedFormat);
+  CHECK(base->verifySig(4, m.data(), m.size(), es0.data(), (uint16_t)es0.size()));
+  auto replicaVerifier = smp->verifierOf(2);
+  SigManager::setClientPublicKeyOf(base, e1.getPubKeyHex(), 2, KeyFormat::HexaDecimalStrippedFormat);
+  CHECK(smp->verifierOf(2) == replicaVerifier);
+  // the CMF map carries the rotated keys, as SigManager.cpp:260 records them
+  const std::string cmf = base->getClientsPublicKeys();
+  CHECK(cmf.find(e0.getPubKeyHex()) != std::string::npos && cmf.find(e1.getPubKeyHex()) != std::string::npos);
+  CHECK(cmf.find(k1.pubHex) == std::string::npos);  // client 4's RSA key was replaced again
+  // a manager that init() did not register gets the reference's own method (RSA only)
+  std::unique_ptr<SigManager> other(SigManager::initInTesting(0, kr.privHex, replicaKeys,
+                                                              KeyFormat::HexaDecimalStrippedFormat, &clientKeys,
+                                                              KeyFormat::HexaDecimalStrippedFormat, ri));
+  bool threw = false;
+  try {
+    SigManager::setClientPublicKeyOf(other.get(), e1.getPubKeyHex(), 5, KeyFormat::HexaDecimalStrippedFormat);
+  } catch (const std::exception&) {
+    threw = true;
+  }
+  CHECK(threw);
+  std::printf("test_host: key rotation through SigManager::instance() stays on the GPU\n");
+  return 0;
+}
+
 // ------------------------------------------------------------------ reference wire formats
 // A packed ClientRequestMsg: header (ClientMsgs.hpp:33-50) | span | request | cid | sig | extra
 static std::string clientRequest(uint16_t client, uint64_t flags, uint64_t seq, const std::string& req,
@@ -500,6 +560,7 @@ static int testAggregatorAndKeySlots() {
 int main() {
   bftEngine::ReplicaConfig::instance().clientTransactionSigningEnabled = true;
   if (testRsa() != 0) return 1;
+  if (testKeyRotation() != 0) return 1;
   // --- IVerifier/ISigner round trip, hex and PEM key formats
   EdDSASigner signer(seedHex(0), KeyFormat::HexaDecimalStrippedFormat);
   std::string pkhex = signer.getPubKeyHex();

@@ -372,3 +372,29 @@ def test_golden_small_batches_fused_kernel(ctx, golden, chunk):
         ctx.unload_keys(tid)
         three.unload_keys(tid3)
         three.close()
+
+
+@pytest.mark.parametrize("n", [1, 17, 47, 64, 65, 130])
+def test_device_path_small_batch_whole_words(n):
+    """cbft_ed25519_verify_batch_device writes ceil(n/64) WHOLE 64-bit verdict words, bits past n
+    = 0, also when the batch runs as the fused small kernel (16-bit pieces per block): the buffer
+    is pre-filled with 0xFF, so a piece no block covers would show up as stray accept bits."""
+    hip = _Hip()
+    nwords = (n + 63) // 64
+    ss = sigsets.make_sigset(n, nkeys=7, msg_len=256, seed=900 + n, invalid_frac=0.2)
+    try:
+        with cb.Context(device=0) as c:
+            tid = c.load_keys(ss.pk)
+            d_kidx, d_sig = hip.to_dev(ss.key_idx), hip.to_dev(ss.sig.reshape(-1))
+            d_blob, d_off, d_len = hip.to_dev(ss.blob), hip.to_dev(ss.off), hip.to_dev(ss.len)
+            out = hip.to_dev(np.full(nwords + 1, 0xFFFFFFFFFFFFFFFF, dtype=np.uint64))
+            c.verify_device(tid, 0, d_kidx, d_sig, d_blob, d_off, d_len, n, out, None)
+            hip.sync()
+            words = np.frombuffer(hip.from_dev(out, (nwords + 1) * 8), dtype=np.uint64)
+            bits = np.unpackbits(words[:nwords].view(np.uint8), bitorder="little").astype(bool)
+            assert np.array_equal(bits[:n], ss.expected)
+            assert not bits[n:].any(), "stale bits past n in the last verdict word"
+            assert words[nwords] == np.uint64(0xFFFFFFFFFFFFFFFF), "wrote past ceil(n/64) words"
+            c.unload_keys(tid)
+    finally:
+        hip.close()

@@ -256,32 +256,34 @@ def test_append_to_empty_table_and_index_bounds(ctx):
 
 
 def test_append_past_budget_rebuilds_at_lower_radix(monkeypatch):
-    """appends check the HBM budget.  With a 20 MB budget a radix-13 table holds one
-    key (10.5 MB), radix 11 six (3.0 MB each), radix 8 thirty-seven (0.53 MB); appending past each
-    limit rebuilds the whole table once at the next radix with the same key indices, and past
-    radix 8 the append fails with CBFT_ENOMEM leaving the table usable."""
-    monkeypatch.setenv("CBFT_COMB_BUDGET_GB", "0.02")
+    """appends check the HBM budget in whole 256-key chunks (what the table really
+    allocates: 2.69 GB per chunk at radix 13, 0.77 GB at 11, 0.135 GB at 8).  With a 1 GB budget
+    a radix-13 table does not fit at all, radix 11 holds one chunk (256 keys) and radix 8 seven
+    (1,792 keys); appending past each limit rebuilds the whole table once at the next radix with
+    the same key indices, and past radix 8 the append fails with CBFT_ENOMEM leaving the table
+    usable."""
+    monkeypatch.setenv("CBFT_COMB_BUDGET_GB", "1.0")
     ss = sigsets.make_sigset(2000, nkeys=40, msg_len=(16, 300), seed=81, invalid_frac=0.1)
     msgs = ss.msgs()
+    rng = np.random.default_rng(5)
+    pk = np.concatenate([ss.pk, rng.integers(0, 256, size=(1800 - 40, 32), dtype=np.uint8)])
     with cb.Context(device=0) as c:
-        tid = c.load_keys(ss.pk[:1], radix=13)
+        tid = c.load_keys(pk[:1], radix=13)  # explicit radix: the budget is not consulted
         assert c.table_size(tid) == (1, 13)
         seen = []
-        for a, b in ((1, 2), (2, 6), (6, 20), (20, 37)):
-            assert c.append_keys(tid, ss.pk[a:b]) == a
-            n, r = c.table_size(tid)
-            seen.append((n, r))
+        for a, b in ((1, 2), (2, 256), (256, 257), (257, 1792)):
+            assert c.append_keys(tid, pk[a:b]) == a
+            seen.append(c.table_size(tid))
             use = np.nonzero(ss.key_idx < b)[0]
             got = cb.bitmap_to_bools(c.verify(tid, ss.key_idx[use], ss.sig[use], [msgs[i] for i in use]), use.size)
             assert np.array_equal(got, ss.expected[use]), (a, b)
-        assert seen == [(2, 11), (6, 11), (20, 8), (37, 8)]
+        assert seen == [(2, 11), (256, 11), (257, 8), (1792, 8)]
         with pytest.raises(cb.CbftError) as e:
-            c.append_keys(tid, ss.pk[37:40])
+            c.append_keys(tid, pk[1792:1793])
         assert e.value.code == -12  # CBFT_ENOMEM
-        assert c.table_size(tid) == (37, 8)
-        use = np.nonzero(ss.key_idx < 37)[0]
-        got = cb.bitmap_to_bools(c.verify(tid, ss.key_idx[use], ss.sig[use], [msgs[i] for i in use]), use.size)
-        assert np.array_equal(got, ss.expected[use])
+        assert c.table_size(tid) == (1792, 8)
+        got = cb.bitmap_to_bools(c.verify(tid, ss.key_idx, ss.sig, msgs), ss.n)
+        assert np.array_equal(got, ss.expected)
         c.unload_keys(tid)
 
 

@@ -1,0 +1,59 @@
+#!/bin/bash
+# Round-4 GPU session steps; each GPU step has its own time limit and the first failure ends the
+# session.  usage: bash tools/gpu_r04.sh step [step ...]
+#   test        pytest -m gpu (one process)
+#   smoke       __graft_entry__.smoke()
+#   bench       python bench.py (driver defaults) -> gpurun_out/bench.json
+#   prof        rocprofv3 --kernel-trace --stats over a short bench -> gpurun_out/prof/
+#   pmc_head    PMC passes over the headline workload -> gpurun_out/pmc_ed25519_headline.json
+#   pmc_small   PMC passes over the p50 path (batches of 1,024) -> gpurun_out/pmc_ed25519_small.json
+#   pmc_mixed   PMC passes over config #3 -> gpurun_out/pmc_ed25519_mixed.json
+#   pmc_bls     kernel stats + PMC passes over the BLS config #4 probe -> gpurun_out/pmc_bls.json
+#   ab          interleaved A/B of $LIBS (tools/ab_libs.sh)
+#   san         host-layer ASan+UBSan / TSan runs (make sanitize first)
+set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
+R=$GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for step in "$@"; do
+  echo "== $step $(date +%T)"
+  case $step in
+    test)
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
+        > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+      tail -3 gpurun_out/pytest_gpu.log ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 \
+        || { echo "smoke failed"; tail -30 gpurun_out/smoke.log; exit 1; }
+      cat gpurun_out/smoke.log ;;
+    bench)
+      timeout -k 10 600 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err \
+        || { echo "bench failed"; tail -30 gpurun_out/bench.err; exit 1; }
+      wc -c gpurun_out/bench.json; tail -c 2500 gpurun_out/bench.json ;;
+    prof)
+      (cd /tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run \
+        -- python3 "$R/bench.py" --steps 20 --warmup 5 --no-cpu) > gpurun_out/prof_bench.json 2> gpurun_out/prof.err \
+        || { echo "rocprof failed"; tail -30 gpurun_out/prof.err; exit 1; }
+      find gpurun_out/prof -name "*kernel_stats.csv" | head -3 ;;
+    pmc_head|pmc_small|pmc_mixed)
+      mode=${step#pmc_}; [ "$mode" = head ] && mode=headline
+      bash tools/pmc_passes.sh "$R/gpurun_out/pmc_$mode" "$R/tools/ed_pmc_probe.py" --mode $mode || exit 1
+      python3 tools/pmc_record.py "$R/gpurun_out/pmc_$mode" "ed_pmc_probe --mode $mode" ed25519_ \
+        > gpurun_out/pmc_ed25519_$mode.json || exit 1 ;;
+    pmc_bls)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/blsprof/trace" -o run \
+        -- python3 "$R/tools/bls_probe.py") > gpurun_out/blsprof_probe.json 2> gpurun_out/blsprof_trace.err \
+        || { echo "bls trace failed"; tail -20 gpurun_out/blsprof_trace.err; exit 1; }
+      cat gpurun_out/blsprof_probe.json
+      bash tools/pmc_passes.sh "$R/gpurun_out/pmc_bls" "$R/tools/bls_probe.py" --reps 1 || exit 1
+      python3 tools/pmc_record.py --longest "$R/gpurun_out/pmc_bls" "bls_probe --reps 1 (config #4)" bls_ \
+        > gpurun_out/pmc_bls.json || exit 1 ;;
+    ab)
+      bash tools/ab_libs.sh || exit 1 ;;
+    san)
+      bash tools/sanitize.sh || { echo "sanitizer runs failed"; exit 1; } ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"

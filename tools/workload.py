@@ -159,6 +159,7 @@ class BlsCert:
     shares: list       # 37-byte shares (id || G1), some "doubled" (bad)
     bad: set           # indices into shares
     expected_sig: bytes
+    sign_probe: tuple = None  # (id, sk, share) of one good share: signing is checked against it
 
 
 def make_bls_cert(n: int = 1024, k: int = 683, extra: int = 0, bad_frac: float = 0.0, seed: int = 2024,
@@ -198,7 +199,9 @@ def make_bls_cert(n: int = 1024, k: int = 683, extra: int = 0, bad_frac: float =
         shares[j] = shares[j][:4] + d.raw
     es = ctypes.create_string_buffer(37)
     lib.shim_sign_share(coeffs[0].to_bytes(32, "big"), 0, msg, len(msg), es)
-    return BlsCert(n, k, pkb.raw, vks, msg, shares, bad, es.raw[4:])
+    good = min(j for j in range(len(shares)) if j not in bad)
+    probe = (ids[good], sks[ids[good]], shares[good])
+    return BlsCert(n, k, pkb.raw, vks, msg, shares, bad, es.raw[4:], probe)
 
 
 def cpu_bls_verify_shares(cert: BlsCert, h33: bytes, threads: int = 16) -> np.ndarray:
