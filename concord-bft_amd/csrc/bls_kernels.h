@@ -59,4 +59,8 @@ hipError_t cbft_bls_launch_verify(const uint8_t* d_msg, uint32_t len, uint32_t* 
                                   const uint32_t* d_gen_lines, uint8_t* d_result, hipStream_t s);
 hipError_t cbft_bls_launch_sign(const uint8_t* d_msg, uint32_t len, const uint32_t* d_sk, uint32_t id,
                                 uint8_t* d_out37, hipStream_t s);
+// the same signature on row-parallel Fp (bls_msm_row.hip): d_H = g1_map(msg) from
+// cbft_bls_launch_hash first; constant operation sequence in the secret scalar
+hipError_t cbft_bls_launch_sign_row(const uint32_t* d_H, const uint32_t* d_sk, const uint8_t* d_msg, uint32_t len,
+                                    uint32_t id, uint8_t* d_out37, hipStream_t s);
 hipError_t cbft_bls_launch_pubkey(const uint32_t* d_sk, uint8_t* d_out65, hipStream_t s);

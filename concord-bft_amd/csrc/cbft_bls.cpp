@@ -543,8 +543,21 @@ int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* 
   CBFT_HIP(c->bls_out.reserve(37));
   if (len) CBFT_HIP(hipMemcpyAsync(c->bls_msg.p, msg, len, hipMemcpyHostToDevice, c->stream));
   CBFT_HIP(hipMemcpyAsync(c->bls_lambda.p, w, sizeof(w), hipMemcpyHostToDevice, c->stream));
-  CBFT_HIP(cbft_bls_launch_sign(c->bls_msg.as<uint8_t>(), len, c->bls_lambda.as<uint32_t>(), id,
-                                c->bls_out.as<uint8_t>(), c->stream));
+  // row-parallel GLV signature (0.4-0.5 ms) unless $CBFT_BLS_SIGN=lane (the one-lane Montgomery
+  // ladder, 4.4 ms: kept as the A/B reference)
+  static const bool lane = [] {
+    const char* e = getenv("CBFT_BLS_SIGN");
+    return e && strcmp(e, "lane") == 0;
+  }();
+  if (lane) {
+    CBFT_HIP(cbft_bls_launch_sign(c->bls_msg.as<uint8_t>(), len, c->bls_lambda.as<uint32_t>(), id,
+                                  c->bls_out.as<uint8_t>(), c->stream));
+  } else {
+    CBFT_HIP(c->bls_H.reserve(BLS_SIG_WORDS * 4));
+    CBFT_HIP(cbft_bls_launch_hash(c->bls_msg.as<uint8_t>(), len, c->bls_H.as<uint32_t>(), c->stream));
+    CBFT_HIP(cbft_bls_launch_sign_row(c->bls_H.as<uint32_t>(), c->bls_lambda.as<uint32_t>(), c->bls_msg.as<uint8_t>(),
+                                      len, id, c->bls_out.as<uint8_t>(), c->stream));
+  }
   CBFT_HIP(hipMemcpyAsync(out37, c->bls_out.p, 37, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipMemsetAsync(c->bls_lambda.p, 0, sizeof(w), c->stream));  // the secret scalar leaves the device
   CBFT_HIP(hipStreamSynchronize(c->stream));

@@ -260,10 +260,68 @@ __device__ __forceinline__ void ed25519_hash_sig(const Ed25519Batch& b, size_t i
   flag = sc_is_canonical(Sw) && key_ok && len_ok;
 }
 
-__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const Ed25519Batch b, uint32_t* h_soa,
-                                                                          uint8_t* flags) {
+// SHA-512 blocks of signature i's R || A || M (what ed25519_hash_sig runs), as a sort bucket
+__device__ __forceinline__ uint32_t hash_bucket(const Ed25519Batch& b, size_t i) {
+  uint32_t len = b.msg_len[i];
+  if (len > CBFT_MAX_MSG_LEN) len = 0;
+  const uint32_t nb = (64u + len + 17u + 127u) / 128u;
+  return nb < CBFT_SHA_BUCKETS - 1 ? nb : CBFT_SHA_BUCKETS - 1;
+}
+
+// Counting sort of a variable-length batch by SHA-512 block count, in three launches:
+// (1) per-bucket counts (LDS histogram per block, one global atomic per non-empty bucket);
+// (2) one block: exclusive scan of the counts into cursors (and counts reset for the next batch);
+// (3) every signature takes a slot of its bucket (LDS ranks per block, one global atomicAdd per
+//     non-empty bucket per block) and writes its index there.  Order inside a bucket is arbitrary:
+//     K1 writes each signature's digest to its own index, so verdicts do not depend on it.
+static_assert(CBFT_SHA_BUCKETS == 256, "the bucket kernels run one thread per bucket in 256-thread blocks");
+__global__ void __launch_bounds__(256) ed25519_bucket_count_kernel(const Ed25519Batch b, uint32_t* counts) {
+  __shared__ uint32_t hist[CBFT_SHA_BUCKETS];
+  hist[threadIdx.x] = 0;
+  __syncthreads();
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= b.n) return;
+  if (i < b.n) atomicAdd(&hist[hash_bucket(b, i)], 1u);
+  __syncthreads();
+  if (hist[threadIdx.x]) atomicAdd(&counts[threadIdx.x], hist[threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(256) ed25519_bucket_scan_kernel(uint32_t* counts, uint32_t* cursors) {
+  __shared__ uint32_t v[CBFT_SHA_BUCKETS];
+  const uint32_t t = threadIdx.x;
+  v[t] = counts[t];
+  __syncthreads();
+  for (uint32_t d = 1; d < CBFT_SHA_BUCKETS; d <<= 1) {  // inclusive Hillis-Steele scan
+    const uint32_t x = t >= d ? v[t - d] : 0u;
+    __syncthreads();
+    v[t] += x;
+    __syncthreads();
+  }
+  cursors[t] = v[t] - counts[t];
+  counts[t] = 0;  // ready for the next batch's counts
+}
+
+__global__ void __launch_bounds__(256) ed25519_bucket_scatter_kernel(const Ed25519Batch b, uint32_t* cursors,
+                                                                     uint32_t* perm) {
+  __shared__ uint32_t hist[CBFT_SHA_BUCKETS], base[CBFT_SHA_BUCKETS];
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t k = 0, rank = 0;
+  if (i < b.n) {
+    k = hash_bucket(b, i);
+    rank = atomicAdd(&hist[k], 1u);
+  }
+  __syncthreads();
+  if (hist[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursors[threadIdx.x], hist[threadIdx.x]);
+  __syncthreads();
+  if (i < b.n) perm[base[k] + rank] = (uint32_t)i;
+}
+
+__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const Ed25519Batch b, const uint32_t* perm,
+                                                                          uint32_t* h_soa, uint8_t* flags) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= b.n) return;
+  const size_t i = perm ? (size_t)perm[g] : g;
   uint32_t hw[8];
   bool flag;
   ed25519_hash_sig(b, i, hw, flag);
@@ -983,6 +1041,9 @@ __global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed2551
 // its entry is requested.
 // ---------------------------------------------------------------------------------------
 #define COMB2_BLOCK 128
+#ifndef CBFT_LADDER_MUL2
+#define CBFT_LADDER_MUL2 0
+#endif
 #define COMB2_MAX_STEPS 24  // additions per lane: radix-2^8 keys + radix-2^16 B = 48 positions
 #ifndef CBFT_COMB2_MIN_WAVES
 #define CBFT_COMB2_MIN_WAVES 2
@@ -1088,6 +1149,39 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
       dnext = digit(jj + 2u);
       request(slot, entry(jj + 2u, dnext));
     }
+#if CBFT_LADDER_MUL2
+    // the same addition with its independent products paired (fe_mul2: two mad chains
+    // interleaved per column): (A, B), C, (T, X), (Y, Z)
+    {
+      ge_p1p1 t;
+      fe A, B, C, D, s1, s2, e1, e2;
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        e1.v[k] = neg ? ew[9 + k] : ew[k];
+        e2.v[k] = neg ? ew[k] : ew[9 + k];
+      }
+      fe_add(s1, P.Y, P.X);
+      fe_sub(s2, P.Y, P.X);
+      fe_mul2(A, s1, e1, B, s2, e2);
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) e1.v[k] = ew[18 + k];
+      fe_mul(C, e1, P.T);
+      fe_add(D, P.Z, P.Z);
+      fe_sub(t.X, A, B);
+      fe_add(t.Y, A, B);
+      fe_add(s1, D, C);
+      fe_carry(s1);
+      fe_sub(e1, D, C);
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        t.Z.v[k] = neg ? e1.v[k] : s1.v[k];
+        t.T.v[k] = neg ? s1.v[k] : e1.v[k];
+      }
+      fe_mul2(P.T, t.X, t.Y, P.X, t.X, t.T);
+      fe_mul2(P.Y, t.Y, t.Z, P.Z, t.Z, t.T);
+    }
+  }
+#else
     ge_p1p1 t;
     {
       // niels (y+x, y-x, 2dxy), negated by swapping y+x <-> y-x and C <-> -C (ge_add_mem)
@@ -1120,6 +1214,7 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
     fe_mul(P.Y, t.Y, t.Z);
     fe_mul(P.Z, t.Z, t.T);
   }
+#endif
   quad_combine<0xB1>(P, false);  // P += partner lane's P
   if (live && q == 0) {
     fe_store_soa(xyz_soa, b.n, i, P.X);
@@ -1196,7 +1291,15 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   if (order && order->wait && order->hash && (e = hipStreamWaitEvent(stream, order->done[0], 0)) != hipSuccess)
     return e;
   if (ev) (void)hipEventRecord(ev[0], stream);
-  hipLaunchKernelGGL(ed25519_hash_kernel, grid, block, 0, stream, b, w.h_soa, w.flags);
+  const bool sorted = w.perm && w.buckets && b.msg_off;
+  if (sorted) {
+    const dim3 g256((unsigned)((b.n + 255) / 256)), b256(256);
+    hipLaunchKernelGGL(ed25519_bucket_count_kernel, g256, b256, 0, stream, b, w.buckets);
+    hipLaunchKernelGGL(ed25519_bucket_scan_kernel, dim3(1), b256, 0, stream, w.buckets, w.buckets + CBFT_SHA_BUCKETS);
+    hipLaunchKernelGGL(ed25519_bucket_scatter_kernel, g256, b256, 0, stream, b, w.buckets + CBFT_SHA_BUCKETS, w.perm);
+  }
+  hipLaunchKernelGGL(ed25519_hash_kernel, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
+                     w.h_soa, w.flags);
   if (order && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;
   if (order && order->wait && (e = hipStreamWaitEvent(stream, order->done[1], 0)) != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[1], stream);

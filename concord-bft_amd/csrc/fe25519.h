@@ -138,56 +138,63 @@ FE_INLINE void mac1216(uint64_t& acc, uint32_t a) {
 #ifndef CBFT_FE_ASMCOL
 #define CBFT_FE_ASMCOL 1
 #endif
+// Repetition helpers: CBFT_RL_n(M) = M(0) M(1) .. M(n-1) (asm text), CBFT_RC_n(M) the same
+// comma-separated (asm operands).
+#define CBFT_RL_1(M) M(0)
+#define CBFT_RL_2(M) CBFT_RL_1(M) M(1)
+#define CBFT_RL_3(M) CBFT_RL_2(M) M(2)
+#define CBFT_RL_4(M) CBFT_RL_3(M) M(3)
+#define CBFT_RL_5(M) CBFT_RL_4(M) M(4)
+#define CBFT_RL_6(M) CBFT_RL_5(M) M(5)
+#define CBFT_RL_7(M) CBFT_RL_6(M) M(6)
+#define CBFT_RL_8(M) CBFT_RL_7(M) M(7)
+#define CBFT_RL_9(M) CBFT_RL_8(M) M(8)
+#define CBFT_RL_10(M) CBFT_RL_9(M) M(9)
+#define CBFT_RC_1(M) M(0)
+#define CBFT_RC_2(M) CBFT_RC_1(M), M(1)
+#define CBFT_RC_3(M) CBFT_RC_2(M), M(2)
+#define CBFT_RC_4(M) CBFT_RC_3(M), M(3)
+#define CBFT_RC_5(M) CBFT_RC_4(M), M(4)
+#define CBFT_RC_6(M) CBFT_RC_5(M), M(5)
+#define CBFT_RC_7(M) CBFT_RC_6(M), M(6)
+#define CBFT_RC_8(M) CBFT_RC_7(M), M(7)
+#define CBFT_RC_9(M) CBFT_RC_8(M), M(8)
+#define CBFT_RC_10(M) CBFT_RC_9(M), M(9)
+
 #define CBFT_MC_LINE(p) "v_mad_u64_u32 %[acc], %[cc], %[x" #p "], %[y" #p "], %[acc]\n\t"
 #define CBFT_MC_IN(p) [x##p] "v"(x[p]), [y##p] "v"(y[p])
+#define CBFT_MC_CASE(n) \
+  else if constexpr (N == n) asm(CBFT_RL_##n(CBFT_MC_LINE) : [acc] "+v"(acc), [cc] "=s"(cc) : CBFT_RC_##n(CBFT_MC_IN));
 // acc += sum_{p < N} x[p] * y[p] as one dependent v_mad_u64_u32 chain (one asm statement)
 template <int N>
 FE_INLINE void mad_chain(uint64_t& acc, const uint32_t* x, const uint32_t* y) {
   uint64_t cc;
-  if constexpr (N == 1) {
-    asm(CBFT_MC_LINE(0) : [acc] "+v"(acc), [cc] "=s"(cc) : CBFT_MC_IN(0));
-  } else if constexpr (N == 2) {
-    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) : [acc] "+v"(acc), [cc] "=s"(cc) : CBFT_MC_IN(0), CBFT_MC_IN(1));
-  } else if constexpr (N == 3) {
-    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2)
-        : [acc] "+v"(acc), [cc] "=s"(cc) : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2));
-  } else if constexpr (N == 4) {
-    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3)
-        : [acc] "+v"(acc), [cc] "=s"(cc) : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3));
-  } else if constexpr (N == 5) {
-    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3) CBFT_MC_LINE(4)
-        : [acc] "+v"(acc), [cc] "=s"(cc)
-        : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3), CBFT_MC_IN(4));
-  } else if constexpr (N == 6) {
-    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3) CBFT_MC_LINE(4) CBFT_MC_LINE(5)
-        : [acc] "+v"(acc), [cc] "=s"(cc)
-        : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3), CBFT_MC_IN(4), CBFT_MC_IN(5));
-  } else if constexpr (N == 7) {
-    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3) CBFT_MC_LINE(4) CBFT_MC_LINE(5)
-            CBFT_MC_LINE(6)
-        : [acc] "+v"(acc), [cc] "=s"(cc)
-        : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3), CBFT_MC_IN(4), CBFT_MC_IN(5), CBFT_MC_IN(6));
-  } else if constexpr (N == 8) {
-    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3) CBFT_MC_LINE(4) CBFT_MC_LINE(5)
-            CBFT_MC_LINE(6) CBFT_MC_LINE(7)
-        : [acc] "+v"(acc), [cc] "=s"(cc)
-        : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3), CBFT_MC_IN(4), CBFT_MC_IN(5), CBFT_MC_IN(6),
-          CBFT_MC_IN(7));
-  } else if constexpr (N == 9) {
-    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3) CBFT_MC_LINE(4) CBFT_MC_LINE(5)
-            CBFT_MC_LINE(6) CBFT_MC_LINE(7) CBFT_MC_LINE(8)
-        : [acc] "+v"(acc), [cc] "=s"(cc)
-        : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3), CBFT_MC_IN(4), CBFT_MC_IN(5), CBFT_MC_IN(6),
-          CBFT_MC_IN(7), CBFT_MC_IN(8));
-  } else if constexpr (N == 10) {
-    asm(CBFT_MC_LINE(0) CBFT_MC_LINE(1) CBFT_MC_LINE(2) CBFT_MC_LINE(3) CBFT_MC_LINE(4) CBFT_MC_LINE(5)
-            CBFT_MC_LINE(6) CBFT_MC_LINE(7) CBFT_MC_LINE(8) CBFT_MC_LINE(9)
-        : [acc] "+v"(acc), [cc] "=s"(cc)
-        : CBFT_MC_IN(0), CBFT_MC_IN(1), CBFT_MC_IN(2), CBFT_MC_IN(3), CBFT_MC_IN(4), CBFT_MC_IN(5), CBFT_MC_IN(6),
-          CBFT_MC_IN(7), CBFT_MC_IN(8), CBFT_MC_IN(9));
-  } else {
-    static_assert(N >= 1 && N <= 10, "mad_chain: 1..10 products");
+  static_assert(N >= 1 && N <= 10, "mad_chain: 1..10 products");
+  if constexpr (N == 0) {
   }
+  CBFT_MC_CASE(1) CBFT_MC_CASE(2) CBFT_MC_CASE(3) CBFT_MC_CASE(4) CBFT_MC_CASE(5)
+  CBFT_MC_CASE(6) CBFT_MC_CASE(7) CBFT_MC_CASE(8) CBFT_MC_CASE(9) CBFT_MC_CASE(10)
+}
+
+// Two independent chains in one asm statement, their mads alternating: a1 += sum x y,
+// a2 += sum u w (a wave then always has an independent mad ready behind a dependent one).
+#define CBFT_MC2_LINE(p)                                                  \
+  "v_mad_u64_u32 %[a1], %[c1], %[x" #p "], %[y" #p "], %[a1]\n\t"       \
+  "v_mad_u64_u32 %[a2], %[c2], %[u" #p "], %[w" #p "], %[a2]\n\t"
+#define CBFT_MC2_IN(p) [x##p] "v"(x[p]), [y##p] "v"(y[p]), [u##p] "v"(u[p]), [w##p] "v"(w[p])
+#define CBFT_MC2_CASE(n)                                                                                  \
+  else if constexpr (N == n) asm(CBFT_RL_##n(CBFT_MC2_LINE)                                               \
+                                 : [a1] "+v"(a1), [a2] "+v"(a2), [c1] "=s"(c1), [c2] "=s"(c2)               \
+                                 : CBFT_RC_##n(CBFT_MC2_IN));
+template <int N>
+FE_INLINE void mad_chain2(uint64_t& a1, const uint32_t* x, const uint32_t* y, uint64_t& a2, const uint32_t* u,
+                          const uint32_t* w) {
+  uint64_t c1, c2;
+  static_assert(N >= 1 && N <= 10, "mad_chain2: 1..10 products");
+  if constexpr (N == 0) {
+  }
+  CBFT_MC2_CASE(1) CBFT_MC2_CASE(2) CBFT_MC2_CASE(3) CBFT_MC2_CASE(4) CBFT_MC2_CASE(5)
+  CBFT_MC2_CASE(6) CBFT_MC2_CASE(7) CBFT_MC2_CASE(8) CBFT_MC2_CASE(9) CBFT_MC2_CASE(10)
 }
 
 // Column k of a x b (products a_i b_{k-i}) plus, when F, a leading fold term f * 1216, as one chain
@@ -272,6 +279,77 @@ FE_INLINE void fe_sq_lo_cols(uint64_t& acc, uint32_t* o, const uint32_t* h, cons
     acc >>= 29;
     fe_sq_lo_cols<K + 1>(acc, o, h, a, a2);
   }
+}
+
+// Two independent products, r1 = a1 b1 and r2 = a2 b2, column by column with the two mad chains
+// interleaved in one asm statement per column (same arithmetic as fe_mul for each).
+template <int K, bool F>
+FE_INLINE void fe_column2(uint64_t& acc1, const fe& a1, const fe& b1, uint32_t f1, uint64_t& acc2, const fe& a2,
+                          const fe& b2, uint32_t f2) {
+  constexpr int LO = K < FE_LIMBS ? 0 : K - FE_LIMBS + 1;
+  constexpr int HI = K < FE_LIMBS ? K : FE_LIMBS - 1;
+  constexpr int N = HI - LO + 1 + (F ? 1 : 0);
+  uint32_t x[N], y[N], u[N], w[N];
+  int p = 0;
+  if (F) {
+    x[0] = f1;
+    y[0] = 1216u;
+    u[0] = f2;
+    w[0] = 1216u;
+    p = 1;
+  }
+#pragma unroll
+  for (int i = LO; i <= HI; i++, p++) {
+    x[p] = a1.v[i];
+    y[p] = b1.v[K - i];
+    u[p] = a2.v[i];
+    w[p] = b2.v[K - i];
+  }
+  mad_chain2<N>(acc1, x, y, acc2, u, w);
+}
+template <int K>
+FE_INLINE void fe_mul2_hi_cols(uint64_t& t1, uint32_t* h1, const fe& a1, const fe& b1, uint64_t& t2, uint32_t* h2,
+                               const fe& a2, const fe& b2) {
+  if constexpr (K < 17) {
+    fe_column2<K, false>(t1, a1, b1, 0u, t2, a2, b2, 0u);
+    h1[K - 9] = (uint32_t)t1 & FE_MASK;
+    t1 >>= 29;
+    h2[K - 9] = (uint32_t)t2 & FE_MASK;
+    t2 >>= 29;
+    fe_mul2_hi_cols<K + 1>(t1, h1, a1, b1, t2, h2, a2, b2);
+  }
+}
+template <int K>
+FE_INLINE void fe_mul2_lo_cols(uint64_t& c1, uint32_t* o1, const uint32_t* h1, const fe& a1, const fe& b1,
+                               uint64_t& c2, uint32_t* o2, const uint32_t* h2, const fe& a2, const fe& b2) {
+  if constexpr (K < 9) {
+    fe_column2<K, true>(c1, a1, b1, h1[K], c2, a2, b2, h2[K]);
+    o1[K] = (uint32_t)c1 & FE_MASK;
+    c1 >>= 29;
+    o2[K] = (uint32_t)c2 & FE_MASK;
+    c2 >>= 29;
+    fe_mul2_lo_cols<K + 1>(c1, o1, h1, a1, b1, c2, o2, h2, a2, b2);
+  }
+}
+FE_INLINE void fe_mul_final(fe& o, uint64_t acc) {
+  uint64_t w = acc * 1216ull + (uint64_t)o.v[0];
+  o.v[0] = (uint32_t)w & FE_MASK;
+  o.v[1] += (uint32_t)(w >> 29);
+}
+// r1 = a1 * b1, r2 = a2 * b2 (either output may alias any input)
+FE_INLINE void fe_mul2(fe& r1, const fe& a1, const fe& b1, fe& r2, const fe& a2, const fe& b2) {
+  fe o1, o2;
+  uint32_t h1[9], h2[9];
+  uint64_t t1 = 0, t2 = 0;
+  fe_mul2_hi_cols<9>(t1, h1, a1, b1, t2, h2, a2, b2);
+  h1[8] = (uint32_t)t1;
+  h2[8] = (uint32_t)t2;
+  uint64_t c1 = 0, c2 = 0;
+  fe_mul2_lo_cols<0>(c1, o1.v, h1, a1, b1, c2, o2.v, h2, a2, b2);
+  fe_mul_final(o1, c1);
+  fe_mul_final(o2, c2);
+  r1 = o1;
+  r2 = o2;
 }
 
 template <bool C = CBFT_FE_CHAIN>

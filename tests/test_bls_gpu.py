@@ -439,3 +439,24 @@ def test_keyset_rotation_per_checkpoint_window(ctx):
     finally:
         for kid in loaded.values():
             ctx.bls_unload_keys(kid)
+
+
+def test_sign_row_ladder_edge_scalars(ctx):
+    """The row-parallel signature (GLV halves, odd-digit windows, selects instead of branches)
+    equals the oracle's sk * g1_map(msg) on scalars that stress the decomposition: 1, 2, 3, r - 1,
+    r - 2, 2^127 +- 1, 2^128, both nontrivial cube roots w of unity mod r and w +- 1 (a GLV half
+    is 0 or +-1), and random keys (even and odd halves of both signs)."""
+    g = 2
+    while pow(g, (B.R - 1) // 3, B.R) == 1:
+        g += 1
+    w = pow(g, (B.R - 1) // 3, B.R)
+    assert (w * w + w + 1) % B.R == 0
+    scal = [1, 2, 3, B.R - 1, B.R - 2, (1 << 127) - 1, 1 << 127, (1 << 127) + 1, 1 << 128, (1 << 200) + 12345]
+    for lam in (w, w * w % B.R):
+        scal += [lam, lam + 1, lam - 1, (2 * lam) % B.R, B.R - lam]
+    rng = random.Random(99)
+    scal += [rng.randrange(1, B.R) for _ in range(24)]
+    msgs = [b"", b"x" * 70, bytes(range(32))]
+    for i, sk in enumerate(scal):
+        m = msgs[i % 3]
+        assert ctx.bls_sign(sk, 1 + i, m) == B.sign_share(sk, 1 + i, m), (i, hex(sk))
