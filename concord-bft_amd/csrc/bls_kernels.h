@@ -63,4 +63,9 @@ hipError_t cbft_bls_launch_sign(const uint8_t* d_msg, uint32_t len, const uint32
 // cbft_bls_launch_hash first; constant operation sequence in the secret scalar
 hipError_t cbft_bls_launch_sign_row(const uint32_t* d_H, const uint32_t* d_sk, const uint8_t* d_msg, uint32_t len,
                                     uint32_t id, uint8_t* d_out37, hipStream_t s);
+// vk = sk * g2 as a row-parallel fixed-base comb (bls_keys.hip): the table (cbft_bls_pub_table_words
+// words) is built once by cbft_bls_launch_pub_table; constant operation sequence in sk
+size_t cbft_bls_pub_table_words();
+hipError_t cbft_bls_launch_pub_table(uint32_t* d_tbl, hipStream_t s);
+hipError_t cbft_bls_launch_pubkey_row(const uint32_t* d_tbl, const uint32_t* d_sk, uint8_t* d_out65, hipStream_t s);
 hipError_t cbft_bls_launch_pubkey(const uint32_t* d_sk, uint8_t* d_out65, hipStream_t s);

@@ -14,6 +14,7 @@
 
 #include "bls_common.h"
 #include "bn254_g2wave.h"
+#include "bn254_g2row.h"
 
 #define LINE_SCRATCH_WORDS (BN_ATE_LINES * 36)  // g2_precompute_lines_batch scratch per key
 
@@ -387,5 +388,181 @@ hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok
 size_t cbft_bls_g2_sum_tmp_words() { return (size_t)2 * BLS_G2_PART_WORDS * G2S_MAX_PARTS; }
 hipError_t cbft_bls_launch_pubkey(const uint32_t* d_sk, uint8_t* d_out65, hipStream_t s) {
   hipLaunchKernelGGL(bls_pubkey_kernel, dim3(1), dim3(64), 0, s, d_sk, d_out65);
+  return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------ public key
+// vk = sk * g2 (IThresholdSigner::getShareVerificationKey, BlsThresholdSigner's publicKey_) as a
+// fixed-base comb: g2 is fixed, so its radix-16 multiples are precomputed once per context,
+//   PUB_T[j][e] = (2e + 1) 16^j g2,  j = 0..63, e = 0..7   (affine, normalised Montgomery limbs)
+// and sk = sum_j d_j 16^j with ODD digits d_j = 2 u_j - 15, u = (sk + 16^64 - 1) / 2 (sk is made
+// odd first and g2 subtracted at the end by a select), so the key is 63 mixed additions of
+// +-PUB_T[j][(|d_j| - 1) / 2]: every entry read and chosen by selects, every sign by a select,
+// the same instruction stream for every key.  Going up from position 0, the partial sum is an odd
+// multiple below 16^j g2 in magnitude, so no addition meets +-its addend (never exceptional).
+// Z is inverted blinded (Z b, variable time, times b; b from SHA-256 of the key).
+#define PUB_POS 64
+#define PUB_ENT 8
+#define PUB_WORDS 36  // x.a | x.b | y.a | y.b, 9 limbs each
+
+__device__ __forceinline__ void f_canon_limbs(uint32_t* o, fp x) {  // canonical Montgomery limbs
+  f_canon(x);
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) o[i] = x.v[i];
+}
+
+// one lane per position j: 16^j g2 by 4 j doublings, then its odd multiples, affine (public)
+__global__ void __launch_bounds__(64) bls_pub_table_kernel(uint32_t* tbl) {
+  const int j = threadIdx.x;
+  if (j >= PUB_POS || blockIdx.x != 0) return;
+  g2j P;
+  fp2_load(P.X, Bn254Consts::G2X);
+  fp2_load(P.Y, Bn254Consts::G2Y);
+  fp2_one(P.Z);
+#pragma nounroll
+  for (int d = 0; d < 4 * j; d++) {
+    g2j t;
+    g2_dbl_j(t, P);
+    P = t;
+  }
+  g2j P2, E = P;
+  g2_dbl_j(P2, P);
+#pragma nounroll
+  for (int e = 0; e < PUB_ENT; e++) {
+    if (e) {
+      g2j t;
+      g2_add_j(t, E, P2);
+      E = t;
+    }
+    g2a a;
+    g2_to_affine<true>(a, E);
+    uint32_t* o = tbl + ((size_t)j * PUB_ENT + e) * PUB_WORDS;
+    f_canon_limbs(o, a.x.a);
+    f_canon_limbs(o + 9, a.x.b);
+    f_canon_limbs(o + 18, a.y.a);
+    f_canon_limbs(o + 27, a.y.b);
+  }
+}
+
+__global__ void __launch_bounds__(64) bls_pubkey_row_kernel(const uint32_t* tbl, const uint32_t* sk, uint8_t* out65) {
+  using Ctx = G2RowCtx<uint32_t, uint64_t>;
+  const Ctx c(0u);
+  uint32_t k[8];
+#pragma unroll
+  for (int i = 0; i < 8; i++) k[i] = sk[i];
+  const uint32_t even = (k[0] & 1u) ^ 1u;
+  uint32_t u[8];
+  {  // u = (sk + even + 2^256 - 1) / 2 = 2^255 + (sk + even - 1) / 2
+    uint64_t cy = 0;
+    uint32_t t[8];
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      cy += (uint64_t)k[i] + (i == 0 ? even : 0u) + 0xffffffffu;
+      t[i] = (uint32_t)cy;
+      cy >>= 32;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) u[i] = (t[i] >> 1) | (i < 7 ? (t[i + 1] << 31) : ((uint32_t)cy << 31));
+  }
+  auto pick = [&](int j, F2R<uint32_t>& qx, F2R<uint32_t>& qy) {
+    const uint32_t nib = (u[j >> 3] >> (4 * (j & 7))) & 15u;  // d = 2 nib - 15
+    const uint32_t dn = nib < 8u ? 1u : 0u;
+    const uint32_t m = dn ? 7u - nib : nib - 8u;
+    const uint32_t* base = tbl + (size_t)j * PUB_ENT * PUB_WORDS;
+    qx = f2r_ld(base);
+    qy = f2r_ld(base + 18);
+#pragma unroll
+    for (int e = 1; e < PUB_ENT; e++) {
+      const F2R<uint32_t> ex = f2r_ld(base + e * PUB_WORDS), ey = f2r_ld(base + e * PUB_WORDS + 18);
+      const bool hit = m == (uint32_t)e;
+      qx.a = rf_sel(hit, ex.a, qx.a);
+      qx.b = rf_sel(hit, ex.b, qx.b);
+      qy.a = rf_sel(hit, ey.a, qy.a);
+      qy.b = rf_sel(hit, ey.b, qy.b);
+    }
+    const F2R<uint32_t> ny{c.sub(c.zero, qy.a), c.sub(c.zero, qy.b)};  // -y + 8q (< 9q)
+    qy.a = c.red(rf_sel(dn != 0u, ny.a, qy.a));
+    qy.b = c.red(rf_sel(dn != 0u, ny.b, qy.b));
+  };
+  G2R<uint32_t> acc;
+  {
+    F2R<uint32_t> qx, qy;
+    pick(0, qx, qy);
+    acc.X = qx;
+    acc.Y = qy;
+    acc.Z = F2R<uint32_t>{c.one, c.zero};
+  }
+#pragma nounroll
+  for (int j = 1; j < PUB_POS; j++) {
+    F2R<uint32_t> qx, qy;
+    pick(j, qx, qy);
+    bool same_y;
+    g2r_madd<false>((F2R<uint32_t>*)nullptr, acc, qx, qy, c, same_y);
+  }
+  bool inf = false;
+  {  // undo the odd fix: acc - g2 when sk was even, computed always, kept by a select
+    const F2R<uint32_t> gx = f2r_ld(tbl), gy0 = f2r_ld(tbl + 18);
+    const F2R<uint32_t> gy{c.red(c.sub(c.zero, gy0.a)), c.red(c.sub(c.zero, gy0.b))};
+    G2R<uint32_t> t = acc;
+    bool same_y = false;
+    const bool ok = g2r_madd<false>((F2R<uint32_t>*)nullptr, t, gx, gy, c, same_y);  // false only for sk = 0
+    const bool take = even != 0u;
+    acc.X.a = rf_sel(take, t.X.a, acc.X.a);
+    acc.X.b = rf_sel(take, t.X.b, acc.X.b);
+    acc.Y.a = rf_sel(take, t.Y.a, acc.Y.a);
+    acc.Y.b = rf_sel(take, t.Y.b, acc.Y.b);
+    acc.Z.a = rf_sel(take, t.Z.a, acc.Z.a);
+    acc.Z.b = rf_sel(take, t.Z.b, acc.Z.b);
+    inf = take && !ok;
+  }
+  g2j J;
+  rf_to_fe(J.X.a, acc.X.a);
+  rf_to_fe(J.X.b, acc.X.b);
+  rf_to_fe(J.Y.a, acc.Y.a);
+  rf_to_fe(J.Y.b, acc.Y.b);
+  rf_to_fe(J.Z.a, acc.Z.a);
+  rf_to_fe(J.Z.b, acc.Z.b);
+  g2a a;
+  if (inf) {
+    a.inf = true;
+    fp2_zero(a.x);
+    fp2_zero(a.y);
+  } else {
+    uint32_t bw[8];
+    {
+      uint8_t buf[32], dig[32];
+      for (int i = 0; i < 8; i++)
+        for (int q = 0; q < 4; q++) buf[4 * i + q] = (uint8_t)(k[i] >> (8 * q)) ^ 0x5c;
+      sha256(dig, buf, 32);
+      for (int i = 0; i < 8; i++)
+        bw[i] = (uint32_t)dig[4 * i] | ((uint32_t)dig[4 * i + 1] << 8) | ((uint32_t)dig[4 * i + 2] << 16) |
+                ((uint32_t)dig[4 * i + 3] << 24);
+      bw[7] &= 0x1fffffffu;  // < 2^253 < q
+      bw[0] |= (bw[0] | bw[1] | bw[2] | bw[3] | bw[4] | bw[5] | bw[6] | bw[7]) == 0u ? 1u : 0u;
+      for (int i = 0; i < 32; i++) buf[i] = 0;
+    }
+    fp b;
+    f_from_words(b, bw);
+    fp2 zb, zi, zi2;
+    fp2_mul_fp(zb, J.Z, b);
+    fp2_inv<true>(zi, zb);  // (Z b)^-1, variable time on a blinded value
+    fp2_mul_fp(zi, zi, b);
+    fp2_sqr(zi2, zi);
+    fp2_mul(a.x, J.X, zi2);
+    fp2_mul(zi2, zi2, zi);
+    fp2_mul(a.y, J.Y, zi2);
+    a.inf = false;
+    for (int i = 0; i < 8; i++) bw[i] = 0;
+  }
+  if (__lane_id() == 0) g2_compress(out65, a);
+}
+
+size_t cbft_bls_pub_table_words() { return (size_t)PUB_POS * PUB_ENT * PUB_WORDS; }
+hipError_t cbft_bls_launch_pub_table(uint32_t* d_tbl, hipStream_t s) {
+  hipLaunchKernelGGL(bls_pub_table_kernel, dim3(1), dim3(64), 0, s, d_tbl);
+  return hipGetLastError();
+}
+hipError_t cbft_bls_launch_pubkey_row(const uint32_t* d_tbl, const uint32_t* d_sk, uint8_t* d_out65, hipStream_t s) {
+  hipLaunchKernelGGL(bls_pubkey_row_kernel, dim3(1), dim3(64), 0, s, d_tbl, d_sk, d_out65);
   return hipGetLastError();
 }

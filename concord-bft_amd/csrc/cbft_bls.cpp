@@ -523,7 +523,22 @@ int cbft_bls_public_key(cbft_ctx* c, const uint8_t* sk32, uint8_t* out65) {
   CBFT_HIP(c->bls_lambda.reserve(8 * 4));
   CBFT_HIP(c->bls_out.reserve(65));
   CBFT_HIP(hipMemcpyAsync(c->bls_lambda.p, w, sizeof(w), hipMemcpyHostToDevice, c->stream));
-  CBFT_HIP(cbft_bls_launch_pubkey(c->bls_lambda.as<uint32_t>(), c->bls_out.as<uint8_t>(), c->stream));
+  // fixed-base comb of g2 on row-parallel Fp (its 64 x 8 table built once per context, ~10 ms),
+  // unless $CBFT_BLS_PUBKEY=lane (the one-lane Montgomery ladder, 17 ms: the A/B reference)
+  static const bool lane = [] {
+    const char* e = getenv("CBFT_BLS_PUBKEY");
+    return e && strcmp(e, "lane") == 0;
+  }();
+  if (lane) {
+    CBFT_HIP(cbft_bls_launch_pubkey(c->bls_lambda.as<uint32_t>(), c->bls_out.as<uint8_t>(), c->stream));
+  } else {
+    if (!c->bls_pub_tbl.p) {
+      CBFT_HIP(c->bls_pub_tbl.reserve(cbft_bls_pub_table_words() * sizeof(uint32_t)));
+      CBFT_HIP(cbft_bls_launch_pub_table(c->bls_pub_tbl.as<uint32_t>(), c->stream));
+    }
+    CBFT_HIP(cbft_bls_launch_pubkey_row(c->bls_pub_tbl.as<uint32_t>(), c->bls_lambda.as<uint32_t>(),
+                                        c->bls_out.as<uint8_t>(), c->stream));
+  }
   CBFT_HIP(hipMemcpyAsync(out65, c->bls_out.p, 65, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipMemsetAsync(c->bls_lambda.p, 0, sizeof(w), c->stream));  // the secret scalar leaves the device
   CBFT_HIP(hipStreamSynchronize(c->stream));

@@ -286,7 +286,8 @@ void cbft_close(cbft_ctx* c) {
   }
   for (DevBuf* b : {&c->bls_gen_lines, &c->bls_msg, &c->bls_H, &c->bls_shares, &c->bls_valid, &c->bls_sig,
                     &c->bls_ids, &c->bls_use, &c->bls_lambda, &c->bls_partial, &c->bls_out,
-                    &c->bls_ms_ok, &c->bls_bitmap, &c->bls_inv, &c->bls_first, &c->bls_flag, &c->bls_g2tmp})
+                    &c->bls_ms_ok, &c->bls_bitmap, &c->bls_inv, &c->bls_first, &c->bls_flag, &c->bls_g2tmp,
+                    &c->bls_pub_tbl})
     b->release();
   (void)hipDeviceSynchronize();  // device-path batches may still run on caller streams
   for (DevBuf* b : {&c->base_table, &c->base_comb, &c->verdicts, &c->sig, &c->msg, &c->off, &c->len, &c->kidx, &c->pk,
@@ -294,7 +295,7 @@ void cbft_close(cbft_ctx* c) {
     b->release();
   c->hstage.release();
   for (WorkSlot& w : c->slots) {
-    for (DevBuf* b : {&w.h, &w.flags, &w.xyz, &w.ps_tbl, &w.ps_aok}) b->release();
+    for (DevBuf* b : {&w.h, &w.flags, &w.xyz, &w.ps_tbl, &w.ps_aok, &w.perm, &w.buckets}) b->release();
     if (w.done) (void)hipEventDestroy(w.done);
   }
   for (hipEvent_t& e : c->ev)

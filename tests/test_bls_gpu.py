@@ -460,3 +460,16 @@ def test_sign_row_ladder_edge_scalars(ctx):
     for i, sk in enumerate(scal):
         m = msgs[i % 3]
         assert ctx.bls_sign(sk, 1 + i, m) == B.sign_share(sk, 1 + i, m), (i, hex(sk))
+
+
+def test_public_key_comb_edge_scalars(ctx):
+    """vk = sk * g2 by the fixed-base comb (odd digits, selects): equal to the oracle's sk * g2 for
+    scalars at the recoding's edges (1, 2, 15, 16, 17, 2^252, r - 1, r - 2, even and odd) and random
+    keys, and the same key twice gives the same bytes (the lazily built table is reused)."""
+    rng = random.Random(123)
+    scal = [1, 2, 3, 15, 16, 17, 255, 256, 1 << 252, (1 << 253) + 1, B.R - 1, B.R - 2, B.R - 16]
+    scal += [rng.randrange(1, B.R) for _ in range(12)]
+    for sk in scal:
+        exp = B.g2_to_bytes(B.ec_mul(sk, B.G2_GEN))
+        assert ctx.bls_public_key(sk) == exp, hex(sk)
+    assert ctx.bls_public_key(scal[-1]) == B.g2_to_bytes(B.ec_mul(scal[-1], B.G2_GEN))
