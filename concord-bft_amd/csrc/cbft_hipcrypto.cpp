@@ -743,7 +743,8 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     for (hipEvent_t& e : c->stage_done)
       if (!e) CBFT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     order.wait = c->stage_used;
-    order.hash = c->stage_order != 2;
+    order.hash = c->stage_order != 2;    // 2: ladders only
+    order.ladder = c->stage_order != 3;  // 3: hashes only (two batches' ladders may share the SIMDs)
     order.done[0] = c->stage_done[0];
     order.done[1] = c->stage_done[1];
   }

@@ -156,7 +156,8 @@ hipError_t cbft_ed25519_launch_prep(const uint8_t* d_pk, size_t nunits, uint32_t
 // (recorded by the previous batch, maybe on another stream); both are re-recorded here.
 struct StageOrder {
   bool wait;
-  bool hash;  // also order the hashes (else only the ladders)
+  bool hash;    // order the hashes
+  bool ladder;  // order the ladders
   hipEvent_t done[2];
 };
 hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& w, hipStream_t stream,

@@ -542,6 +542,14 @@ __global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519B
 // xor 1, xor 2) add the four partial sums: every lane of the quad ends with
 // R' = [S]B + [h](-A).  4,096 waves at 64K signatures: 4 waves per SIMD.
 // ---------------------------------------------------------------------------------------
+// CBFT_LADDER_LAZYSUM: the comb additions feed D + C (D = 2Z, C a product) into the next
+// products without a carry pass.  Its limbs stay < 3 (2^29 + 2^17) < 1.51 * 2^30; it is multiplied
+// by a reduced value (D - C, < 2^29 + 2^17) or by A + B (lazy, < 2^30 + 2^18): a column of nine such
+// products is < 9 * 2^30.59 * 2^30.0003 = 2^63.76, plus the fold (< 2^29 * 1216) and the carry in
+// (< 2^35): below 2^64, and the top column's carry (h8) stays < 2^32.  The product is reduced as usual.
+#ifndef CBFT_LADDER_LAZYSUM
+#define CBFT_LADDER_LAZYSUM 0
+#endif
 #define COMB_STRIDE 32  // words per entry: one 128-B line (y+x | y-x | 2dxy, 9 limbs each, + pad)
 #define COMB_CHUNK 128  // multiples built per table-build lane
 #define COMB_TMP_WORDS_PER_LANE (COMB_CHUNK * CACHED_WORDS)
@@ -882,7 +890,7 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
       fe_sub(t.X, A, B);
       fe_add(t.Y, A, B);
       fe_add(s, D, C);
-      fe_carry(s);
+      if (!CBFT_LADDER_LAZYSUM) fe_carry(s);
       fe_sub(e, D, C);
 #pragma unroll
       for (int k = 0; k < FE_LIMBS; k++) {
@@ -1170,7 +1178,7 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
       fe_sub(t.X, A, B);
       fe_add(t.Y, A, B);
       fe_add(s1, D, C);
-      fe_carry(s1);
+      if (!CBFT_LADDER_LAZYSUM) fe_carry(s1);
       fe_sub(e1, D, C);
 #pragma unroll
       for (int k = 0; k < FE_LIMBS; k++) {
@@ -1201,7 +1209,7 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
       fe_sub(t.X, A, B);
       fe_add(t.Y, A, B);
       fe_add(s, D, C);
-      fe_carry(s);
+      if (!CBFT_LADDER_LAZYSUM) fe_carry(s);
       fe_sub(e, D, C);
 #pragma unroll
       for (int k = 0; k < FE_LIMBS; k++) {
@@ -1301,7 +1309,8 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   hipLaunchKernelGGL(ed25519_hash_kernel, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
                      w.h_soa, w.flags);
   if (order && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;
-  if (order && order->wait && (e = hipStreamWaitEvent(stream, order->done[1], 0)) != hipSuccess) return e;
+  if (order && order->wait && order->ladder && (e = hipStreamWaitEvent(stream, order->done[1], 0)) != hipSuccess)
+    return e;
   if (ev) (void)hipEventRecord(ev[1], stream);
   if (comb && w.comb_lanes == 2) {
     hipLaunchKernelGGL(ed25519_comb2_ladder_kernel, dim3((unsigned)((2 * b.n + COMB2_BLOCK - 1) / COMB2_BLOCK)),

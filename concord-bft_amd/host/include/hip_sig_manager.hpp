@@ -9,12 +9,13 @@
 // no data members of its own.
 //
 //   init(...)          SigManager::init's signature and key mapping (SigManager.cpp:34-111): replica
-//                      keys one index each, client keys one index per id set; the base class is
-//                      constructed with the RSA keys only (its constructor builds Crypto++
-//                      RSAVerifiers, SigManager.cpp:146, and registers RSA client keys for
-//                      getClientsPublicKeys, :151-156), then every principal's verifier is
-//                      replaced by a GPU one (HipEdDSAVerifier / HipRSAVerifier, one object per
-//                      distinct key as the reference shares them, :139-150).  An Ed25519 own key
+//                      keys one index each, client keys one index per id set; every principal
+//                      gets a GPU verifier (HipEdDSAVerifier / HipRSAVerifier, one object per
+//                      distinct key as the reference shares them, :139-150).  The base class is
+//                      constructed without verification keys when the CMF client-key map is
+//                      available (the external clients' keys are recorded for
+//                      getClientsPublicKeys as :151-156 records them), else with the RSA keys
+//                      only (its constructor then builds and records them, :146-156).  An Ed25519 own key
 //                      signs with EdDSASigner; an RSA one with the reference's RSASigner (:138).
 //   verifySig          inherited unchanged: it calls IVerifier::verify, i.e. the GPU verifier
 //                      (concurrent Ed25519 calls are coalesced into batches by the engine).
@@ -238,9 +239,22 @@ class HipSigManager : public bftEngine::impl::SigManager {
     return r;
   }
 
+  // With the CMF client-key map at hand (CBFT_WITH_CLIENT_KEYS_MAP) the base is constructed with
+  // NO verification keys -- it would build a Crypto++ RSAVerifier per RSA key (SigManager.cpp:146)
+  // only for this constructor to replace it -- and the external clients' keys are entered into
+  // the map here, as SigManager.cpp:151-156 enters them.  Without the map the base gets the RSA
+  // subset, which it records itself.
   HipSigManager(PrincipalId myId, uint16_t numReplicas, const std::pair<std::string, Fmt>& myKey, const KeyList& keys,
                 const Mapping& mapping, bool signing, ReplicasInfo& replicasInfo, const RsaSubset& rsa)
+#if defined(CBFT_WITH_CLIENT_KEYS_MAP)
+      : Base(myId, numReplicas, rsa.myKey, KeyList{}, Mapping{}, signing, replicasInfo) {
+    for (const auto& [pid, k] : mapping)
+      if (k < keys.size() && replicasInfo_.isIdOfExternalClient(pid))
+        bftEngine::impl::clientsPublicKeys_.ids_to_keys[pid] =
+            concord::messages::keys_and_signatures::PublicKey{keys[k].first, (uint8_t)keys[k].second};
+#else
       : Base(myId, numReplicas, rsa.myKey, rsa.keys, rsa.mapping, signing, replicasInfo) {
+#endif
     if (!myKey.first.empty() && !mySigner_) mySigner_ = makeSigner(myKey.first, myKey.second);
     std::map<uint16_t, std::shared_ptr<concord::util::crypto::IVerifier>> byIndex;
     for (const auto& [pid, k] : mapping) {

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -14,7 +15,12 @@
 #include <mutex>
 #include <shared_mutex>
 #include <stdexcept>
+#include <thread>
 #include <vector>
+
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #include "cbft_hipcrypto.h"
 
@@ -148,8 +154,14 @@ static int engineRadix() {
 // 40 + 24 pool threads, ReplicaConfig.hpp:202-212): callers queue their request; one of them
 // leads a batch as soon as fewer than maxInflight_ batches are on the GPU, taking everything
 // queued by then.  A lone caller goes straight to the GPU; under load, requests that arrive
-// while batches run are verified together in the next one.  Each request waits on its own
-// condition variable (woken for its verdict or to lead), never on a shared one.
+// while batches run are verified together in the next one.
+//
+// Waiting.  Each request waits on its own 32-bit state word (futex), never on the queue's mutex:
+// the leader of a batch publishes every verdict with one release store per request and wakes
+// only the requests that went to sleep.  A woken request reads its verdict and returns without
+// touching q_mu_ (with condition variables on the queue mutex, the ~20 requests of a batch woke
+// into a convoy on that mutex: round 3's per-request profile).  A waiter first spins for a few
+// microseconds ($CBFT_ENGINE_SPIN_US, default 20) with yields, then sleeps.
 class Ed25519Engine {
  public:
   static constexpr int kMaxInflight = 4;  // profiles/r03_host_bench_sweep.txt (zero-copy, blocking-sync small batches)
@@ -274,40 +286,40 @@ class Ed25519Engine {
     if (sigLen != 64 || len > kMaxMsg) return false;
     LatencyHistogram::Scope timer(recorders().ed25519_verify);
     Pending p{v, data, len, sig, sigLen};
-    std::unique_lock<std::mutex> lk(q_mu_);
-    queue_.push_back(&p);
-    if (!leader_ && inflight_ < maxInflight_) {  // a GPU slot is free: go now, with whatever is queued
-      p.lead = true;
-      leader_ = true;
-    }
-    while (!p.done) {
-      if (!p.lead) {
-        p.cv.wait(lk);  // woken only for this request: its verdict, or its turn to lead
-        continue;
+    {
+      std::lock_guard<std::mutex> lk(q_mu_);
+      queue_.push_back(&p);
+      if (!leader_ && inflight_ < maxInflight_) {  // a GPU slot is free: go now, with whatever is queued
+        p.state.store(kLead, std::memory_order_relaxed);
+        leader_ = true;
       }
-      // lead one batch: everything queued so far (up to kMaxBatch)
-      p.lead = false;
+    }
+    for (;;) {
+      const int st = waitState(p);
+      if (st == kDone) return p.verdict;
+      // kLead: lead one batch, everything queued so far (up to kMaxBatch)
+      p.state.store(kWaiting, std::memory_order_relaxed);
       std::vector<Pending*> batch;
-      if (queue_.size() <= kMaxBatch) {
-        batch.swap(queue_);
-      } else {
-        batch.assign(queue_.begin(), queue_.begin() + kMaxBatch);
-        queue_.erase(queue_.begin(), queue_.begin() + kMaxBatch);
+      {
+        std::lock_guard<std::mutex> lk(q_mu_);
+        if (queue_.size() <= kMaxBatch) {
+          batch.swap(queue_);
+        } else {
+          batch.assign(queue_.begin(), queue_.begin() + kMaxBatch);
+          queue_.erase(queue_.begin(), queue_.begin() + kMaxBatch);
+        }
+        leader_ = false;
+        inflight_++;
+        appointLocked();  // requests that queued meanwhile may lead the next batch if a slot is free
       }
-      leader_ = false;
-      inflight_++;
-      appointLocked();  // requests that queued meanwhile may lead the next batch if a slot is free
-      lk.unlock();
       runBatch(batch);
-      lk.lock();
-      inflight_--;
-      for (Pending* q : batch) {
-        q->done = true;
-        if (q != &p) q->cv.notify_one();
+      {
+        std::lock_guard<std::mutex> lk(q_mu_);
+        inflight_--;
+        appointLocked();
       }
-      appointLocked();
+      for (Pending* q : batch) post(*q, kDone);  // verdicts were written by runBatch
     }
-    return p.verdict;
   }
 
   EngineStats stats() {
@@ -318,27 +330,47 @@ class Ed25519Engine {
 
  private:
   static constexpr size_t kMaxMsg = 0xFFFFFF00u;
+  // request states; a waiter about to sleep marks its word kSleeping (the poster then wakes it)
+  static constexpr int kWaiting = 0, kLead = 1, kDone = 2, kSleeping = 3;
   struct Pending {
     const HipEdDSAVerifier* v;
     const char* data;
     size_t len;
     const char* sig;
     size_t sigLen;
-    bool done = false;
     bool verdict = false;
-    bool lead = false;
-    std::condition_variable cv;
+    std::atomic<int> state{kWaiting};
   };
+  static long futex(std::atomic<int>* w, int op, int val) {
+    return syscall(SYS_futex, reinterpret_cast<int*>(w), op | FUTEX_PRIVATE_FLAG, val, nullptr, nullptr, 0);
+  }
+  // this request's next state (kLead or kDone): spin briefly, then sleep on the futex word
+  int waitState(Pending& p) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+      int st = p.state.load(std::memory_order_acquire);
+      if (st == kLead || st == kDone) return st;
+      if (std::chrono::steady_clock::now() - t0 < spin_) {
+        std::this_thread::yield();
+        continue;
+      }
+      if (st == kWaiting && !p.state.compare_exchange_strong(st, kSleeping, std::memory_order_acq_rel)) continue;
+      futex(&p.state, FUTEX_WAIT, kSleeping);  // returns when the word is no longer kSleeping
+    }
+  }
+  // hand request q its next state; wake it only if it went to sleep
+  static void post(Pending& q, int st) {
+    if (q.state.exchange(st, std::memory_order_acq_rel) == kSleeping) futex(&q.state, FUTEX_WAKE, 1);
+  }
 
   // With no leader and a free GPU slot, the oldest queued request leads the next batch (q_mu_
   // held).  Waking only that one request, and each finished request only once, keeps 64 pool
-  // threads from stampeding on one condition variable at every batch boundary.
+  // threads from stampeding at every batch boundary.
   void appointLocked() {
     if (leader_ || queue_.empty() || inflight_ >= maxInflight_) return;
     Pending* h = queue_.front();
-    h->lead = true;
     leader_ = true;
-    h->cv.notify_one();
+    post(*h, kLead);
   }
 
   void runBatch(std::vector<Pending*>& batch) {
@@ -400,6 +432,10 @@ class Ed25519Engine {
   }();
   bool leader_ = false;
   int inflight_ = 0;
+  std::chrono::microseconds spin_{[] {  // $CBFT_ENGINE_SPIN_US: spin before sleeping (default 20 us)
+    const char* e = std::getenv("CBFT_ENGINE_SPIN_US");
+    return e ? std::atoi(e) : 20;
+  }()};
   std::atomic<uint64_t> batches_{0}, items_{0}, gpu_errors_{0};
 };
 

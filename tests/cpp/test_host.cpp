@@ -530,8 +530,9 @@ static int testAggregatorAndKeySlots() {
   sm->verifySigBatch(items, out);
   CHECK(ctr("signature_verification_failed_on_unrecognized_participant_id") == 1);
   CHECK(agg->Pushes("signature_manager") == 3);
-  std::string cpk = sm->getClientsPublicKeys();  // CMF-encoded; Ed25519 clients are not listed (see header)
+  std::string cpk = sm->getClientsPublicKeys();  // CMF-encoded, every external client's key (SigManager.cpp:151-156)
   CHECK(cpk.size() >= 6);
+  CHECK(cpk.find(c4.getPubKeyHex()) != std::string::npos);
 
   // key rotation: the new key is registered while the old one is still referenced, then the old
   // slot is freed; the second rotation therefore reuses a freed slot and the table does not grow

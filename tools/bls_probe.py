@@ -32,6 +32,9 @@ for s in use:
     bitmap[(i - 1) // 8] |= 1 << ((i - 1) % 8)
 msig = ctx.bls_combine(use, multisig=True)
 assert ctx.bls_verify_multisig(kid, cert.msg, msig, bytes(bitmap))
+sid, sk, share = cert.sign_probe
+assert ctx.bls_sign(sk, sid, cert.msg) == share, "signData differs from the expected share"
+assert ctx.bls_public_key(sk) == cert.vks[sid - 1], "sk * g2 differs from the key set's vk"
 out = {}
 for name, fn in (("keyset_load", lambda: ctx.bls_unload_keys(ctx.bls_load_keys(cert.pk, cert.vks))),
                  ("keyset_load_1key", lambda: ctx.bls_unload_keys(ctx.bls_load_keys(cert.pk, []))),
@@ -39,7 +42,9 @@ for name, fn in (("keyset_load", lambda: ctx.bls_unload_keys(ctx.bls_load_keys(c
                  ("combine", lambda: ctx.bls_combine(use)),
                  ("verify", lambda: ctx.bls_verify(kid, cert.msg, comb)),
                  ("multisig_combine", lambda: ctx.bls_combine(use, multisig=True)),
-                 ("multisig_verify", lambda: ctx.bls_verify_multisig(kid, cert.msg, msig, bytes(bitmap)))):
+                 ("multisig_verify", lambda: ctx.bls_verify_multisig(kid, cert.msg, msig, bytes(bitmap))),
+                 ("sign", lambda: ctx.bls_sign(cert.sign_probe[1], cert.sign_probe[0], cert.msg)),
+                 ("public_key", lambda: ctx.bls_public_key(cert.sign_probe[1]))):
     ts = []
     for _ in range(a.reps):
         t0 = time.perf_counter()

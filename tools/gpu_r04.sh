@@ -9,6 +9,8 @@
 #   pmc_small   PMC passes over the p50 path (batches of 1,024) -> gpurun_out/pmc_ed25519_small.json
 #   pmc_mixed   PMC passes over config #3 -> gpurun_out/pmc_ed25519_mixed.json
 #   pmc_bls     kernel stats + PMC passes over the BLS config #4 probe -> gpurun_out/pmc_bls.json
+#   phases      phase times of the fused small-batch kernel (build/lib_edphases.so, -DCBFT_ED_PHASES=1)
+#   trace       kernel trace of the device-resident two-stream pipeline (overlap of the stages)
 #   ab          interleaved A/B of $LIBS (tools/ab_libs.sh)
 #   san         host-layer ASan+UBSan / TSan runs (make sanitize first)
 set -o pipefail
@@ -51,6 +53,17 @@ for step in "$@"; do
         > gpurun_out/pmc_bls.json || exit 1 ;;
     ab)
       bash tools/ab_libs.sh || exit 1 ;;
+    phases)
+      CBFT_LIB=$R/build/lib_edphases.so timeout -k 10 120 python3 -u tools/ed_small_probe.py > gpurun_out/ed_phases.log 2>&1 \
+        || { echo "phase probe failed"; tail -20 gpurun_out/ed_phases.log; exit 1; }
+      grep -E "us|verdicts" gpurun_out/ed_phases.log | head -20 ;;
+    trace)
+      (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$R/gpurun_out/trace" -o run \
+        -- python3 "$R/tools/dev_pipe_probe.py") > gpurun_out/trace_probe.log 2>&1 \
+        || { echo "trace failed"; tail -20 gpurun_out/trace_probe.log; exit 1; }
+      tail -2 gpurun_out/trace_probe.log
+      f=$(find gpurun_out/trace -name "*kernel_trace.csv" | head -1)
+      python3 tools/trace_timeline.py "$f" ed25519_ --skip 60 --count 40 ;;
     san)
       bash tools/sanitize.sh || { echo "sanitizer runs failed"; exit 1; } ;;
     *) echo "unknown step $step"; exit 2 ;;
