@@ -395,8 +395,8 @@ hipError_t cbft_bls_launch_pubkey(const uint32_t* d_sk, uint8_t* d_out65, hipStr
 // vk = sk * g2 (IThresholdSigner::getShareVerificationKey, BlsThresholdSigner's publicKey_) as a
 // fixed-base comb: g2 is fixed, so its radix-16 multiples are precomputed once per context,
 //   PUB_T[j][e] = (2e + 1) 16^j g2,  j = 0..63, e = 0..7   (affine, normalised Montgomery limbs)
-// and sk = sum_j d_j 16^j with ODD digits d_j = 2 u_j - 15, u = (sk + 16^64 - 1) / 2 (sk is made
-// odd first and g2 subtracted at the end by a select), so the key is 63 mixed additions of
+// and sk = sum_j d_j 16^j with ODD digits d_j = 2 u_j - 15, u = (sk + 16^64 - 1) / 2 (an even sk is
+// replaced by the odd r - sk and the result negated, both by selects), so the key is 63 mixed additions of
 // +-PUB_T[j][(|d_j| - 1) / 2]: every entry read and chosen by selects, every sign by a select,
 // the same instruction stream for every key.  Going up from position 0, the partial sum is an odd
 // multiple below 16^j g2 in magnitude, so no addition meets +-its addend (never exceptional).
@@ -450,14 +450,27 @@ __global__ void __launch_bounds__(64) bls_pubkey_row_kernel(const uint32_t* tbl,
   uint32_t k[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) k[i] = sk[i];
-  const uint32_t even = (k[0] & 1u) ^ 1u;
+  // an even sk is replaced by the odd r - sk (selected, not branched) and the point negated at the
+  // end: k' in [1, r - 1], so no partial sum of the comb ever meets +-its addend mod r
+  const uint32_t even = (k[0] & 1u) ^ 1u, emask = 0u - even;
+  {
+    const uint32_t rw[8] = {0x0000000du, 0xa1000000u, 0x00000010u, 0xff9f8000u,
+                            0x00000007u, 0xba344d80u, 0x40000001u, 0x25236482u};
+    int64_t br = 0;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int64_t d = (int64_t)rw[i] - k[i] + br;
+      k[i] = ((uint32_t)d & emask) | (k[i] & ~emask);
+      br = d >> 32;
+    }
+  }
   uint32_t u[8];
-  {  // u = (sk + even + 2^256 - 1) / 2 = 2^255 + (sk + even - 1) / 2
+  {  // u = (k' + 2^256 - 1) / 2 = 2^255 + (k' - 1) / 2
     uint64_t cy = 0;
     uint32_t t[8];
 #pragma unroll
     for (int i = 0; i < 8; i++) {
-      cy += (uint64_t)k[i] + (i == 0 ? even : 0u) + 0xffffffffu;
+      cy += (uint64_t)k[i] + 0xffffffffu;
       t[i] = (uint32_t)cy;
       cy >>= 32;
     }
@@ -499,22 +512,12 @@ __global__ void __launch_bounds__(64) bls_pubkey_row_kernel(const uint32_t* tbl,
     bool same_y;
     g2r_madd<false>((F2R<uint32_t>*)nullptr, acc, qx, qy, c, same_y);
   }
-  bool inf = false;
-  {  // undo the odd fix: acc - g2 when sk was even, computed always, kept by a select
-    const F2R<uint32_t> gx = f2r_ld(tbl), gy0 = f2r_ld(tbl + 18);
-    const F2R<uint32_t> gy{c.red(c.sub(c.zero, gy0.a)), c.red(c.sub(c.zero, gy0.b))};
-    G2R<uint32_t> t = acc;
-    bool same_y = false;
-    const bool ok = g2r_madd<false>((F2R<uint32_t>*)nullptr, t, gx, gy, c, same_y);  // false only for sk = 0
-    const bool take = even != 0u;
-    acc.X.a = rf_sel(take, t.X.a, acc.X.a);
-    acc.X.b = rf_sel(take, t.X.b, acc.X.b);
-    acc.Y.a = rf_sel(take, t.Y.a, acc.Y.a);
-    acc.Y.b = rf_sel(take, t.Y.b, acc.Y.b);
-    acc.Z.a = rf_sel(take, t.Z.a, acc.Z.a);
-    acc.Z.b = rf_sel(take, t.Z.b, acc.Z.b);
-    inf = take && !ok;
+  {  // sk even: sk g2 = -(r - sk) g2 (the negation selected)
+    const F2R<uint32_t> ny{c.red(c.sub(c.zero, acc.Y.a)), c.red(c.sub(c.zero, acc.Y.b))};
+    acc.Y.a = rf_sel(even != 0u, ny.a, acc.Y.a);
+    acc.Y.b = rf_sel(even != 0u, ny.b, acc.Y.b);
   }
+  const bool inf = false;  // k' in [1, r - 1]: never the point at infinity
   g2j J;
   rf_to_fe(J.X.a, acc.X.a);
   rf_to_fe(J.X.b, acc.X.b);

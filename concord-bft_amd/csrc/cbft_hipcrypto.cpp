@@ -149,6 +149,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   if (const char* e = getenv("CBFT_STAGE_ORDER_MIN")) c->stage_order_min = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_SMALL_MAX")) c->small_max = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_SHA_SORT_MIN")) c->sha_sort_min = (size_t)atoll(e);
+  if (const char* e = getenv("CBFT_SMALL_WAVES")) c->small_waves = atoi(e) == 3 ? 3 : 2;
   if (const char* e = getenv("CBFT_ZERO_COPY")) c->zero_copy = atoi(e);
   if (const char* e = getenv("CBFT_BLOCKING_SYNC")) c->blocking_sync = atoi(e);
   if (const char* e = getenv("CBFT_SMALL_STREAMS")) c->nsmall = std::max(1, std::min(CBFT_SMALL_STREAMS, atoi(e)));
@@ -731,7 +732,7 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     // pair ladder (fewer additions in total, 2 waves/SIMD) once a batch fills the chip with it;
     // the quad ladder (half the additions per lane) for the latency of small batches
     w.comb_lanes = c->ladder_lanes ? c->ladder_lanes : (n >= 32768 ? 2 : 4);
-    w.small = small;
+    w.small = small ? c->small_waves : 0;
   }
   // Stage order pays for big batches (their stages fill the chip; see cbft_ctx::stage_order).
   // Small batches are latency-bound single waves per stage: ordering them only serialises

@@ -798,9 +798,13 @@ __device__ __forceinline__ void add256(uint32_t* s, const uint32_t* off) {
 template <int BLOCK>
 __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, uint32_t q, const uint32_t* h_in,
                                               const uint32_t* btbl, const CombLadder& cl, int32_t* sdig, uint4* stage,
-                                              ge_p3& P) {
-  const uint32_t ntot = cl.a.npos + cl.b.npos;
-  const uint32_t first = q * cl.nper;
+                                              ge_p3& P, uint32_t kbase = 0, uint32_t kend = 0, int nper = 0) {
+  // the quad's positions [kbase, kend) (default: all of them), nper per lane
+  if (kend == 0) {
+    kend = cl.a.npos + cl.b.npos;
+    nper = cl.nper;
+  }
+  const uint32_t first = kbase + q * (uint32_t)nper;
   // Digits of this lane's additions (signed, up to +-2^21), kept in LDS ([step][thread]:
   // conflict-free) so the addition loop holds no digit registers.
   {
@@ -824,7 +828,7 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
       const uint32_t half = 1u << (w - 1);
       // top digit in [0, 2^(w-1)]; only S >= L (flagged, rejected in K4) can exceed it
       int d = pos == top ? (int)(ch < half ? ch : half) : (int)ch - (int)half;
-      if (jj >= cl.nper || k >= ntot) d = 0;
+      if (jj >= nper || k >= kend) d = 0;
       sdig[jj * BLOCK + threadIdx.x] = d;
     }
   }
@@ -833,7 +837,7 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
     const uint32_t k = first + jj;
     const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
     if (k < (uint32_t)cl.a.npos) return akey + ((size_t)k * cl.a.entries() + ad) * COMB_STRIDE;
-    const uint32_t pos = k < ntot ? k - cl.a.npos : 0u;  // past the last position: identity
+    const uint32_t pos = k < kend ? k - cl.a.npos : 0u;  // past the range: identity (entry 0)
     return btbl + ((size_t)pos * cl.b.entries() + ad) * COMB_STRIDE;
   };
   auto digit = [&](int jj) { return sdig[jj * BLOCK + threadIdx.x]; };
@@ -852,7 +856,7 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
   int d = digit(0);
   request(entry(0, d));
 #pragma nounroll
-  for (int jj = 0; jj < cl.nper; jj++) {
+  for (int jj = 0; jj < nper; jj++) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t ew[28];
 #pragma unroll
@@ -865,7 +869,7 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry jj is in VGPRs: the slot is free
     const bool neg = d < 0;
-    if (jj + 1 < cl.nper) {
+    if (jj + 1 < nper) {
       d = digit(jj + 1);
 #if !CBFT_LADDER_NOFETCH  // (probe builds only: compute without the table traffic, wrong verdicts)
       request(entry(jj + 1, d));
@@ -1031,6 +1035,111 @@ __global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed2551
     verdict16[blockIdx.x] = (uint16_t)bits;
     // the last block also zeroes the 16-bit pieces of its 64-bit verdict word that no block
     // covers, so the call writes whole ceil(n/64) words (bits past n = 0) like the ballot kernels
+    if (blockIdx.x == gridDim.x - 1)
+      for (uint32_t p = blockIdx.x + 1; (p & 3u) != 0u; p++) verdict16[p] = 0;
+  }
+}
+
+// The same verdicts with the work of a block of 16 signatures on THREE waves (three SIMDs):
+// wave 0 hashes, then sums [h](-A) over its quads (the key comb's positions only) and adds the
+// [S]B half; wave 1 sums [S]B (B's comb positions: S is known before the hash) and hands it over
+// in LDS; wave 2 decodes R.  Wave 0's critical path loses B's additions (12 of 32 positions).
+// Selected by $CBFT_SMALL_WAVES=3.
+#define SMALL3_BLOCK 192
+__global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25519Batch b, const uint32_t* btbl,
+                                                                      const CombLadder cl, uint16_t* verdict16) {
+  __shared__ int32_t sdig[2][COMB_MAX_STEPS * 64];
+  __shared__ uint4 stage[2][7 * 64];
+  __shared__ uint32_t rdec[SMALL_SIGS][2 * FE_LIMBS + 1];  // x_R | y_R | decodes
+  __shared__ uint32_t sbp[SMALL_SIGS][4 * FE_LIMBS];       // [S]B as X | Y | Z | T
+  const uint32_t ln = threadIdx.x & 63u, wave = threadIdx.x >> 6, q = ln & 3u, sl = ln >> 2;
+  size_t i = (size_t)blockIdx.x * SMALL_SIGS + sl;
+  const bool live = i < b.n;
+  if (!live) i = b.n - 1;
+  const uint32_t na = (uint32_t)cl.a.npos, ntot = na + (uint32_t)cl.b.npos;
+  if (wave == 2) {
+    uint32_t Rw[8];
+    load_words8(Rw, b.sig + i * 64);
+    ge_p3 R;
+    bool ok = ge_frombytes(R, Rw);
+    bool top = (Rw[7] & 0x7fffffffu) == 0x7fffffffu && Rw[0] >= 0xffffffedu;
+#pragma unroll
+    for (int k = 1; k < 7; k++) top = top && Rw[k] == 0xffffffffu;
+    ok = ok && !top && !(fe_iszero(R.X) && (Rw[7] >> 31));
+    if (q == 0) {
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        rdec[sl][k] = R.X.v[k];
+        rdec[sl][FE_LIMBS + k] = R.Y.v[k];
+      }
+      rdec[sl][2 * FE_LIMBS] = ok ? 1u : 0u;
+    }
+    __syncthreads();
+    return;
+  }
+  if (wave == 1) {  // [S]B: B's positions [na, ntot) over the quad; the digits need no hash
+    const uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    ge_p3 P;
+    comb_quad_sum<64>(b, i, q, zero, btbl, cl, sdig[1], stage[1], P, na, ntot, (int)((ntot - na + 3) / 4));
+    quad_combine<0xB1>(P, true);
+    quad_combine<0x4E>(P, true);
+    if (q == 0) {
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        sbp[sl][k] = P.X.v[k];
+        sbp[sl][FE_LIMBS + k] = P.Y.v[k];
+        sbp[sl][2 * FE_LIMBS + k] = P.Z.v[k];
+        sbp[sl][3 * FE_LIMBS + k] = P.T.v[k];
+      }
+    }
+    __syncthreads();
+    return;
+  }
+  uint32_t hs[8];
+  bool flag;
+  ed25519_hash_sig(b, i, hs, flag);
+  ge_p3 P;
+  comb_quad_sum<64>(b, i, q, hs, btbl, cl, sdig[0], stage[0], P, 0, na, (int)((na + 3) / 4));
+  quad_combine<0xB1>(P, true);
+  quad_combine<0x4E>(P, true);
+  __syncthreads();  // wave 1's [S]B, wave 2's R
+  {
+    ge_p3 Q;
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) {
+      Q.X.v[k] = sbp[sl][k];
+      Q.Y.v[k] = sbp[sl][FE_LIMBS + k];
+      Q.Z.v[k] = sbp[sl][2 * FE_LIMBS + k];
+      Q.T.v[k] = sbp[sl][3 * FE_LIMBS + k];
+    }
+    ge_cached c;
+    ge_p3_to_cached(c, Q);
+    ge_p1p1 t;
+    ge_add(t, P, c, false);
+    fe_mul(P.X, t.X, t.T);
+    fe_mul(P.Y, t.Y, t.Z);
+    fe_mul(P.Z, t.Z, t.T);
+  }
+  fe xr, yr, t;
+#pragma unroll
+  for (int k = 0; k < FE_LIMBS; k++) {
+    xr.v[k] = rdec[sl][k];
+    yr.v[k] = rdec[sl][FE_LIMBS + k];
+  }
+  bool same = rdec[sl][2 * FE_LIMBS] != 0;
+  fe_mul<false>(t, xr, P.Z);
+  fe_sub(t, P.X, t);
+  same = same && fe_iszero(t);
+  fe_mul<false>(t, yr, P.Z);
+  fe_sub(t, P.Y, t);
+  same = same && fe_iszero(t);
+  const bool verdict = live && same && flag && b.keys.aok(batch_unit(b, i));
+  const uint64_t bal = __ballot(verdict);
+  uint32_t bits = 0;
+#pragma unroll
+  for (int s2 = 0; s2 < SMALL_SIGS; s2++) bits |= (uint32_t)((bal >> (4 * s2)) & 1u) << s2;
+  if (ln == 0) {
+    verdict16[blockIdx.x] = (uint16_t)bits;
     if (blockIdx.x == gridDim.x - 1)
       for (uint32_t p = blockIdx.x + 1; (p & 3u) != 0u; p++) verdict16[p] = 0;
   }
@@ -1291,8 +1400,12 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
     if (w.comb.nper > COMB_MAX_STEPS) return hipErrorInvalidValue;
     if (ev)
       for (int k = 0; k < 3; k++) (void)hipEventRecord(ev[k], stream);
-    hipLaunchKernelGGL(ed25519_small_kernel, dim3((unsigned)((b.n + SMALL_SIGS - 1) / SMALL_SIGS)), dim3(SMALL_BLOCK), 0, stream,
-                       b, w.base_comb, w.comb, reinterpret_cast<uint16_t*>(w.verdict_words));
+    if (w.small == 3)
+      hipLaunchKernelGGL(ed25519_small3_kernel, dim3((unsigned)((b.n + SMALL_SIGS - 1) / SMALL_SIGS)), dim3(SMALL3_BLOCK), 0,
+                         stream, b, w.base_comb, w.comb, reinterpret_cast<uint16_t*>(w.verdict_words));
+    else
+      hipLaunchKernelGGL(ed25519_small_kernel, dim3((unsigned)((b.n + SMALL_SIGS - 1) / SMALL_SIGS)), dim3(SMALL_BLOCK), 0,
+                         stream, b, w.base_comb, w.comb, reinterpret_cast<uint16_t*>(w.verdict_words));
     if (ev) (void)hipEventRecord(ev[3], stream);
     return hipGetLastError();
   }

@@ -427,3 +427,20 @@ def test_hash_block_count_sort(golden, n, monkeypatch):
         tid = c.load_keys(ss.pk)
         got = _bools(c.verify_packed(tid, ss.key_idx, ss.sig, ss.blob, ss.off, ss.len), n)
     assert np.array_equal(got, ss.expected)
+
+
+@pytest.mark.parametrize("chunk", [1, 17, 300, 1024])
+def test_golden_small_batches_three_wave_kernel(golden, chunk, monkeypatch):
+    """$CBFT_SMALL_WAVES=3: the fused kernel with [S]B on its own wave and R's decode on a third
+    gives the golden verdicts batch for batch, partial words and tail quads included."""
+    monkeypatch.setenv("CBFT_SMALL_WAVES", "3")
+    keys = sorted({v.pk for v in golden})
+    index = {k: i for i, k in enumerate(keys)}
+    exp = np.array([bool(v.verdict) for v in golden])
+    with cb.Context(device=0) as c:
+        tid = c.load_keys(keys)
+        for lo in range(0, len(golden), chunk):
+            part = golden[lo:lo + chunk]
+            got = _bools(c.verify(tid, [index[v.pk] for v in part], [v.sig for v in part], [v.msg for v in part]),
+                         len(part))
+            assert np.array_equal(got, exp[lo:lo + chunk]), f"batch at {lo}"
