@@ -805,6 +805,9 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
     nper = cl.nper;
   }
   const uint32_t first = kbase + q * (uint32_t)nper;
+  // thread index within the BLOCK-thread group the caller's sdig / stage belong to (a caller may
+  // hand each wave of a bigger block its own arrays with BLOCK = 64)
+  const uint32_t tid = threadIdx.x & (BLOCK - 1);
   // Digits of this lane's additions (signed, up to +-2^21), kept in LDS ([step][thread]:
   // conflict-free) so the addition loop holds no digit registers.
   {
@@ -829,7 +832,7 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
       // top digit in [0, 2^(w-1)]; only S >= L (flagged, rejected in K4) can exceed it
       int d = pos == top ? (int)(ch < half ? ch : half) : (int)ch - (int)half;
       if (jj >= nper || k >= kend) d = 0;
-      sdig[jj * BLOCK + threadIdx.x] = d;
+      sdig[jj * BLOCK + tid] = d;
     }
   }
   const uint32_t* akey = b.keys.comb(batch_unit(b, i));
@@ -840,14 +843,14 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
     const uint32_t pos = k < kend ? k - cl.a.npos : 0u;  // past the range: identity (entry 0)
     return btbl + ((size_t)pos * cl.b.entries() + ad) * COMB_STRIDE;
   };
-  auto digit = [&](int jj) { return sdig[jj * BLOCK + threadIdx.x]; };
+  auto digit = [&](int jj) { return sdig[jj * BLOCK + tid]; };
   ge_p3_0(P);
   // Table entries are staged through LDS with global_load_lds (no VGPR destination): entry
   // jj+1's 7 x 16 B are requested as soon as entry jj has been read out of LDS, so its HBM /
   // Infinity-Cache latency overlaps the rest of addition jj.  LDS image per wave:
   // [chunk 0..6][lane][16 B] (lane-linear, as one global_load_lds_dwordx4 writes it), 7 KB.
-  uint4(*st)[64] = reinterpret_cast<uint4(*)[64]>(stage + (threadIdx.x >> 6) * 7 * 64);
-  const uint32_t ln = threadIdx.x & 63u;
+  uint4(*st)[64] = reinterpret_cast<uint4(*)[64]>(stage + (tid >> 6) * 7 * 64);
+  const uint32_t ln = tid & 63u;
   auto request = [&](const uint32_t* e) {
 #pragma unroll
     for (int c = 0; c < 7; c++)
