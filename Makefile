@@ -5,20 +5,20 @@ CSRC    := concord-bft_amd/csrc
 LIB     := concord-bft_amd/libcbft_hipcrypto.so
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Iinclude -I$(CSRC) -Wall -Wno-unused-function
 ORACLE_LIB := oracle/libcbft_oracle.so
-# The row-parallel BN-P254 code (bn254_row.h: row_shr / row_shl moves with zero fill) is built
+# The row-parallel field code (bn254_row.h, fe25519_row.h: row_shr / row_shl moves with zero fill) is built
 # without LLVM's DPP combiner: on this toolchain (ROCm 7.2 LLVM, gfx950) folding those moves into
 # their consumers left non-zero values in lanes that must read 0 (a G2 addition came out wrong in
 # one inlined copy and right in another; tools/microbench/g2r_dbg2.hip reproduces it, and the
 # host SIMD emulation of the same source is exact).  Costs one v_mov_dpp per move.
 ROWFLAGS := -mllvm -amdgpu-dpp-combine=false
 
-.PHONY: all lib oracle clean shim sanitize
-all: lib oracle cpu host shim
+.PHONY: all lib oracle clean shim fe_row_shim sanitize
+all: lib oracle cpu host shim fe_row_shim
 
 lib: $(LIB)
 
 $(CSRC)/ed25519_verify.o: $(CSRC)/ed25519_verify.hip $(CSRC)/*.h
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(ROWFLAGS) -c $< -o $@
 
 $(CSRC)/cbft_hipcrypto.o: $(CSRC)/cbft_hipcrypto.cpp include/cbft_hipcrypto.h $(CSRC)/ed25519_verify.h $(CSRC)/cbft_internal.h $(CSRC)/rsa_verify.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
@@ -89,6 +89,12 @@ SHIM := tests/cpp/libbn254_shim.so
 shim: $(SHIM)
 $(SHIM): tests/cpp/bn254_shim.cpp $(CSRC)/bn254_*.h $(CSRC)/bls_ops.h $(CSRC)/sha256.h
 	g++ -O3 -funroll-loops -std=c++17 -fPIC -shared -Wall -Wno-unknown-pragmas -I$(CSRC) -o $@ $< -lpthread
+
+# host build of the row-parallel GF(2^255 - 19) code (fe25519_row.h) for tests/test_fe_row.py
+FE_ROW_SHIM := tests/cpp/libfe_row_shim.so
+fe_row_shim: $(FE_ROW_SHIM)
+$(FE_ROW_SHIM): tests/cpp/fe_row_shim.cpp tests/cpp/row_emu.h $(CSRC)/fe25519_row.h $(CSRC)/row_lanes.h
+	g++ -O2 -std=c++17 -fPIC -shared -Wall -Wno-unknown-pragmas -I$(CSRC) -Itests/cpp -o $@ $<
 
 # Host-layer sanitizer builds (host code only: the HIP library itself is not instrumented).
 # ASan+UBSan and TSan variants of the C++ host library and its tests; run on a GPU box with

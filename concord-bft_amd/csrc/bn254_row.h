@@ -23,11 +23,7 @@
 #pragma once
 #include "bn254_field.h"
 
-#if defined(__HIPCC__)
-#define RF_HD __device__ __forceinline__
-#else
-#define RF_HD inline
-#endif
+#include "row_lanes.h"
 
 // 8q in the redundant limb form used by rf_sub: limb i in [2^30, 2^31) for i < 8 (limb 8 =
 // 8q's top limb - 2), so a + Q8R - b is limb-wise non-negative for any row-normal b < 4q.
@@ -52,52 +48,6 @@ struct RfConsts {
   static constexpr uint32_t TOP_RECIP = 1764;  // floor(2^32 / (floor(q / 2^232) + 1))
 };
 
-// ------------------------------------------------------------------------------ lane ops
-#if defined(__HIPCC__)
-template <int I>
-RF_HD uint32_t rl_bcast(uint32_t x) {  // lane I of each row -> the whole row
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x150 + I, 0xF, 0xF, false);
-}
-template <int I>
-RF_HD uint32_t rl_shr(uint32_t x) {  // lane k <- lane k - I of the row, 0 below
-  if (I == 0) return x;
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x110 + I, 0xF, 0xF, true);
-}
-template <int I>
-RF_HD uint32_t rl_shl(uint32_t x) {  // lane k <- lane k + I of the row, 0 above
-  if (I == 0) return x;
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x100 + I, 0xF, 0xF, true);
-}
-RF_HD uint32_t rl_index(uint32_t) { return __lane_id() & 15u; }
-RF_HD uint32_t rl_row(uint32_t) { return __lane_id() >> 4; }
-// the value the same row lane holds in row S (ds_bpermute: the LDS crossbar, no LDS memory)
-template <int S>
-RF_HD uint32_t rl_from_row(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_ds_bpermute((int)((S << 6) | ((__lane_id() & 15u) << 2)), (int)x);
-}
-RF_HD uint32_t rf_lo(uint64_t w) { return (uint32_t)w; }
-RF_HD uint32_t rf_hi(uint64_t w) { return (uint32_t)(w >> 32); }
-RF_HD uint64_t rf_w(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
-RF_HD uint64_t rf_mad(uint32_t a, uint32_t b, uint64_t c) { return (uint64_t)a * b + c; }
-RF_HD uint32_t rf_sel(bool c, uint32_t a, uint32_t b) { return c ? a : b; }
-RF_HD uint64_t rf_sel(bool c, uint64_t a, uint64_t b) { return c ? a : b; }
-RF_HD uint32_t rf_const(uint32_t, uint32_t v) { return v; }
-RF_HD uint64_t rf_const64(uint32_t, uint64_t v) { return v; }
-// 64-bit lane shifts by 29 as 32-bit funnel shifts (v_alignbit_b32) of the register halves
-RF_HD uint64_t rf_shr29(uint64_t w) {
-  const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
-  return (uint64_t)__builtin_amdgcn_alignbit(hi, lo, 29) | ((uint64_t)(hi >> 29) << 32);
-}
-RF_HD uint64_t rf_sra29(uint64_t w) {
-  const uint32_t lo = (uint32_t)w, hi = (uint32_t)(w >> 32);
-  return (uint64_t)__builtin_amdgcn_alignbit(hi, lo, 29) | ((uint64_t)(uint32_t)((int32_t)hi >> 29) << 32);
-}
-RF_HD uint64_t rf_ballot(bool c) { return __ballot(c); }
-RF_HD uint32_t rl_lane(uint32_t) { return __lane_id(); }
-RF_HD uint64_t rf_widen(uint32_t x) { return x; }
-RF_HD uint64_t rf_mul64(uint32_t a, uint32_t b) { return (uint64_t)a * b; }
-RF_HD uint32_t rf_bit(uint64_t mask, uint32_t lane) { return (uint32_t)(mask >> lane) & 1u; }
-#endif
 
 // ------------------------------------------------------------------------------ arithmetic
 // limb i of a 9-limb constant in row lane i (0 elsewhere)

@@ -268,60 +268,53 @@ __device__ __forceinline__ uint32_t hash_bucket(const Ed25519Batch& b, size_t i)
   return nb < CBFT_SHA_BUCKETS - 1 ? nb : CBFT_SHA_BUCKETS - 1;
 }
 
-// Counting sort of a variable-length batch by SHA-512 block count, in three launches:
-// (1) per-bucket counts (LDS histogram per block, one global atomic per non-empty bucket);
-// (2) one block: exclusive scan of the counts into cursors (and counts reset for the next batch);
-// (3) every signature takes a slot of its bucket (LDS ranks per block, one global atomicAdd per
-//     non-empty bucket per block) and writes its index there.  Order inside a bucket is arbitrary:
-//     K1 writes each signature's digest to its own index, so verdicts do not depend on it.
-static_assert(CBFT_SHA_BUCKETS == 256, "the bucket kernels run one thread per bucket in 256-thread blocks");
-__global__ void __launch_bounds__(256) ed25519_bucket_count_kernel(const Ed25519Batch b, uint32_t* counts) {
-  __shared__ uint32_t hist[CBFT_SHA_BUCKETS];
-  hist[threadIdx.x] = 0;
-  __syncthreads();
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < b.n) atomicAdd(&hist[hash_bucket(b, i)], 1u);
-  __syncthreads();
-  if (hist[threadIdx.x]) atomicAdd(&counts[threadIdx.x], hist[threadIdx.x]);
-}
-
-__global__ void __launch_bounds__(256) ed25519_bucket_scan_kernel(uint32_t* counts, uint32_t* cursors) {
-  __shared__ uint32_t v[CBFT_SHA_BUCKETS];
-  const uint32_t t = threadIdx.x;
-  v[t] = counts[t];
-  __syncthreads();
-  for (uint32_t d = 1; d < CBFT_SHA_BUCKETS; d <<= 1) {  // inclusive Hillis-Steele scan
-    const uint32_t x = t >= d ? v[t - d] : 0u;
+// K1.  SORT (variable-length batches): the block's BLOCK signatures are hashed in order of their
+// SHA-512 block count -- an LDS counting sort (ranks by LDS atomics, so the order inside a bucket
+// is arbitrary; each digest goes to its signature's own index, so verdicts do not depend on it),
+// thread t then hashing the t-th signature of that order.  With log-uniform 64..4,096-B messages
+// an unsorted wave runs every lane through the ~33 blocks of its longest message while the mean
+// is ~9; sorted within 512 signatures, a wave spans 1/8 of the block-count quantiles.  A block
+// whose signatures all share one block count (fixed-size messages) keeps the identity order.
+template <int BLOCK, bool SORT>
+__global__ void __launch_bounds__(BLOCK) ed25519_hash_kernel(const Ed25519Batch b, uint32_t* h_soa, uint8_t* flags) {
+  size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (SORT) {
+    __shared__ uint32_t hist[CBFT_SHA_BUCKETS], order[BLOCK], kmin, kmax;
+    static_assert(CBFT_SHA_BUCKETS == 64, "one wave scans the bucket counts");
+    if (threadIdx.x < CBFT_SHA_BUCKETS) hist[threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+      kmin = CBFT_SHA_BUCKETS;
+      kmax = 0;
+    }
     __syncthreads();
-    v[t] += x;
+    const bool live = i < b.n;
+    uint32_t k = 0, rank = 0;
+    if (live) {
+      k = hash_bucket(b, i);
+      rank = atomicAdd(&hist[k], 1u);
+      atomicMin(&kmin, k);
+      atomicMax(&kmax, k);
+    }
     __syncthreads();
+    if (kmin < kmax) {  // block-uniform
+      if (threadIdx.x < CBFT_SHA_BUCKETS) {  // wave 0: exclusive scan of the 64 counts
+        const uint32_t v = hist[threadIdx.x];
+        uint32_t x = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t y = __shfl_up(x, d, 64);
+          if ((int)threadIdx.x >= d) x += y;
+        }
+        hist[threadIdx.x] = x - v;
+      }
+      __syncthreads();
+      if (live) order[hist[k] + rank] = threadIdx.x;
+      __syncthreads();
+      // the live signatures fill order[0, live count); threads past it are past n anyway
+      if (live) i = (size_t)blockIdx.x * BLOCK + order[threadIdx.x];
+    }
   }
-  cursors[t] = v[t] - counts[t];
-  counts[t] = 0;  // ready for the next batch's counts
-}
-
-__global__ void __launch_bounds__(256) ed25519_bucket_scatter_kernel(const Ed25519Batch b, uint32_t* cursors,
-                                                                     uint32_t* perm) {
-  __shared__ uint32_t hist[CBFT_SHA_BUCKETS], base[CBFT_SHA_BUCKETS];
-  hist[threadIdx.x] = 0;
-  __syncthreads();
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  uint32_t k = 0, rank = 0;
-  if (i < b.n) {
-    k = hash_bucket(b, i);
-    rank = atomicAdd(&hist[k], 1u);
-  }
-  __syncthreads();
-  if (hist[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursors[threadIdx.x], hist[threadIdx.x]);
-  __syncthreads();
-  if (i < b.n) perm[base[k] + rank] = (uint32_t)i;
-}
-
-__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const Ed25519Batch b, const uint32_t* perm,
-                                                                          uint32_t* h_soa, uint8_t* flags) {
-  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= b.n) return;
-  const size_t i = perm ? (size_t)perm[g] : g;
+  if (i >= b.n) return;
   uint32_t hw[8];
   bool flag;
   ed25519_hash_sig(b, i, hw, flag);
@@ -955,7 +948,49 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
 // the block's 16 signatures go out as one 16-bit word; no per-signature state goes through HBM.
 // ---------------------------------------------------------------------------------------
 #define SMALL_SIGS 16
-#define SMALL_BLOCK 128
+// R decoders per block: CBFT_DECODE_ROW = 1 puts each signature's square-root chain on a 16-lane
+// DPP row (ge_frombytes_row), four waves for the block's 16 signatures; 0 keeps one wave with a
+// lane quad per signature on the one-lane chain.
+#ifndef CBFT_DECODE_ROW
+#define CBFT_DECODE_ROW 1
+#endif
+#define SMALL_DEC_WAVES (CBFT_DECODE_ROW ? 4 : 1)
+#define SMALL_BLOCK (64 * (1 + SMALL_DEC_WAVES))
+
+// Decode wave dw of a small-kernel block: x_R | y_R | (R decodes && y canonical && not (x = 0
+// with the sign bit set)) of its signatures into rdec.
+__device__ __forceinline__ void small_decode_r(const Ed25519Batch& b, uint32_t blk, uint32_t dw, uint32_t ln,
+                                               uint32_t (*rdec)[2 * FE_LIMBS + 1]) {
+  const uint32_t sl = CBFT_DECODE_ROW ? dw * 4 + (ln >> 4) : (ln >> 2);
+  const bool writer = CBFT_DECODE_ROW ? (ln & 15u) == 0 : (ln & 3u) == 0;
+  size_t i = (size_t)blk * SMALL_SIGS + sl;
+  if (i >= b.n) i = b.n - 1;
+  uint32_t Rw[8];
+  load_words8(Rw, b.sig + i * 64);
+  fe X, Y;
+  bool ok;
+  if (CBFT_DECODE_ROW) {
+    ok = ge_frombytes_row(X, Y, Rw);
+  } else {
+    ge_p3 R;
+    ok = ge_frombytes(R, Rw);
+    X = R.X;
+    Y = R.Y;
+  }
+  // y < p: the 255-bit y is not one of 2^255 - 19 .. 2^255 - 1
+  bool top = (Rw[7] & 0x7fffffffu) == 0x7fffffffu && Rw[0] >= 0xffffffedu;
+#pragma unroll
+  for (int k = 1; k < 7; k++) top = top && Rw[k] == 0xffffffffu;
+  ok = ok && !top && !(fe_iszero(X) && (Rw[7] >> 31));
+  if (writer) {
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) {
+      rdec[sl][k] = X.v[k];
+      rdec[sl][FE_LIMBS + k] = Y.v[k];
+    }
+    rdec[sl][2 * FE_LIMBS] = ok ? 1u : 0u;
+  }
+}
 __global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed25519Batch b, const uint32_t* btbl,
                                                                     const CombLadder cl, uint16_t* verdict16) {
   __shared__ int32_t sdig[COMB_MAX_STEPS * 64];
@@ -971,30 +1006,14 @@ __global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed2551
 #else
 #define ED_STAMP(k)
 #endif
-  if (wave == 1) {
+  if (wave >= 1) {
 #if CBFT_ED_PHASES
     const uint64_t d0 = wall_clock64();
 #endif
-    uint32_t Rw[8];
-    load_words8(Rw, b.sig + i * 64);
-    ge_p3 R;
-    bool ok = ge_frombytes(R, Rw);
+    small_decode_r(b, blockIdx.x, wave - 1, ln, rdec);
 #if CBFT_ED_PHASES
     if (blockIdx.x == 0 && ln == 0) printf("ed25519_small block 0: R decode %.1f us\n", (wall_clock64() - d0) * 0.01);
 #endif
-    // y < p: the 255-bit y is not one of 2^255 - 19 .. 2^255 - 1
-    bool top = (Rw[7] & 0x7fffffffu) == 0x7fffffffu && Rw[0] >= 0xffffffedu;
-#pragma unroll
-    for (int k = 1; k < 7; k++) top = top && Rw[k] == 0xffffffffu;
-    ok = ok && !top && !(fe_iszero(R.X) && (Rw[7] >> 31));
-    if (q == 0) {
-#pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) {
-        rdec[sl][k] = R.X.v[k];
-        rdec[sl][FE_LIMBS + k] = R.Y.v[k];
-      }
-      rdec[sl][2 * FE_LIMBS] = ok ? 1u : 0u;
-    }
     __syncthreads();
     return;
   }
@@ -1048,7 +1067,7 @@ __global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed2551
 // [S]B half; wave 1 sums [S]B (B's comb positions: S is known before the hash) and hands it over
 // in LDS; wave 2 decodes R.  Wave 0's critical path loses B's additions (12 of 32 positions).
 // Selected by $CBFT_SMALL_WAVES=3.
-#define SMALL3_BLOCK 192
+#define SMALL3_BLOCK (64 * (2 + SMALL_DEC_WAVES))
 __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25519Batch b, const uint32_t* btbl,
                                                                       const CombLadder cl, uint16_t* verdict16) {
   __shared__ int32_t sdig[2][COMB_MAX_STEPS * 64];
@@ -1060,23 +1079,8 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
   const bool live = i < b.n;
   if (!live) i = b.n - 1;
   const uint32_t na = (uint32_t)cl.a.npos, ntot = na + (uint32_t)cl.b.npos;
-  if (wave == 2) {
-    uint32_t Rw[8];
-    load_words8(Rw, b.sig + i * 64);
-    ge_p3 R;
-    bool ok = ge_frombytes(R, Rw);
-    bool top = (Rw[7] & 0x7fffffffu) == 0x7fffffffu && Rw[0] >= 0xffffffedu;
-#pragma unroll
-    for (int k = 1; k < 7; k++) top = top && Rw[k] == 0xffffffffu;
-    ok = ok && !top && !(fe_iszero(R.X) && (Rw[7] >> 31));
-    if (q == 0) {
-#pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) {
-        rdec[sl][k] = R.X.v[k];
-        rdec[sl][FE_LIMBS + k] = R.Y.v[k];
-      }
-      rdec[sl][2 * FE_LIMBS] = ok ? 1u : 0u;
-    }
+  if (wave >= 2) {
+    small_decode_r(b, blockIdx.x, wave - 2, ln, rdec);
     __syncthreads();
     return;
   }
@@ -1415,15 +1419,12 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   if (order && order->wait && order->hash && (e = hipStreamWaitEvent(stream, order->done[0], 0)) != hipSuccess)
     return e;
   if (ev) (void)hipEventRecord(ev[0], stream);
-  const bool sorted = w.perm && w.buckets && b.msg_off;
-  if (sorted) {
-    const dim3 g256((unsigned)((b.n + 255) / 256)), b256(256);
-    hipLaunchKernelGGL(ed25519_bucket_count_kernel, g256, b256, 0, stream, b, w.buckets);
-    hipLaunchKernelGGL(ed25519_bucket_scan_kernel, dim3(1), b256, 0, stream, w.buckets, w.buckets + CBFT_SHA_BUCKETS);
-    hipLaunchKernelGGL(ed25519_bucket_scatter_kernel, g256, b256, 0, stream, b, w.buckets + CBFT_SHA_BUCKETS, w.perm);
-  }
-  hipLaunchKernelGGL(ed25519_hash_kernel, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
-                     w.h_soa, w.flags);
+  if (w.sha_sort && b.msg_off)
+    hipLaunchKernelGGL((ed25519_hash_kernel<CBFT_SHA_SORT_BLOCK, true>),
+                       dim3((unsigned)((b.n + CBFT_SHA_SORT_BLOCK - 1) / CBFT_SHA_SORT_BLOCK)), dim3(CBFT_SHA_SORT_BLOCK),
+                       0, stream, b, w.h_soa, w.flags);
+  else
+    hipLaunchKernelGGL((ed25519_hash_kernel<CBFT_VERIFY_BLOCK, false>), grid, block, 0, stream, b, w.h_soa, w.flags);
   if (order && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;
   if (order && order->wait && order->ladder && (e = hipStreamWaitEvent(stream, order->done[1], 0)) != hipSuccess)
     return e;

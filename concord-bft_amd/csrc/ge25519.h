@@ -8,6 +8,7 @@
 // Limb bounds of every field value are annotated (R = reduced, Lz = lazy), see fe25519.h.
 #pragma once
 #include "fe25519.h"
+#include "fe25519_row.h"
 
 struct ge_p2 {
   fe X, Y, Z;
@@ -160,6 +161,55 @@ FE_INLINE bool ge_frombytes(ge_p3& h, const uint32_t* w) {
   uint32_t sign = w[7] >> 31;
   if (fe_isnegative(h.X) != sign) fe_neg(h.X, h.X);
   fe_mul(h.T, h.X, h.Y);
+  return ok;
+}
+
+// ge_frombytes for a whole 16-lane DPP row holding the same w: the square-root chain runs in the
+// row-parallel field (fe25519_row.h, ~2x less latency per squaring on a lone wave), the checks
+// and the sign in the one-lane field as above.  Same point, same verdict; X and Y only (the small
+// kernels' projective comparison needs no T).
+FE_INLINE void rfe_to_fe(fe& r, uint32_t x) {
+  r.v[0] = rl_bcast_w<0>(x);
+  r.v[1] = rl_bcast_w<1>(x);
+  r.v[2] = rl_bcast_w<2>(x);
+  r.v[3] = rl_bcast_w<3>(x);
+  r.v[4] = rl_bcast_w<4>(x);
+  r.v[5] = rl_bcast_w<5>(x);
+  r.v[6] = rl_bcast_w<6>(x);
+  r.v[7] = rl_bcast_w<7>(x);
+  r.v[8] = rl_bcast_w<8>(x);
+  fe_carry(r);
+}
+FE_INLINE bool ge_frombytes_row(fe& X, fe& Y, const uint32_t* w) {
+  typedef uint32_t U;
+  typedef uint64_t W;
+  fe_from_words(Y, w);
+  const U tag = 0u;
+  const U one = rl_index(tag) == 0u ? 1u : 0u;
+  const U y = rfe_row_const(Y.v, tag);
+  const U yy = rfe_sq<U, W>(y);
+  const U u = rfe_sub(yy, one);                                   // y^2 - 1
+  const U v = rfe_carry(rfe_mul<U, W>(yy, rfe_row_const(kFeD, tag)) + one);  // d y^2 + 1
+  const U v3 = rfe_mul<U, W>(rfe_sq<U, W>(v), v);
+  U x = rfe_mul<U, W>(rfe_mul<U, W>(rfe_sq<U, W>(v3), v), u);    // u v^7
+  x = rfe_pow22523<U, W>(x);
+  x = rfe_mul<U, W>(rfe_mul<U, W>(x, v3), u);                     // u v^3 (u v^7)^((p-5)/8)
+  const U vxx = rfe_mul<U, W>(rfe_sq<U, W>(x), v);
+  fe fu, fvxx, chk;
+  rfe_to_fe(X, x);
+  rfe_to_fe(fu, u);
+  rfe_to_fe(fvxx, vxx);
+  fe_sub(chk, fvxx, fu);
+  bool ok = true;
+  if (!fe_iszero(chk)) {
+    fe_add(chk, fvxx, fu);
+    if (!fe_iszero(chk)) ok = false;
+    fe sm1;
+    fe_load_const(sm1, kFeSqrtM1);
+    fe_mul(X, X, sm1);
+  }
+  const uint32_t sign = w[7] >> 31;
+  if (fe_isnegative(X) != sign) fe_neg(X, X);
   return ok;
 }
 

@@ -112,6 +112,10 @@ inline HU rl_bcast(const HU& a) {
   return r;
 }
 template <int I>
+inline HU rl_bcast_w(const HU& a) {
+  return rl_bcast<I>(a);
+}
+template <int I>
 inline HU rl_shr(const HU& a) {
   HU r;
   for (int l = 0; l < 64; l++) r.x[l] = (l & 15) >= I ? a.x[l - I] : 0u;

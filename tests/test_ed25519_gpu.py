@@ -402,9 +402,10 @@ def test_device_path_small_batch_whole_words(n):
 
 @pytest.mark.parametrize("n", [1, 100, 257, 5000])
 def test_hash_block_count_sort(golden, n, monkeypatch):
-    """Variable-length batches hash in order of their SHA-512 block count (a counting sort into a
-    permutation before K1): verdicts equal OpenSSL's and the unsorted path's for every signature,
-    across ragged sizes and lengths straddling block boundaries (0..4,096 B, golden lengths too)."""
+    """Variable-length batches hash in order of their SHA-512 block count (an LDS counting sort in
+    each K1 block): verdicts equal OpenSSL's and the unsorted path's for every signature, across
+    ragged sizes (partial last blocks) and lengths straddling block boundaries (0..4,096 B, golden
+    lengths too)."""
     keys = sorted({v.pk for v in golden})
     index = {k: i for i, k in enumerate(keys)}
     vs = [golden[i % len(golden)] for i in range(n)]
@@ -417,7 +418,7 @@ def test_hash_block_count_sort(golden, n, monkeypatch):
         with cb.Context(device=0) as c:
             tid = c.load_keys(keys)
             out[label] = _bools(c.verify(tid, *args), n)
-            # a second batch through the same work slot: the bucket counters were reset
+            # a second batch through the same context
             out[label + "2"] = _bools(c.verify(tid, *args), n)
     for k, v in out.items():
         assert np.array_equal(v, exp), k

@@ -4,6 +4,7 @@
 #   in-tree library; the optional @ part sets environment variables for that variant)
 # Per variant and round: tools/ladder_probe.py (isolated stage times, verdicts checked) and a
 # 100-step bench.py without extras (headline + device-resident value), each under its own limit.
+# MODE=mixed: tools/mixed_probe.py only (config #3 device-resident rate and hash stage).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
 mkdir -p gpurun_out/ab
@@ -13,6 +14,12 @@ for r in $(seq 1 "${ROUNDS:-2}"); do
     label=${lv%%=*}; spec=${lv#*=}; lib=${spec%%@*}; envs=""
     [[ $spec == *@* ]] && envs=$(echo "${spec#*@}" | tr ',' ' ')
     [ "$lib" = default ] && lib=$PWD/concord-bft_amd/libcbft_hipcrypto.so
+    if [ "${MODE:-}" = mixed ]; then  # config #3 device-resident rate + hash stage only
+      env $envs CBFT_LIB=$lib timeout -k 10 200 python -u tools/mixed_probe.py > gpurun_out/ab/mixed_${label}_$r.json 2> gpurun_out/ab/mixed_${label}_$r.err \
+        || { echo "mixed $label failed"; tail -5 gpurun_out/ab/mixed_${label}_$r.err; exit 1; }
+      echo "$label r$r mixed: $(tail -1 gpurun_out/ab/mixed_${label}_$r.json)"
+      continue
+    fi
     env $envs CBFT_LIB=$lib timeout -k 10 200 python -u tools/ladder_probe.py --reps 20 > gpurun_out/ab/probe_${label}_$r.json 2> gpurun_out/ab/probe_${label}_$r.err \
       || { echo "probe $label failed"; tail -5 gpurun_out/ab/probe_${label}_$r.err; exit 1; }
     env $envs CBFT_LIB=$lib timeout -k 10 200 python -u bench.py --steps 100 --warmup 10 --no-extras --no-cpu --latency-runs 100 > gpurun_out/ab/bench_${label}_$r.json 2> gpurun_out/ab/bench_${label}_$r.err \

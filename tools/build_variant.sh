@@ -1,19 +1,16 @@
 #!/bin/bash
-# Build a variant of libcbft_hipcrypto with extra compile flags, for A/B runs on the GPU box
-# (select it there with CBFT_LIB=<path>).  Usage: tools/build_variant.sh <out.so> <flags...>
+# Build an A/B variant of libcbft_hipcrypto.so: ed25519_verify.hip recompiled with extra -D flags,
+# linked with the default objects of every other TU (run `make lib` first).
+#   tools/build_variant.sh NAME "-DCBFT_DECODE_ROW=0 ..."   -> build/lib_NAME.so
 set -e
 cd "$(dirname "$0")/.."
-out=$1; shift
-tmp=$(mktemp -d)
-pids=()
-for src in ed25519_verify.hip cbft_hipcrypto.cpp bls_kernels.hip bls_msm_row.hip bls_pairing.hip bls_keys.hip cbft_bls.cpp rsa_verify.hip cbft_rsa.cpp; do
-  extra=()
-  case $src in bls_keys.hip|bls_msm_row.hip|bls_pairing.hip) extra=(-mllvm -amdgpu-dpp-combine=false);; esac  # see Makefile ROWFLAGS
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Iconcord-bft_amd/csrc -Wno-unused-function "${extra[@]}" "$@" \
-    -c concord-bft_amd/csrc/$src -o "$tmp/${src%.*}.o" &
-  pids+=($!)
-done
-for p in "${pids[@]}"; do wait "$p" || { echo "compile failed"; rm -rf "$tmp"; exit 1; }; done
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out" "$tmp"/*.o
-rm -rf "$tmp"
-echo "built $out ($*)"
+name=$1; shift
+defs="$*"
+C=concord-bft_amd/csrc
+mkdir -p build
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -I$C -Wall -Wno-unused-function \
+  -mllvm -amdgpu-dpp-combine=false $defs -c $C/ed25519_verify.hip -o build/ed_$name.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/lib_$name.so build/ed_$name.o \
+  $C/cbft_hipcrypto.o $C/bls_kernels.o $C/bls_msm_row.o $C/bls_pairing.o $C/bls_keys.o $C/cbft_bls.o $C/rsa_verify.o $C/cbft_rsa.o
+rm -f build/ed_$name.o
+echo "build/lib_$name.so ($defs)"

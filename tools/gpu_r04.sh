@@ -12,6 +12,7 @@
 #   phases      phase times of the fused small-batch kernel (build/lib_edphases.so, -DCBFT_ED_PHASES=1)
 #   trace       kernel trace of the device-resident two-stream pipeline (overlap of the stages)
 #   ab          interleaved A/B of $LIBS (tools/ab_libs.sh)
+#   abmix       the same over config #3 only (tools/mixed_probe.py)
 #   san         host-layer ASan+UBSan / TSan runs (make sanitize first)
 set -o pipefail
 cd "$GRAFT_REPO_ROOT" || exit 1
@@ -53,6 +54,8 @@ for step in "$@"; do
         > gpurun_out/pmc_bls.json || exit 1 ;;
     ab)
       bash tools/ab_libs.sh || exit 1 ;;
+    abmix)
+      MODE=mixed bash tools/ab_libs.sh || exit 1 ;;
     phases)
       CBFT_LIB=$R/build/lib_edphases.so timeout -k 10 120 python3 -u tools/ed_small_probe.py > gpurun_out/ed_phases.log 2>&1 \
         || { echo "phase probe failed"; tail -20 gpurun_out/ed_phases.log; exit 1; }
