@@ -23,9 +23,9 @@ $(CSRC)/ed25519_verify.o: $(CSRC)/ed25519_verify.hip $(CSRC)/*.h
 $(CSRC)/cbft_hipcrypto.o: $(CSRC)/cbft_hipcrypto.cpp include/cbft_hipcrypto.h $(CSRC)/ed25519_verify.h $(CSRC)/cbft_internal.h $(CSRC)/rsa_verify.h
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
-BLS_DEPS := $(CSRC)/bls_kernels.h $(CSRC)/bls_common.h $(CSRC)/bn254_*.h $(CSRC)/bls_ops.h $(CSRC)/sha256.h $(CSRC)/bls_glv.h
+BLS_DEPS := $(CSRC)/bls_kernels.h $(CSRC)/bls_common.h $(CSRC)/bn254_*.h $(CSRC)/row_lanes.h $(CSRC)/bls_ops.h $(CSRC)/sha256.h $(CSRC)/bls_glv.h
 $(CSRC)/bls_kernels.o: $(CSRC)/bls_kernels.hip $(BLS_DEPS)
-	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+	$(HIPCC) $(HIPFLAGS) $(ROWFLAGS) -c $< -o $@
 
 $(CSRC)/bls_pairing.o: $(CSRC)/bls_pairing.hip $(BLS_DEPS)
 	$(HIPCC) $(HIPFLAGS) $(ROWFLAGS) -c $< -o $@

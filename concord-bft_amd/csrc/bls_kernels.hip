@@ -14,11 +14,11 @@
 #include "bls_common.h"
 #include "bn254_g1quad.h"
 
-// one wave: the candidates are tried 64 at a time (g1_map_wave)
+// one wave: the candidates are tried four at a time, one per DPP row (g1_map_row)
 __global__ void __launch_bounds__(64) bls_hash_kernel(const uint8_t* msg, uint32_t len, uint32_t* H) {
   if (blockIdx.x != 0) return;
   g1a h;
-  g1_map_wave(h, msg, len);
+  g1_map_row(h, msg, len);
   if (threadIdx.x == 0) g1a_store(H, h);
 }
 

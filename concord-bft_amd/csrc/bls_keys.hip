@@ -533,16 +533,11 @@ __global__ void __launch_bounds__(64) bls_pubkey_row_kernel(const uint32_t* tbl,
   } else {
     uint32_t bw[8];
     {
-      uint8_t buf[32], dig[32];
-      for (int i = 0; i < 8; i++)
-        for (int q = 0; q < 4; q++) buf[4 * i + q] = (uint8_t)(k[i] >> (8 * q)) ^ 0x5c;
-      sha256(dig, buf, 32);
-      for (int i = 0; i < 8; i++)
-        bw[i] = (uint32_t)dig[4 * i] | ((uint32_t)dig[4 * i + 1] << 8) | ((uint32_t)dig[4 * i + 2] << 16) |
-                ((uint32_t)dig[4 * i + 3] << 24);
+      uint32_t hs[8];  // SHA-256 of the key's bytes xored with 0x5c
+      sha256_key_msg(hs, k, 0x5c, nullptr, 0);
+      for (int i = 0; i < 8; i++) bw[i] = sha256_bswap(hs[i]);
       bw[7] &= 0x1fffffffu;  // < 2^253 < q
       bw[0] |= (bw[0] | bw[1] | bw[2] | bw[3] | bw[4] | bw[5] | bw[6] | bw[7]) == 0u ? 1u : 0u;
-      for (int i = 0; i < 32; i++) buf[i] = 0;
     }
     fp b;
     f_from_words(b, bw);

@@ -323,6 +323,13 @@ __global__ void __launch_bounds__(128) bls_sign_row_kernel(const uint32_t* H, co
                                                            uint32_t len, uint32_t id, uint8_t* out37) {
   __shared__ uint32_t xch[3 * 16];
   const int wave = threadIdx.x >> 6;
+#if CBFT_BLS_PHASES  // probe builds: phase times of each wave (10 ns ticks), printed by lane 0
+  uint64_t ph[6];
+#define SIGN_STAMP(k) ph[k] = wall_clock64()
+#else
+#define SIGN_STAMP(k)
+#endif
+  SIGN_STAMP(0);
   const uint32_t tag = 0;
   const RCtx c(tag);
   g1a h;
@@ -375,6 +382,7 @@ __global__ void __launch_bounds__(128) bls_sign_row_kernel(const uint32_t* H, co
   g1r_dbl(P2, P, c);
 #pragma unroll
   for (int m = 1; m < 8; m++) g1r_add(T[m], T[m - 1], P2, c);  // unrolled: T stays in registers
+  SIGN_STAMP(1);
   auto pick = [&](int w, RPt& e) {  // +-T[(|d_w| - 1) / 2] by selects over all entries
     const uint32_t nib = (u[w >> 3] >> (4 * (w & 7))) & 15u;  // d = 2 nib - 15
     const uint32_t dn = nib < 8u ? 1u : 0u;                    // d < 0
@@ -406,6 +414,7 @@ __global__ void __launch_bounds__(128) bls_sign_row_kernel(const uint32_t* H, co
     g1r_add(t, acc, e, c);
     acc = t;
   }
+  SIGN_STAMP(2);
   bool inf = false;
   {  // undo the odd fix: acc - base when k was even (computed always, kept by a select)
     RPt nb, t;
@@ -435,7 +444,13 @@ __global__ void __launch_bounds__(128) bls_sign_row_kernel(const uint32_t* H, co
     if (l == 0) xinf = inf ? 1 : 0;
   }
   __syncthreads();
+#if CBFT_BLS_PHASES
+  if (__lane_id() == 0)
+    printf("sign wave %d (us): table %.1f windows %.1f to-exchange %.1f\n", wave, (ph[1] - ph[0]) * 0.01,
+           (ph[2] - ph[1]) * 0.01, (wall_clock64() - ph[2]) * 0.01);
+#endif
   if (wave != 0) return;
+  SIGN_STAMP(3);
   {
     RPt o;
     const uint32_t rl = __lane_id() & 15u;
@@ -457,18 +472,11 @@ __global__ void __launch_bounds__(128) bls_sign_row_kernel(const uint32_t* H, co
   } else {
     uint32_t bw[8];
     {
-      uint8_t buf[32 + 64], dig[32];  // SHA-256(sk || msg[0 .. 64)) is the blind's seed
-      for (int i = 0; i < 8; i++)
-        for (int q = 0; q < 4; q++) buf[4 * i + q] = (uint8_t)(k[i] >> (8 * q));
-      const uint32_t m = len < 64u ? len : 64u;
-      for (uint32_t i = 0; i < m; i++) buf[32 + i] = msg[i];
-      sha256(dig, buf, 32 + m);
-      for (int i = 0; i < 8; i++)
-        bw[i] = (uint32_t)dig[4 * i] | ((uint32_t)dig[4 * i + 1] << 8) | ((uint32_t)dig[4 * i + 2] << 16) |
-                ((uint32_t)dig[4 * i + 3] << 24);
+      uint32_t hs[8];  // SHA-256(sk || msg[0 .. 64)) is the blind's seed
+      sha256_key_msg(hs, k, 0, msg, len < 64u ? len : 64u);
+      for (int i = 0; i < 8; i++) bw[i] = sha256_bswap(hs[i]);  // digest bytes as little-endian words
       bw[7] &= 0x1fffffffu;  // < 2^253 < q
       bw[0] |= (bw[0] | bw[1] | bw[2] | bw[3] | bw[4] | bw[5] | bw[6] | bw[7]) == 0u ? 1u : 0u;
-      for (int i = 0; i < 32 + 64; i++) buf[i] = 0;
     }
     fp b, zb, zi, zi2;
     f_from_words(b, bw);
@@ -489,6 +497,9 @@ __global__ void __launch_bounds__(128) bls_sign_row_kernel(const uint32_t* H, co
     out37[3] = (uint8_t)id;
     g1_compress(out37 + 4, a);
   }
+#if CBFT_BLS_PHASES
+  if (__lane_id() == 0) printf("sign finish (us): %.1f\n", (wall_clock64() - ph[3]) * 0.01);
+#endif
 }
 
 // H = g1_map(msg) into d_H (bls_hash_kernel), then the row-parallel signature

@@ -160,7 +160,7 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
   fp f;
   if (wave < 2) {
     g1a P;
-    g1_map_wave(P, msg, len);
+    g1_map_row(P, msg, len);
     BLS_PHASE(wave == 0 ? 4 : 12);
     if (wave == 0 && g.lane == 0 && H_out) g1a_store(H_out, P);
     if (wave == 0)
@@ -270,7 +270,7 @@ __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uin
     if (g.lane == 0) progress = BN_ATE_LINES + 1;  // release the consumer whatever happened
   } else if (wave == 1) {
     g1a P;
-    g1_map_wave(P, msg, len);
+    g1_map_row(P, msg, len);
     BLS_PHASE(5);
     const uint32_t* l[1] = {lines};
     p36_miller<1, true>(f, &P, l, g, &progress);
@@ -324,7 +324,7 @@ __global__ void __launch_bounds__(64) bls_prep_kernel(const uint8_t* msg, uint32
   if (blockIdx.x == 0) {
     if (!H) return;
     g1a P;
-    g1_map_wave(P, msg, len);
+    g1_map_row(P, msg, len);
     if ((threadIdx.x & 63) == 0) g1a_store(H, P);
     return;
   }

@@ -169,6 +169,30 @@ RF_HD bool rf_row0_equals(U xn, U c) {
   return (rf_ballot(xn == c) & 0xFFFFull) == 0xFFFFull;
 }
 
+// a^e on row-parallel Fp for the window schedule of f_pow_sw (bn254_field.h: same windows, same
+// table of odd powers), each product on the row: ~2x less latency than the one-lane chain.
+// a row-normal < 2q; result row-normal < 2q.  The window index is uniform across the wave.
+template <class Sched, class U, class W>
+RF_HD U rf_pow_sw(U a, U qrow) {
+  U t[8];
+  t[0] = a;
+  const U a2 = rf_mul<U, W>(a, a, qrow);
+#pragma unroll
+  for (int k = 1; k < 8; k++) t[k] = rf_mul<U, W>(t[k - 1], a2, qrow);
+  U acc = t[0];
+  for (int w = 0; w < Sched::S.n; w++) {
+    for (int q = 0; q < Sched::S.nsq[w]; q++) acc = rf_mul<U, W>(acc, acc, qrow);
+    const int idx = Sched::S.v[w] >> 1;
+    U e = t[0];
+#pragma unroll
+    for (int k = 1; k < 8; k++)
+      if (idx == k) e = t[k];
+    acc = w == 0 ? e : rf_mul<U, W>(acc, e, qrow);
+  }
+  for (int q = 0; q < Sched::S.tail; q++) acc = rf_mul<U, W>(acc, acc, qrow);
+  return acc;
+}
+
 // ------------------------------------------------------------------------------ conversions
 // one-lane fp (every lane the same value) <-> row element
 template <class U, class F>

@@ -296,7 +296,7 @@ void cbft_close(cbft_ctx* c) {
     b->release();
   c->hstage.release();
   for (WorkSlot& w : c->slots) {
-    for (DevBuf* b : {&w.h, &w.flags, &w.xyz, &w.ps_tbl, &w.ps_aok}) b->release();
+    for (DevBuf* b : {&w.h, &w.flags, &w.xyz, &w.ps_tbl, &w.ps_aok, &w.perm, &w.buckets}) b->release();
     if (w.done) (void)hipEventDestroy(w.done);
   }
   for (hipEvent_t& e : c->ev)
@@ -691,9 +691,16 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     // the slot's previous batch (maybe on another stream) must be done with its buffers
     if (slot.used) CBFT_HIP(hipStreamWaitEvent(s, slot.done, 0));
   }
-  // variable-length batches from $CBFT_SHA_SORT_MIN signatures (default 1; 0 = never) hash in
-  // order of their SHA-512 block count within each K1 block (SURVEY.md §7 hard part ii)
+  // variable-length batches from $CBFT_SHA_SORT_MIN signatures (default 4,096; 0 = never) hash
+  // in order of their SHA-512 block count (SURVEY.md §7 hard part ii)
   const bool sort = !small && d_off && c->sha_sort_min && n >= c->sha_sort_min;
+  if (sort) {
+    CBFT_HIP(slot.perm.reserve(n * sizeof(uint32_t)));
+    if (!slot.buckets.p) {  // counts | cursors | uniform flag
+      CBFT_HIP(slot.buckets.reserve((2 * CBFT_SHA_BUCKETS + 1) * sizeof(uint32_t)));
+      CBFT_HIP(hipMemsetAsync(slot.buckets.p, 0, (2 * CBFT_SHA_BUCKETS + 1) * sizeof(uint32_t), s));  // counts start at 0
+    }
+  }
 
   Ed25519Batch b{n, d_pk, d_kidx, KeyChunks{nullptr, 0}, d_sig, d_msg, d_off, d_len,
                  kt ? kt->nkeys : (uint32_t)n, fixed_len};
@@ -707,7 +714,10 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   w.flags = slot.flags.as<uint8_t>();
   w.xyz_soa = slot.xyz.as<uint32_t>();
   w.verdict_words = d_verdicts;
-  w.sha_sort = sort ? 1 : 0;
+  if (sort) {
+    w.perm = slot.perm.as<uint32_t>();
+    w.buckets = slot.buckets.as<uint32_t>();
+  }
   if (table_id == CBFT_NO_KEY_TABLE) {
     // per-signature keys: decode + precompute per signature
     CBFT_HIP(cbft_ed25519_launch_prep(d_pk, n, slot.ps_tbl.as<uint32_t>(), slot.ps_aok.as<uint8_t>(), s));

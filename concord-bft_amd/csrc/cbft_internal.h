@@ -107,6 +107,7 @@ struct BlsKeySet {
 #define CBFT_WORK_SLOTS 2
 struct WorkSlot {
   DevBuf h, flags, xyz, ps_tbl, ps_aok;
+  DevBuf perm, buckets;  // hash order of a variable-length batch (counting sort by SHA-512 blocks)
   hipEvent_t done = nullptr;
   bool used = false;
 };
@@ -177,7 +178,7 @@ struct cbft_ctx {
   // $CBFT_SMALL_MAX, 0 = never): the per-request coalescer's batches
   size_t small_max = 1024;
   int small_waves = 2;  // fused small-batch kernel: 2 waves per 16 signatures, or 3 ($CBFT_SMALL_WAVES)
-  size_t sha_sort_min = 1;  // variable-length batches from this size hash in block-count order (per K1 block)
+  size_t sha_sort_min = 4096;  // variable-length batches from this size hash in block-count order
   int blocking_sync = 1;  // small batches' waiters sleep ($CBFT_BLOCKING_SYNC)
   int zero_copy = 1;  // fused small batches read pinned inputs and write verdicts in place ($CBFT_ZERO_COPY)
   int b_radix = CBFT_COMB_B_RADIX;  // radix of B's comb table ($CBFT_B_RADIX, 16..22)

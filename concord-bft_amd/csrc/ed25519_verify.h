@@ -124,14 +124,13 @@ struct Ed25519Work {
   uint32_t* xyz_soa;           // 27 x n words
   uint64_t* verdict_words;     // ceil(n/64) words; bit (i % 64) of word i/64 = accept
   int small;                   // key-table batch in ONE launch (ed25519_small_kernel): small batches
-  // Variable-length batch: K1 blocks of CBFT_SHA_SORT_BLOCK signatures hash them in order of their
-  // SHA-512 block count (a counting sort in LDS), so a wave's lanes run about the same number of
-  // blocks.
-  int sha_sort;
+  // Variable-length batches: hash signatures in order of their SHA-512 block count (a counting
+  // sort into perm before K1), so a wave's lanes run the same number of blocks.  Nullable.
+  uint32_t* perm;              // n words
+  uint32_t* buckets;           // CBFT_SHA_BUCKETS x 2 + 1 words (counts, cursors, uniform flag)
 };
 // Block-count buckets of the hash sort: bucket min(nblocks, CBFT_SHA_BUCKETS - 1).
-#define CBFT_SHA_BUCKETS 64
-#define CBFT_SHA_SORT_BLOCK 512
+#define CBFT_SHA_BUCKETS 256
 
 size_t cbft_ed25519_table_words_per_unit();
 // staging words for `lanes` table-build lanes (18 KB each)

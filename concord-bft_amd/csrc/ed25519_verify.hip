@@ -268,53 +268,69 @@ __device__ __forceinline__ uint32_t hash_bucket(const Ed25519Batch& b, size_t i)
   return nb < CBFT_SHA_BUCKETS - 1 ? nb : CBFT_SHA_BUCKETS - 1;
 }
 
-// K1.  SORT (variable-length batches): the block's BLOCK signatures are hashed in order of their
-// SHA-512 block count -- an LDS counting sort (ranks by LDS atomics, so the order inside a bucket
-// is arbitrary; each digest goes to its signature's own index, so verdicts do not depend on it),
-// thread t then hashing the t-th signature of that order.  With log-uniform 64..4,096-B messages
-// an unsorted wave runs every lane through the ~33 blocks of its longest message while the mean
-// is ~9; sorted within 512 signatures, a wave spans 1/8 of the block-count quantiles.  A block
-// whose signatures all share one block count (fixed-size messages) keeps the identity order.
-template <int BLOCK, bool SORT>
-__global__ void __launch_bounds__(BLOCK) ed25519_hash_kernel(const Ed25519Batch b, uint32_t* h_soa, uint8_t* flags) {
-  size_t i = (size_t)blockIdx.x * BLOCK + threadIdx.x;
-  if (SORT) {
-    __shared__ uint32_t hist[CBFT_SHA_BUCKETS], order[BLOCK], kmin, kmax;
-    static_assert(CBFT_SHA_BUCKETS == 64, "one wave scans the bucket counts");
-    if (threadIdx.x < CBFT_SHA_BUCKETS) hist[threadIdx.x] = 0;
-    if (threadIdx.x == 0) {
-      kmin = CBFT_SHA_BUCKETS;
-      kmax = 0;
-    }
+// Counting sort of a variable-length batch by SHA-512 block count, in three launches:
+// (1) per-bucket counts (LDS histogram per block, one global atomic per non-empty bucket);
+// (2) one block: exclusive scan of the counts into cursors (and counts reset for the next batch),
+//     and a flag word: 1 when every signature has the same block count (fixed-size messages),
+//     in which case (3) does nothing and K1 keeps the identity order (and its locality);
+// (3) every signature takes a slot of its bucket (LDS ranks per block, one global atomicAdd per
+//     non-empty bucket per block) and writes its index there.  Order inside a bucket is arbitrary:
+//     K1 writes each signature's digest to its own index, so verdicts do not depend on it.
+static_assert(CBFT_SHA_BUCKETS == 256, "the bucket kernels run one thread per bucket in 256-thread blocks");
+__global__ void __launch_bounds__(256) ed25519_bucket_count_kernel(const Ed25519Batch b, uint32_t* counts) {
+  __shared__ uint32_t hist[CBFT_SHA_BUCKETS];
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < b.n) atomicAdd(&hist[hash_bucket(b, i)], 1u);
+  __syncthreads();
+  if (hist[threadIdx.x]) atomicAdd(&counts[threadIdx.x], hist[threadIdx.x]);
+}
+
+__global__ void __launch_bounds__(256) ed25519_bucket_scan_kernel(uint32_t* counts, uint32_t* cursors) {
+  __shared__ uint32_t v[CBFT_SHA_BUCKETS];
+  const uint32_t t = threadIdx.x;
+  v[t] = counts[t];
+  __syncthreads();
+  for (uint32_t d = 1; d < CBFT_SHA_BUCKETS; d <<= 1) {  // inclusive Hillis-Steele scan
+    const uint32_t x = t >= d ? v[t - d] : 0u;
     __syncthreads();
-    const bool live = i < b.n;
-    uint32_t k = 0, rank = 0;
-    if (live) {
-      k = hash_bucket(b, i);
-      rank = atomicAdd(&hist[k], 1u);
-      atomicMin(&kmin, k);
-      atomicMax(&kmax, k);
-    }
+    v[t] += x;
     __syncthreads();
-    if (kmin < kmax) {  // block-uniform
-      if (threadIdx.x < CBFT_SHA_BUCKETS) {  // wave 0: exclusive scan of the 64 counts
-        const uint32_t v = hist[threadIdx.x];
-        uint32_t x = v;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-          const uint32_t y = __shfl_up(x, d, 64);
-          if ((int)threadIdx.x >= d) x += y;
-        }
-        hist[threadIdx.x] = x - v;
-      }
-      __syncthreads();
-      if (live) order[hist[k] + rank] = threadIdx.x;
-      __syncthreads();
-      // the live signatures fill order[0, live count); threads past it are past n anyway
-      if (live) i = (size_t)blockIdx.x * BLOCK + order[threadIdx.x];
-    }
   }
-  if (i >= b.n) return;
+  const uint32_t c = counts[t];
+  cursors[t] = v[t] - c;
+  counts[t] = 0;  // ready for the next batch's counts
+  if (t == 0) cursors[CBFT_SHA_BUCKETS] = 0;
+  __syncthreads();
+  if (c != 0 && c == v[CBFT_SHA_BUCKETS - 1]) cursors[CBFT_SHA_BUCKETS] = 1;  // one bucket holds all
+}
+
+__global__ void __launch_bounds__(256) ed25519_bucket_scatter_kernel(const Ed25519Batch b, uint32_t* cursors,
+                                                                     uint32_t* perm) {
+  __shared__ uint32_t hist[CBFT_SHA_BUCKETS], base[CBFT_SHA_BUCKETS];
+  if (cursors[CBFT_SHA_BUCKETS]) return;  // uniform: K1 keeps the identity order
+  hist[threadIdx.x] = 0;
+  __syncthreads();
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t k = 0, rank = 0;
+  if (i < b.n) {
+    k = hash_bucket(b, i);
+    rank = atomicAdd(&hist[k], 1u);
+  }
+  __syncthreads();
+  if (hist[threadIdx.x]) base[threadIdx.x] = atomicAdd(&cursors[threadIdx.x], hist[threadIdx.x]);
+  __syncthreads();
+  if (i < b.n) perm[base[k] + rank] = (uint32_t)i;
+}
+
+// perm: the block-count order (nullable); uniform: its flag word (perm unused when set)
+__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const Ed25519Batch b, const uint32_t* perm,
+                                                                          const uint32_t* uniform, uint32_t* h_soa,
+                                                                          uint8_t* flags) {
+  const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= b.n) return;
+  const size_t i = perm && !*uniform ? (size_t)perm[g] : g;
   uint32_t hw[8];
   bool flag;
   ed25519_hash_sig(b, i, hw, flag);
@@ -945,17 +961,30 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
 // (x_R, y_R) projectively (X = x_R Z, Y = y_R Z): the encoding is a bijection between points and
 // canonical encodings, and the decoder picks x by the sign bit.  The R decode (a square-root
 // chain) runs under the hash and the comb instead of an inversion after them.  The verdicts of
-// the block's 16 signatures go out as one 16-bit word; no per-signature state goes through HBM.
+// the block's signatures go out as one 8- or 16-bit piece; no per-signature state goes through HBM.
 // ---------------------------------------------------------------------------------------
-#define SMALL_SIGS 16
 // R decoders per block: CBFT_DECODE_ROW = 1 puts each signature's square-root chain on a 16-lane
-// DPP row (ge_frombytes_row), four waves for the block's 16 signatures; 0 keeps one wave with a
-// lane quad per signature on the one-lane chain.
+// DPP row (ge_frombytes_row), two waves for the block's 8 signatures, so a block is 3 waves (4 in
+// the three-wave form) and every wave has a SIMD of its own (a fifth wave would share one: measured
+// on gfx950, the decode wave that shares wave 0's SIMD takes 80 us against 42 us, and slows the
+// hash); 0 keeps one wave with a lane quad per signature on the one-lane chain, 16 signatures.
 #ifndef CBFT_DECODE_ROW
 #define CBFT_DECODE_ROW 1
 #endif
-#define SMALL_DEC_WAVES (CBFT_DECODE_ROW ? 4 : 1)
+#define SMALL_SIGS (CBFT_DECODE_ROW ? 8 : 16)
+#define SMALL_DEC_WAVES (CBFT_DECODE_ROW ? 2 : 1)
 #define SMALL_BLOCK (64 * (1 + SMALL_DEC_WAVES))
+
+// The block's verdict bits (bit s = signature blk * SMALL_SIGS + s) as SMALL_SIGS / 8 bytes; the
+// last block also zeroes the bytes of its 64-bit verdict word that no block covers, so the call
+// writes whole ceil(n/64) words (bits past n = 0) like the ballot kernels.
+__device__ __forceinline__ void small_store_bits(uint8_t* vb, uint32_t bits) {
+  constexpr uint32_t BYTES = SMALL_SIGS / 8;
+#pragma unroll
+  for (uint32_t k = 0; k < BYTES; k++) vb[blockIdx.x * BYTES + k] = (uint8_t)(bits >> (8 * k));
+  if (blockIdx.x == gridDim.x - 1)
+    for (uint32_t p = (blockIdx.x + 1) * BYTES; (p & 7u) != 0u; p++) vb[p] = 0;
+}
 
 // Decode wave dw of a small-kernel block: x_R | y_R | (R decodes && y canonical && not (x = 0
 // with the sign bit set)) of its signatures into rdec.
@@ -992,13 +1021,14 @@ __device__ __forceinline__ void small_decode_r(const Ed25519Batch& b, uint32_t b
   }
 }
 __global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed25519Batch b, const uint32_t* btbl,
-                                                                    const CombLadder cl, uint16_t* verdict16) {
+                                                                    const CombLadder cl, uint8_t* verdict_bytes) {
   __shared__ int32_t sdig[COMB_MAX_STEPS * 64];
   __shared__ uint4 stage[7 * 64];
   __shared__ uint32_t rdec[SMALL_SIGS][2 * FE_LIMBS + 1];  // x_R | y_R | decodes
-  const uint32_t ln = threadIdx.x & 63u, wave = threadIdx.x >> 6, q = ln & 3u, sl = ln >> 2;
+  // quads past the block's signatures (lanes 32..63 with 8 signatures) repeat quads 0..7 unused
+  const uint32_t ln = threadIdx.x & 63u, wave = threadIdx.x >> 6, q = ln & 3u, sl = (ln >> 2) & (SMALL_SIGS - 1);
   size_t i = (size_t)blockIdx.x * SMALL_SIGS + sl;
-  const bool live = i < b.n;
+  const bool live = i < b.n && (ln >> 2) < SMALL_SIGS;
   if (!live) i = b.n - 1;
 #if CBFT_ED_PHASES  // probe builds: block 0's phase times (10 ns ticks), printed by lane 0
   uint64_t ph[6];
@@ -1053,13 +1083,7 @@ __global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed2551
   uint32_t bits = 0;
 #pragma unroll
   for (int s2 = 0; s2 < SMALL_SIGS; s2++) bits |= (uint32_t)((bal >> (4 * s2)) & 1u) << s2;
-  if (ln == 0) {
-    verdict16[blockIdx.x] = (uint16_t)bits;
-    // the last block also zeroes the 16-bit pieces of its 64-bit verdict word that no block
-    // covers, so the call writes whole ceil(n/64) words (bits past n = 0) like the ballot kernels
-    if (blockIdx.x == gridDim.x - 1)
-      for (uint32_t p = blockIdx.x + 1; (p & 3u) != 0u; p++) verdict16[p] = 0;
-  }
+  if (ln == 0) small_store_bits(verdict_bytes, bits);
 }
 
 // The same verdicts with the work of a block of 16 signatures on THREE waves (three SIMDs):
@@ -1069,15 +1093,15 @@ __global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed2551
 // Selected by $CBFT_SMALL_WAVES=3.
 #define SMALL3_BLOCK (64 * (2 + SMALL_DEC_WAVES))
 __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25519Batch b, const uint32_t* btbl,
-                                                                      const CombLadder cl, uint16_t* verdict16) {
+                                                                      const CombLadder cl, uint8_t* verdict_bytes) {
   __shared__ int32_t sdig[2][COMB_MAX_STEPS * 64];
   __shared__ uint4 stage[2][7 * 64];
   __shared__ uint32_t rdec[SMALL_SIGS][2 * FE_LIMBS + 1];  // x_R | y_R | decodes
   __shared__ uint32_t sbp[SMALL_SIGS][4 * FE_LIMBS];       // [S]B as X | Y | Z | T
-  const uint32_t ln = threadIdx.x & 63u, wave = threadIdx.x >> 6, q = ln & 3u, sl = ln >> 2;
+  const uint32_t ln = threadIdx.x & 63u, wave = threadIdx.x >> 6, q = ln & 3u, sl = (ln >> 2) & (SMALL_SIGS - 1);
   size_t i = (size_t)blockIdx.x * SMALL_SIGS + sl;
-  const bool live = i < b.n;
-  if (!live) i = b.n - 1;
+  const bool live = i < b.n && (ln >> 2) < SMALL_SIGS;
+  if (i >= b.n) i = b.n - 1;
   const uint32_t na = (uint32_t)cl.a.npos, ntot = na + (uint32_t)cl.b.npos;
   if (wave >= 2) {
     small_decode_r(b, blockIdx.x, wave - 2, ln, rdec);
@@ -1090,7 +1114,7 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
     comb_quad_sum<64>(b, i, q, zero, btbl, cl, sdig[1], stage[1], P, na, ntot, (int)((ntot - na + 3) / 4));
     quad_combine<0xB1>(P, true);
     quad_combine<0x4E>(P, true);
-    if (q == 0) {
+    if (q == 0 && (ln >> 2) < SMALL_SIGS) {
 #pragma unroll
       for (int k = 0; k < FE_LIMBS; k++) {
         sbp[sl][k] = P.X.v[k];
@@ -1145,11 +1169,7 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
   uint32_t bits = 0;
 #pragma unroll
   for (int s2 = 0; s2 < SMALL_SIGS; s2++) bits |= (uint32_t)((bal >> (4 * s2)) & 1u) << s2;
-  if (ln == 0) {
-    verdict16[blockIdx.x] = (uint16_t)bits;
-    if (blockIdx.x == gridDim.x - 1)
-      for (uint32_t p = blockIdx.x + 1; (p & 3u) != 0u; p++) verdict16[p] = 0;
-  }
+  if (ln == 0) small_store_bits(verdict_bytes, bits);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1409,22 +1429,25 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
       for (int k = 0; k < 3; k++) (void)hipEventRecord(ev[k], stream);
     if (w.small == 3)
       hipLaunchKernelGGL(ed25519_small3_kernel, dim3((unsigned)((b.n + SMALL_SIGS - 1) / SMALL_SIGS)), dim3(SMALL3_BLOCK), 0,
-                         stream, b, w.base_comb, w.comb, reinterpret_cast<uint16_t*>(w.verdict_words));
+                         stream, b, w.base_comb, w.comb, reinterpret_cast<uint8_t*>(w.verdict_words));
     else
       hipLaunchKernelGGL(ed25519_small_kernel, dim3((unsigned)((b.n + SMALL_SIGS - 1) / SMALL_SIGS)), dim3(SMALL_BLOCK), 0,
-                         stream, b, w.base_comb, w.comb, reinterpret_cast<uint16_t*>(w.verdict_words));
+                         stream, b, w.base_comb, w.comb, reinterpret_cast<uint8_t*>(w.verdict_words));
     if (ev) (void)hipEventRecord(ev[3], stream);
     return hipGetLastError();
   }
   if (order && order->wait && order->hash && (e = hipStreamWaitEvent(stream, order->done[0], 0)) != hipSuccess)
     return e;
   if (ev) (void)hipEventRecord(ev[0], stream);
-  if (w.sha_sort && b.msg_off)
-    hipLaunchKernelGGL((ed25519_hash_kernel<CBFT_SHA_SORT_BLOCK, true>),
-                       dim3((unsigned)((b.n + CBFT_SHA_SORT_BLOCK - 1) / CBFT_SHA_SORT_BLOCK)), dim3(CBFT_SHA_SORT_BLOCK),
-                       0, stream, b, w.h_soa, w.flags);
-  else
-    hipLaunchKernelGGL((ed25519_hash_kernel<CBFT_VERIFY_BLOCK, false>), grid, block, 0, stream, b, w.h_soa, w.flags);
+  const bool sorted = w.perm && w.buckets && b.msg_off;
+  if (sorted) {
+    const dim3 g256((unsigned)((b.n + 255) / 256)), b256(256);
+    hipLaunchKernelGGL(ed25519_bucket_count_kernel, g256, b256, 0, stream, b, w.buckets);
+    hipLaunchKernelGGL(ed25519_bucket_scan_kernel, dim3(1), b256, 0, stream, w.buckets, w.buckets + CBFT_SHA_BUCKETS);
+    hipLaunchKernelGGL(ed25519_bucket_scatter_kernel, g256, b256, 0, stream, b, w.buckets + CBFT_SHA_BUCKETS, w.perm);
+  }
+  hipLaunchKernelGGL(ed25519_hash_kernel, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
+                     sorted ? (const uint32_t*)(w.buckets + 2 * CBFT_SHA_BUCKETS) : nullptr, w.h_soa, w.flags);
   if (order && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;
   if (order && order->wait && order->ladder && (e = hipStreamWaitEvent(stream, order->done[1], 0)) != hipSuccess)
     return e;

@@ -18,13 +18,13 @@
 #if defined(__HIPCC__)
 template <int I>
 RF_HD uint32_t rl_bcast(uint32_t x) {  // lane I of each row -> the whole row
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x150 + I, 0xF, 0xF, false);
-}
-// the same broadcast without an "old" operand: row_newbcast writes every lane, so the result
-// needs no zeroed destination (update_dpp(0, ...) costs a v_mov 0 per broadcast)
-template <int I>
-RF_HD uint32_t rl_bcast_w(uint32_t x) {
+  // row_newbcast writes every lane, so no "old" operand: update_dpp(0, ...) would cost a v_mov 0
+  // per broadcast for a destination value no lane keeps
   return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x150 + I, 0xF, 0xF, false);
+}
+template <int I>
+RF_HD uint32_t rl_bcast_w(uint32_t x) {  // alias (fe25519_row.h)
+  return rl_bcast<I>(x);
 }
 template <int I>
 RF_HD uint32_t rl_shr(uint32_t x) {  // lane k <- lane k - I of the row, 0 below

@@ -88,3 +88,44 @@ BN_HD void sha256(uint8_t* out, const uint8_t* msg, uint32_t len) {
     out[4 * i + 3] = (uint8_t)h[i];
   }
 }
+
+BN_HD uint32_t sha256_bswap(uint32_t x) {
+  return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+}
+
+// h = SHA-256 state after hashing K || msg[0 .. m), m <= 64, where K is the 32 little-endian bytes
+// of key[0..8) each xored with x.  Every block word is built at a compile-time index, so the
+// padded message stays in registers (sha256() over a byte-indexed local buffer of run-time length
+// lives in scratch memory on the GPU: ~2,200 instructions of byte addressing per block).  The
+// digest bytes are the big-endian bytes of h[0..8).
+BN_HD void sha256_key_msg(uint32_t* h, const uint32_t* key, uint8_t x, const uint8_t* msg, uint32_t m) {
+  const uint32_t h0[8] = {0x6a09e667u, 0xbb67ae85u, 0x3c6ef372u, 0xa54ff53au,
+                          0x510e527fu, 0x9b05688cu, 0x1f83d9abu, 0x5be0cd19u};
+  for (int i = 0; i < 8; i++) h[i] = h0[i];
+  const uint32_t xx = 0x01010101u * x, total = 32u + m, nblk = (total + 9u + 63u) / 64u;
+  uint32_t blk[32];
+#pragma unroll
+  for (int j = 0; j < 32; j++) {
+    uint32_t w = 0;
+    if (j < 8) {
+      w = sha256_bswap(key[j] ^ xx);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const uint32_t pos = (uint32_t)(4 * j + q - 32);
+        const uint32_t byte = pos < m ? msg[pos] : (pos == m ? 0x80u : 0u);
+        w = (w << 8) | byte;
+      }
+    }
+    blk[j] = w;
+  }
+  if (nblk == 1) {
+    blk[14] = 0;
+    blk[15] = total << 3;
+  } else {
+    blk[30] = 0;
+    blk[31] = total << 3;
+  }
+  sha256_block(h, blk);
+  if (nblk == 2) sha256_block(h, blk + 16);
+}

@@ -93,6 +93,48 @@ int shim_fp_inv(const uint8_t* x32, uint8_t* out_var, uint8_t* out_fermat) {
   return std::memcmp(w, w2, sizeof w) == 0 ? 1 : 0;
 }
 
+// rf_pow_sw (bn254_row.h) for the square-root schedule on four emulated rows against the one-lane
+// f_pow_sw, for four values x (32-byte big-endian, < p): writes the four row results (big-endian
+// canonical) and returns 1 when each equals the one-lane result and no product broke its bounds.
+int shim_rf_sqrt_pow(const uint8_t* x128, uint8_t* out128) {
+  HU in;
+  fp lane[4];
+  for (int r = 0; r < 4; r++) {
+    uint32_t w[8];
+    be32_to_words(w, x128 + 32 * r);
+    f_from_words(lane[r], w);
+    for (int i = 0; i < BN_LIMBS; i++) in.x[16 * r + i] = lane[r].v[i];
+  }
+  const long v0 = g_rf_bound_violations;
+  const HU qrow = rf_row_const(FpParams::Q, in);
+  const HU y = rf_pow_sw<FpSqrtSchedule, HU, HW>(in, qrow);
+  int ok = g_rf_bound_violations == v0;
+  for (int r = 0; r < 4; r++) {
+    fp a, b;
+    uint32_t c = 0;
+    for (int i = 0; i < BN_LIMBS; i++) {
+      const uint32_t t = y.x[16 * r + i] + c;
+      a.v[i] = i < BN_LIMBS - 1 ? (t & BN_MASK) : t;
+      c = t >> 29;
+    }
+    f_pow_sw<FpParams, FpSqrtSchedule>(b, lane[r]);
+    uint32_t wa[8], wb[8];
+    f_to_words(wa, a);
+    f_to_words(wb, b);
+    words_to_be32(out128 + 32 * r, wa);
+    ok = ok && std::memcmp(wa, wb, sizeof wa) == 0;
+  }
+  return ok;
+}
+
+// sha256_key_msg (sha256.h: the BLS blinds' register-resident SHA-256) -> 32-byte digest
+void shim_sha256_key_msg(const uint32_t* key8, uint32_t x, const uint8_t* msg, uint32_t m, uint8_t* out32) {
+  uint32_t h[8];
+  sha256_key_msg(h, key8, (uint8_t)x, msg, m);
+  for (int i = 0; i < 8; i++)
+    for (int q = 0; q < 4; q++) out32[4 * i + q] = (uint8_t)(h[i] >> (24 - 8 * q));
+}
+
 // ---- the lazy cyclotomic squaring (bn254_cycsq.h) on an emulated pair36 wave ----------------
 static uint64_t sm64(uint64_t& x) {
   uint64_t z = (x += 0x9e3779b97f4a7c15ull);

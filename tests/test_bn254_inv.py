@@ -227,3 +227,34 @@ def test_row_g2_subgroup_on_cofactor_torsion():
         bad = lib.shim_g2r_subgroup_scaled(k1 * 7 + k2, 8, words(k1), words(k2), ctypes.byref(tested))
         assert bad == 0
         assert tested.value >= want - 1  # a point may have no component in the target subgroup
+
+
+def test_row_sqrt_power_matches_one_lane(shim):
+    """rf_pow_sw (bn254_row.h), the row-parallel square-root power of g1_map_row, on four emulated
+    DPP rows: x^((p+1)/4) mod p, equal to the one-lane f_pow_sw, every product within its bounds."""
+    rng = random.Random(0x5A27)
+    xs = [0, 1, 2, 3, P - 1, P - 2, (P - 1) // 2, 2**253, 2**254 % P] + [rng.randrange(P) for _ in range(63)]
+    xs += [1] * (-len(xs) % 4)
+    for k in range(0, len(xs), 4):
+        buf = b"".join(x.to_bytes(32, "big") for x in xs[k:k + 4])
+        out = ctypes.create_string_buffer(128)
+        assert shim.shim_rf_sqrt_pow(buf, out) == 1
+        for r in range(4):
+            assert int.from_bytes(out.raw[32 * r:32 * r + 32], "big") == pow(xs[k + r], (P + 1) // 4, P)
+
+
+def test_sha256_key_msg_matches_hashlib(shim):
+    """sha256_key_msg (sha256.h), the register-resident SHA-256 of the BLS signing / key blinds:
+    SHA-256(key bytes ^ x || msg[:m]) for m = 0..64 (one and two blocks, every padding boundary)."""
+    import hashlib
+    import struct
+
+    rng = random.Random(0x256)
+    for m in range(65):
+        key = [rng.getrandbits(32) for _ in range(8)]
+        x = rng.choice((0, 0x5C))
+        msg = bytes(rng.getrandbits(8) for _ in range(m))
+        out = ctypes.create_string_buffer(32)
+        shim.shim_sha256_key_msg((ctypes.c_uint32 * 8)(*key), x, msg, m, out)
+        kb = bytes(b ^ x for b in struct.pack("<8I", *key))
+        assert out.raw == hashlib.sha256(kb + msg).digest(), m

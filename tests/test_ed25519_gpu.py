@@ -402,10 +402,10 @@ def test_device_path_small_batch_whole_words(n):
 
 @pytest.mark.parametrize("n", [1, 100, 257, 5000])
 def test_hash_block_count_sort(golden, n, monkeypatch):
-    """Variable-length batches hash in order of their SHA-512 block count (an LDS counting sort in
-    each K1 block): verdicts equal OpenSSL's and the unsorted path's for every signature, across
-    ragged sizes (partial last blocks) and lengths straddling block boundaries (0..4,096 B, golden
-    lengths too)."""
+    """Variable-length batches hash in order of their SHA-512 block count (a counting sort into a
+    permutation before K1; a batch whose messages share one block count keeps the identity order):
+    verdicts equal OpenSSL's and the unsorted path's for every signature, across ragged sizes and
+    lengths straddling block boundaries (0..4,096 B, golden lengths too)."""
     keys = sorted({v.pk for v in golden})
     index = {k: i for i, k in enumerate(keys)}
     vs = [golden[i % len(golden)] for i in range(n)]
@@ -418,16 +418,20 @@ def test_hash_block_count_sort(golden, n, monkeypatch):
         with cb.Context(device=0) as c:
             tid = c.load_keys(keys)
             out[label] = _bools(c.verify(tid, *args), n)
-            # a second batch through the same context
+            # a second batch through the same work slot: the bucket counters were reset
             out[label + "2"] = _bools(c.verify(tid, *args), n)
     for k, v in out.items():
         assert np.array_equal(v, exp), k
-    ss = sigsets.make_sigset(n, nkeys=16, msg_len=(1, 4096), seed=77 + n, invalid_frac=0.1)
     monkeypatch.setenv("CBFT_SHA_SORT_MIN", "1")
-    with cb.Context(device=0) as c:
-        tid = c.load_keys(ss.pk)
-        got = _bools(c.verify_packed(tid, ss.key_idx, ss.sig, ss.blob, ss.off, ss.len), n)
-    assert np.array_equal(got, ss.expected)
+    # random lengths, then one length for all (every signature in one bucket: the identity order)
+    for msg_len in ((1, 4096), 200):
+        ss = sigsets.make_sigset(n, nkeys=16, msg_len=msg_len, seed=77 + n, invalid_frac=0.1)
+        with cb.Context(device=0) as c:
+            tid = c.load_keys(ss.pk)
+            got = _bools(c.verify_packed(tid, ss.key_idx, ss.sig, ss.blob, ss.off, ss.len), n)
+            got2 = _bools(c.verify_packed(tid, ss.key_idx, ss.sig, ss.blob, ss.off, ss.len), n)
+        assert np.array_equal(got, ss.expected), msg_len
+        assert np.array_equal(got2, ss.expected), msg_len
 
 
 @pytest.mark.parametrize("chunk", [1, 17, 300, 1024])

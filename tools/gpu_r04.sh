@@ -12,6 +12,7 @@
 #   phases      phase times of the fused small-batch kernel (build/lib_edphases.so, -DCBFT_ED_PHASES=1)
 #   trace       kernel trace of the device-resident two-stream pipeline (overlap of the stages)
 #   ab          interleaved A/B of $LIBS (tools/ab_libs.sh)
+#   blsphases   phase times of the BLS signing kernel (build/lib_blsphases.so, -DCBFT_BLS_PHASES=1)
 #   abmix       the same over config #3 only (tools/mixed_probe.py)
 #   san         host-layer ASan+UBSan / TSan runs (make sanitize first)
 set -o pipefail
@@ -54,6 +55,10 @@ for step in "$@"; do
         > gpurun_out/pmc_bls.json || exit 1 ;;
     ab)
       bash tools/ab_libs.sh || exit 1 ;;
+    blsphases)
+      CBFT_LIB=$R/build/lib_blsphases.so timeout -k 10 120 python3 -u tools/bls_probe.py --reps 2 > gpurun_out/bls_phases.log 2>&1 \
+        || { echo "bls phase probe failed"; tail -20 gpurun_out/bls_phases.log; exit 1; }
+      grep -E "sign|{" gpurun_out/bls_phases.log | tail -12 ;;
     abmix)
       MODE=mixed bash tools/ab_libs.sh || exit 1 ;;
     phases)

@@ -14,6 +14,9 @@ import workload  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--steps", type=int, default=40)
 args = ap.parse_args()
+import torch  # noqa: E402  (initialised first, as bench.py does)
+
+torch.cuda.set_device(0)
 ss = workload.make_sigset(65536, nkeys=4096, msg_len=(64, 4096), seed=0xBADC0DE, invalid_frac=0.10, threads=16)
 with cb.Context(device=0) as ctx:
     tid = ctx.load_keys(ss.pk)
