@@ -669,9 +669,11 @@ int cbft_ed25519_unload_keys(cbft_ctx* c, uint32_t id) {
 }
 
 // Launch the verify pipeline for a batch whose inputs are already on the device.
+// uniform_blocks: the caller knows every message has the same SHA-512 block count (no sort)
 static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, const uint32_t* d_kidx,
                          const uint8_t* d_sig, const uint8_t* d_msg, const uint64_t* d_off, const uint32_t* d_len,
-                         uint32_t fixed_len, size_t n, uint64_t* d_verdicts, hipStream_t s) {
+                         uint32_t fixed_len, size_t n, uint64_t* d_verdicts, hipStream_t s,
+                         bool uniform_blocks = false) {
   int rc = reserve_work(c, n);
   if (rc) return rc;
   KeyTable* kt = nullptr;
@@ -693,7 +695,7 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   }
   // variable-length batches from $CBFT_SHA_SORT_MIN signatures (default 4,096; 0 = never) hash
   // in order of their SHA-512 block count (SURVEY.md §7 hard part ii)
-  const bool sort = !small && d_off && c->sha_sort_min && n >= c->sha_sort_min;
+  const bool sort = !small && d_off && !uniform_blocks && c->sha_sort_min && n >= c->sha_sort_min;
   if (sort) {
     CBFT_HIP(slot.perm.reserve(n * sizeof(uint32_t)));
     if (!slot.buckets.p) {  // counts | cursors | uniform flag
@@ -829,15 +831,20 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
   }
   // message bytes to move: [blo, bhi) of the blob (offsets need not start at 0)
   uint64_t blo = 0, bhi = 0;
+  uint32_t lmin = 0, lmax = 0;  // message lengths: one SHA-512 block count for all -> no hash sort
   if (fixed) {
     bhi = (uint64_t)fixed_len * n;
   } else if (n) {
     blo = UINT64_MAX;
+    lmin = UINT32_MAX;
     for (size_t i = 0; i < n; i++) {
       blo = std::min<uint64_t>(blo, msg_off[i]);
       bhi = std::max<uint64_t>(bhi, msg_off[i] + msg_len[i]);
+      lmin = std::min(lmin, msg_len[i]);
+      lmax = std::max(lmax, msg_len[i]);
     }
   }
+  const bool uniform_blocks = (64u + (uint64_t)lmin + 17u + 127u) / 128u == (64u + (uint64_t)lmax + 17u + 127u) / 128u;
   const uint64_t blob = bhi - blo;
   if (blob && !msg_blob) return CBFT_EINVAL;
   int rc = reserve_work(c, n);
@@ -911,7 +918,7 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
     rc = launch_locked(c, table_id, nullptr, reinterpret_cast<const uint32_t*>(zin + o_key), zin + o_sig,
                        zin + o_msg - blo, fixed ? nullptr : reinterpret_cast<const uint64_t*>(zin + o_off),
                        fixed ? nullptr : reinterpret_cast<const uint32_t*>(zin + o_len), fixed_len, n,
-                       static_cast<uint64_t*>(s.hverd.dev), cs);
+                       static_cast<uint64_t*>(s.hverd.dev), cs, uniform_blocks);
     if (rc) return rc;
     s.wait_ev = c->blocking_sync ? s.done_blk : s.done;
     CBFT_HIP(hipEventRecord(s.wait_ev, cs));
@@ -972,7 +979,7 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
   rc = launch_locked(c, table_id, kt ? nullptr : din + o_key, kt ? reinterpret_cast<const uint32_t*>(din + o_key) : nullptr,
                      din + o_sig, din + o_msg - blo, fixed ? nullptr : reinterpret_cast<const uint64_t*>(din + o_off),
                      fixed ? nullptr : reinterpret_cast<const uint32_t*>(din + o_len), fixed_len, n,
-                     s.verd.as<uint64_t>(), cs);
+                     s.verd.as<uint64_t>(), cs, uniform_blocks);
   if (rc) return rc;
   CBFT_HIP(hipMemcpyAsync(s.hverd.p, s.verd.p, nw * 8, hipMemcpyDeviceToHost, cs));
   CBFT_HIP(hipEventRecord(s.done, cs));

@@ -167,26 +167,35 @@ __global__ void __launch_bounds__(64) ed25519_base_table_kernel(uint32_t* tbl, i
 // K1: h = SHA-512(R || A || M) mod L, S < L check
 // ---------------------------------------------------------------------------------------
 
-// NW big-endian 64-bit words of (M || 0x80 || 0 ...) starting at M-relative offset base.
+// NW big-endian 64-bit words of (M || 0x80 || 0 ...) starting at M-relative offset base, in two
+// steps so a caller can issue the loads of the next window before compressing the current one:
+// fetch_msg_dwords loads the 2 NW + 1 dwords, assemble_msg_words aligns, masks and marks them.
 // Only dwords that overlap [m, m+len) are loaded (an aligned dword holding >= 1 message byte
 // never faults), so callers need no padding after the blob.
 //
 // Branch-free: dword k is read from index min(k, kmax) (kmax = last dword holding a byte of
 // M), or from `safe` (any readable dword) when no dword of this window holds one; bytes at or
 // past len are then masked off arithmetically, so a wave never splits on message length.
+#ifndef CBFT_SHA_PREFETCH  // 1: K1 loads block j + 1's message words before compressing block j
+#define CBFT_SHA_PREFETCH 1
+#endif
 template <int NW>
-__device__ __forceinline__ void load_msg_words(uint64_t* W, const uint8_t* m, uint32_t len, uint32_t base,
-                                               const uint32_t* safe) {
+__device__ __forceinline__ void fetch_msg_dwords(uint32_t* d, const uint8_t* m, uint32_t len, uint32_t base,
+                                                 const uint32_t* safe) {
   const uintptr_t a = (uintptr_t)(m + base);
   const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
   const uint32_t sh = (uint32_t)(a & 3);
   const int kmax = ((int)len - 1 - (int)base + (int)sh) >> 2;  // < 0: window is past M
-  uint32_t d[2 * NW + 1];
 #pragma unroll
   for (int k = 0; k < 2 * NW + 1; k++) {
     const uint32_t* src = kmax >= 0 ? q + (k < kmax ? k : kmax) : safe;
     d[k] = *src;
   }
+}
+template <int NW>
+__device__ __forceinline__ void assemble_msg_words(uint64_t* W, const uint32_t* d, const uint8_t* m, uint32_t len,
+                                                   uint32_t base) {
+  const uint32_t sh = (uint32_t)((uintptr_t)(m + base) & 3);
 #pragma unroll
   for (int j = 0; j < NW; j++) {
     const uint32_t lo = __builtin_amdgcn_alignbyte(d[2 * j + 1], d[2 * j], sh);
@@ -234,16 +243,20 @@ __device__ __forceinline__ void ed25519_hash_sig(const Ed25519Batch& b, size_t i
   sha512_init(H);
   const uint32_t total = 64u + len;
   const uint32_t nblocks = (total + 17u + 127u) / 128u;
+  uint32_t d[33];  // the message dwords of the next block, loaded while the current one compresses
+  fetch_msg_dwords<8>(d, m, len, 0u, safe);
   for (uint32_t blk = 0; blk < nblocks; blk++) {
+    if (!CBFT_SHA_PREFETCH && blk > 0) fetch_msg_dwords<16>(d, m, len, 128u * blk - 64u, safe);
     if (blk == 0) {  // R || A || M[0..63]
 #pragma unroll
       for (int j = 0; j < 4; j++) W[j] = ((uint64_t)bswap32(Rw[2 * j]) << 32) | bswap32(Rw[2 * j + 1]);
 #pragma unroll
       for (int j = 0; j < 4; j++) W[4 + j] = ((uint64_t)bswap32(Aw[2 * j]) << 32) | bswap32(Aw[2 * j + 1]);
-      load_msg_words<8>(W + 8, m, len, 0u, safe);
+      assemble_msg_words<8>(W + 8, d, m, len, 0u);
     } else {
-      load_msg_words<16>(W, m, len, 128u * blk - 64u, safe);
+      assemble_msg_words<16>(W, d, m, len, 128u * blk - 64u);
     }
+    if (CBFT_SHA_PREFETCH && blk + 1 < nblocks) fetch_msg_dwords<16>(d, m, len, 128u * blk + 64u, safe);
     if (blk == nblocks - 1) {
       W[14] = 0;
       W[15] = (uint64_t)total << 3;

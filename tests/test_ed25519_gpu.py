@@ -374,14 +374,17 @@ def test_golden_small_batches_fused_kernel(ctx, golden, chunk):
         three.close()
 
 
-@pytest.mark.parametrize("n", [1, 17, 47, 64, 65, 130])
-def test_device_path_small_batch_whole_words(n):
+@pytest.mark.parametrize("n,msg_len", [(1, 256), (9, 256), (17, 256), (47, 256), (64, 256), (65, 256), (130, 256),
+                                       (5000, 256), (5000, (1, 2048))])
+def test_device_path_small_batch_whole_words(n, msg_len):
     """cbft_ed25519_verify_batch_device writes ceil(n/64) WHOLE 64-bit verdict words, bits past n
-    = 0, also when the batch runs as the fused small kernel (16-bit pieces per block): the buffer
-    is pre-filled with 0xFF, so a piece no block covers would show up as stray accept bits."""
+    = 0, also when the batch runs as the fused small kernel (8-signature pieces per block): the
+    buffer is pre-filled with 0xFF, so a piece no block covers would show up as stray accept bits.
+    n = 5,000: the three-kernel path with the device-side hash sort (one block count for all
+    messages: the uniform flag keeps the identity order; random lengths: the permutation)."""
     hip = _Hip()
     nwords = (n + 63) // 64
-    ss = sigsets.make_sigset(n, nkeys=7, msg_len=256, seed=900 + n, invalid_frac=0.2)
+    ss = sigsets.make_sigset(n, nkeys=7, msg_len=msg_len, seed=900 + n, invalid_frac=0.2)
     try:
         with cb.Context(device=0) as c:
             tid = c.load_keys(ss.pk)
