@@ -177,7 +177,9 @@ struct cbft_ctx {
   // key-table batches up to this size run as one fused launch (ed25519_small_kernel;
   // $CBFT_SMALL_MAX, 0 = never): the per-request coalescer's batches
   size_t small_max = 1024;
-  int small_waves = 2;  // fused small-batch kernel: 2 waves per 16 signatures, or 3 ($CBFT_SMALL_WAVES)
+  // fused small-batch kernel ($CBFT_SMALL_WAVES): 3 = [S]B on a wave of its own beside the hash +
+  // [h](-A) wave and the two R-decode waves (per-request p50 69 us vs 73 us for 2: one wave for both sums)
+  int small_waves = 3;
   size_t sha_sort_min = 4096;  // variable-length batches from this size hash in block-count order
   int blocking_sync = 1;  // small batches' waiters sleep ($CBFT_BLOCKING_SYNC)
   int zero_copy = 1;  // fused small batches read pinned inputs and write verdicts in place ($CBFT_ZERO_COPY)

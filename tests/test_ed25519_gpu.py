@@ -437,11 +437,13 @@ def test_hash_block_count_sort(golden, n, monkeypatch):
         assert np.array_equal(got2, ss.expected), msg_len
 
 
+@pytest.mark.parametrize("waves", [2, 3])
 @pytest.mark.parametrize("chunk", [1, 17, 300, 1024])
-def test_golden_small_batches_three_wave_kernel(golden, chunk, monkeypatch):
-    """$CBFT_SMALL_WAVES=3: the fused kernel with [S]B on its own wave and R's decode on a third
-    gives the golden verdicts batch for batch, partial words and tail quads included."""
-    monkeypatch.setenv("CBFT_SMALL_WAVES", "3")
+def test_golden_small_batches_three_wave_kernel(golden, chunk, waves, monkeypatch):
+    """$CBFT_SMALL_WAVES=3 (the default): the fused kernel with [S]B on its own wave beside the hash
+    and [h](-A) wave and the R-decode waves; 2: both sums on one wave.  Each gives the golden
+    verdicts batch for batch, partial words and tail quads included."""
+    monkeypatch.setenv("CBFT_SMALL_WAVES", str(waves))
     keys = sorted({v.pk for v in golden})
     index = {k: i for i, k in enumerate(keys)}
     exp = np.array([bool(v.verdict) for v in golden])

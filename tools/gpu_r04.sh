@@ -13,6 +13,7 @@
 #   trace       kernel trace of the device-resident two-stream pipeline (overlap of the stages)
 #   ab          interleaved A/B of $LIBS (tools/ab_libs.sh)
 #   blsphases   phase times of the BLS signing kernel (build/lib_blsphases.so, -DCBFT_BLS_PHASES=1)
+#   reqsweep    per-request path under $VARIANTS (tools/gpu_reqsweep.sh)
 #   abmix       the same over config #3 only (tools/mixed_probe.py)
 #   san         host-layer ASan+UBSan / TSan runs (make sanitize first)
 set -o pipefail
@@ -59,6 +60,8 @@ for step in "$@"; do
       CBFT_LIB=$R/build/lib_blsphases.so timeout -k 10 120 python3 -u tools/bls_probe.py --reps 2 > gpurun_out/bls_phases.log 2>&1 \
         || { echo "bls phase probe failed"; tail -20 gpurun_out/bls_phases.log; exit 1; }
       grep -E "sign|{" gpurun_out/bls_phases.log | tail -12 ;;
+    reqsweep)
+      bash tools/gpu_reqsweep.sh || exit 1 ;;
     abmix)
       MODE=mixed bash tools/ab_libs.sh || exit 1 ;;
     phases)

@@ -1,7 +1,15 @@
+# Per-request path sweep on the GPU box: tools/host_bench (64 threads x 2000 single verify()
+# calls) under engine / context knobs, one summary line each.  VARIANTS="label@ENV=V,ENV=V ..."
 set -o pipefail
+cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-for rep in 1 2; do for f in 4 6 8; do
-  CBFT_ENGINE_INFLIGHT=$f timeout -k 10 120 tools/host_bench 64 2000 1024 16 > gpurun_out/hb3_f${f}_$rep.json || exit 1
-  python3 -c "
-import json; d=json.load(open('gpurun_out/hb3_f${f}_$rep.json')); print('inflight $f rep $rep', {k: (d[k]['verifies_per_s'], d[k]['p50_us'], d[k]['calls_per_batch']) for k in ('verify_mt','verifysig_mt','single')})"
-done; done
+mkdir -p gpurun_out/reqsweep
+for rep in $(seq 1 "${ROUNDS:-1}"); do
+  for v in ${VARIANTS:-base@X=0}; do
+    label=${v%%@*}; envs=$(echo "${v#*@}" | tr ',' ' ')
+    out=gpurun_out/reqsweep/${label}_$rep.json
+    env $envs timeout -k 10 120 tools/host_bench ${THREADS:-64} 2000 1024 16 > $out || { echo "host_bench $label failed"; exit 1; }
+    python3 -c "
+import json; d=json.load(open('$out')); print('$label r$rep', {k: (round(d[k]['verifies_per_s']), d[k]['p50_us'], d[k].get('calls_per_batch')) for k in ('verify_mt','single')})"
+  done
+done
