@@ -405,7 +405,9 @@ def main():
             parity["rsa_2048_bench_sets"] = {"n": 2 * args.batch, "mismatch": 0}
         detail = _write_detail({"parity": parity, "roofline": roofline, "mixed_config3": mixed, "bls_config4": bls,
                                 "rsa_2048": rsa, "per_request_path": per_request, "single_process_multi_gpu": single})
-        small_k, small_stat = _pmc_record("pmc_ed25519_small.json", "ed25519_small_kernel")
+        # the fused small-batch kernel in its default form ($CBFT_SMALL_WAVES: 3 -> small3, 2 -> small)
+        small_name = "ed25519_small_kernel" if os.environ.get("CBFT_SMALL_WAVES") == "2" else "ed25519_small3_kernel"
+        small_k, small_stat = _pmc_record("pmc_ed25519_small.json", small_name)
         # The line: the contract's keys first, then side measurements, and LAST what the driver's
         # stdout tail must keep: the second half of the metric (p50 @ 1K), the
         # device-resident ceiling, the per-request path, the key-table load and the BLS timings.

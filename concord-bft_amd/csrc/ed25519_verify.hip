@@ -817,7 +817,7 @@ __device__ __forceinline__ void add256(uint32_t* s, const uint32_t* off) {
 // nper mixed additions from the key's and B's comb tables, entries staged through LDS one
 // addition ahead (sdig: COMB_MAX_STEPS x BLOCK ints, stage: BLOCK / 64 x 7 x 64 uint4 of LDS).
 // The caller combines the quad's four partial sums.
-template <int BLOCK>
+template <int BLOCK, int DEPTH = 1>
 __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, uint32_t q, const uint32_t* h_in,
                                               const uint32_t* btbl, const CombLadder& cl, int32_t* sdig, uint4* stage,
                                               ge_p3& P, uint32_t kbase = 0, uint32_t kend = 0, int nper = 0) {
@@ -867,23 +867,37 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
   };
   auto digit = [&](int jj) { return sdig[jj * BLOCK + tid]; };
   ge_p3_0(P);
-  // Table entries are staged through LDS with global_load_lds (no VGPR destination): entry
-  // jj+1's 7 x 16 B are requested as soon as entry jj has been read out of LDS, so its HBM /
-  // Infinity-Cache latency overlaps the rest of addition jj.  LDS image per wave:
-  // [chunk 0..6][lane][16 B] (lane-linear, as one global_load_lds_dwordx4 writes it), 7 KB.
-  uint4(*st)[64] = reinterpret_cast<uint4(*)[64]>(stage + (tid >> 6) * 7 * 64);
+  // Table entries are staged through LDS with global_load_lds (no VGPR destination), DEPTH entries
+  // in flight: entry jj + DEPTH's 7 x 16 B are requested as soon as entry jj has been read out of
+  // its LDS slot, so the HBM / Infinity-Cache latency (random reads over tens of GB: TLB misses)
+  // overlaps DEPTH additions.  LDS image per wave and slot: [chunk 0..6][lane][16 B] (lane-linear,
+  // as one global_load_lds_dwordx4 writes it), 7 KB; the caller's stage holds DEPTH slots per wave.
+  uint4(*st0)[64] = reinterpret_cast<uint4(*)[64]>(stage + (tid >> 6) * DEPTH * 7 * 64);
   const uint32_t ln = tid & 63u;
-  auto request = [&](const uint32_t* e) {
+  auto request = [&](const uint32_t* e, int slot) {
+    uint4(*st)[64] = st0 + slot * 7;
 #pragma unroll
     for (int c = 0; c < 7; c++)
       __builtin_amdgcn_global_load_lds(e + 4 * c, (__attribute__((address_space(3))) void*)&st[c][0], 16, 0, 0);
   };
   int d = digit(0);
-  request(entry(0, d));
+  int dq[DEPTH];  // digits of the entries in flight, by slot
+#pragma unroll
+  for (int s = 0; s < DEPTH; s++) {
+    dq[s] = s == 0 ? d : digit(s);
+    if (s < nper) request(entry(s, dq[s]), s);
+  }
 #pragma nounroll
   for (int jj = 0; jj < nper; jj++) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int slot = jj % DEPTH;
+    // entry jj has arrived once at most DEPTH - 1 later requests (7 loads each) are outstanding;
+    // in the last DEPTH - 1 iterations fewer are, so wait for all
+    if (DEPTH > 1 && jj + DEPTH <= nper)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(7 * (DEPTH - 1)) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     uint32_t ew[28];
+    uint4(*st)[64] = st0 + slot * 7;
 #pragma unroll
     for (int c = 0; c < 7; c++) {
       const uint4 v = st[c][ln];
@@ -893,11 +907,18 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
       ew[4 * c + 3] = v.w;
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // entry jj is in VGPRs: the slot is free
-    const bool neg = d < 0;
-    if (jj + 1 < nper) {
-      d = digit(jj + 1);
+    int dcur = dq[0];
+#pragma unroll
+    for (int s = 1; s < DEPTH; s++)
+      if (slot == s) dcur = dq[s];
+    const bool neg = dcur < 0;
+    if (jj + DEPTH < nper) {
+      const int dn = digit(jj + DEPTH);
+#pragma unroll
+      for (int s = 0; s < DEPTH; s++)
+        if (slot == s) dq[s] = dn;
 #if !CBFT_LADDER_NOFETCH  // (probe builds only: compute without the table traffic, wrong verdicts)
-      request(entry(jj + 1, d));
+      request(entry(jj + DEPTH, dn), slot);
 #endif
     }
     ge_p1p1 t;
@@ -985,6 +1006,14 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
 #define CBFT_DECODE_ROW 1
 #endif
 #define SMALL_SIGS (CBFT_DECODE_ROW ? 8 : 16)
+// comb-table entries in flight per lane in the fused kernels (LDS: 7 KB per entry and comb wave).
+// PMC of the one-entry form: 44 % of the kernel's wave cycles in s_waitcnt (the key table's
+// random reads over tens of GB), but p50 @ 1K and the lone verify measured the same at 1, 2 and 4
+// in flight (A/B on one box): the waits are off the critical path (wave 0's SHA-512)
+#ifndef CBFT_SMALL_DEPTH
+#define CBFT_SMALL_DEPTH 2
+#endif
+#define SMALL_DEPTH CBFT_SMALL_DEPTH
 #define SMALL_DEC_WAVES (CBFT_DECODE_ROW ? 2 : 1)
 #define SMALL_BLOCK (64 * (1 + SMALL_DEC_WAVES))
 
@@ -1036,7 +1065,7 @@ __device__ __forceinline__ void small_decode_r(const Ed25519Batch& b, uint32_t b
 __global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed25519Batch b, const uint32_t* btbl,
                                                                     const CombLadder cl, uint8_t* verdict_bytes) {
   __shared__ int32_t sdig[COMB_MAX_STEPS * 64];
-  __shared__ uint4 stage[7 * 64];
+  __shared__ uint4 stage[SMALL_DEPTH * 7 * 64];
   __shared__ uint32_t rdec[SMALL_SIGS][2 * FE_LIMBS + 1];  // x_R | y_R | decodes
   // quads past the block's signatures (lanes 32..63 with 8 signatures) repeat quads 0..7 unused
   const uint32_t ln = threadIdx.x & 63u, wave = threadIdx.x >> 6, q = ln & 3u, sl = (ln >> 2) & (SMALL_SIGS - 1);
@@ -1066,7 +1095,7 @@ __global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed2551
   ed25519_hash_sig(b, i, hs, flag);
   ED_STAMP(1);
   ge_p3 P;
-  comb_quad_sum<64>(b, i, q, hs, btbl, cl, sdig, stage, P);
+  comb_quad_sum<64, SMALL_DEPTH>(b, i, q, hs, btbl, cl, sdig, stage, P);
   ED_STAMP(2);
   quad_combine<0xB1>(P, true);
   quad_combine<0x4E>(P, false);
@@ -1108,7 +1137,7 @@ __global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed2551
 __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25519Batch b, const uint32_t* btbl,
                                                                       const CombLadder cl, uint8_t* verdict_bytes) {
   __shared__ int32_t sdig[2][COMB_MAX_STEPS * 64];
-  __shared__ uint4 stage[2][7 * 64];
+  __shared__ uint4 stage[2][SMALL_DEPTH * 7 * 64];
   __shared__ uint32_t rdec[SMALL_SIGS][2 * FE_LIMBS + 1];  // x_R | y_R | decodes
   __shared__ uint32_t sbp[SMALL_SIGS][4 * FE_LIMBS];       // [S]B as X | Y | Z | T
   const uint32_t ln = threadIdx.x & 63u, wave = threadIdx.x >> 6, q = ln & 3u, sl = (ln >> 2) & (SMALL_SIGS - 1);
@@ -1124,7 +1153,7 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
   if (wave == 1) {  // [S]B: B's positions [na, ntot) over the quad; the digits need no hash
     const uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     ge_p3 P;
-    comb_quad_sum<64>(b, i, q, zero, btbl, cl, sdig[1], stage[1], P, na, ntot, (int)((ntot - na + 3) / 4));
+    comb_quad_sum<64, SMALL_DEPTH>(b, i, q, zero, btbl, cl, sdig[1], stage[1], P, na, ntot, (int)((ntot - na + 3) / 4));
     quad_combine<0xB1>(P, true);
     quad_combine<0x4E>(P, true);
     if (q == 0 && (ln >> 2) < SMALL_SIGS) {
@@ -1143,7 +1172,7 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
   bool flag;
   ed25519_hash_sig(b, i, hs, flag);
   ge_p3 P;
-  comb_quad_sum<64>(b, i, q, hs, btbl, cl, sdig[0], stage[0], P, 0, na, (int)((na + 3) / 4));
+  comb_quad_sum<64, SMALL_DEPTH>(b, i, q, hs, btbl, cl, sdig[0], stage[0], P, 0, na, (int)((na + 3) / 4));
   quad_combine<0xB1>(P, true);
   quad_combine<0x4E>(P, true);
   __syncthreads();  // wave 1's [S]B, wave 2's R
