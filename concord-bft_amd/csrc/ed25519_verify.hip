@@ -273,6 +273,93 @@ __device__ __forceinline__ void ed25519_hash_sig(const Ed25519Batch& b, size_t i
   flag = sc_is_canonical(Sw) && key_ok && len_ok;
 }
 
+// ed25519_hash_sig split over two waves (the fused three-wave kernel): sig_sha_blocks is the
+// block count of signature i's R || A || M; ed25519_sched_sig (the [S]B wave, lane q of the
+// signature's quad) writes K[t] + W[t] of blocks 1 + q, 5 + q, ... into kw[block][0..80) in LDS
+// while ed25519_hash_sig_kw (wave 0) compresses block 0 itself, then (after the caller's barrier,
+// `sync`) runs only the rounds of blocks 1, 2, ...  Same digest, same flag.
+__device__ __forceinline__ uint32_t sig_sha_blocks(const Ed25519Batch& b, size_t i) {
+  uint32_t len = b.msg_off ? b.msg_len[i] : b.fixed_len;
+  if (len > CBFT_MAX_MSG_LEN) len = 0;
+  return (64u + len + 17u + 127u) / 128u;
+}
+#define KW_STRIDE 81  // 80 words + 1: the 8 signatures' rows fall on different LDS banks
+__device__ __forceinline__ void ed25519_sched_sig(const Ed25519Batch& b, size_t i, uint32_t q, uint64_t* kw) {
+  const uint32_t key = batch_unit(b, i);
+  uint32_t Aw[8], Rw[8];
+  load_words8(Aw, b.key_idx ? b.keys.pk(key) : b.pk + (size_t)key * 32);
+  load_words8(Rw, b.sig + i * 64);
+  const uint8_t* m = b.msg_off ? b.msg + b.msg_off[i] : b.msg + i * (size_t)b.fixed_len;
+  uint32_t len = b.msg_off ? b.msg_len[i] : b.fixed_len;
+  if (len > CBFT_MAX_MSG_LEN) len = 0;
+  const uint32_t* safe = reinterpret_cast<const uint32_t*>(b.sig + i * 64);
+  const uint32_t total = 64u + len;
+  const uint32_t nblocks = (total + 17u + 127u) / 128u;
+  for (uint32_t blk = 1 + q; blk < nblocks; blk += 4) {
+    uint64_t W[16];
+    uint32_t d[33];
+    if (blk == 0) {
+#pragma unroll
+      for (int j = 0; j < 4; j++) W[j] = ((uint64_t)bswap32(Rw[2 * j]) << 32) | bswap32(Rw[2 * j + 1]);
+#pragma unroll
+      for (int j = 0; j < 4; j++) W[4 + j] = ((uint64_t)bswap32(Aw[2 * j]) << 32) | bswap32(Aw[2 * j + 1]);
+      fetch_msg_dwords<8>(d, m, len, 0u, safe);
+      assemble_msg_words<8>(W + 8, d, m, len, 0u);
+    } else {
+      fetch_msg_dwords<16>(d, m, len, 128u * blk - 64u, safe);
+      assemble_msg_words<16>(W, d, m, len, 128u * blk - 64u);
+    }
+    if (blk == nblocks - 1) {
+      W[14] = 0;
+      W[15] = (uint64_t)total << 3;
+    }
+    sha512_schedule_kw(kw + blk * KW_STRIDE, W);
+  }
+}
+template <class Sync>
+__device__ __forceinline__ void ed25519_hash_sig_kw(const Ed25519Batch& b, size_t i, const uint64_t* kw, uint32_t* hw,
+                                                    bool& flag, Sync sync) {
+  const uint32_t key = batch_unit(b, i);
+  const bool key_ok = !b.key_idx || b.key_idx[i] < b.nkeys;
+  uint32_t Aw[8], Rw[8], Sw[8];
+  load_words8(Aw, b.key_idx ? b.keys.pk(key) : b.pk + (size_t)key * 32);
+  load_words8(Rw, b.sig + i * 64);
+  load_words8(Sw, b.sig + i * 64 + 32);
+  const uint8_t* m = b.msg_off ? b.msg + b.msg_off[i] : b.msg + i * (size_t)b.fixed_len;
+  uint32_t len = b.msg_off ? b.msg_len[i] : b.fixed_len;
+  const bool len_ok = len <= CBFT_MAX_MSG_LEN;
+  if (!len_ok) len = 0;
+  const uint32_t* safe = reinterpret_cast<const uint32_t*>(b.sig + i * 64);
+  const uint32_t total = 64u + len;
+  const uint32_t nblocks = (total + 17u + 127u) / 128u;
+  uint64_t H[8], W[16];
+  sha512_init(H);
+  {  // block 0: R || A || M[0..63]
+    uint32_t d[17];
+#pragma unroll
+    for (int j = 0; j < 4; j++) W[j] = ((uint64_t)bswap32(Rw[2 * j]) << 32) | bswap32(Rw[2 * j + 1]);
+#pragma unroll
+    for (int j = 0; j < 4; j++) W[4 + j] = ((uint64_t)bswap32(Aw[2 * j]) << 32) | bswap32(Aw[2 * j + 1]);
+    fetch_msg_dwords<8>(d, m, len, 0u, safe);
+    assemble_msg_words<8>(W + 8, d, m, len, 0u);
+    if (nblocks == 1) {
+      W[14] = 0;
+      W[15] = (uint64_t)total << 3;
+    }
+    sha512_compress(H, W);
+  }
+  sync();  // the other blocks' schedules are in kw
+  for (uint32_t blk = 1; blk < nblocks; blk++) sha512_rounds_kw(H, kw + blk * KW_STRIDE);
+  uint32_t dig[16];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    dig[2 * k] = bswap32((uint32_t)(H[k] >> 32));
+    dig[2 * k + 1] = bswap32((uint32_t)H[k]);
+  }
+  sc_reduce512(hw, dig);
+  flag = sc_is_canonical(Sw) && key_ok && len_ok;
+}
+
 // SHA-512 blocks of signature i's R || A || M (what ed25519_hash_sig runs), as a sort bucket
 __device__ __forceinline__ uint32_t hash_bucket(const Ed25519Batch& b, size_t i) {
   uint32_t len = b.msg_len[i];
@@ -1014,6 +1101,13 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
 #define CBFT_SMALL_DEPTH 2
 #endif
 #define SMALL_DEPTH CBFT_SMALL_DEPTH
+// three-wave kernel: the [S]B wave writes the SHA-512 message schedules (K[t] + W[t]) of messages
+// up to SMALL_KW_BLOCKS blocks (64 + len + 17 <= 1,024 B) to LDS first, so wave 0's hash is rounds
+// only (CBFT_SMALL_SPLIT_HASH=0: wave 0 hashes alone)
+#ifndef CBFT_SMALL_SPLIT_HASH
+#define CBFT_SMALL_SPLIT_HASH 1
+#endif
+#define SMALL_KW_BLOCKS 8
 #define SMALL_DEC_WAVES (CBFT_DECODE_ROW ? 2 : 1)
 #define SMALL_BLOCK (64 * (1 + SMALL_DEC_WAVES))
 
@@ -1030,6 +1124,7 @@ __device__ __forceinline__ void small_store_bits(uint8_t* vb, uint32_t bits) {
 
 // Decode wave dw of a small-kernel block: x_R | y_R | (R decodes && y canonical && not (x = 0
 // with the sign bit set)) of its signatures into rdec.
+template <bool SYNC = false>  // SYNC: the wave joins one extra __syncthreads() (see ge_frombytes_row)
 __device__ __forceinline__ void small_decode_r(const Ed25519Batch& b, uint32_t blk, uint32_t dw, uint32_t ln,
                                                uint32_t (*rdec)[2 * FE_LIMBS + 1]) {
   const uint32_t sl = CBFT_DECODE_ROW ? dw * 4 + (ln >> 4) : (ln >> 2);
@@ -1041,8 +1136,9 @@ __device__ __forceinline__ void small_decode_r(const Ed25519Batch& b, uint32_t b
   fe X, Y;
   bool ok;
   if (CBFT_DECODE_ROW) {
-    ok = ge_frombytes_row(X, Y, Rw);
+    ok = ge_frombytes_row<SYNC>(X, Y, Rw);
   } else {
+    if (SYNC) __syncthreads();
     ge_p3 R;
     ok = ge_frombytes(R, Rw);
     X = R.X;
@@ -1140,17 +1236,31 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
   __shared__ uint4 stage[2][SMALL_DEPTH * 7 * 64];
   __shared__ uint32_t rdec[SMALL_SIGS][2 * FE_LIMBS + 1];  // x_R | y_R | decodes
   __shared__ uint32_t sbp[SMALL_SIGS][4 * FE_LIMBS];       // [S]B as X | Y | Z | T
+  __shared__ uint64_t kw[SMALL_SIGS][SMALL_KW_BLOCKS * KW_STRIDE];  // SHA-512 K[t] + W[t] per block
   const uint32_t ln = threadIdx.x & 63u, wave = threadIdx.x >> 6, q = ln & 3u, sl = (ln >> 2) & (SMALL_SIGS - 1);
   size_t i = (size_t)blockIdx.x * SMALL_SIGS + sl;
   const bool live = i < b.n && (ln >> 2) < SMALL_SIGS;
   if (i >= b.n) i = b.n - 1;
   const uint32_t na = (uint32_t)cl.a.npos, ntot = na + (uint32_t)cl.b.npos;
-  if (wave >= 2) {
-    small_decode_r(b, blockIdx.x, wave - 2, ln, rdec);
+  // Every wave joins two barriers: "schedules written" (wave 1 -> wave 0, which compresses block 0
+  // meanwhile; the decode waves join it ~12 us into their square-root chain) and "sums and
+  // decodes done".  The split hash runs when
+  // every signature of the block fits SMALL_KW_BLOCKS SHA-512 blocks (a wave-uniform ballot that
+  // waves 0 and 1 compute alike); otherwise wave 0 hashes on its own as before.
+  const bool split = CBFT_SMALL_SPLIT_HASH && __ballot(sig_sha_blocks(b, i) > SMALL_KW_BLOCKS) == 0;
+  if (wave >= 2) {  // (without the split every wave passes the first barrier at its start)
+    if (split) {
+      small_decode_r<true>(b, blockIdx.x, wave - 2, ln, rdec);
+    } else {
+      __syncthreads();
+      small_decode_r<false>(b, blockIdx.x, wave - 2, ln, rdec);
+    }
     __syncthreads();
     return;
   }
   if (wave == 1) {  // [S]B: B's positions [na, ntot) over the quad; the digits need no hash
+    if (split && (ln >> 2) < SMALL_SIGS) ed25519_sched_sig(b, i, q, kw[sl]);
+    __syncthreads();
     const uint32_t zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     ge_p3 P;
     comb_quad_sum<64, SMALL_DEPTH>(b, i, q, zero, btbl, cl, sdig[1], stage[1], P, na, ntot, (int)((ntot - na + 3) / 4));
@@ -1170,12 +1280,42 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
   }
   uint32_t hs[8];
   bool flag;
-  ed25519_hash_sig(b, i, hs, flag);
+#if CBFT_ED_PHASES
+  uint64_t ph3[5];
+  ph3[0] = wall_clock64();
+#endif
+  if (split) {
+    ed25519_hash_sig_kw(b, i, kw[sl], hs, flag, [&] {
+#if CBFT_ED_PHASES
+      ph3[1] = wall_clock64();
+#endif
+      __syncthreads();  // wave 1's message schedules (block 0 is done meanwhile)
+    });
+  } else {
+    __syncthreads();
+#if CBFT_ED_PHASES
+    ph3[1] = wall_clock64();
+#endif
+    ed25519_hash_sig(b, i, hs, flag);
+  }
+#if CBFT_ED_PHASES
+  ph3[2] = wall_clock64();
+#endif
   ge_p3 P;
   comb_quad_sum<64, SMALL_DEPTH>(b, i, q, hs, btbl, cl, sdig[0], stage[0], P, 0, na, (int)((na + 3) / 4));
   quad_combine<0xB1>(P, true);
   quad_combine<0x4E>(P, true);
+#if CBFT_ED_PHASES
+  ph3[3] = wall_clock64();
+#endif
   __syncthreads();  // wave 1's [S]B, wave 2's R
+#if CBFT_ED_PHASES
+  ph3[4] = wall_clock64();
+  if (blockIdx.x == 0 && ln == 0)
+    printf("ed25519_small3 block 0 (us): to-barrier %.1f hash-after %.1f A-comb %.1f wait-B/R %.1f (split %d)\n",
+           (ph3[1] - ph3[0]) * 0.01, (ph3[2] - ph3[1]) * 0.01, (ph3[3] - ph3[2]) * 0.01, (ph3[4] - ph3[3]) * 0.01,
+           split ? 1 : 0);
+#endif
   {
     ge_p3 Q;
 #pragma unroll

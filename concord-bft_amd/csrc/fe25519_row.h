@@ -96,9 +96,13 @@ RF_HD U rfe_sqn(U z, int n) {
   return z;
 }
 
-// z^((p - 5) / 8) = z^(2^252 - 3): the chain of fe_pow22523 (fe25519.h)
-template <class U, class W>
-RF_HD U rfe_pow22523(U z) {
+// z^((p - 5) / 8) = z^(2^252 - 3): the chain of fe_pow22523 (fe25519.h).  mid() runs after ~80 of
+// its 265 operations (a caller's workgroup barrier placed inside the chain).
+struct RfeNoop {
+  RF_HD void operator()() const {}
+};
+template <class U, class W, class F = RfeNoop>
+RF_HD U rfe_pow22523(U z, F mid = F()) {
   const U z2 = rfe_sq<U, W>(z);                              // 2
   const U z9 = rfe_mul<U, W>(rfe_sqn<U, W>(z2, 2), z);       // 9
   const U z11 = rfe_mul<U, W>(z9, z2);                       // 11
@@ -107,7 +111,9 @@ RF_HD U rfe_pow22523(U z) {
   U t1 = rfe_mul<U, W>(rfe_sqn<U, W>(t0, 10), t0);           // 2^20 - 1
   t1 = rfe_mul<U, W>(rfe_sqn<U, W>(t1, 20), t1);             // 2^40 - 1
   t0 = rfe_mul<U, W>(rfe_sqn<U, W>(t1, 10), t0);             // 2^50 - 1
-  t1 = rfe_mul<U, W>(rfe_sqn<U, W>(t0, 50), t0);             // 2^100 - 1
+  t1 = rfe_sqn<U, W>(t0, 25);
+  mid();                                                     // ~80 of the chain's 265 operations
+  t1 = rfe_mul<U, W>(rfe_sqn<U, W>(t1, 25), t0);             // 2^100 - 1
   t1 = rfe_mul<U, W>(rfe_sqn<U, W>(t1, 100), t1);            // 2^200 - 1
   t0 = rfe_mul<U, W>(rfe_sqn<U, W>(t1, 50), t0);             // 2^250 - 1
   return rfe_mul<U, W>(rfe_sqn<U, W>(t0, 2), z);             // 2^252 - 3

@@ -180,6 +180,9 @@ FE_INLINE void rfe_to_fe(fe& r, uint32_t x) {
   r.v[8] = rl_bcast_w<8>(x);
   fe_carry(r);
 }
+// SYNC: one __syncthreads() inside the square-root chain (the three-wave fused kernel's
+// "schedules written" barrier, which the decode waves reach ~12 us in, when waves 0 and 1 do)
+template <bool SYNC = false>
 FE_INLINE bool ge_frombytes_row(fe& X, fe& Y, const uint32_t* w) {
   typedef uint32_t U;
   typedef uint64_t W;
@@ -192,7 +195,9 @@ FE_INLINE bool ge_frombytes_row(fe& X, fe& Y, const uint32_t* w) {
   const U v = rfe_carry(rfe_mul<U, W>(yy, rfe_row_const(kFeD, tag)) + one);  // d y^2 + 1
   const U v3 = rfe_mul<U, W>(rfe_sq<U, W>(v), v);
   U x = rfe_mul<U, W>(rfe_mul<U, W>(rfe_sq<U, W>(v3), v), u);    // u v^7
-  x = rfe_pow22523<U, W>(x);
+  x = rfe_pow22523<U, W>(x, [] {
+    if (SYNC) __syncthreads();
+  });
   x = rfe_mul<U, W>(rfe_mul<U, W>(x, v3), u);                     // u v^3 (u v^7)^((p-5)/8)
   const U vxx = rfe_mul<U, W>(rfe_sq<U, W>(x), v);
   fe fu, fvxx, chk;

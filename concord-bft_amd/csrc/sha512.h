@@ -212,6 +212,54 @@ __device__ __forceinline__ void sha512_compress(uint64_t* H, uint64_t* W) {
 }
 #endif  // CBFT_SHA_PAIRS
 
+// The compression function in two halves that two waves can run: sha512_schedule_kw expands a
+// block's 16 words into kw[t] = K[t] + W[t], t = 0..79 (one wave writes them to LDS), and
+// sha512_rounds_kw runs the 80 rounds from kw (another wave, reading LDS): the rounds' wave skips
+// the schedule's ~1,400 instructions per block, a third of the compression.
+__device__ __forceinline__ void sha512_schedule_kw(uint64_t* kw, uint64_t* W) {
+#pragma unroll
+  for (int j = 0; j < 16; j++) kw[j] = kSha512K[j] + W[j];
+#pragma nounroll
+  for (int r = 16; r < 80; r += 16) {
+#pragma unroll
+    for (int j = 0; j < 16; j++) {
+      const uint64_t w15 = W[(j + 1) & 15], w2 = W[(j + 14) & 15];
+      const uint64_t s0 = bitop3_64<0x96>(rotr64<1>(w15), rotr64<8>(w15), shr64<7>(w15));
+      const uint64_t s1 = bitop3_64<0x96>(rotr64<19>(w2), rotr64<61>(w2), shr64<6>(w2));
+      W[j] = W[j] + s0 + W[(j + 9) & 15] + s1;
+      kw[r + j] = kSha512K[r + j] + W[j];
+    }
+  }
+}
+__device__ __forceinline__ void sha512_rounds_kw(uint64_t* H, const uint64_t* kw) {
+  uint64_t a = H[0], b = H[1], c = H[2], d = H[3], e = H[4], f = H[5], g = H[6], h = H[7];
+#pragma nounroll
+  for (int r = 0; r < 80; r += 16) {
+    uint64_t k[16];
+#pragma unroll
+    for (int j = 0; j < 16; j++) k[j] = kw[r + j];
+#pragma unroll
+    for (int j = 0; j < 16; j += 8) {
+      SHA512_ROUND(a, b, c, d, e, f, g, h, k[j + 0]);
+      SHA512_ROUND(h, a, b, c, d, e, f, g, k[j + 1]);
+      SHA512_ROUND(g, h, a, b, c, d, e, f, k[j + 2]);
+      SHA512_ROUND(f, g, h, a, b, c, d, e, k[j + 3]);
+      SHA512_ROUND(e, f, g, h, a, b, c, d, k[j + 4]);
+      SHA512_ROUND(d, e, f, g, h, a, b, c, k[j + 5]);
+      SHA512_ROUND(c, d, e, f, g, h, a, b, k[j + 6]);
+      SHA512_ROUND(b, c, d, e, f, g, h, a, k[j + 7]);
+    }
+  }
+  H[0] += a;
+  H[1] += b;
+  H[2] += c;
+  H[3] += d;
+  H[4] += e;
+  H[5] += f;
+  H[6] += g;
+  H[7] += h;
+}
+
 __device__ __forceinline__ void sha512_init(uint64_t* H) {
   H[0] = 0x6a09e667f3bcc908ull;
   H[1] = 0xbb67ae8584caa73bull;
