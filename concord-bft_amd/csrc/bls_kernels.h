@@ -60,7 +60,8 @@ hipError_t cbft_bls_launch_verify(const uint8_t* d_msg, uint32_t len, uint32_t* 
 hipError_t cbft_bls_launch_sign(const uint8_t* d_msg, uint32_t len, const uint32_t* d_sk, uint32_t id,
                                 uint8_t* d_out37, hipStream_t s);
 // the same signature on row-parallel Fp (bls_msm_row.hip): d_H = g1_map(msg) from
-// cbft_bls_launch_hash first; constant operation sequence in the secret scalar
+// cbft_bls_launch_hash first, or nullptr (the kernel hashes); constant operation sequence in the
+// secret scalar
 hipError_t cbft_bls_launch_sign_row(const uint32_t* d_H, const uint32_t* d_sk, const uint8_t* d_msg, uint32_t len,
                                     uint32_t id, uint8_t* d_out37, hipStream_t s);
 // vk = sk * g2 as a row-parallel fixed-base comb (bls_keys.hip): the table (cbft_bls_pub_table_words

@@ -333,7 +333,12 @@ __global__ void __launch_bounds__(128) bls_sign_row_kernel(const uint32_t* H, co
   const uint32_t tag = 0;
   const RCtx c(tag);
   g1a h;
-  g1a_load(h, H);  // g1_map never returns infinity
+  // H = g1_map(msg): precomputed (H != nullptr), or computed here by each wave (both waves need
+  // it; the same deterministic result), which saves the hash kernel's launch and H's round trip
+  if (H)
+    g1a_load(h, H);  // g1_map never returns infinity
+  else
+    g1_map_row(h, msg, len);
   uint32_t k[8];
 #pragma unroll
   for (int i = 0; i < 8; i++) k[i] = sk[i];

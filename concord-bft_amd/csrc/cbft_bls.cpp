@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <vector>
 #include <thread>
 
 #include "bls_kernels.h"
@@ -553,11 +554,16 @@ int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* 
   be32_scalar_words(w, sk32);
   std::lock_guard<std::mutex> g(c->mu);
   CBFT_HIP(hipSetDevice(c->device));
-  CBFT_HIP(c->bls_msg.reserve(len + 1));
-  CBFT_HIP(c->bls_lambda.reserve(8 * 4));
+  // one H2D: the scalar's words, then the message (bls_msg = [sk words | msg])
+  const size_t msg_at = sizeof(w);
+  CBFT_HIP(c->bls_msg.reserve(msg_at + len + 1));
   CBFT_HIP(c->bls_out.reserve(37));
-  if (len) CBFT_HIP(hipMemcpyAsync(c->bls_msg.p, msg, len, hipMemcpyHostToDevice, c->stream));
-  CBFT_HIP(hipMemcpyAsync(c->bls_lambda.p, w, sizeof(w), hipMemcpyHostToDevice, c->stream));
+  std::vector<uint8_t> in(msg_at + len);  // alive (and the scalar in it) until the stream is done
+  std::memcpy(in.data(), w, sizeof(w));
+  if (len) std::memcpy(in.data() + msg_at, msg, len);
+  CBFT_HIP(hipMemcpyAsync(c->bls_msg.p, in.data(), in.size(), hipMemcpyHostToDevice, c->stream));
+  const uint32_t* d_sk = c->bls_msg.as<uint32_t>();
+  const uint8_t* d_msg = c->bls_msg.as<uint8_t>() + msg_at;
   // row-parallel GLV signature (0.4-0.5 ms) unless $CBFT_BLS_SIGN=lane (the one-lane Montgomery
   // ladder, 4.4 ms: kept as the A/B reference)
   static const bool lane = [] {
@@ -565,18 +571,15 @@ int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* 
     return e && strcmp(e, "lane") == 0;
   }();
   if (lane) {
-    CBFT_HIP(cbft_bls_launch_sign(c->bls_msg.as<uint8_t>(), len, c->bls_lambda.as<uint32_t>(), id,
-                                  c->bls_out.as<uint8_t>(), c->stream));
-  } else {
-    CBFT_HIP(c->bls_H.reserve(BLS_SIG_WORDS * 4));
-    CBFT_HIP(cbft_bls_launch_hash(c->bls_msg.as<uint8_t>(), len, c->bls_H.as<uint32_t>(), c->stream));
-    CBFT_HIP(cbft_bls_launch_sign_row(c->bls_H.as<uint32_t>(), c->bls_lambda.as<uint32_t>(), c->bls_msg.as<uint8_t>(),
-                                      len, id, c->bls_out.as<uint8_t>(), c->stream));
+    CBFT_HIP(cbft_bls_launch_sign(d_msg, len, d_sk, id, c->bls_out.as<uint8_t>(), c->stream));
+  } else {  // the hash to G1 inside the signing kernel (H = nullptr)
+    CBFT_HIP(cbft_bls_launch_sign_row(nullptr, d_sk, d_msg, len, id, c->bls_out.as<uint8_t>(), c->stream));
   }
   CBFT_HIP(hipMemcpyAsync(out37, c->bls_out.p, 37, hipMemcpyDeviceToHost, c->stream));
-  CBFT_HIP(hipMemsetAsync(c->bls_lambda.p, 0, sizeof(w), c->stream));  // the secret scalar leaves the device
+  CBFT_HIP(hipMemsetAsync(c->bls_msg.p, 0, sizeof(w), c->stream));  // the secret scalar leaves the device
   CBFT_HIP(hipStreamSynchronize(c->stream));
   secure_zero(w, sizeof(w));
+  secure_zero(in.data(), sizeof(w));
   return CBFT_OK;
 }
 
