@@ -526,7 +526,21 @@ def _bls_brief(bls):
                      "combine_ms", "verify_ms", "optimistic_ms", "multisig_ms", "sign_ms", "public_key_ms",
                      "keyset_load_ms") if k in bls}
     rf = bls.get("roofline") or {}
-    out["kernels_pmc"] = rf.get("kernels")
+    # compact for the driver's ~2 KB stdout tail: the kernels on the certificate / sign / key paths
+    # as [mean us, VALU-active fraction, MAD64 fraction of peak]; every kernel's record is in the
+    # detail file (bench_detail_last.json) and profiles/pmc_bls.json
+    ks = rf.get("kernels") or {}
+    keep = ("bls_share_verify_kernel", "bls_verify_kernel", "bls_verify_multisig_kernel", "bls_msm_row_kernel",
+            "bls_sign_row_kernel", "bls_pubkey_row_kernel", "bls_keys_row_kernel")
+    brief = {}
+    for name, k in ks.items():
+        base = name.split("(")[0].split("<")[0].replace("void ", "")
+        if base in keep and k.get("duration_ms") is not None:
+            brief[name.replace("void ", "").split("(")[0]] = [round(k["duration_ms"] * 1e3, 1),
+                                                                round(k.get("valu_active_frac") or 0, 3),
+                                                                round(k.get("mad_frac_of_peak") or 0, 4)]
+    out["kernels_pmc"] = brief or None
+    out["kernels_pmc_fields"] = "mean us, valu_active, mad_frac_of_peak"
     out["pmc_source"] = rf.get("source")
     if bls.get("cpu_baseline"):
         out["cpu_baseline_shares_per_s"] = bls["cpu_baseline"]["value"]
