@@ -67,6 +67,9 @@ ABI = [
     ("cbft_ed25519_verify_batch_device", ctypes.c_int,
      [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
       ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
+    ("cbft_ed25519_verify_fixed_device", ctypes.c_int,
+     [ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+      ctypes.c_uint32, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p]),
     ("cbft_sync", ctypes.c_int, [ctypes.c_void_p]),
     ("cbft_set_profiling", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     ("cbft_stage_times_ms", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]),
@@ -332,6 +335,14 @@ class Context:
             self.handle, tid, ctypes.c_void_p(d_pk), ctypes.c_void_p(d_key_idx), ctypes.c_void_p(d_sig),
             ctypes.c_void_p(d_msg), ctypes.c_void_p(d_off), ctypes.c_void_p(d_len), n,
             ctypes.c_void_p(d_verdict_words), ctypes.c_void_p(stream)), "cbft_ed25519_verify_batch_device")
+
+    def verify_fixed_device(self, tid: int, d_pk: int, d_key_idx: int, d_sig: int, d_msg: int, msg_len: int,
+                            n: int, d_verdict_words: int, stream: int = 0):
+        """Fixed-length messages (message i at d_msg + i * msg_len); raw device addresses."""
+        _check(self.lib.cbft_ed25519_verify_fixed_device(
+            self.handle, tid, ctypes.c_void_p(d_pk), ctypes.c_void_p(d_key_idx), ctypes.c_void_p(d_sig),
+            ctypes.c_void_p(d_msg), msg_len, n, ctypes.c_void_p(d_verdict_words), ctypes.c_void_p(stream)),
+            "cbft_ed25519_verify_fixed_device")
 
     def sync(self):
         _check(self.lib.cbft_sync(self.handle), "cbft_sync")

@@ -1144,4 +1144,17 @@ int cbft_ed25519_verify_batch_device(cbft_ctx* c, uint32_t table_id, const uint8
   return launch_locked(c, table_id, d_pk, d_key_idx, d_sig, d_msg, d_off, d_len, 0, n, d_verdicts, s);
 }
 
+int cbft_ed25519_verify_fixed_device(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, const uint32_t* d_key_idx,
+                                     const uint8_t* d_sig, const uint8_t* d_msg, uint32_t msg_len, size_t n,
+                                     uint64_t* d_verdicts, void* stream) {
+  if (!c || (n && (!d_sig || !d_verdicts || (msg_len && !d_msg)))) return CBFT_EINVAL;
+  if (table_id == CBFT_NO_KEY_TABLE && n && !d_pk) return CBFT_EINVAL;
+  if (!c->kids.empty()) return CBFT_EINVAL;  // device pointers belong to one GPU: use its own context
+  if (n == 0) return CBFT_OK;
+  std::lock_guard<std::mutex> g(c->mu);
+  CBFT_HIP(hipSetDevice(c->device));
+  hipStream_t s = stream ? static_cast<hipStream_t>(stream) : c->stream;
+  return launch_locked(c, table_id, d_pk, d_key_idx, d_sig, d_msg, nullptr, nullptr, msg_len, n, d_verdicts, s);
+}
+
 }  // extern "C"

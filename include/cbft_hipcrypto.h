@@ -178,6 +178,12 @@ int cbft_ed25519_verify_batch_device(cbft_ctx* ctx, uint32_t key_table_id, const
                                      const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg_blob,
                                      const uint64_t* d_msg_off, const uint32_t* d_msg_len, size_t n,
                                      uint64_t* d_verdict_words, void* stream);
+/* The same for fixed-length messages (message i = d_msg[i * msg_len, (i + 1) * msg_len)), the
+ * device-resident form of cbft_ed25519_verify_fixed_async: no offset / length arrays to read and
+ * no block-count sort before the hash kernel. */
+int cbft_ed25519_verify_fixed_device(cbft_ctx* ctx, uint32_t key_table_id, const uint8_t* d_pk,
+                                     const uint32_t* d_key_idx, const uint8_t* d_sig, const uint8_t* d_msg,
+                                     uint32_t msg_len, size_t n, uint64_t* d_verdict_words, void* stream);
 int cbft_sync(cbft_ctx* ctx);
 
 /* Instrumentation: when enabled, each verify records HIP events on its stream around its

@@ -403,6 +403,40 @@ def test_device_path_small_batch_whole_words(n, msg_len):
         hip.close()
 
 
+@pytest.mark.parametrize("n", [1, 9, 1000, 5000])
+def test_fixed_device_path(n):
+    """cbft_ed25519_verify_fixed_device (message i at d_msg + i * L) gives the verdicts of the
+    variable-length device call and of OpenSSL, on the fused small kernel (n <= 1,024) and the
+    three-kernel path, whole verdict words."""
+    hip = _Hip()
+    nwords = (n + 63) // 64
+    L = 200
+    ss = sigsets.make_sigset(n, nkeys=5, msg_len=L, seed=4200 + n, invalid_frac=0.2)
+    assert np.array_equal(ss.off, np.arange(n, dtype=ss.off.dtype) * L)
+    try:
+        with cb.Context(device=0) as c:
+            tid = c.load_keys(ss.pk)
+            d_kidx, d_sig = hip.to_dev(ss.key_idx), hip.to_dev(ss.sig.reshape(-1))
+            d_blob, d_off, d_len = hip.to_dev(ss.blob), hip.to_dev(ss.off), hip.to_dev(ss.len)
+            outs = []
+            for fixed in (True, False):
+                out = hip.to_dev(np.full(nwords, 0xFFFFFFFFFFFFFFFF, dtype=np.uint64))
+                if fixed:
+                    c.verify_fixed_device(tid, 0, d_kidx, d_sig, d_blob, L, n, out, None)
+                else:
+                    c.verify_device(tid, 0, d_kidx, d_sig, d_blob, d_off, d_len, n, out, None)
+                hip.sync()
+                words = np.frombuffer(hip.from_dev(out, nwords * 8), dtype=np.uint64)
+                bits = np.unpackbits(words.view(np.uint8), bitorder="little").astype(bool)
+                assert not bits[n:].any()
+                outs.append(bits[:n])
+            assert np.array_equal(outs[0], ss.expected)
+            assert np.array_equal(outs[1], ss.expected)
+            c.unload_keys(tid)
+    finally:
+        hip.close()
+
+
 @pytest.mark.parametrize("n", [1, 100, 257, 5000])
 def test_hash_block_count_sort(golden, n, monkeypatch):
     """Variable-length batches hash in order of their SHA-512 block count (a counting sort into a
