@@ -440,7 +440,7 @@ def main():
             "per_request_path": _per_request_brief(per_request),
             "key_table_load_ms": key_load_ms,
             "device_resident_value": dev_value,
-            "p50_small_kernel_pmc": _pmc_brief(small_k, small_stat),
+            "p50_small_kernel_pmc": _pmc_tail(small_k, small_stat),
             "p50_latency_ms_batch1k_python_lists": lat_py,
             "p50_latency_ms_batch1k": lat,
         }
@@ -478,6 +478,16 @@ def _pmc_brief(k, status):
             if k.get(key) is not None:
                 out[key] = round(k[key], 4) if isinstance(k[key], float) else k[key]
     return out
+
+
+def _pmc_tail(k, status):
+    """A short form for the end of the line (the driver keeps ~2 KB of stdout): the full fields
+    are in the record under profiles/."""
+    if not k:
+        return {"source": status}
+    return {"us": round(k["duration_ms"] * 1e3, 1) if k.get("duration_ms") else None,
+            "valu_active": round(k.get("valu_active_frac") or 0, 3), "waitcnt": round(k.get("waitcnt_frac") or 0, 3),
+            "waves_per_simd": k.get("waves_per_simd"), "stamp": status.split("csrc tree ")[-1].rstrip(")")}
 
 
 def _write_detail(rec: dict) -> str:
