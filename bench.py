@@ -72,7 +72,8 @@ def parse():
     ap.add_argument("--msg-len", type=int, default=256)
     ap.add_argument("--nkeys", type=int, default=4096)
     ap.add_argument("--comb-radix", type=int, default=13,
-                    help="radix 2^r of the per-key comb tables (8..13; 13 = 10.5 MB per key, 43 GB at 4,096 keys)")
+                    help="radix 2^r of the per-key comb tables (8..15; 13 = 10.5 MB per key, 43 GB at 4,096 keys; "
+                         "15 = 35.7 MB per key, 146 GB)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = every core we may use)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-runs", type=int, default=200)
@@ -308,7 +309,7 @@ def main():
     # table + radix-2^w_B B table), 7 field multiplications each, 81 + 9 v_mad_u64_u32 per
     # multiplication (9 x 29-bit limbs, fe25519.h); the pair / quad combines are parallelisation
     # overhead and not counted.  Bound: the MAD64 pipe (half the INT32 issue rate).
-    npos = {8: 32, 9: 29, 10: 26, 11: 23, 12: 22, 13: 20}[args.comb_radix] + \
+    npos = {8: 32, 9: 29, 10: 26, 11: 23, 12: 22, 13: 20, 14: 19, 15: 17}[args.comb_radix] + \
         {16: 16, 17: 15, 18: 15, 19: 14, 20: 13, 21: 13, 22: 12}[b_radix]
     mads_per_unit = npos * 7 * 90
     achieved = mads_per_unit * n / (ladder_ms * 1e-3)

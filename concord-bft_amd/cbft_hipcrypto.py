@@ -264,7 +264,7 @@ class Context:
 
     # ------------------------------------------------------------------ keys
     def load_keys(self, pks: Iterable[bytes] | np.ndarray, radix: int = 0) -> int:
-        """Upload a key table; radix = comb radix 2^radix of the per-key tables (8..13, 0 = default)."""
+        """Upload a key table; radix = comb radix 2^radix of the per-key tables (8..15, 0 = default)."""
         arr = _as_rows(pks, 32)
         tid = ctypes.c_uint32()
         _check(self.lib.cbft_ed25519_load_keys_ex(self.handle, _ptr(arr), arr.shape[0], radix, ctypes.byref(tid)),

@@ -34,7 +34,7 @@ int cbft_fail(hipError_t e, const char* what, const char* file, int line) {
 // table-build lanes per launch (bounds the projective staging buffer: 18 KB per lane)
 static const size_t kCombBuildLanes = 262144;  // 4 waves per SIMD; 4.7 GB of staging
 
-// comb radix of a key table: explicit (8..13), else $CBFT_COMB_RADIX, else the widest radix
+// comb radix of a key table: explicit (8..15), else $CBFT_COMB_RADIX, else the widest radix
 // whose tables for nkeys keys fit the per-table budget ($CBFT_COMB_BUDGET_GB, default 64 GB of
 // the 288 GB HBM): 13 (10.5 MB/key, 9 additions per lane) up to ~6,100 keys, 11 (3.0 MB/key,
 // 10) up to ~21,000, then 8 (0.53 MB/key, 12).
@@ -49,10 +49,12 @@ static int key_radix(int requested, uint32_t nkeys) {
   if (requested) return requested;
   if (const char* e = getenv("CBFT_COMB_RADIX")) {
     const int r = atoi(e);
-    if (r >= 8 && r <= 13) return r;
+    if (r >= 8 && r <= 15) return r;
   }
   double budget = 64.0;
   if (const char* e = getenv("CBFT_COMB_BUDGET_GB")) budget = atof(e);
+  // (14 and 15 only on request: at 4,096 keys radix 15's 146 GB of tables saves 3 of 32 additions
+  // but its entry reads miss the TLB more, and the pair ladder took 139 us against 110 at 13)
   for (int r : {13, 11}) {
     if (table_bytes(nkeys, r) <= budget * 1e9) return r;
   }
@@ -394,7 +396,7 @@ static int append_keys(cbft_ctx* c, uint32_t id, const uint8_t* pk, uint32_t nke
 
 int cbft_ed25519_load_keys_ex(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, int comb_radix, uint32_t* out_id) {
   if (!c || !out_id || (nkeys && !pk)) return CBFT_EINVAL;
-  if (comb_radix && (comb_radix < 8 || comb_radix > 13)) return CBFT_EINVAL;
+  if (comb_radix && (comb_radix < 8 || comb_radix > 15)) return CBFT_EINVAL;
   if (!c->kids.empty()) {  // replicate the table on every device, concurrently (ids stay in step)
     std::vector<uint32_t> ids(c->kids.size(), 0);
     const int rc = for_each_kid(c, [&](size_t g) {

@@ -53,7 +53,7 @@ def test_golden_key_table(ctx, golden):
         ctx.unload_keys(tid)
 
 
-@pytest.mark.parametrize("radix", [8, 9, 10, 12, 13])
+@pytest.mark.parametrize("radix", [8, 9, 10, 12, 13, 14, 15])
 def test_golden_key_table_radix(ctx, golden, radix):
     """Every comb radix gives the golden verdicts (the default radix is covered above)."""
     keys = sorted({v.pk for v in golden})
@@ -90,7 +90,7 @@ def test_load_keys_bad_radix(ctx):
     lib = ctx.lib
     tid = ctypes.c_uint32()
     key = (ctypes.c_uint8 * 32)()
-    for r in (7, 14, -1):
+    for r in (7, 16, -1):
         assert lib.cbft_ed25519_load_keys_ex(ctx.handle, key, 1, r, ctypes.byref(tid)) == -22
 
 

@@ -20,9 +20,9 @@ for r in $(seq 1 "${ROUNDS:-2}"); do
       echo "$label r$r mixed: $(tail -1 gpurun_out/ab/mixed_${label}_$r.json)"
       continue
     fi
-    env $envs CBFT_LIB=$lib timeout -k 10 200 python -u tools/ladder_probe.py --reps 20 > gpurun_out/ab/probe_${label}_$r.json 2> gpurun_out/ab/probe_${label}_$r.err \
+    env $envs CBFT_LIB=$lib timeout -k 10 200 python -u tools/ladder_probe.py --reps 20 ${PROBE_ARGS:-} > gpurun_out/ab/probe_${label}_$r.json 2> gpurun_out/ab/probe_${label}_$r.err \
       || { echo "probe $label failed"; tail -5 gpurun_out/ab/probe_${label}_$r.err; exit 1; }
-    env $envs CBFT_LIB=$lib timeout -k 10 200 python -u bench.py --steps 100 --warmup 10 --no-extras --no-cpu --latency-runs 100 > gpurun_out/ab/bench_${label}_$r.json 2> gpurun_out/ab/bench_${label}_$r.err \
+    env $envs CBFT_LIB=$lib timeout -k 10 200 python -u bench.py --steps 100 --warmup 10 --no-extras --no-cpu --latency-runs 100 ${BENCH_ARGS:-} > gpurun_out/ab/bench_${label}_$r.json 2> gpurun_out/ab/bench_${label}_$r.err \
       || { echo "bench $label failed"; tail -5 gpurun_out/ab/bench_${label}_$r.err; exit 1; }
     python3 - "$label" "$r" <<'PY'
 import json, sys
