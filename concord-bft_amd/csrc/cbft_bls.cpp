@@ -559,6 +559,25 @@ int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* 
   CBFT_HIP(c->bls_msg.reserve(msg_at + len + 1));
   CBFT_HIP(c->bls_out.reserve(37));
   std::vector<uint8_t> in(msg_at + len);  // alive (and the scalar in it) until the stream is done
+  // every exit, error paths included: the stream has finished reading `in`, the device copy of
+  // the scalar is cleared, and both host copies are zeroed
+  struct Wipe {
+    cbft_ctx* c;
+    uint32_t* w;
+    std::vector<uint8_t>& in;
+    bool cleared = false;  // the success path queued the device clear and synchronised
+    ~Wipe() {
+      if (!cleared) {
+        (void)hipStreamSynchronize(c->stream);
+        if (c->bls_msg.p) {
+          (void)hipMemsetAsync(c->bls_msg.p, 0, 8 * sizeof(uint32_t), c->stream);
+          (void)hipStreamSynchronize(c->stream);
+        }
+      }
+      secure_zero(w, 8 * sizeof(uint32_t));
+      secure_zero(in.data(), in.size() < 32 ? in.size() : 32);
+    }
+  } wipe{c, w, in};
   std::memcpy(in.data(), w, sizeof(w));
   if (len) std::memcpy(in.data() + msg_at, msg, len);
   CBFT_HIP(hipMemcpyAsync(c->bls_msg.p, in.data(), in.size(), hipMemcpyHostToDevice, c->stream));
@@ -578,8 +597,7 @@ int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* 
   CBFT_HIP(hipMemcpyAsync(out37, c->bls_out.p, 37, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipMemsetAsync(c->bls_msg.p, 0, sizeof(w), c->stream));  // the secret scalar leaves the device
   CBFT_HIP(hipStreamSynchronize(c->stream));
-  secure_zero(w, sizeof(w));
-  secure_zero(in.data(), sizeof(w));
+  wipe.cleared = true;  // (Wipe zeroes the host copies)
   return CBFT_OK;
 }
 
