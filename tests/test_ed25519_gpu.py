@@ -488,3 +488,29 @@ def test_golden_small_batches_three_wave_kernel(golden, chunk, waves, monkeypatc
             got = _bools(c.verify(tid, [index[v.pk] for v in part], [v.sig for v in part], [v.msg for v in part]),
                          len(part))
             assert np.array_equal(got, exp[lo:lo + chunk]), f"batch at {lo}"
+
+
+@pytest.mark.parametrize("lens", [
+    (943, 0, 47, 48, 111, 112, 941, 942),     # every message fits 8 SHA-512 blocks: the split hash
+    (944, 0, 47, 48, 111, 112, 941, 942),     # one 9-block message: the block hashes on wave 0 alone
+    (1, 2, 3, 4, 5, 6, 7, 8),                  # one block each
+])
+def test_split_hash_block_boundaries(lens):
+    """The three-wave fused kernel's two-wave SHA-512 (message schedules of blocks 1.. written to
+    LDS by the [S]B wave) against OpenSSL, for one 8-signature block mixing lengths at the block
+    boundaries and at the split's 8-block limit (64 + 943 + 17 = 1,024 B), honest and corrupted
+    signatures alike."""
+    parts = [sigsets.make_sigset(2, nkeys=2, msg_len=L, seed=7000 + j, invalid_frac=0.5) for j, L in enumerate(lens)]
+    pk = np.concatenate([p.pk for p in parts])
+    kidx, sigs, msgs, exp = [], [], [], []
+    for j, p in enumerate(parts):
+        for t in range(2):
+            kidx.append(2 * j + int(p.key_idx[t]))
+            sigs.append(bytes(p.sig[t]))
+            msgs.append(bytes(p.blob[int(p.off[t]): int(p.off[t]) + int(p.len[t])]))
+            exp.append(bool(p.expected[t]))
+    order = list(range(0, 16, 2)) + list(range(1, 16, 2))  # one block holds all eight lengths
+    with cb.Context(device=0) as c:
+        tid = c.load_keys(pk)
+        got = _bools(c.verify(tid, [kidx[k] for k in order], [sigs[k] for k in order], [msgs[k] for k in order]), 16)
+    assert np.array_equal(got, np.array([exp[k] for k in order]))
