@@ -834,6 +834,7 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
   // message bytes to move: [blo, bhi) of the blob (offsets need not start at 0)
   uint64_t blo = 0, bhi = 0;
   uint32_t lmin = 0, lmax = 0;  // message lengths: one SHA-512 block count for all -> no hash sort
+  bool packed = !fixed && n;    // message i at msg_off[0] + i * msg_len[0], one length for all
   if (fixed) {
     bhi = (uint64_t)fixed_len * n;
   } else if (n) {
@@ -844,9 +845,21 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
       bhi = std::max<uint64_t>(bhi, msg_off[i] + msg_len[i]);
       lmin = std::min(lmin, msg_len[i]);
       lmax = std::max(lmax, msg_len[i]);
+      packed = packed && msg_len[i] == msg_len[0] && msg_off[i] == msg_off[0] + (uint64_t)i * msg_len[0];
     }
   }
   const bool uniform_blocks = (64u + (uint64_t)lmin + 17u + 127u) / 128u == (64u + (uint64_t)lmax + 17u + 127u) / 128u;
+  // Same-length messages laid end to end (a packed blob: SigManager's batches of equal-size
+  // requests, the per-request engine's coalesced calls of one size) run as a fixed-length batch:
+  // no offset / length arrays to move, and the kernels read message i at i * len directly (no
+  // dependent offset read, which on the zero-copy path is a PCIe round trip)
+  if (packed) {
+    fixed = true;
+    fixed_len = msg_len[0];
+    blo = msg_off[0];
+    bhi = blo + (uint64_t)fixed_len * n;
+  }
+  const uint64_t mbase = fixed ? 0 : blo;  // message addresses in the image: o_msg + (off - mbase)
   const uint64_t blob = bhi - blo;
   if (blob && !msg_blob) return CBFT_EINVAL;
   int rc = reserve_work(c, n);
@@ -918,7 +931,7 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
       if (parts[k].bytes) std::memcpy(s.pack.as<uint8_t>(parts[k].off), parts[k].src, parts[k].bytes);
     const uint8_t* zin = static_cast<const uint8_t*>(s.pack.dev);
     rc = launch_locked(c, table_id, nullptr, reinterpret_cast<const uint32_t*>(zin + o_key), zin + o_sig,
-                       zin + o_msg - blo, fixed ? nullptr : reinterpret_cast<const uint64_t*>(zin + o_off),
+                       zin + o_msg - mbase, fixed ? nullptr : reinterpret_cast<const uint64_t*>(zin + o_off),
                        fixed ? nullptr : reinterpret_cast<const uint32_t*>(zin + o_len), fixed_len, n,
                        static_cast<uint64_t*>(s.hverd.dev), cs, uniform_blocks);
     if (rc) return rc;
@@ -979,7 +992,7 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
     CBFT_HIP(hipStreamWaitEvent(cs, s.copied, 0));
   }
   rc = launch_locked(c, table_id, kt ? nullptr : din + o_key, kt ? reinterpret_cast<const uint32_t*>(din + o_key) : nullptr,
-                     din + o_sig, din + o_msg - blo, fixed ? nullptr : reinterpret_cast<const uint64_t*>(din + o_off),
+                     din + o_sig, din + o_msg - mbase, fixed ? nullptr : reinterpret_cast<const uint64_t*>(din + o_off),
                      fixed ? nullptr : reinterpret_cast<const uint32_t*>(din + o_len), fixed_len, n,
                      s.verd.as<uint64_t>(), cs, uniform_blocks);
   if (rc) return rc;
