@@ -38,6 +38,20 @@ RF_HD uint32_t rl_shl(uint32_t x) {  // lane k <- lane k + I of the row, 0 above
 }
 RF_HD uint32_t rl_index(uint32_t) { return __lane_id() & 15u; }
 RF_HD uint32_t rl_row(uint32_t) { return __lane_id() >> 4; }
+// every row's value to every row: r[s] = x of row s (same row lane), s = 0..3, by one
+// v_permlane16_swap (odd rows of one copy <-> even rows of the other: [x0 x0 x2 x2] and
+// [x1 x1 x3 x3]) and two v_permlane32_swap (upper <-> lower 32 lanes: [x0 x0 x0 x0] and
+// [x2 x2 x2 x2] from the first, x1 / x3 from the second).  gfx950 VALU lane swaps: no LDS
+// crossbar trip, no s_waitcnt.
+RF_HD void rl_all_rows(uint32_t x, uint32_t* r) {
+  const auto p = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+  const auto q0 = __builtin_amdgcn_permlane32_swap(p[0], p[0], false, false);
+  const auto q1 = __builtin_amdgcn_permlane32_swap(p[1], p[1], false, false);
+  r[0] = q0[0];
+  r[1] = q1[0];
+  r[2] = q0[1];
+  r[3] = q1[1];
+}
 // the value the same row lane holds in row S (ds_bpermute: the LDS crossbar, no LDS memory)
 template <int S>
 RF_HD uint32_t rl_from_row(uint32_t x) {

@@ -127,6 +127,10 @@ inline HU rl_shl(const HU& a) {
   for (int l = 0; l < 64; l++) r.x[l] = (l & 15) + I < 16 ? a.x[l + I] : 0u;
   return r;
 }
+inline void rl_all_rows(const HU& a, HU* r) {
+  for (int s = 0; s < 4; s++)
+    for (int l = 0; l < 64; l++) r[s].x[l] = a.x[16 * s + (l & 15)];
+}
 template <int S>
 inline HU rl_from_row(const HU& a) {
   HU r;
