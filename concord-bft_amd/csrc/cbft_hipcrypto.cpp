@@ -151,6 +151,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   if (const char* e = getenv("CBFT_STAGE_ORDER_MIN")) c->stage_order_min = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_SMALL_MAX")) c->small_max = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_SHA_SORT_MIN")) c->sha_sort_min = (size_t)atoll(e);
+  if (const char* e = getenv("CBFT_SHA_LONG")) c->sha_long = atoi(e);
   if (const char* e = getenv("CBFT_SMALL_WAVES")) c->small_waves = atoi(e) == 3 ? 3 : 2;
   if (const char* e = getenv("CBFT_ZERO_COPY")) c->zero_copy = atoi(e);
   if (const char* e = getenv("CBFT_BLOCKING_SYNC")) c->blocking_sync = atoi(e);
@@ -300,6 +301,9 @@ void cbft_close(cbft_ctx* c) {
   for (WorkSlot& w : c->slots) {
     for (DevBuf* b : {&w.h, &w.flags, &w.xyz, &w.ps_tbl, &w.ps_aok, &w.perm, &w.buckets}) b->release();
     if (w.done) (void)hipEventDestroy(w.done);
+    if (w.fork) (void)hipEventDestroy(w.fork);
+    if (w.join) (void)hipEventDestroy(w.join);
+    if (w.aux) (void)hipStreamDestroy(w.aux);
   }
   for (hipEvent_t& e : c->ev)
     if (e) (void)hipEventDestroy(e);
@@ -700,9 +704,14 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   const bool sort = !small && d_off && !uniform_blocks && c->sha_sort_min && n >= c->sha_sort_min;
   if (sort) {
     CBFT_HIP(slot.perm.reserve(n * sizeof(uint32_t)));
-    if (!slot.buckets.p) {  // counts | cursors | uniform flag
-      CBFT_HIP(slot.buckets.reserve((2 * CBFT_SHA_BUCKETS + 1) * sizeof(uint32_t)));
-      CBFT_HIP(hipMemsetAsync(slot.buckets.p, 0, (2 * CBFT_SHA_BUCKETS + 1) * sizeof(uint32_t), s));  // counts start at 0
+    if (!slot.buckets.p) {  // counts | cursors | uniform flag | n_short
+      CBFT_HIP(slot.buckets.reserve((2 * CBFT_SHA_BUCKETS + 2) * sizeof(uint32_t)));
+      CBFT_HIP(hipMemsetAsync(slot.buckets.p, 0, (2 * CBFT_SHA_BUCKETS + 2) * sizeof(uint32_t), s));  // counts start at 0
+    }
+    if (c->sha_long && !slot.aux) {
+      CBFT_HIP(hipStreamCreateWithFlags(&slot.aux, hipStreamNonBlocking));
+      CBFT_HIP(hipEventCreateWithFlags(&slot.fork, hipEventDisableTiming));
+      CBFT_HIP(hipEventCreateWithFlags(&slot.join, hipEventDisableTiming));
     }
   }
 
@@ -721,6 +730,11 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   if (sort) {
     w.perm = slot.perm.as<uint32_t>();
     w.buckets = slot.buckets.as<uint32_t>();
+    if (c->sha_long) {
+      w.aux = slot.aux;
+      w.fork_ev = slot.fork;
+      w.join_ev = slot.join;
+    }
   }
   if (table_id == CBFT_NO_KEY_TABLE) {
     // per-signature keys: decode + precompute per signature

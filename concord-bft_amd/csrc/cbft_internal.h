@@ -108,6 +108,8 @@ struct BlsKeySet {
 struct WorkSlot {
   DevBuf h, flags, xyz, ps_tbl, ps_aok;
   DevBuf perm, buckets;  // hash order of a variable-length batch (counting sort by SHA-512 blocks)
+  hipStream_t aux = nullptr;                        // long-message hash stream (ed25519_hash_long_kernel)
+  hipEvent_t fork = nullptr, join = nullptr;
   hipEvent_t done = nullptr;
   bool used = false;
 };
@@ -181,6 +183,7 @@ struct cbft_ctx {
   // [h](-A) wave and the two R-decode waves (per-request p50 69 us vs 73 us for 2: one wave for both sums)
   int small_waves = 3;
   size_t sha_sort_min = 4096;  // variable-length batches from this size hash in block-count order
+  int sha_long = 1;             // their long messages on a second stream ($CBFT_SHA_LONG, 0 = off)
   int blocking_sync = 1;  // small batches' waiters sleep ($CBFT_BLOCKING_SYNC)
   int zero_copy = 1;  // fused small batches read pinned inputs and write verdicts in place ($CBFT_ZERO_COPY)
   int b_radix = CBFT_COMB_B_RADIX;  // radix of B's comb table ($CBFT_B_RADIX, 16..22)

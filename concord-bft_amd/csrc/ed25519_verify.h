@@ -127,10 +127,21 @@ struct Ed25519Work {
   // Variable-length batches: hash signatures in order of their SHA-512 block count (a counting
   // sort into perm before K1), so a wave's lanes run the same number of blocks.  Nullable.
   uint32_t* perm;              // n words
-  uint32_t* buckets;           // CBFT_SHA_BUCKETS x 2 + 1 words (counts, cursors, uniform flag)
+  uint32_t* buckets;           // CBFT_SHA_BUCKETS x 2 + 2 words (counts, cursors, uniform flag, n_short)
+  // Messages of >= CBFT_SHA_LONG_BLOCKS SHA-512 blocks (the sorted order's tail) hash on a second
+  // stream in blocks of two waves, one expanding the message schedules into LDS, the other running
+  // the rounds (ed25519_hash_long_kernel); null aux = off.
+  hipStream_t aux;
+  hipEvent_t fork_ev, join_ev;
 };
 // Block-count buckets of the hash sort: bucket min(nblocks, CBFT_SHA_BUCKETS - 1).
 #define CBFT_SHA_BUCKETS 256
+#ifndef CBFT_SHA_LONG_BLOCKS
+#define CBFT_SHA_LONG_BLOCKS 12
+#endif
+#ifndef CBFT_SHA_LONG_GROUPS
+#define CBFT_SHA_LONG_GROUPS 192
+#endif
 
 size_t cbft_ed25519_table_words_per_unit();
 // staging words for `lanes` table-build lanes (18 KB each)

@@ -402,6 +402,15 @@ __global__ void __launch_bounds__(256) ed25519_bucket_scan_kernel(uint32_t* coun
   cursors[t] = v[t] - c;
   counts[t] = 0;  // ready for the next batch's counts
   if (t == 0) cursors[CBFT_SHA_BUCKETS] = 0;
+  // n_short: signatures below CBFT_SHA_LONG_BLOCKS blocks (the long ones follow them in the order;
+  // with one bucket for all, 0 or n, which the identity order also satisfies), but at most
+  // CBFT_SHA_LONG_GROUPS x 64 positions for the long kernel: its blocks (83 KB of LDS each) must
+  // all be resident at once, or its last groups would run a second full chain after the others
+  if (t == CBFT_SHA_LONG_BLOCKS) {
+    const uint32_t n = v[CBFT_SHA_BUCKETS - 1], cap = 64u * CBFT_SHA_LONG_GROUPS;
+    const uint32_t ns = v[t] - c;
+    cursors[CBFT_SHA_BUCKETS + 1] = n - ns > cap ? n - cap : ns;
+  }
   __syncthreads();
   if (c != 0 && c == v[CBFT_SHA_BUCKETS - 1]) cursors[CBFT_SHA_BUCKETS] = 1;  // one bucket holds all
 }
@@ -424,16 +433,101 @@ __global__ void __launch_bounds__(256) ed25519_bucket_scatter_kernel(const Ed255
   if (i < b.n) perm[base[k] + rank] = (uint32_t)i;
 }
 
-// perm: the block-count order (nullable); uniform: its flag word (perm unused when set)
+// perm: the block-count order (nullable); uniform: its flag word (perm unused when set);
+// nshort (nullable): positions from *nshort on are ed25519_hash_long_kernel's
 __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const Ed25519Batch b, const uint32_t* perm,
-                                                                          const uint32_t* uniform, uint32_t* h_soa,
-                                                                          uint8_t* flags) {
+                                                                          const uint32_t* uniform, const uint32_t* nshort,
+                                                                          uint32_t* h_soa, uint8_t* flags) {
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= b.n) return;
+  if (g >= b.n || (nshort && g >= *nshort)) return;
   const size_t i = perm && !*uniform ? (size_t)perm[g] : g;
   uint32_t hw[8];
   bool flag;
   ed25519_hash_sig(b, i, hw, flag);
+#pragma unroll
+  for (int k = 0; k < 8; k++) h_soa[k * b.n + i] = hw[k];
+  flags[i] = flag ? 1 : 0;
+}
+
+// K1 for the sorted order's tail (messages of >= CBFT_SHA_LONG_BLOCKS blocks): 64 signatures per
+// block of two waves.  Wave 1 expands block j's message schedule (K[t] + W[t], sha512_schedule_kw)
+// into one of two LDS slots while wave 0 runs block j - 1's rounds from the other
+// (sha512_rounds_kw): each signature's serial chain loses the schedule, ~a third of a
+// compression, which is what bounds config #3's hash stage (a 4,096-B message is 33 blocks on one
+// lane).  Runs on a second stream beside ed25519_hash_kernel (which skips these positions); one
+// barrier per block, the same count in both waves (the group's most blocks).
+#define HASH_LONG_BLOCK 128
+__global__ void __launch_bounds__(HASH_LONG_BLOCK) ed25519_hash_long_kernel(const Ed25519Batch b, const uint32_t* perm,
+                                                                            const uint32_t* uniform,
+                                                                            const uint32_t* nshort, uint32_t* h_soa,
+                                                                            uint8_t* flags) {
+  __shared__ uint64_t kwl[2][64 * KW_STRIDE];
+  const size_t g0 = (size_t)*nshort + (size_t)blockIdx.x * 64;
+  if (g0 >= b.n) return;  // the whole block
+  const uint32_t ln = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  const bool ident = *uniform != 0;
+  const size_t g = g0 + ln;
+  const bool live = g < b.n;
+  const size_t i = ident ? (live ? g : g0) : (size_t)perm[live ? g : g0];
+  const uint32_t nb = live ? sig_sha_blocks(b, i) : 0u;
+  uint32_t nbmax = nb;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) nbmax = max(nbmax, (uint32_t)__shfl_xor((int)nbmax, d, 64));
+  uint64_t* slot0 = &kwl[0][ln * KW_STRIDE];
+  uint64_t* slot1 = &kwl[1][ln * KW_STRIDE];
+  if (wave == 1) {  // schedules
+    const uint32_t key = batch_unit(b, i);
+    uint32_t Aw[8], Rw[8];
+    load_words8(Aw, b.key_idx ? b.keys.pk(key) : b.pk + (size_t)key * 32);
+    load_words8(Rw, b.sig + i * 64);
+    const uint8_t* m = b.msg_off ? b.msg + b.msg_off[i] : b.msg + i * (size_t)b.fixed_len;
+    uint32_t len = b.msg_off ? b.msg_len[i] : b.fixed_len;
+    if (len > CBFT_MAX_MSG_LEN) len = 0;
+    const uint32_t* safe = reinterpret_cast<const uint32_t*>(b.sig + i * 64);
+    const uint32_t total = 64u + len;
+    uint32_t d[33];
+    fetch_msg_dwords<8>(d, m, len, 0u, safe);
+    for (uint32_t blk = 0; blk < nbmax; blk++) {
+      if (blk < nb) {
+        uint64_t W[16];
+        if (blk == 0) {
+#pragma unroll
+          for (int j = 0; j < 4; j++) W[j] = ((uint64_t)bswap32(Rw[2 * j]) << 32) | bswap32(Rw[2 * j + 1]);
+#pragma unroll
+          for (int j = 0; j < 4; j++) W[4 + j] = ((uint64_t)bswap32(Aw[2 * j]) << 32) | bswap32(Aw[2 * j + 1]);
+          assemble_msg_words<8>(W + 8, d, m, len, 0u);
+        } else {
+          assemble_msg_words<16>(W, d, m, len, 128u * blk - 64u);
+        }
+        if (blk + 1 < nb) fetch_msg_dwords<16>(d, m, len, 128u * blk + 64u, safe);  // next block's words
+        if (blk == nb - 1) {
+          W[14] = 0;
+          W[15] = (uint64_t)total << 3;
+        }
+        sha512_schedule_kw((blk & 1) ? slot1 : slot0, W);
+      }
+      __syncthreads();  // block blk's schedules are in LDS; block blk - 1's rounds are done
+    }
+    return;
+  }
+  uint64_t H[8];  // wave 0: rounds
+  sha512_init(H);
+  for (uint32_t blk = 0; blk < nbmax; blk++) {
+    __syncthreads();
+    if (blk < nb) sha512_rounds_kw(H, (blk & 1) ? slot1 : slot0);
+  }
+  if (!live) return;
+  uint32_t dig[16], hw[8], Sw[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    dig[2 * k] = bswap32((uint32_t)(H[k] >> 32));
+    dig[2 * k + 1] = bswap32((uint32_t)H[k]);
+  }
+  sc_reduce512(hw, dig);
+  load_words8(Sw, b.sig + i * 64 + 32);
+  const uint32_t len = b.msg_off ? b.msg_len[i] : b.fixed_len;
+  const bool key_ok = !b.key_idx || b.key_idx[i] < b.nkeys;
+  const bool flag = sc_is_canonical(Sw) && key_ok && len <= CBFT_MAX_MSG_LEN;
 #pragma unroll
   for (int k = 0; k < 8; k++) h_soa[k * b.n + i] = hw[k];
   flags[i] = flag ? 1 : 0;
@@ -1628,8 +1722,18 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
     hipLaunchKernelGGL(ed25519_bucket_scan_kernel, dim3(1), b256, 0, stream, w.buckets, w.buckets + CBFT_SHA_BUCKETS);
     hipLaunchKernelGGL(ed25519_bucket_scatter_kernel, g256, b256, 0, stream, b, w.buckets + CBFT_SHA_BUCKETS, w.perm);
   }
+  const uint32_t* uniform_w = sorted ? (const uint32_t*)(w.buckets + 2 * CBFT_SHA_BUCKETS) : nullptr;
+  const uint32_t* nshort_w = sorted && w.aux ? (const uint32_t*)(w.buckets + 2 * CBFT_SHA_BUCKETS + 1) : nullptr;
+  if (nshort_w) {  // the long messages on the second stream, beside the short ones
+    if ((e = hipEventRecord(w.fork_ev, stream)) != hipSuccess || (e = hipStreamWaitEvent(w.aux, w.fork_ev, 0)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(ed25519_hash_long_kernel, dim3((unsigned)((b.n + 63) / 64)), dim3(HASH_LONG_BLOCK), 0, w.aux, b,
+                       (const uint32_t*)w.perm, uniform_w, nshort_w, w.h_soa, w.flags);
+    if ((e = hipEventRecord(w.join_ev, w.aux)) != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(ed25519_hash_kernel, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
-                     sorted ? (const uint32_t*)(w.buckets + 2 * CBFT_SHA_BUCKETS) : nullptr, w.h_soa, w.flags);
+                     uniform_w, nshort_w, w.h_soa, w.flags);
+  if (nshort_w && (e = hipStreamWaitEvent(stream, w.join_ev, 0)) != hipSuccess) return e;
   if (order && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;
   if (order && order->wait && order->ladder && (e = hipStreamWaitEvent(stream, order->done[1], 0)) != hipSuccess)
     return e;

@@ -375,13 +375,14 @@ def test_golden_small_batches_fused_kernel(ctx, golden, chunk):
 
 
 @pytest.mark.parametrize("n,msg_len", [(1, 256), (9, 256), (17, 256), (47, 256), (64, 256), (65, 256), (130, 256),
-                                       (5000, 256), (5000, (1, 2048))])
+                                       (5000, 256), (5000, (1, 2048)), (5000, 2048), (13000, 2048)])
 def test_device_path_small_batch_whole_words(n, msg_len):
     """cbft_ed25519_verify_batch_device writes ceil(n/64) WHOLE 64-bit verdict words, bits past n
     = 0, also when the batch runs as the fused small kernel (8-signature pieces per block): the
     buffer is pre-filled with 0xFF, so a piece no block covers would show up as stray accept bits.
     n = 5,000: the three-kernel path with the device-side hash sort (one block count for all
-    messages: the uniform flag keeps the identity order; random lengths: the permutation)."""
+    messages: the uniform flag keeps the identity order; random lengths: the permutation); 2,048-B
+    messages are long (ed25519_hash_long_kernel): all of 5,000, or the last 64 x 192 of 13,000."""
     hip = _Hip()
     nwords = (n + 63) // 64
     ss = sigsets.make_sigset(n, nkeys=7, msg_len=msg_len, seed=900 + n, invalid_frac=0.2)
