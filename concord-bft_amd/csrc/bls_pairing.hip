@@ -28,12 +28,11 @@ struct PairXchg {
 };
 
 __device__ __forceinline__ void xchg_put(PairXchg& x, const fp& f, const P36& g) {
-  if (g.lane < 36)
-    for (int i = 0; i < BN_LIMBS; i++) x.f[g.lane][i] = f.v[i];
+  if (g.own)
+    for (int i = 0; i < BN_LIMBS; i++) x.f[g.e][i] = f.v[i];
 }
 __device__ __forceinline__ void xchg_get(fp& f, const PairXchg& x, const P36& g) {
-  const int l = g.lane < 36 ? g.lane : g.lane - 36;  // shadows read the lane they mirror
-  for (int i = 0; i < BN_LIMBS; i++) f.v[i] = x.f[l][i];
+  for (int i = 0; i < BN_LIMBS; i++) f.v[i] = x.f[g.e][i];  // shadows read the slot they mirror
 }
 
 // shares: k x 37 bytes.  out: valid[k] (1 = verified), sig[k] (parsed affine point, 19 words),

@@ -4,7 +4,12 @@
 // each of the 12 Fp components of f = sum_k e_k w^k (e_k in Fp2) its own lane; here every
 // component gets THREE lanes (sub-lanes s = 0, 1, 2; lane 12 s + 2 k + h holds component h of
 // e_k, lanes 36..63 shadow lanes 0..27) and the products an Fp12 operation needs are dealt out
-// to the sub-lanes, then summed with two ds_bpermute gathers:
+// to the sub-lanes, then summed.  The other component of a lane's coefficient sits in the partner
+// lane (lane ^ 1): a DPP quad_perm move; the coefficient fetches and the sub-lane sums are
+// ds_bpermute gathers.
+//   CBFT_P36_ROWS = 1 (A/B only): sub-lane s in DPP row s (lane 16 s + 2 k + h, row positions
+//   12..15 shadow 8..11, row 3 shadows row 0), the sub-lane sum one rl_all_rows permlane gather.
+//   Measured 1.3 % (verify) to 2 % (multisig verify) slower than the bpermute sums.
 //   op          Fp mults per lane   (bn254_pair12.h)
 //   mul         4                   12    6 split products per component, 2 per sub-lane
 //   sqr         2                    8    even k: two diagonal squares on s = 0, one cross
@@ -19,39 +24,91 @@
 #pragma once
 #include "bn254_cycsq.h"
 #include "bn254_pair12.h"
+#include "row_lanes.h"
+
+#ifndef CBFT_P36_ROWS
+#define CBFT_P36_ROWS 0
+#endif
 
 struct P36 {
   int k;     // coefficient 0..5
   int h;     // component: 0 = real, 1 = imaginary
   int s;     // sub-lane 0..2
   int lane;  // lane within the wave
+  int e;     // 12 s + 2 k + h: the lane's slot among the 36 (Miller value exchange)
+  bool own;  // not a shadow: the lane owning slot e
 };
 
 __device__ __forceinline__ P36 p36_lane() {
   P36 g;
   g.lane = threadIdx.x & 63;
+#if CBFT_P36_ROWS
+  const int r = g.lane >> 4, q = g.lane & 15;
+  const int c = q < 12 ? q : q - 4;
+  g.s = r < 3 ? r : 0;
+  g.own = r < 3 && q < 12;
+#else
   const int e = g.lane < 36 ? g.lane : g.lane - 36;
   const int c = e % 12;
   g.s = e / 12;
+  g.own = g.lane < 36;
+#endif
   g.k = c >> 1;
   g.h = c & 1;
+  g.e = 12 * g.s + c;
   return g;
 }
 
-__device__ __forceinline__ int p36_src(int k2, int h2, int s2) { return 12 * s2 + 2 * k2 + h2; }
+__device__ __forceinline__ int p36_src(int k2, int h2, int s2) {
+  return (CBFT_P36_ROWS ? 16 : 12) * s2 + 2 * k2 + h2;
+}
 
-// (my component, the other component) of coefficient k2 of x
+// (q0, q1, q2) = part of sub-lanes 0, 1, 2 of this lane's component
+__device__ __forceinline__ void p36_gather3(fp& q0, fp& q1, fp& q2, const fp& part, const P36& g) {
+#if CBFT_P36_ROWS
+  (void)g;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+    uint32_t r[4];
+    rl_all_rows(part.v[i], r);
+    q0.v[i] = r[0];
+    q1.v[i] = r[1];
+    q2.v[i] = r[2];
+  }
+#else
+  fp_shfl(q0, part, p36_src(g.k, g.h, 0));
+  fp_shfl(q1, part, p36_src(g.k, g.h, 1));
+  fp_shfl(q2, part, p36_src(g.k, g.h, 2));
+#endif
+}
+
+// r = x of the partner lane (same k and s, the other component h): lane ^ 1 in both layouts,
+// shadows included, as a DPP quad_perm [1, 0, 3, 2] move instead of a ds_bpermute (CBFT_P36_DPP = 0:
+// the bpermute form)
+#ifndef CBFT_P36_DPP
+#define CBFT_P36_DPP 1
+#endif
+__device__ __forceinline__ void fp_swap_h(fp& r, const fp& x, const P36& g) {
+#if CBFT_P36_DPP
+  (void)g;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)x.v[i], 0xB1, 0xF, 0xF, false);
+#else
+  fp_shfl(r, x, g.lane ^ 1);
+#endif
+}
+
+// (my component, the other component) of coefficient k2 of x.  The partner lane fetches the same
+// coefficient (k2 depends on k and s only), so its result is my other component.
 __device__ __forceinline__ void p36_fetch(fp& m, fp& o, const fp& x, int k2, const P36& g) {
   fp_shfl(m, x, p36_src(k2, g.h, g.s));
-  fp_shfl(o, x, p36_src(k2, 1 - g.h, g.s));
+  fp_swap_h(o, m, g);
 }
 
 // r = sum over the three sub-lanes of component (k, h) of part, in the order 0, 1, 2
 __device__ __forceinline__ void p36_sum3(fp& r, const fp& part, const P36& g) {
   fp q0, q1, q2;
-  fp_shfl(q0, part, p36_src(g.k, g.h, 0));
-  fp_shfl(q1, part, p36_src(g.k, g.h, 1));
-  fp_shfl(q2, part, p36_src(g.k, g.h, 2));
+  p36_gather3(q0, q1, q2, part, g);
   f_add(r, q0, q1);
   f_add(r, r, q2);
 }
@@ -59,7 +116,7 @@ __device__ __forceinline__ void p36_sum3(fp& r, const fp& part, const P36& g) {
 // my component of xi * z, z held componentwise by this lane and its partner (same k, s)
 __device__ __forceinline__ void p36_xi(fp& r, const fp& z, const P36& g) {
   fp zo;
-  fp_shfl(zo, z, p36_src(g.k, 1 - g.h, g.s));
+  fp_swap_h(zo, z, g);
   p12_cxi(r, z, zo, g.h);
 }
 
@@ -83,11 +140,9 @@ __device__ __forceinline__ void p36_mul(fp& r, const fp& a, const fp& b, const P
   }
   fp acc, accw, ao, z, z0, z1, z2;
   cm_terms(acc, accw, T[0], T[1], T[2], T[3], g.h, wrap[0], wrap[1]);
-  fp_shfl(ao, accw, p36_src(g.k, 1 - g.h, g.s));
+  fp_swap_h(ao, accw, g);
   cm_xi(z, acc, accw, ao, g.h);
-  fp_shfl(z0, z, p36_src(g.k, g.h, 0));
-  fp_shfl(z1, z, p36_src(g.k, g.h, 1));
-  fp_shfl(z2, z, p36_src(g.k, g.h, 2));
+  p36_gather3(z0, z1, z2, z, g);
   cm_sum3(r, z0, z1, z2);
 }
 
@@ -113,11 +168,9 @@ __device__ __forceinline__ void p36_sqr(fp& r, const fp& a, const P36& g) {
   f_zero(zero);
   // diag: x^2 term -> acc, z^2 term -> accw (the second diagonal term wraps); cross: P1 +- P2
   cm_terms(acc, accw, P1, diag ? zero : P2, diag ? P2 : zero, zero, g.h, !diag && cwrap, true);
-  fp_shfl(ao, accw, p36_src(g.k, 1 - g.h, g.s));
+  fp_swap_h(ao, accw, g);
   cm_xi(z, acc, accw, ao, g.h);
-  fp_shfl(z0, z, p36_src(g.k, g.h, 0));
-  fp_shfl(z1, z, p36_src(g.k, g.h, 1));
-  fp_shfl(z2, z, p36_src(g.k, g.h, 2));
+  p36_gather3(z0, z1, z2, z, g);
   cm_sum3(r, z0, z1, z2);
 }
 
@@ -127,19 +180,27 @@ __device__ __forceinline__ void p36_cyc_sqr(fp& r, const fp& a, const P36& g) {
   // lazy form (bn254_cycsq.h): 4 gathers of 9 limbs, one Fp multiplication, one reduction
   const int sx = (g.k == 0 || g.k == 3) ? 0 : ((g.k == 1 || g.k == 4) ? 2 : 1);
   const bool odd = (g.k & 1) != 0;
-  fp t, R, Wm, Wo, U, V, T, X2, Y2, G3, v, vo;
+  fp t, R, Wm, Wo, U, V, T, X2, Y2, G3, v, vo, Z3;
   fp_shfl(t, a, p36_src(g.k < 3 ? g.k + 3 : g.k - 3, g.h, g.s));
   cs_pre(R, a, t, g.s);
   const int c = g.s == 1 ? sx + 3 : sx;
   fp_shfl(Wm, R, p36_src(c, g.h, g.s));
-  fp_shfl(Wo, R, p36_src(c, 1 - g.h, g.s));
+  fp_swap_h(Wo, Wm, g);
   cs_operands(U, V, Wm, Wo, g.h);
   f_mul(T, U, V);
+  // (x+y)^2_h (odd k) | y^2_h' (even k: the partner's sub-lane 1)
+#if CBFT_P36_ROWS
+  p36_gather3(X2, Y2, Z3, T, g);
+  fp_swap_h(G3, Y2, g);
+  if (odd) G3 = Z3;
+#else
   fp_shfl(X2, T, p36_src(g.k, g.h, 0));
   fp_shfl(Y2, T, p36_src(g.k, g.h, 1));
-  fp_shfl(G3, T, odd ? p36_src(g.k, g.h, 2) : p36_src(g.k, 1 - g.h, 1));  // (x+y)^2_h | y^2_h'
+  fp_shfl(G3, T, odd ? p36_src(g.k, g.h, 2) : p36_src(g.k, 1 - g.h, 1));
+  (void)Z3;
+#endif
   cs_combine(v, X2, Y2, G3, g.k, g.h);
-  fp_shfl(vo, v, p36_src(g.k, 1 - g.h, g.s));
+  fp_swap_h(vo, v, g);
   cs_finish(r, v, vo, a, g.k, g.h);
 }
 
@@ -261,7 +322,7 @@ __device__ __forceinline__ void p36_frob(fp& r, const fp& x, const P36& g) {
     p12_sel2(gm, t, g.k == 5);
   }
   fp co;
-  fp_shfl(co, c, p36_src(g.k, 1 - g.h, g.s));
+  fp_swap_h(co, c, g);
   const fp gmm = g.h ? gm.b : gm.a, gmo = g.h ? gm.a : gm.b;
   p12_cmul(r, c, co, gmm, gmo, g.h);
 }
