@@ -104,7 +104,9 @@ struct BlsKeySet {
 // consecutive device-path batches on different streams overlap (batch i's finish and batch
 // i+1's hash run together, each alone would leave the SIMDs half idle); a slot's `done` event
 // orders its reuse after its previous batch.
+#ifndef CBFT_WORK_SLOTS
 #define CBFT_WORK_SLOTS 2
+#endif
 struct WorkSlot {
   DevBuf h, flags, xyz, ps_tbl, ps_aok;
   DevBuf perm, buckets;  // hash order of a variable-length batch (counting sort by SHA-512 blocks)

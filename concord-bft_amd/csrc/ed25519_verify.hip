@@ -1331,6 +1331,9 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
   __shared__ uint32_t rdec[SMALL_SIGS][2 * FE_LIMBS + 1];  // x_R | y_R | decodes
   __shared__ uint32_t sbp[SMALL_SIGS][4 * FE_LIMBS];       // [S]B as X | Y | Z | T
   __shared__ uint64_t kw[SMALL_SIGS][SMALL_KW_BLOCKS * KW_STRIDE];  // SHA-512 K[t] + W[t] per block
+#if CBFT_ED_PHASES
+  __shared__ uint64_t phend[6];  // per wave: end of its part (decode waves: also their start, +2)
+#endif
   const uint32_t ln = threadIdx.x & 63u, wave = threadIdx.x >> 6, q = ln & 3u, sl = (ln >> 2) & (SMALL_SIGS - 1);
   size_t i = (size_t)blockIdx.x * SMALL_SIGS + sl;
   const bool live = i < b.n && (ln >> 2) < SMALL_SIGS;
@@ -1343,12 +1346,19 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
   // waves 0 and 1 compute alike); otherwise wave 0 hashes on its own as before.
   const bool split = CBFT_SMALL_SPLIT_HASH && __ballot(sig_sha_blocks(b, i) > SMALL_KW_BLOCKS) == 0;
   if (wave >= 2) {  // (without the split every wave passes the first barrier at its start)
+#if CBFT_ED_PHASES
+    if (ln == 0) phend[wave] = wall_clock64();  // start of the decode (overwritten at its end)
+    if (ln == 0) phend[wave + 2] = phend[wave];
+#endif
     if (split) {
       small_decode_r<true>(b, blockIdx.x, wave - 2, ln, rdec);
     } else {
       __syncthreads();
       small_decode_r<false>(b, blockIdx.x, wave - 2, ln, rdec);
     }
+#if CBFT_ED_PHASES
+    if (ln == 0) phend[wave] = wall_clock64();  // (printed by wave 0 after the last barrier)
+#endif
     __syncthreads();
     return;
   }
@@ -1369,6 +1379,9 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
         sbp[sl][3 * FE_LIMBS + k] = P.T.v[k];
       }
     }
+#if CBFT_ED_PHASES
+    if (ln == 0) phend[1] = wall_clock64();
+#endif
     __syncthreads();
     return;
   }
@@ -1405,10 +1418,15 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
   __syncthreads();  // wave 1's [S]B, wave 2's R
 #if CBFT_ED_PHASES
   ph3[4] = wall_clock64();
+  // every time from wave 0's start; the printf runs after the last barrier (a device printf takes
+  // tens of microseconds and would otherwise stretch the wave that calls it)
   if (blockIdx.x == 0 && ln == 0)
-    printf("ed25519_small3 block 0 (us): to-barrier %.1f hash-after %.1f A-comb %.1f wait-B/R %.1f (split %d)\n",
-           (ph3[1] - ph3[0]) * 0.01, (ph3[2] - ph3[1]) * 0.01, (ph3[3] - ph3[2]) * 0.01, (ph3[4] - ph3[3]) * 0.01,
-           split ? 1 : 0);
+    printf("ed25519_small3 block 0 (us from start): block-0 compress %.1f, rounds done %.1f, A-comb done %.1f | "
+           "[S]B done %.1f | R decode %.1f-%.1f, %.1f-%.1f | barrier %.1f (split %d)\n",
+           (ph3[1] - ph3[0]) * 0.01, (ph3[2] - ph3[0]) * 0.01, (ph3[3] - ph3[0]) * 0.01,
+           ((int64_t)(phend[1] - ph3[0])) * 0.01, ((int64_t)(phend[4] - ph3[0])) * 0.01,
+           ((int64_t)(phend[2] - ph3[0])) * 0.01, ((int64_t)(phend[5] - ph3[0])) * 0.01,
+           ((int64_t)(phend[3] - ph3[0])) * 0.01, (ph3[4] - ph3[0]) * 0.01, split ? 1 : 0);
 #endif
   {
     ge_p3 Q;

@@ -27,13 +27,14 @@ def to_dev(a, dt):
 
 d_sig, d_blob = to_dev(ss.sig.reshape(-1), np.uint8), to_dev(ss.blob, np.uint8)
 d_off, d_len, d_k = to_dev(ss.off, np.int64), to_dev(ss.len, np.int32), to_dev(ss.key_idx, np.int32)
-streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
-outs = [torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev) for _ in range(2)]
+NS = int(os.environ.get("NSTREAMS", "2"))  # streams the batches alternate over
+streams = [torch.cuda.Stream(device=dev) for _ in range(NS)]
+outs = [torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev) for _ in range(NS)]
 
 
 def step(j):  # fixed-length device call, as bench.py's device-resident figure (config #2)
     ctx.verify_fixed_device(tid, 0, d_k.data_ptr(), d_sig.data_ptr(), d_blob.data_ptr(), 256, n,
-                            outs[j % 2].data_ptr(), streams[j % 2].cuda_stream)
+                            outs[j % NS].data_ptr(), streams[j % NS].cuda_stream)
 
 
 for j in range(5):
@@ -46,5 +47,5 @@ torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 for o in outs:
     assert np.array_equal(cb.bitmap_to_bools(o.cpu().numpy().view(np.uint8).tobytes(), n), ss.expected)
-print(f"device-resident {n * 30 / dt / 1e6:.1f} M/s, {dt / 30 * 1e6:.1f} us/step", flush=True)
+print(f"streams {NS} device-resident {n * 30 / dt / 1e6:.1f} M/s, {dt / 30 * 1e6:.1f} us/step", flush=True)
 ctx.close()
