@@ -99,6 +99,55 @@ __device__ __forceinline__ void g2j_load(g2j& a, const uint32_t* o) {
     }
 }
 
+// fp_sqrt (bn254_field.h) on the lane's DPP row: y = a^((p+1)/4) by rf_pow_sw, true iff y^2 == a.
+// Every lane of a row must hold the same a, and all 64 lanes of the wave must call it together.
+__device__ __forceinline__ bool fp_sqrt_row(fp& y, const fp& a) {
+  const uint32_t tag = 0;
+  const uint32_t qrow = rf_row_const(FpParams::Q, tag);
+  rf_to_fe(y, rf_pow_sw<FpSqrtSchedule, uint32_t, uint64_t>(rf_from_fe(a, tag), qrow));
+  fp t;
+  f_sqr(t, y);
+  return f_eq(t, a);
+}
+
+// g1_decompress (bn254_pairing.h: RELIC ep_read_bin, pack = 1) with the square root on the lane's
+// DPP row: the same point and verdict for every 33-byte input.  Every lane of a row must hold the
+// same bytes and all 64 lanes of the wave must call it together: the root is taken whatever the
+// encoding (a malformed one is rejected after it), so no row leaves the row-parallel code early.
+__device__ __forceinline__ bool g1_decompress_row(g1a& r, const uint8_t* b) {
+  const uint8_t pre = b[0];
+  uint8_t o = 0;
+  for (int i = 1; i < 33; i++) o |= b[i];
+  uint32_t w[8];
+  be32_to_words(w, b + 1);
+  fp x, rhs, b2, y;
+  f_from_words(x, w);  // any 256-bit value: used only when x < p
+  f_sqr(rhs, x);
+  f_mul(rhs, rhs, x);
+  uint32_t two[8] = {2, 0, 0, 0, 0, 0, 0, 0};
+  f_from_words(b2, two);
+  f_add(rhs, rhs, b2);
+  const bool sq = fp_sqrt_row(y, rhs);
+  if (pre == 0) {  // infinity: 0x00 || 0^32
+    r.inf = true;
+    f_zero(r.x);
+    f_zero(r.y);
+    return o == 0;
+  }
+  r.inf = false;
+  if ((pre != 2 && pre != 3) || !words_lt_p(w) || !sq) return false;
+  r.x = x;
+  if (f_relic_bit(y) != (uint32_t)(pre & 1)) f_neg(y, y);
+  r.y = y;
+  return true;
+}
+
+// bls_parse_share (bls_ops.h) with g1_decompress_row: the same contract as g1_decompress_row
+__device__ __forceinline__ bool bls_parse_share_row(uint32_t& id, g1a& s, const uint8_t* b) {
+  id = ((uint32_t)b[0] << 24) | ((uint32_t)b[1] << 16) | ((uint32_t)b[2] << 8) | b[3];
+  return g1_decompress_row(s, b + 4);
+}
+
 // g1_map with the try-and-increment candidates tried four at a time, one per DPP row, the square
 // root on row-parallel Fp: candidate x + 4 i + row in row `row`; the lowest row whose x^3 + 2 is a
 // square wins (the point the sequential loop returns), every lane gets it.  1.07 rounds on
@@ -109,9 +158,8 @@ __device__ __forceinline__ void g1_map_row(g1a& r, const uint8_t* msg, uint32_t 
   sha256(d, msg, len);
   uint32_t w[8];
   be32_to_words(w, d);
-  fp x, two, rhs, y, off, step, t2;
+  fp x, two, rhs, y, off, step;
   f_from_words(x, w);
-  const uint32_t tag = 0;
   const uint32_t row = (threadIdx.x & 63) >> 4;
   uint32_t t[8] = {2, 0, 0, 0, 0, 0, 0, 0};
   f_from_words(two, t);
@@ -120,14 +168,11 @@ __device__ __forceinline__ void g1_map_row(g1a& r, const uint8_t* msg, uint32_t 
   t[0] = 4;
   f_from_words(step, t);
   f_add(x, x, off);
-  const uint32_t qrow = rf_row_const(FpParams::Q, tag);
   for (;;) {
     f_sqr(rhs, x);
     f_mul(rhs, rhs, x);
     f_add(rhs, rhs, two);
-    rf_to_fe(y, rf_pow_sw<FpSqrtSchedule, uint32_t, uint64_t>(rf_from_fe(rhs, tag), qrow));
-    f_sqr(t2, y);
-    const bool ok = f_eq(t2, rhs);
+    const bool ok = fp_sqrt_row(y, rhs);
     const unsigned long long m = __ballot(ok);
     if (m) {
       const int src = __ffsll(m) - 1;

@@ -13,6 +13,9 @@
 
 #include "bls_common.h"
 #include "bn254_g1quad.h"
+#ifndef CBFT_BLS_PHASES
+#define CBFT_BLS_PHASES 0  // probe builds: bls_msm_finish_kernel prints its phase times
+#endif
 
 // one wave: the candidates are tried four at a time, one per DPP row (g1_map_row)
 __global__ void __launch_bounds__(64) bls_hash_kernel(const uint8_t* msg, uint32_t len, uint32_t* H) {
@@ -219,27 +222,54 @@ __global__ void __launch_bounds__(64) bls_msm_finish_kernel(const uint32_t* part
                                                             uint32_t* sig_aff, uint32_t* out_jac) {
   __shared__ uint32_t sp[MSM_QUADS / 2][27];
   if (blockIdx.x != 0) return;
+#if CBFT_BLS_PHASES
+  uint64_t ph[5];
+  ph[0] = wall_clock64();
+#endif
   const int qd = threadIdx.x >> 2, q = threadIdx.x & 3;
   g1j acc;
-  g1_set_inf(acc);
+  if (nparts == 1) {  // the row MSM's single partial: no sum (the 16-quad tree cost ~32 us)
+    if (qd != 0) return;
+    g1j_get(acc, partial, 1);
+#if CBFT_BLS_PHASES
+    ph[1] = ph[2] = wall_clock64();
+#endif
+  } else {
+    g1_set_inf(acc);
 #pragma unroll 1
-  for (uint32_t b = qd; b < nparts; b += MSM_QUADS) {
-    g1j o;
-    g1j_get(o, partial + 27 * (size_t)b, 1);
-    g1q_add(acc, acc, o, q);
+    for (uint32_t b = qd; b < nparts; b += MSM_QUADS) {
+      g1j o;
+      g1j_get(o, partial + 27 * (size_t)b, 1);
+      g1q_add(acc, acc, o, q);
+    }
+#if CBFT_BLS_PHASES
+    ph[1] = wall_clock64();
+#endif
+    g1q_block_sum(acc, sp, qd, q);
+#if CBFT_BLS_PHASES
+    ph[2] = wall_clock64();
+#endif
+    if (qd != 0) return;
   }
-  g1q_block_sum(acc, sp, qd, q);
-  if (qd != 0) return;
   if (out_jac) {
     g1j_put(out_jac, 1, acc, q);
     return;
   }
   g1a a;
   g1_to_affine<true>(a, acc);  // the combined signature is public: variable-time inversion
+#if CBFT_BLS_PHASES
+  ph[3] = wall_clock64();
+#endif
   if (q == 0) {
     g1_compress(out33, a);
     if (sig_aff) g1a_store(sig_aff, a);
   }
+#if CBFT_BLS_PHASES
+  ph[4] = wall_clock64();
+  if (threadIdx.x == 0)
+    printf("msm finish (us): partials %.1f block-sum %.1f to-affine %.1f compress %.1f (nparts %u)\n",
+           (ph[1] - ph[0]) * 0.01, (ph[2] - ph[1]) * 0.01, (ph[3] - ph[2]) * 0.01, (ph[4] - ph[3]) * 0.01, nparts);
+#endif
 }
 
 // sigma_i = sk_i * g1_map(msg) as a 37-byte share (BlsThresholdSigner::signData,

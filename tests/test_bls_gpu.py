@@ -37,6 +37,13 @@ def test_share_verification_verdicts(ctx):
     cases.append((17).to_bytes(4, "big") + good[0][4:])         # id > n
     cases.append(good[5][:4] + b"\x05" + good[5][5:])           # bad prefix
     cases.append(good[5][:4] + b"\x02" + B.P.to_bytes(32, "big"))  # x >= p
+    # x^3 + 2 not a square (no point), under both prefixes
+    x = next(x for x in range(1, 100) if pow((x ** 3 + 2) % B.P, (B.P - 1) // 2, B.P) != 1)
+    cases.append(good[6][:4] + b"\x02" + x.to_bytes(32, "big"))
+    cases.append(good[6][:4] + b"\x03" + x.to_bytes(32, "big"))
+    cases.append(good[7][:4] + bytes(33))                          # infinity: e(O, g2) != e(H, vk)
+    cases.append(good[7][:4] + b"\x00" + b"\x01" + bytes(31))     # bad infinity encoding
+    cases.append(good[8][:4] + bytes([good[8][4] ^ 1]) + good[8][5:])  # the other root's prefix
     kid = ctx.bls_load_keys(pk, vks)
     try:
         assert all(ctx.bls_key_status(kid, n))
