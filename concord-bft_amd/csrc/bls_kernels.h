@@ -54,9 +54,13 @@ size_t cbft_bls_g2_sum_tmp_words();
 hipError_t cbft_bls_launch_verify_multisig(const uint32_t* d_parts, uint32_t count, const uint8_t* d_msg, uint32_t len,
                                            const uint8_t* d_sig33, const uint32_t* d_gen_lines, uint8_t* d_pk_ok,
                                            uint8_t* d_result, hipStream_t s);
+// d_H_in (nullable): H = g1_map(msg) already on the device (the kernel does not hash);
+// d_sig_aff (nullable): the signature as the affine point a combine produced (BLS_SIG_WORDS), used
+// instead of decompressing d_sig33 -- the same point, and a combine's output always decodes
 hipError_t cbft_bls_launch_verify(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, const uint8_t* d_sig33,
                                   const uint32_t* d_pk_lines, const uint8_t* d_pk_ok,
-                                  const uint32_t* d_gen_lines, uint8_t* d_result, hipStream_t s);
+                                  const uint32_t* d_gen_lines, uint8_t* d_result, hipStream_t s,
+                                  const uint32_t* d_H_in = nullptr, const uint32_t* d_sig_aff = nullptr);
 hipError_t cbft_bls_launch_sign(const uint8_t* d_msg, uint32_t len, const uint32_t* d_sk, uint32_t id,
                                 uint8_t* d_out37, hipStream_t s);
 // the same signature on row-parallel Fp (bls_msm_row.hip): d_H = g1_map(msg) from

@@ -150,7 +150,8 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
 __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t* msg, uint32_t len, uint32_t* H_out,
                                                                   const uint8_t* sig33, const uint32_t* pk_lines,
                                                                   const uint8_t* pk_ok, const uint32_t* gen_lines,
-                                                                  uint8_t* result) {
+                                                                  uint8_t* result, const uint32_t* H_in,
+                                                                  const uint32_t* sig_aff) {
   __shared__ PairXchg xc[3];  // the values of waves 1, 2, 3
   if (blockIdx.x != 0) return;
   const int wave = threadIdx.x >> 6;
@@ -159,7 +160,10 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
   fp f;
   if (wave < 2) {
     g1a P;
-    g1_map_row(P, msg, len);
+    if (H_in)
+      g1a_load(P, H_in);  // hashed by an earlier kernel of the same call
+    else
+      g1_map_row(P, msg, len);
     BLS_PHASE(wave == 0 ? 4 : 12);
     if (wave == 0 && g.lane == 0 && H_out) g1a_store(H_out, P);
     if (wave == 0)
@@ -169,7 +173,11 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
     BLS_PHASE(wave == 0 ? 5 : 13);
   } else {
     g1a s;
-    const bool ok = g1_decompress_row(s, sig33);
+    bool ok = true;
+    if (sig_aff)
+      g1a_load(s, sig_aff);  // the combine's own point: decompressing its 33 bytes gives it back
+    else
+      ok = g1_decompress_row(s, sig33);
     BLS_PHASE(wave == 2 ? 2 : 14);
     if (ok && !s.inf) {
       g1a P = s;
@@ -368,9 +376,10 @@ hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uin
 }
 hipError_t cbft_bls_launch_verify(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, const uint8_t* d_sig33,
                                   const uint32_t* d_pk_lines, const uint8_t* d_pk_ok,
-                                  const uint32_t* d_gen_lines, uint8_t* d_result, hipStream_t s) {
+                                  const uint32_t* d_gen_lines, uint8_t* d_result, hipStream_t s,
+                                  const uint32_t* d_H_in, const uint32_t* d_sig_aff) {
   hipLaunchKernelGGL(bls_verify_kernel, dim3(1), dim3(VERIFY_BLOCK), 0, s, d_msg, len, d_H, d_sig33, d_pk_lines,
-                     d_pk_ok, d_gen_lines, d_result);
+                     d_pk_ok, d_gen_lines, d_result, d_H_in, d_sig_aff);
   return hipGetLastError();
 }
 hipError_t cbft_bls_launch_verify_multisig(const uint32_t* d_parts, uint32_t count, const uint8_t* d_msg, uint32_t len,

@@ -367,20 +367,24 @@ int cbft_bls_combine_threshold(cbft_ctx* c, uint32_t id, const uint8_t* msg, uin
   CBFT_HIP(c->bls_partial.reserve((size_t)(2 * k + 16) * BLS_JAC_WORDS * 4));  // row MSM levels
   CBFT_HIP(c->bls_out.reserve(BLS_JAC_WORDS * 4));
   CBFT_HIP(c->bls_flag.reserve(1));
+  CBFT_HIP(c->bls_aff.reserve(BLS_SIG_WORDS * 4));
   if (!c->bls_inv.p) {
     CBFT_HIP(c->bls_inv.reserve((size_t)BLS_INV_TABLE * 9 * 4));
     CBFT_HIP(cbft_bls_launch_inv_table(c->bls_inv.as<uint32_t>(), c->stream));
   }
   if (k) CBFT_HIP(hipMemcpyAsync(c->bls_first.p, first.data(), k, hipMemcpyHostToDevice, c->stream));
-  // combine over d_use, then verify the device-resident result: result byte -> bls_flag
+  // combine over d_use, then verify the device-resident result: result byte -> bls_flag.  The verify
+  // takes H from bls_prep (same message, same call) and the combined point in affine form from the
+  // combine's finish kernel: no second hash to G1, no decompression before its Miller loops.
   auto combine_verify = [&]() -> int {
     CBFT_HIP(cbft_bls_launch_combine(c->bls_sig.as<uint32_t>(), c->bls_ids.as<uint32_t>(), c->bls_use.as<uint8_t>(),
                                      k, 0, k, 0, c->bls_inv.as<uint32_t>(), c->bls_lambda.as<uint32_t>(),
-                                     c->bls_partial.as<uint32_t>(), c->bls_out.as<uint8_t>(), nullptr, nullptr,
-                                     c->stream));
+                                     c->bls_partial.as<uint32_t>(), c->bls_out.as<uint8_t>(), c->bls_aff.as<uint32_t>(),
+                                     nullptr, c->stream));
     CBFT_HIP(cbft_bls_launch_verify(c->bls_msg.as<uint8_t>(), len, nullptr, c->bls_out.as<uint8_t>(),
                                     ks->lines.as<uint32_t>(), ks->ok.as<uint8_t>(),
-                                    c->bls_gen_lines.as<uint32_t>(), c->bls_flag.as<uint8_t>(), c->stream));
+                                    c->bls_gen_lines.as<uint32_t>(), c->bls_flag.as<uint8_t>(), c->stream,
+                                    k ? c->bls_H.as<uint32_t>() : nullptr, c->bls_aff.as<uint32_t>()));
     return CBFT_OK;
   };
   std::vector<uint8_t> v(k ? k : 1, 0);

@@ -220,6 +220,7 @@ struct cbft_ctx {
   bool rsa_ev_valid = false;
   DevBuf bls_gen_lines, bls_msg, bls_H, bls_shares, bls_valid, bls_sig, bls_ids, bls_use, bls_lambda,
       bls_partial, bls_out, bls_ms_ok, bls_bitmap, bls_inv, bls_first, bls_flag, bls_g2tmp;
+  DevBuf bls_aff;      // the last combine's signature as an affine point (BLS_SIG_WORDS)
   DevBuf bls_pub_tbl;  // fixed-base comb of g2 for cbft_bls_public_key (built at its first call)
 };
 

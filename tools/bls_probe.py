@@ -35,6 +35,9 @@ assert ctx.bls_verify_multisig(kid, cert.msg, msig, bytes(bitmap))
 sid, sk, share = cert.sign_probe
 assert ctx.bls_sign(sk, sid, cert.msg) == share, "signData differs from the expected share"
 assert ctx.bls_public_key(sk) == cert.vks[sid - 1], "sk * g2 differs from the key set's vk"
+for opt in (False, True):
+    sig_t, ok_t, _ = ctx.bls_combine_threshold(kid, cert.msg, cert.shares, optimistic=opt)
+    assert ok_t and sig_t == cert.expected_sig, "combine_threshold differs"
 out = {}
 for name, fn in (("keyset_load", lambda: ctx.bls_unload_keys(ctx.bls_load_keys(cert.pk, cert.vks))),
                  ("keyset_load_1key", lambda: ctx.bls_unload_keys(ctx.bls_load_keys(cert.pk, []))),
@@ -43,6 +46,8 @@ for name, fn in (("keyset_load", lambda: ctx.bls_unload_keys(ctx.bls_load_keys(c
                  ("verify", lambda: ctx.bls_verify(kid, cert.msg, comb)),
                  ("multisig_combine", lambda: ctx.bls_combine(use, multisig=True)),
                  ("multisig_verify", lambda: ctx.bls_verify_multisig(kid, cert.msg, msig, bytes(bitmap))),
+                 ("certificate_fused", lambda: ctx.bls_combine_threshold(kid, cert.msg, cert.shares, optimistic=False)),
+                 ("certificate_policy", lambda: ctx.bls_combine_threshold(kid, cert.msg, cert.shares, optimistic=True)),
                  ("sign", lambda: ctx.bls_sign(cert.sign_probe[1], cert.sign_probe[0], cert.msg)),
                  ("public_key", lambda: ctx.bls_public_key(cert.sign_probe[1]))):
     ts = []
