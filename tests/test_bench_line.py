@@ -66,5 +66,5 @@ def test_line_tail_order():
     assert keys[0] == "metric"
     assert keys[-1] == "p50_latency_ms_batch1k"
     tail = keys[-8:]
-    for k in ("device_resident_value", "key_table_load_ms", "per_request_path", "bls_config4"):
+    for k in ("pcie_inclusive_value", "key_table_load_ms", "per_request_path", "bls_config4"):
         assert k in tail, (k, tail)

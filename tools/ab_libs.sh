@@ -29,8 +29,8 @@ import json, sys
 label, r = sys.argv[1], sys.argv[2]
 p = json.loads(open(f"gpurun_out/ab/probe_{label}_{r}.json").read().strip().splitlines()[-1])
 b = json.loads(open(f"gpurun_out/ab/bench_{label}_{r}.json").read().strip().splitlines()[-1])
-print(f"{label} r{r}: iso us {p['us']} ok={p['verdicts_ok']} | value {b['value']/1e6:.1f} M/s "
-      f"device {b['device_resident_value']/1e6:.1f} M/s ladder_pipe {b['roofline']['kernel_ms']*1e3:.1f} us "
+print(f"{label} r{r}: iso us {p['us']} ok={p['verdicts_ok']} | value (HBM-resident) {b['value']/1e6:.1f} M/s "
+      f"pcie-incl {b['pcie_inclusive_value']/1e6:.1f} M/s ladder_pipe {b['roofline']['kernel_ms']*1e3:.1f} us "
       f"frac {b['roofline']['frac']:.3f} p50@1K {b.get('p50_latency_ms_batch1k') or 0:.4f} ms", flush=True)
 PY
   done
