@@ -1,5 +1,5 @@
 """Device-resident Ed25519 pipeline for a rocprofv3 kernel trace: 64K x 256 B batches over 4,096
-keys (radix 13), alternating over two streams as bench.py's device_resident_value does, 30 steps
+keys (radix 13), alternating over two streams as bench.py's headline value does, 30 steps
 after 5 warm-up steps; prints the wall-clock rate.  The trace shows how hash, ladder and finish of
 consecutive batches overlap (tools/trace_timeline.py)."""
 import os
