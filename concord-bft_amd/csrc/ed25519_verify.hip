@@ -1479,18 +1479,12 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
 // its entry is requested.
 // ---------------------------------------------------------------------------------------
 #define COMB2_BLOCK 128
-// Entry stages per wave (7 KB of LDS each).  Two keep entries jj+1 and jj+2 in flight under
-// addition jj at 2 waves per SIMD (16 KB per wave with the scalars); one (9 KB per wave) lets 16
-// waves share a CU's 160 KB, so a second batch's ladder can run beside the first.
-#ifndef CBFT_COMB2_SLOTS
-#define CBFT_COMB2_SLOTS 2
-#endif
 #ifndef CBFT_LADDER_MUL2
 #define CBFT_LADDER_MUL2 0
 #endif
 #define COMB2_MAX_STEPS 24  // additions per lane: radix-2^8 keys + radix-2^16 B = 48 positions
 #ifndef CBFT_COMB2_MIN_WAVES
-#define CBFT_COMB2_MIN_WAVES (CBFT_COMB2_SLOTS == 1 ? 4 : 2)
+#define CBFT_COMB2_MIN_WAVES 2
 #endif
 
 __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
@@ -1504,22 +1498,20 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
   const uint32_t na = (uint32_t)cl.a.npos, ntot = na + (uint32_t)cl.b.npos;
   const uint32_t nper = (ntot + 1u) >> 1;
   const uint32_t first = q * nper;
-  __shared__ uint4 stage[COMB2_BLOCK / 64][CBFT_COMB2_SLOTS][7][64];  // per wave: lane-linear 7 KB entry images
-  // One recoded scalar per lane: lane 0 of a pair keeps h + offA, lane 1 S + offB, and a lane that
-  // needs the other scalar's digits reads its partner's column (2 KB per wave instead of 4)
-  __shared__ uint32_t sc[8][COMB2_BLOCK];
+  __shared__ uint4 stage[COMB2_BLOCK / 64][2][7][64];  // per wave: two lane-linear 7 KB entry images
+  __shared__ uint32_t sc[16][COMB2_BLOCK];              // h + offA (words 0..7), S + offB (8..15)
   {
-    uint32_t hs[8];
-    if (q == 0) {
+    uint32_t hs[8], ss[8];
 #pragma unroll
-      for (int k = 0; k < 8; k++) hs[k] = h_soa[k * b.n + i];
-      add256(hs, cl.offA);
-    } else {
-      load_words8(hs, b.sig + i * 64 + 32);
-      add256(hs, cl.offB);
+    for (int k = 0; k < 8; k++) hs[k] = h_soa[k * b.n + i];
+    load_words8(ss, b.sig + i * 64 + 32);
+    add256(hs, cl.offA);
+    add256(ss, cl.offB);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+      sc[k][threadIdx.x] = hs[k];
+      sc[8 + k][threadIdx.x] = ss[k];
     }
-#pragma unroll
-    for (int k = 0; k < 8; k++) sc[k][threadIdx.x] = hs[k];
   }
   // signed digit of this lane's step jj (0 = the identity entry past the last position)
   auto digit = [&](uint32_t jj) -> int {
@@ -1529,9 +1521,9 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
     const uint32_t pos = isA ? k : k - na;
     const uint32_t w = isA ? (uint32_t)cl.a.w : (uint32_t)cl.b.w;
     const uint32_t top = (isA ? (uint32_t)cl.a.npos : (uint32_t)cl.b.npos) - 1u;
-    const uint32_t off = pos * w, wi = off >> 5, col = (threadIdx.x & ~1u) | (isA ? 0u : 1u);
-    const uint32_t lo = sc[wi][col];
-    const uint32_t hi = wi < 7u ? sc[wi + 1u][col] : 0u;  // bits >= 256 read as 0
+    const uint32_t off = pos * w, wi = off >> 5, base = isA ? 0u : 8u;
+    const uint32_t lo = sc[base + wi][threadIdx.x];
+    const uint32_t hi = wi < 7u ? sc[base + wi + 1u][threadIdx.x] : 0u;  // bits >= 256 read as 0
     const uint32_t ch = (uint32_t)((((uint64_t)hi << 32) | lo) >> (off & 31u)) & ((1u << w) - 1u);
     const uint32_t half = 1u << (w - 1u);
     // top digit in [0, 2^(w-1)]; only S >= L (flagged, rejected in K4) can exceed it
@@ -1552,28 +1544,18 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
       __builtin_amdgcn_global_load_lds(e + 4 * c, (__attribute__((address_space(3))) void*)&stage[wv][slot][c][0], 16,
                                        0, 0);
   };
-  __builtin_amdgcn_wave_barrier();  // the pair's scalars (one wave) are in LDS before digit() reads them
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   ge_p3 P;
   ge_p3_0(P);
   int dcur = digit(0), dnext = digit(1);
   request(0, entry(0, dcur));
-#if CBFT_COMB2_SLOTS == 2
   if (nper > 1u) request(1, entry(1, dnext));
-#endif
 #pragma nounroll
   for (uint32_t jj = 0; jj < nper; jj++) {
-#if CBFT_COMB2_SLOTS == 2
     const uint32_t slot = jj & 1u;
     if (jj + 1u < nper)
       asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // entry jj landed; jj + 1 may still fly
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
-    const uint32_t slot = 0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // entry jj landed (the only one in flight)
-#endif
     // The stage is read with asm ds_reads: the compiler would otherwise see LDS reads after
     // global_load_lds writes and wait for ALL of them (vmcnt(0)), serialising the two stages.
     uint32_t ew[28];
@@ -1601,17 +1583,10 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
     }
     const bool neg = dcur < 0;
     dcur = dnext;
-#if CBFT_COMB2_SLOTS == 2
     if (jj + 2u < nper) {
       dnext = digit(jj + 2u);
       request(slot, entry(jj + 2u, dnext));
     }
-#else
-    if (jj + 1u < nper) {
-      dnext = digit(jj + 2u);
-      request(0, entry(jj + 1u, dcur));
-    }
-#endif
 #if CBFT_LADDER_MUL2
     // the same addition with its independent products paired (fe_mul2: two mad chains
     // interleaved per column): (A, B), C, (T, X), (Y, Z)
