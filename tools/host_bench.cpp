@@ -17,6 +17,8 @@
 
 #include <algorithm>
 #include <atomic>
+#include <sys/resource.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -59,7 +61,15 @@ double pct(std::vector<double>& v, double q) {
 struct LegResult {
   double per_s, p50_us, p99_us;
   uint64_t batches, calls, mismatches;
+  double cores_busy;  // process CPU time (user + system) / wall time over the leg
 };
+
+double cpuSeconds() {
+  rusage u{};
+  getrusage(RUSAGE_SELF, &u);
+  return (double)u.ru_utime.tv_sec + 1e-6 * (double)u.ru_utime.tv_usec + (double)u.ru_stime.tv_sec +
+         1e-6 * (double)u.ru_stime.tv_usec;
+}
 
 template <class Fn>
 LegResult runThreads(int T, int calls, const std::vector<Work>& w, Fn fn) {
@@ -83,23 +93,26 @@ LegResult runThreads(int T, int calls, const std::vector<Work>& w, Fn fn) {
       }
     });
   while (ready.load() < T) std::this_thread::yield();
+  const double cpu0 = cpuSeconds();
   const auto t0 = Clock::now();
   go = true;
   for (auto& x : th) x.join();
   const double secs = std::chrono::duration<double>(Clock::now() - t0).count();
+  const double cpu = cpuSeconds() - cpu0;
   std::vector<double> all;
   for (auto& l : lat) all.insert(all.end(), l.begin(), l.end());
   LegResult r{(double)T * calls / secs, pct(all, 0.5), pct(all, 0.99), ed25519EngineStats().batches - b0,
-              (uint64_t)T * calls, bad.load()};
+              (uint64_t)T * calls, bad.load(), cpu / secs};
   return r;
 }
 
 void printLeg(const char* name, const LegResult& r, int threads, bool last = false) {
   std::printf("\"%s\": {\"threads\": %d, \"calls\": %llu, \"verifies_per_s\": %.1f, \"p50_us\": %.1f, "
-              "\"p99_us\": %.1f, \"gpu_batches\": %llu, \"calls_per_batch\": %.2f, \"mismatches\": %llu}%s",
+              "\"p99_us\": %.1f, \"gpu_batches\": %llu, \"calls_per_batch\": %.2f, \"mismatches\": %llu, "
+              "\"cores_busy\": %.2f, \"cpu_us_per_call\": %.2f}%s",
               name, threads, (unsigned long long)r.calls, r.per_s, r.p50_us, r.p99_us, (unsigned long long)r.batches,
-              r.batches ? (double)r.calls / (double)r.batches : 0.0, (unsigned long long)r.mismatches,
-              last ? "" : ", ");
+              r.batches ? (double)r.calls / (double)r.batches : 0.0, (unsigned long long)r.mismatches, r.cores_busy,
+              r.per_s > 0 ? 1e6 * r.cores_busy / r.per_s : 0.0, last ? "" : ", ");
 }
 }  // namespace
 
