@@ -108,3 +108,13 @@ sanitize: $(LIB) $(MIRROR_SRC) $(HOST_SRC)
 	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 -DCONCORD_BFT_TESTING $(HOST_INC) -o $(SAN_DIR)/test_host_$$t tests/cpp/test_host.cpp -L$(SAN_DIR) -lcbft_host_$$t -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -lpthread -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' && \
 	  g++ -O1 -g -fno-omit-frame-pointer -fsanitize=$$s -std=c++17 $(HOST_INC) -o $(SAN_DIR)/test_bls_host_$$t tests/cpp/test_bls_host.cpp -L$(SAN_DIR) -lcbft_host_$$t -Lconcord-bft_amd -lcbft_hipcrypto -lcrypto -lpthread -Wl,-rpath,'$$ORIGIN' -Wl,-rpath,'$$ORIGIN/../../../concord-bft_amd' || exit 1; \
 	done
+
+# Microbenchmarks and probes under tools/microbench (not part of `all`; `make microbench`).
+MB := tools/microbench
+MICROBENCH := $(MB)/intrate $(MB)/intrate2 $(MB)/concurrency $(MB)/rowfp $(MB)/permlane_check $(MB)/pack_probe
+microbench: $(MICROBENCH)
+$(MB)/%: $(MB)/%.hip
+	$(HIPCC) --offload-arch=$(ARCH) -O3 -std=c++17 -I$(CSRC) -Iinclude -o $@ $<
+$(MB)/pack_probe: $(MB)/pack_probe.cpp
+	$(HIPCC) -O2 -std=c++17 -o $@ $< -lpthread
+.PHONY: microbench

@@ -518,15 +518,57 @@ static void be32_scalar_words(uint32_t* w, const uint8_t* sk32) {
            ((uint32_t)sk32[31 - 4 * q - 1] << 8) | sk32[31 - 4 * q];
 }
 
+// sk mod r in place (r = the BN-P254 group order, 8 little-endian words).  The row kernels take
+// k in [1, r): sk * P = (sk mod r) * P for every P of order r, so a key >= r is reduced (at most 6
+// subtractions below 2^256); sk = 0 (mod r) is no key and is refused.  Variable time in the
+// number of subtractions only for keys >= r, which no key generator produces.
+static bool scalar_mod_r(uint32_t* w) {
+  static const uint32_t R[8] = {0x0000000d, 0xa1000000, 0x00000010, 0xff9f8000,
+                                0x00000007, 0xba344d80, 0x40000001, 0x25236482};
+  for (;;) {
+    int q = 7;
+    while (q >= 0 && w[q] == R[q]) q--;
+    if (q >= 0 && w[q] < R[q]) break;  // w < r
+    uint64_t borrow = 0;                // w >= r: w -= r
+    for (int i = 0; i < 8; i++) {
+      const uint64_t d = (uint64_t)w[i] - R[i] - borrow;
+      w[i] = (uint32_t)d;
+      borrow = (d >> 63) & 1;
+    }
+  }
+  uint32_t any = 0;
+  for (int i = 0; i < 8; i++) any |= w[i];
+  return any != 0;
+}
+
 int cbft_bls_public_key(cbft_ctx* c, const uint8_t* sk32, uint8_t* out65) {
   c = cbft_dev0(c);
   if (!c || !sk32 || !out65) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);  // held until the wipe below has run
   uint32_t w[8];
+  // every exit, error paths included (the guard exists before the scalar is read): once the
+  // scalar went to the device, the stream has finished with it and the device copy is cleared;
+  // the host copy is zeroed
+  struct Wipe {
+    cbft_ctx* c;
+    uint32_t* w;
+    bool on_device = false;
+    bool cleared = false;
+    ~Wipe() {
+      if (on_device && !cleared) {
+        (void)hipStreamSynchronize(c->stream);
+        (void)hipMemsetAsync(c->bls_lambda.p, 0, 8 * sizeof(uint32_t), c->stream);
+        (void)hipStreamSynchronize(c->stream);
+      }
+      secure_zero(w, 8 * sizeof(uint32_t));
+    }
+  } wipe{c, w};
   be32_scalar_words(w, sk32);
-  std::lock_guard<std::mutex> g(c->mu);
+  if (!scalar_mod_r(w)) return CBFT_EINVAL;
   CBFT_HIP(hipSetDevice(c->device));
   CBFT_HIP(c->bls_lambda.reserve(8 * 4));
   CBFT_HIP(c->bls_out.reserve(65));
+  wipe.on_device = true;
   CBFT_HIP(hipMemcpyAsync(c->bls_lambda.p, w, sizeof(w), hipMemcpyHostToDevice, c->stream));
   // fixed-base comb of g2 on row-parallel Fp (its 64 x 8 table built once per context, ~10 ms),
   // unless $CBFT_BLS_PUBKEY=lane (the one-lane Montgomery ladder, 17 ms: the A/B reference)
@@ -547,31 +589,28 @@ int cbft_bls_public_key(cbft_ctx* c, const uint8_t* sk32, uint8_t* out65) {
   CBFT_HIP(hipMemcpyAsync(out65, c->bls_out.p, 65, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipMemsetAsync(c->bls_lambda.p, 0, sizeof(w), c->stream));  // the secret scalar leaves the device
   CBFT_HIP(hipStreamSynchronize(c->stream));
-  secure_zero(w, sizeof(w));
+  wipe.cleared = true;
   return CBFT_OK;
 }
 
 int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* msg, uint32_t len, uint8_t* out37) {
   c = cbft_dev0(c);
   if (!c || !sk32 || !out37 || (len && !msg)) return CBFT_EINVAL;
+  std::lock_guard<std::mutex> g(c->mu);  // held until the wipe below has run
   uint32_t w[8];
-  be32_scalar_words(w, sk32);
-  std::lock_guard<std::mutex> g(c->mu);
-  CBFT_HIP(hipSetDevice(c->device));
-  // one H2D: the scalar's words, then the message (bls_msg = [sk words | msg])
   const size_t msg_at = sizeof(w);
-  CBFT_HIP(c->bls_msg.reserve(msg_at + len + 1));
-  CBFT_HIP(c->bls_out.reserve(37));
   std::vector<uint8_t> in(msg_at + len);  // alive (and the scalar in it) until the stream is done
-  // every exit, error paths included: the stream has finished reading `in`, the device copy of
-  // the scalar is cleared, and both host copies are zeroed
+  // every exit, error paths included (the wipe exists before the scalar is read): once the
+  // scalar went to the device, the stream has finished reading `in` and the device copy is
+  // cleared; both host copies are zeroed
   struct Wipe {
     cbft_ctx* c;
     uint32_t* w;
     std::vector<uint8_t>& in;
-    bool cleared = false;  // the success path queued the device clear and synchronised
+    bool on_device = false;  // an H2D of the scalar was queued
+    bool cleared = false;    // the success path queued the device clear and synchronised
     ~Wipe() {
-      if (!cleared) {
+      if (on_device && !cleared) {
         (void)hipStreamSynchronize(c->stream);
         if (c->bls_msg.p) {
           (void)hipMemsetAsync(c->bls_msg.p, 0, 8 * sizeof(uint32_t), c->stream);
@@ -582,8 +621,15 @@ int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* 
       secure_zero(in.data(), in.size() < 32 ? in.size() : 32);
     }
   } wipe{c, w, in};
+  be32_scalar_words(w, sk32);
+  if (!scalar_mod_r(w)) return CBFT_EINVAL;
+  CBFT_HIP(hipSetDevice(c->device));
+  // one H2D: the scalar's words, then the message (bls_msg = [sk words | msg])
+  CBFT_HIP(c->bls_msg.reserve(msg_at + len + 1));
+  CBFT_HIP(c->bls_out.reserve(37));
   std::memcpy(in.data(), w, sizeof(w));
   if (len) std::memcpy(in.data() + msg_at, msg, len);
+  wipe.on_device = true;
   CBFT_HIP(hipMemcpyAsync(c->bls_msg.p, in.data(), in.size(), hipMemcpyHostToDevice, c->stream));
   const uint32_t* d_sk = c->bls_msg.as<uint32_t>();
   const uint8_t* d_msg = c->bls_msg.as<uint8_t>() + msg_at;

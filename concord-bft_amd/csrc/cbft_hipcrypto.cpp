@@ -398,30 +398,22 @@ int cbft_sync(cbft_ctx* c) {
 static int append_keys(cbft_ctx* c, uint32_t id, const uint8_t* pk, uint32_t nkeys, uint32_t* out_first,
                        bool check_budget);
 
-int cbft_ed25519_load_keys_ex(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, int comb_radix, uint32_t* out_id) {
-  if (!c || !out_id || (nkeys && !pk)) return CBFT_EINVAL;
-  if (comb_radix && (comb_radix < 8 || comb_radix > 15)) return CBFT_EINVAL;
-  if (!c->kids.empty()) {  // replicate the table on every device, concurrently (ids stay in step)
-    std::vector<uint32_t> ids(c->kids.size(), 0);
-    const int rc = for_each_kid(c, [&](size_t g) {
-      return cbft_ed25519_load_keys_ex(c->kids[g], pk, nkeys, comb_radix, &ids[g]);
-    });
-    if (rc) return rc;
-    for (uint32_t id : ids)
-      if (id != ids[0]) return CBFT_EIO;
-    *out_id = ids[0];
-    return CBFT_OK;
-  }
+// Load a key table on one device under `id` (a multi-device context's parent picks the id, so
+// every device holds the table under the same id), or under the device's next id when id == 0.
+static int load_keys_on(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, int comb_radix, uint32_t want_id,
+                        uint32_t* out_id) {
   CBFT_HIP(hipSetDevice(c->device));
   auto kt = std::make_shared<KeyTable>();
   kt->geo = cbft_comb_geom(key_radix(comb_radix, nkeys));
   CBFT_HIP(kt->chunk_ptrs.reserve(CBFT_MAX_KEY_CHUNKS * sizeof(void*)));
-  uint32_t id;
+  uint32_t id = want_id;
   {
     std::lock_guard<std::mutex> g(c->mu);
-    id = c->next_table_id++;
-    if (id == CBFT_NO_KEY_TABLE) id = c->next_table_id++;
-    c->tables.emplace(id, kt);
+    if (!id) {
+      id = c->next_table_id++;
+      if (id == CBFT_NO_KEY_TABLE) id = c->next_table_id++;
+    }
+    if (!c->tables.emplace(id, kt).second) return CBFT_EIO;
   }
   if (nkeys) {
     uint32_t first = 0;
@@ -430,6 +422,36 @@ int cbft_ed25519_load_keys_ex(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, in
       (void)cbft_ed25519_unload_keys(c, id);
       return rc;
     }
+  }
+  *out_id = id;
+  return CBFT_OK;
+}
+
+int cbft_ed25519_load_keys_ex(cbft_ctx* c, const uint8_t* pk, uint32_t nkeys, int comb_radix, uint32_t* out_id) {
+  if (!c || !out_id || (nkeys && !pk)) return CBFT_EINVAL;
+  if (comb_radix && (comb_radix < 8 || comb_radix > 15)) return CBFT_EINVAL;
+  if (c->kids.empty()) return load_keys_on(c, pk, nkeys, comb_radix, 0, out_id);
+  // replicate the table on every device, concurrently, under one id the parent allocates; if any
+  // device fails, the devices that loaded it unload it again (no device keeps a table the others
+  // lack, and the ids stay in step for every later load)
+  uint32_t id;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    id = c->next_table_id++;
+    if (id == CBFT_NO_KEY_TABLE) id = c->next_table_id++;
+  }
+  std::vector<int> rcs(c->kids.size(), CBFT_OK);
+  (void)for_each_kid(c, [&](size_t g) {
+    uint32_t got = 0;
+    return rcs[g] = load_keys_on(c->kids[g], pk, nkeys, comb_radix, id, &got);
+  });
+  int rc = CBFT_OK;
+  for (int r : rcs)
+    if (r && !rc) rc = r;
+  if (rc) {
+    for (size_t g = 0; g < c->kids.size(); g++)
+      if (rcs[g] == CBFT_OK) (void)cbft_ed25519_unload_keys(c->kids[g], id);
+    return rc;
   }
   *out_id = id;
   return CBFT_OK;

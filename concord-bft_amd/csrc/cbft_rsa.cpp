@@ -47,19 +47,12 @@ static int rsa_launch_locked(cbft_ctx* c, RsaKeyTable& kt, const uint32_t* d_kid
 
 extern "C" {
 
-int cbft_rsa_load_keys(cbft_ctx* c, const uint8_t* moduli, const uint32_t* exponents, uint32_t nkeys,
-                       uint32_t* out_id) {
-  if (!c || !out_id || (nkeys && (!moduli || !exponents))) return CBFT_EINVAL;
-  if (!c->kids.empty()) {  // every device, concurrently; the ids stay in step
-    std::vector<uint32_t> ids(c->kids.size(), 0);
-    const int rc = for_each_kid(c, [&](size_t g) { return cbft_rsa_load_keys(c->kids[g], moduli, exponents, nkeys, &ids[g]); });
-    if (rc) return rc;
-    for (uint32_t i : ids)
-      if (i != ids[0]) return CBFT_EIO;
-    *out_id = ids[0];
-    return CBFT_OK;
-  }
+// One device's key records under `want_id` (chosen by a multi-device parent, so every device
+// holds the table under the same id) or under the device's next id when want_id == 0.
+static int rsa_load_on(cbft_ctx* c, const uint8_t* moduli, const uint32_t* exponents, uint32_t nkeys,
+                       uint32_t want_id, uint32_t* out_id) {
   std::lock_guard<std::mutex> g(c->mu);
+  if (want_id && c->rsa_tables.count(want_id)) return CBFT_EIO;
   CBFT_HIP(hipSetDevice(c->device));
   RsaKeyTable kt;
   kt.nkeys = nkeys;
@@ -80,8 +73,36 @@ int cbft_rsa_load_keys(cbft_ctx* c, const uint8_t* moduli, const uint32_t* expon
       return cbft_fail(e, "rsa key records", __FILE__, __LINE__);
     }
   }
-  const uint32_t id = c->next_rsa_id++;
+  const uint32_t id = want_id ? want_id : c->next_rsa_id++;
   c->rsa_tables.emplace(id, std::move(kt));
+  *out_id = id;
+  return CBFT_OK;
+}
+
+int cbft_rsa_load_keys(cbft_ctx* c, const uint8_t* moduli, const uint32_t* exponents, uint32_t nkeys,
+                       uint32_t* out_id) {
+  if (!c || !out_id || (nkeys && (!moduli || !exponents))) return CBFT_EINVAL;
+  if (c->kids.empty()) return rsa_load_on(c, moduli, exponents, nkeys, 0, out_id);
+  // every device, concurrently, under one id the parent allocates; a device that failed leaves
+  // no table behind on the others (they unload theirs), so ids stay in step for later loads
+  uint32_t id;
+  {
+    std::lock_guard<std::mutex> g(c->mu);
+    id = c->next_rsa_id++;
+  }
+  std::vector<int> rcs(c->kids.size(), CBFT_OK);
+  (void)for_each_kid(c, [&](size_t g) {
+    uint32_t got = 0;
+    return rcs[g] = rsa_load_on(c->kids[g], moduli, exponents, nkeys, id, &got);
+  });
+  int rc = CBFT_OK;
+  for (int r : rcs)
+    if (r && !rc) rc = r;
+  if (rc) {
+    for (size_t g = 0; g < c->kids.size(); g++)
+      if (rcs[g] == CBFT_OK) (void)cbft_rsa_unload_keys(c->kids[g], id);
+    return rc;
+  }
   *out_id = id;
   return CBFT_OK;
 }

@@ -16,12 +16,19 @@
 //                                        PreProcessor::checkClientBatchMsgCorrectness
 //                                        (PreProcessor.cpp:557-590): every element is validated,
 //                                        the loop does not stop at an invalid one
+//   PreProcessor::checkPreProcessBatchReqMsgCorrectness  PreProcessor.cpp:877-902: the non-primary's
+//                                        pre-execution batch; validateMessage per embedded
+//                                        PreProcessRequestMsg (PreProcessRequestMsg.cpp:80-113, one
+//                                        verifySig each), after PreProcessBatchRequestMsg::validate
+//                                        + checkElements (PreProcessBatchRequestMsg.cpp:44-89);
+//                                        every element is validated, invalid ones are counted
 //   PreProcessResultMsg::validatePreProcessResultSignatures  PreProcessResultMsg.cpp:57-99: f+1
 //                                        replica signatures over SHA3-256(result || result code ||
 //                                        client id || seq num) (PreProcessResultHashCreator.hpp:19-35)
 //
 // Wire structs are packed little-endian restatements of the reference's (ClientMsgs.hpp:23-50,
-// PrePrepareMsg.hpp:33-53, MessageBase.hpp:30-33) in namespace concord::hip::wire (their layout is
+// PrePrepareMsg.hpp:33-53, MessageBase.hpp:30-33, PreProcessRequestMsg.hpp:65-81,
+// PreProcessBatchRequestMsg.hpp:45-55) in namespace concord::hip::wire (their layout is
 // checked against the reference's own structs by tests/test_reference_boundary.py).  Outcomes
 // equal the serial reference loop's: the same request fails first with the same kind of error,
 // and SigManager's counters move for exactly the signatures the serial loop would have verified.
@@ -74,6 +81,37 @@ struct ClientBatchRequestMsgHeader {  // ClientMsgs.hpp:25-31
   uint32_t dataSize;
 };
 
+// preprocessor::PreProcessRequestMsg::Header (PreProcessRequestMsg.hpp:65-81); RequestType is a
+// plain enum (4 B), SeqNum / ViewNum int64_t, NodeIdType uint16_t (PrimitiveTypes.hpp:29-36)
+struct PreProcessRequestMsgHeader {
+  MessageBaseHeader header;  // msgType PreProcessRequest (501)
+  uint32_t reqType;
+  int64_t reqSeqNum;
+  uint16_t clientId;
+  uint16_t reqOffsetInBatch;
+  uint16_t senderId;
+  uint32_t requestLength;
+  uint32_t cidLength;
+  uint32_t spanContextSize;
+  uint64_t reqRetryId;
+  uint16_t reqSignatureLength;
+  uint64_t primaryBlockId;
+  uint32_t result;
+  int64_t viewNum;
+};
+
+// preprocessor::PreProcessBatchRequestMsg::Header (PreProcessBatchRequestMsg.hpp:45-55)
+struct PreProcessBatchRequestMsgHeader {
+  MessageBaseHeader header;  // msgType PreProcessBatchRequest (503)
+  uint32_t reqType;
+  uint16_t clientId;
+  uint16_t senderId;
+  uint32_t cidLength;
+  uint32_t numOfMessagesInBatch;
+  uint32_t requestsSize;
+  int64_t viewNum;
+};
+
 struct PrePrepareMsgHeader {  // PrePrepareMsg.hpp:34-46
   MessageBaseHeader header;
   int64_t viewNum;
@@ -90,6 +128,11 @@ struct PrePrepareMsgHeader {  // PrePrepareMsg.hpp:34-46
 static_assert(sizeof(ClientRequestMsgHeader) == 50, "ClientRequestMsgHeader is 50 B");
 static_assert(sizeof(ClientBatchRequestMsgHeader) == 16, "ClientBatchRequestMsgHeader is 16 B");
 static_assert(sizeof(PrePrepareMsgHeader) == 86, "PrePrepareMsg::Header is 86 B");
+static_assert(sizeof(PreProcessRequestMsgHeader) == 66, "PreProcessRequestMsg::Header is 66 B");
+static_assert(sizeof(PreProcessBatchRequestMsgHeader) == 34, "PreProcessBatchRequestMsg::Header is 34 B");
+
+// MsgCode.hpp:46-51
+enum : uint16_t { kPreProcessRequestMsgType = 501, kPreProcessBatchRequestMsgType = 503 };
 
 // Flag bits (Replica.hpp:44-51, SimpleClient.hpp:43-51)
 enum : uint64_t {
@@ -149,6 +192,53 @@ size_t validatePrePrepareRequests(const char* body, uint64_t size, const Replica
 // returns the per-element outcome.
 RequestValidation validateClientBatchRequestMsg(const char* body, uint64_t size, const ReplicasInfo& repInfo,
                                                 const HipSigManager& sigManager);
+
+// PreProcessBatchRequestMsg::validate (PreProcessBatchRequestMsg.cpp:44-61) with checkElements
+// (:63-89) for the message [body, body + size) received from networkSender: throws
+// std::runtime_error where the reference throws.  The reference reads every element header
+// without a bounds check (checkElements, getPreProcessRequestMsgs:114-147); here an element that
+// does not fit in the message also throws (the reference's behaviour there is undefined).
+void validatePreProcessBatchRequestMsg(const char* body, uint64_t size, PrincipalId networkSender,
+                                       const ReplicasInfo& repInfo, const HipSigManager& sigManager);
+
+// The replica state PreProcessor::checkPreProcessBatchReqMsgCorrectness consults
+// (PreProcessor.cpp:848-873, 877-885): the current view and the three prerequisites of
+// checkPreProcessReqPrerequisites.  None depends on the message.
+struct PreProcessReplicaState {
+  int64_t currentView = 0;
+  bool collectingState = false;
+  bool isCurrentPrimary = false;
+  bool currentViewIsActive = true;
+};
+
+// Per-element outcome of checkPreProcessBatchReqMsgCorrectness.
+enum class PreProcessOutcome : uint8_t {
+  Valid,
+  Ignored,  // checkPreProcessReqPrerequisites failed (metric preProcReqIgnored)
+  Invalid,  // validateMessage failed: PreProcessRequestMsg::validate threw (metric preProcReqInvalid)
+};
+
+struct PreProcessBatchValidation {
+  bool valid = false;         // the function's return value
+  bool viewMismatch = false;  // batch viewNum != current view: rejected before any element
+  std::vector<PreProcessOutcome> outcome;
+  std::vector<std::string> error;  // PreProcessRequestMsg::validate's message for Invalid elements
+  uint32_t ignored = 0;            // preProcReqIgnored increments
+  uint32_t invalid = 0;            // preProcReqInvalid increments
+};
+
+// PreProcessor::checkPreProcessBatchReqMsgCorrectness (PreProcessor.cpp:877-902) for a batch that
+// passed validatePreProcessBatchRequestMsg.  The serial loop rebuilds every element as a
+// PreProcessRequestMsg (sender and client = the batch header's, getPreProcessRequestMsgs) and calls
+// validateMessage → PreProcessRequestMsg::validate (PreProcessRequestMsg.cpp:80-113), i.e.
+// SigManager::verifySig once per signed element, and does not stop at an invalid one.  Here every
+// element's non-cryptographic checks run first, then the signatures of the elements that reach
+// the signature check are verified in ONE SigManager::verifySigBatch; outcomes, metric increments
+// and SigManager's counters equal the serial loop's.
+PreProcessBatchValidation checkPreProcessBatchReqMsgCorrectness(const char* body, uint64_t size,
+                                                                const PreProcessReplicaState& state,
+                                                                const ReplicasInfo& repInfo,
+                                                                const HipSigManager& sigManager);
 
 // PreProcessResultMsg::validatePreProcessResultSignatures (PreProcessResultMsg.cpp:57-99) for the
 // ClientRequestMsg-format message [body, body + size) whose extra data holds the serialized result

@@ -161,7 +161,8 @@ static int engineRadix() {
 // only the requests that went to sleep.  A woken request reads its verdict and returns without
 // touching q_mu_ (with condition variables on the queue mutex, the ~20 requests of a batch woke
 // into a convoy on that mutex: round 3's per-request profile).  A waiter first spins for a few
-// microseconds ($CBFT_ENGINE_SPIN_US, default 20) with yields, then sleeps.
+// microseconds with yields when $CBFT_ENGINE_SPIN_US is set (default 0: it sleeps at once, the fastest
+// setting in profiles/r04_ab/spin0_*.json), then sleeps.
 class Ed25519Engine {
  public:
   static constexpr int kMaxInflight = 4;  // profiles/r03_host_bench_sweep.txt (zero-copy, blocking-sync small batches)

@@ -210,6 +210,119 @@ RequestValidation validateClientBatchRequestMsg(const char* body, uint64_t size,
   return validateClientRequests(reqs, repInfo, sm, false);
 }
 
+namespace {
+
+// One element of a PreProcessBatchRequestMsg: its header and where it starts.
+struct PreProcessElement {
+  PreProcessRequestMsgHeader h;
+  const char* start;
+};
+
+// Walk the elements of a PreProcessBatchRequestMsg (getPreProcessRequestMsgs,
+// PreProcessBatchRequestMsg.cpp:114-147), bounds-checked: each element is its header, span,
+// request, cid and signature.  Throws when an element does not fit in the message.
+std::vector<PreProcessElement> preProcessElements(const char* body, uint64_t size,
+                                                  const PreProcessBatchRequestMsgHeader& bh) {
+  std::vector<PreProcessElement> out;
+  out.reserve(bh.numOfMessagesInBatch);
+  uint64_t pos = sizeof(PreProcessBatchRequestMsgHeader) + (uint64_t)bh.cidLength;
+  for (uint32_t k = 0; k < bh.numOfMessagesInBatch; k++) {
+    if (pos + sizeof(PreProcessRequestMsgHeader) > size)
+      throw std::runtime_error("PreProcessBatchRequestMsg: element header outside the message");
+    PreProcessElement e;
+    std::memcpy(&e.h, body + pos, sizeof e.h);
+    e.start = body + pos;
+    const uint64_t es = sizeof(PreProcessRequestMsgHeader) + (uint64_t)e.h.spanContextSize + e.h.requestLength +
+                        e.h.cidLength + e.h.reqSignatureLength;
+    if (pos + es > size) throw std::runtime_error("PreProcessBatchRequestMsg: element outside the message");
+    out.push_back(e);
+    pos += es;
+  }
+  return out;
+}
+
+}  // namespace
+
+void validatePreProcessBatchRequestMsg(const char* body, uint64_t size, PrincipalId networkSender,
+                                       const ReplicasInfo& repInfo, const HipSigManager& sm) {
+  static const char* kWhat = "void preprocessor::PreProcessBatchRequestMsg::validate(const ReplicasInfo&) const";
+  if (size < sizeof(PreProcessBatchRequestMsgHeader)) throw std::runtime_error(kWhat);
+  PreProcessBatchRequestMsgHeader bh;
+  std::memcpy(&bh, body, sizeof bh);
+  if (size < sizeof(PreProcessBatchRequestMsgHeader) + (uint64_t)bh.requestsSize) throw std::runtime_error(kWhat);
+  if (bh.header.msgType != kPreProcessBatchRequestMsgType) throw std::runtime_error(kWhat);
+  if (networkSender == repInfo.myId()) throw std::runtime_error(kWhat);
+  // checkElements (PreProcessBatchRequestMsg.cpp:63-89)
+  if (!bh.numOfMessagesInBatch || bh.numOfMessagesInBatch > kMaxClientBatchSize) throw std::runtime_error(kWhat);
+  const bool signing = sm.clientSigningEnabled();
+  for (const PreProcessElement& e : preProcessElements(body, size, bh)) {
+    const uint16_t expectedSigLen = signing ? sm.getSigLength(e.h.clientId) : 0;
+    if (expectedSigLen != e.h.reqSignatureLength || size < e.h.requestLength || size < e.h.cidLength)
+      throw std::runtime_error(kWhat);
+  }
+}
+
+PreProcessBatchValidation checkPreProcessBatchReqMsgCorrectness(const char* body, uint64_t size,
+                                                                const PreProcessReplicaState& state,
+                                                                const ReplicasInfo& repInfo,
+                                                                const HipSigManager& sm) {
+  PreProcessBatchValidation out;
+  if (size < sizeof(PreProcessBatchRequestMsgHeader))
+    throw std::runtime_error("PreProcessBatchRequestMsg: shorter than its header");
+  PreProcessBatchRequestMsgHeader bh;
+  std::memcpy(&bh, body, sizeof bh);
+  const std::vector<PreProcessElement> elems = preProcessElements(body, size, bh);  // getPreProcessRequestMsgs
+  if (bh.viewNum != state.currentView) {
+    out.viewMismatch = true;
+    return out;
+  }
+  const size_t n = elems.size();
+  out.outcome.assign(n, PreProcessOutcome::Valid);
+  out.error.assign(n, std::string());
+  // checkPreProcessReqPrerequisites (PreProcessor.cpp:848-873): replica state only
+  const bool prerequisites = !state.collectingState && !state.isCurrentPrimary && state.currentViewIsActive;
+  std::vector<SigBatchItem> items;
+  std::vector<size_t> owner;
+  for (size_t k = 0; k < n; k++) {
+    if (!prerequisites) {
+      out.outcome[k] = PreProcessOutcome::Ignored;
+      out.ignored++;
+      continue;
+    }
+    // PreProcessRequestMsg::validate (PreProcessRequestMsg.cpp:80-113) on the rebuilt message:
+    // its size and type hold by construction; its sender is the batch header's senderId
+    const PreProcessRequestMsgHeader& h = elems[k].h;
+    if (bh.senderId == repInfo.myId()) {
+      out.outcome[k] = PreProcessOutcome::Invalid;
+      out.error[k] = "void preprocessor::PreProcessRequestMsg::validate(const ReplicasInfo&) const";
+      out.invalid++;
+      continue;
+    }
+    if (h.reqSignatureLength == 0) continue;  // no signature: valid
+    if (!sm.clientSigningEnabled())           // a ConcordAssert in the reference
+      throw std::logic_error("PreProcessRequestMsg::validate: signed request with client signing disabled");
+    const char* req = elems[k].start + sizeof(PreProcessRequestMsgHeader) + h.spanContextSize;  // requestBuf()
+    // verifySig(header->clientId, ...): the rebuilt message's clientId is the batch's
+    items.push_back(SigBatchItem{bh.clientId, req, h.requestLength, req + h.requestLength + h.cidLength,
+                                 h.reqSignatureLength});
+    owner.push_back(k);
+  }
+  std::vector<bool> verdict;
+  if (!items.empty()) sm.verifySigBatch(items, verdict, false);  // every element is validated
+  for (size_t j = 0; j < items.size(); j++) {
+    if (verdict[j]) continue;
+    const size_t k = owner[j];
+    const PreProcessRequestMsgHeader& h = elems[k].h;
+    out.outcome[k] = PreProcessOutcome::Invalid;
+    out.error[k] = "Signature verification failed for: clientId: " + std::to_string(bh.clientId) +
+                   ", reqSeqNum: " + std::to_string(h.reqSeqNum) + ", requestLength: " +
+                   std::to_string(h.requestLength) + ", reqSignatureLength: " + std::to_string(h.reqSignatureLength);
+    out.invalid++;
+  }
+  out.valid = out.ignored == 0 && out.invalid == 0;
+  return out;
+}
+
 std::string preProcessResultHash(const char* result, uint32_t len, uint32_t resultCode, uint16_t clientId,
                                  uint64_t reqSeqNum) {
   unsigned char md[32];

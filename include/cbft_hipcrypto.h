@@ -96,7 +96,8 @@ int cbft_host_free(cbft_ctx* ctx, void* p);
  * decode is accepted into the table; every signature under it verifies false. */
 int cbft_ed25519_load_keys(cbft_ctx* ctx, const uint8_t* pk /* nkeys x 32 */, uint32_t nkeys,
                            uint32_t* out_key_table_id);
-/* Same, choosing the radix 2^comb_radix of the per-key fixed-base comb tables (8..13).  0 = the
+/* Same, choosing the radix 2^comb_radix of the per-key fixed-base comb tables (8..15; 14 and 15
+ * only on explicit request: 20.9 / 41.9 MB per key).  0 = the
  * default: $CBFT_COMB_RADIX if set, else the widest of 13 / 11 / 8 whose tables fit
  * $CBFT_COMB_BUDGET_GB (default 64).  Memory per key = npos x (2^(radix-1) + 1) x 128 B:
  * radix 8: 0.53 MB (32 additions per [h]A), 11: 3.0 MB (23), 13: 10.5 MB (20).  The verdicts do

@@ -396,6 +396,157 @@ static int testMessages(SigManager& sm, const ReplicasInfo& ri, std::vector<EdDS
   return 0;
 }
 
+// A PreProcessRequestMsg as PreProcessBatchRequestMsg embeds it: header (PreProcessRequestMsg.hpp:
+// 65-81) | span | request | cid | signature
+static std::string preProcessElement(uint16_t client, int64_t seq, const std::string& span, const std::string& req,
+                                     const std::string& cid, const std::string& sig) {
+  PreProcessRequestMsgHeader h{};
+  h.header.msgType = kPreProcessRequestMsgType;
+  h.header.spanContextSize = (uint32_t)span.size();
+  h.reqSeqNum = seq;
+  h.clientId = client;
+  h.senderId = 1;
+  h.requestLength = (uint32_t)req.size();
+  h.cidLength = (uint32_t)cid.size();
+  h.spanContextSize = (uint32_t)span.size();
+  h.reqSignatureLength = (uint16_t)sig.size();
+  h.result = 1;
+  h.viewNum = 3;
+  return std::string(reinterpret_cast<const char*>(&h), sizeof h) + span + req + cid + sig;
+}
+
+// A PreProcessBatchRequestMsg (PreProcessBatchRequestMsg.hpp:45-55) from replica `sender`
+static std::string preProcessBatch(uint16_t client, uint16_t sender, int64_t view, const std::vector<std::string>& elems) {
+  PreProcessBatchRequestMsgHeader h{};
+  h.header.msgType = kPreProcessBatchRequestMsgType;
+  h.clientId = client;
+  h.senderId = sender;
+  const std::string cid = "pp-batch-cid";
+  h.cidLength = (uint32_t)cid.size();
+  h.numOfMessagesInBatch = (uint32_t)elems.size();
+  std::string body;
+  for (auto& e : elems) body += e;
+  h.requestsSize = (uint32_t)body.size();
+  h.viewNum = view;
+  return std::string(reinterpret_cast<const char*>(&h), sizeof h) + cid + body;
+}
+
+// PreProcessor::checkPreProcessBatchReqMsgCorrectness on a non-primary: the batched walk against
+// the serial loop it replaces (validateMessage → PreProcessRequestMsg::validate → verifySig per
+// element, PreProcessor.cpp:877-902): same per-element outcomes, same metric increments, same
+// SigManager counters.
+template <class SignerOf>
+static int testPreProcessBatch(SigManager& sm, const ReplicasInfo& ri, SignerOf signerOf) {
+  std::mt19937 g(2024);
+  const uint16_t client = 9;
+  const int n = 48;
+  std::vector<std::string> reqs, elems;
+  for (int i = 0; i < n; i++) {
+    std::string p(16 + g() % 700, '\0');
+    for (auto& ch : p) ch = (char)g();
+    reqs.push_back(p);
+    const std::string span = i % 5 == 0 ? std::string(i % 3 + 1, 's') : std::string();
+    elems.push_back(preProcessElement(client, 500 + i, span, p, "cid-" + std::to_string(i), signerOf(client).sign(p)));
+  }
+  PreProcessReplicaState st;
+  st.currentView = 3;
+  // the serial loop, element by element, through SigManager::verifySig
+  auto serial = [&](const std::vector<std::string>& es, std::vector<PreProcessOutcome>& out) {
+    out.clear();
+    for (const std::string& e : es) {
+      PreProcessRequestMsgHeader h;
+      std::memcpy(&h, e.data(), sizeof h);
+      const char* req = e.data() + sizeof h + h.spanContextSize;
+      out.push_back(sm.verifySig(client, req, h.requestLength, req + h.requestLength + h.cidLength,
+                                 h.reqSignatureLength)
+                        ? PreProcessOutcome::Valid
+                        : PreProcessOutcome::Invalid);
+    }
+  };
+  // (1) a valid batch: one signature batch, every element verified
+  {
+    const std::string b = preProcessBatch(client, 1, 3, elems);
+    validatePreProcessBatchRequestMsg(b.data(), b.size(), 1, ri, sm);
+    const auto before = sm.counterValues();
+    PreProcessBatchValidation v = checkPreProcessBatchReqMsgCorrectness(b.data(), b.size(), st, ri, sm);
+    CHECK(v.valid && v.outcome.size() == (size_t)n && v.ignored == 0 && v.invalid == 0);
+    CHECK(sm.counterValues().externalVerified - before.externalVerified == (uint64_t)n);
+  }
+  // (2) bad signatures at elements 3, 17 and 47, a corrupted request at 30: those are Invalid,
+  // the rest Valid, every element verified (the loop does not stop); outcomes and counters equal
+  // the serial loop's
+  {
+    std::vector<std::string> e2 = elems;
+    for (int k : {3, 17, 47}) e2[k][e2[k].size() - 9] ^= 0x40;  // a signature byte
+    e2[30][sizeof(PreProcessRequestMsgHeader) + 2] ^= 1;        // a request byte
+    const std::string b = preProcessBatch(client, 1, 3, e2);
+    validatePreProcessBatchRequestMsg(b.data(), b.size(), 1, ri, sm);
+    auto c0 = sm.counterValues();
+    std::vector<PreProcessOutcome> ref;
+    serial(e2, ref);
+    auto c1 = sm.counterValues();
+    PreProcessBatchValidation v = checkPreProcessBatchReqMsgCorrectness(b.data(), b.size(), st, ri, sm);
+    auto c2 = sm.counterValues();
+    CHECK(!v.valid && v.invalid == 4 && v.ignored == 0);
+    CHECK(v.outcome == ref);
+    for (int k = 0; k < n; k++) CHECK((v.outcome[k] == PreProcessOutcome::Invalid) == (k == 3 || k == 17 || k == 30 || k == 47));
+    CHECK(v.error[17].find("Signature verification failed") != std::string::npos);
+    CHECK(c2.externalVerified - c1.externalVerified == c1.externalVerified - c0.externalVerified);
+    CHECK(c2.externalFailed - c1.externalFailed == c1.externalFailed - c0.externalFailed);
+    CHECK(c2.externalFailed - c1.externalFailed == 4);
+  }
+  // (3) PreProcessBatchRequestMsg::validate / checkElements failures throw, nothing is verified
+  {
+    const auto before = sm.counterValues();
+    auto throws = [&](const std::string& b, uint16_t netSender) {
+      try {
+        validatePreProcessBatchRequestMsg(b.data(), b.size(), netSender, ri, sm);
+      } catch (const std::runtime_error&) {
+        return true;
+      }
+      return false;
+    };
+    std::vector<std::string> e3 = elems;
+    e3[7] = preProcessElement(client, 7, "", reqs[7], "c", std::string(63, 'x'));  // signature length != 64
+    CHECK(throws(preProcessBatch(client, 1, 3, e3), 1));
+    CHECK(throws(preProcessBatch(client, 1, 3, elems), 0));                 // sent by this replica
+    CHECK(throws(preProcessBatch(client, 1, 3, {}), 1));                    // empty batch
+    std::string wrongType = preProcessBatch(client, 1, 3, elems);
+    wrongType[0] = 1;
+    CHECK(throws(wrongType, 1));
+    std::string truncated = preProcessBatch(client, 1, 3, elems);
+    truncated.resize(truncated.size() - 10);
+    CHECK(throws(truncated, 1));
+    std::vector<std::string> unsigned_ = {preProcessElement(client, 1, "", "payload", "c", "")};
+    CHECK(throws(preProcessBatch(client, 1, 3, unsigned_), 1));  // signing on: 64 B expected
+    CHECK(verifiedTotal(sm) == before.externalVerified + before.externalFailed + before.replicaVerified +
+                                   before.replicaFailed);
+  }
+  // (4) the batch's own replica sender is this replica: every element Invalid, none verified;
+  // (5) a view mismatch or an unmet prerequisite: rejected / Ignored, none verified
+  {
+    const uint64_t before = verifiedTotal(sm);
+    const std::string self = preProcessBatch(client, 0, 3, elems);
+    PreProcessBatchValidation v = checkPreProcessBatchReqMsgCorrectness(self.data(), self.size(), st, ri, sm);
+    CHECK(!v.valid && v.invalid == (uint32_t)n);
+    const std::string b = preProcessBatch(client, 1, 4, elems);
+    v = checkPreProcessBatchReqMsgCorrectness(b.data(), b.size(), st, ri, sm);
+    CHECK(!v.valid && v.viewMismatch && v.outcome.empty());
+    PreProcessReplicaState collecting = st;
+    collecting.collectingState = true;
+    const std::string b3 = preProcessBatch(client, 1, 3, elems);
+    v = checkPreProcessBatchReqMsgCorrectness(b3.data(), b3.size(), collecting, ri, sm);
+    CHECK(!v.valid && v.ignored == (uint32_t)n && v.invalid == 0);
+    PreProcessReplicaState primary = st;
+    primary.isCurrentPrimary = true;
+    v = checkPreProcessBatchReqMsgCorrectness(b3.data(), b3.size(), primary, ri, sm);
+    CHECK(v.ignored == (uint32_t)n);
+    CHECK(verifiedTotal(sm) == before);
+  }
+  std::printf("test_host: PreProcessBatchRequestMsg checks batched, outcomes and counters equal the serial loop\n");
+  return 0;
+}
+
 // PreProcessResultMsg::validatePreProcessResultSignatures with f + 1 = 2 replica signatures.
 static int testPreProcessResult(const SigManager& sm, std::vector<EdDSASigner>& signers) {
   const std::string result = "pre-execution result bytes";
@@ -694,6 +845,7 @@ int main() {
   sm.sign(d.data(), d.size(), os, 64);
   CHECK(sm.verifySig(0, d.data(), d.size(), os, 64));
   if (testMessages(sm, ri, signers, signerOf) != 0) return 1;
+  if (testPreProcessBatch(sm, ri, signerOf) != 0) return 1;
   if (testPreProcessResult(sm, signers) != 0) return 1;
   if (testConcurrent() != 0) return 1;
   if (testAggregatorAndKeySlots() != 0) return 1;

@@ -467,6 +467,12 @@ def test_sign_row_ladder_edge_scalars(ctx):
     for i, sk in enumerate(scal):
         m = msgs[i % 3]
         assert ctx.bls_sign(sk, 1 + i, m) == B.sign_share(sk, 1 + i, m), (i, hex(sk))
+    # keys outside [1, r): reduced mod r (sk * H has order r), 0 mod r refused
+    for sk in (B.R + 1, B.R + 2, 2 * B.R - 1, (1 << 256) - 1):
+        assert ctx.bls_sign(sk, 7, b"m") == B.sign_share(sk % B.R, 7, b"m"), hex(sk)
+    for sk in (0, B.R, 2 * B.R):
+        with pytest.raises(cb.CbftError):
+            ctx.bls_sign(sk, 7, b"m")
 
 
 def test_public_key_comb_edge_scalars(ctx):
@@ -480,3 +486,8 @@ def test_public_key_comb_edge_scalars(ctx):
         exp = B.g2_to_bytes(B.ec_mul(sk, B.G2_GEN))
         assert ctx.bls_public_key(sk) == exp, hex(sk)
     assert ctx.bls_public_key(scal[-1]) == B.g2_to_bytes(B.ec_mul(scal[-1], B.G2_GEN))
+    for sk in (B.R + 1, B.R + 16, 5 * B.R + 3, (1 << 256) - 1):
+        assert ctx.bls_public_key(sk) == B.g2_to_bytes(B.ec_mul(sk % B.R, B.G2_GEN)), hex(sk)
+    for sk in (0, B.R, 3 * B.R):
+        with pytest.raises(cb.CbftError):
+            ctx.bls_public_key(sk)

@@ -37,7 +37,8 @@ def _include_flags():
     return ["-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(HOST, "include"),
             "-I" + os.path.join(REF, "util", "include"), "-I" + os.path.join(REF, "bftengine", "src", "bftengine"),
             "-I" + os.path.join(REF, "bftengine", "include", "bftengine"),
-            "-I" + os.path.join(REF, "threshsign", "include"), "-I" + os.path.join(REF, "logging", "include")]
+            "-I" + os.path.join(REF, "threshsign", "include"), "-I" + os.path.join(REF, "logging", "include"),
+            "-I" + os.path.join(REF, "bftengine", "src", "preprocessor", "messages")]
 
 
 @pytest.fixture(scope="module")
