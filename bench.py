@@ -44,6 +44,7 @@ for p in (os.path.join(ROOT, "concord-bft_amd"), os.path.join(ROOT, "tools")):
     sys.path.insert(0, p)
 
 import cbft_hipcrypto as cb  # noqa: E402  (ctypes binding; the library loads at the first Context)
+import gpu_clocks  # noqa: E402  (sclk / mclk through amdsmi, best effort)
 import parity_gate  # noqa: E402  (golden-data verdict gate, run before anything is timed)
 import tree_hash  # noqa: E402  (csrc stamp: PMC records are attached only to the tree they describe)
 import workload  # noqa: E402
@@ -159,6 +160,7 @@ def main():
     numa = _bind_near_gpu(torch, dev.index) if world > 1 else None
     cores, quota = _cpu_cores()
     cpu_threads = args.cpu_threads or cores
+    clocks = gpu_clocks.Clocks(torch, dev.index)
 
     # ---- workload: this rank's static shard (weak scaling), signed by host OpenSSL
     n, L = args.batch, args.msg_len
@@ -260,12 +262,12 @@ def main():
 
     assert np.array_equal(ss.off, np.arange(n, dtype=ss.off.dtype) * L), "config #2 blob is n x L bytes"
 
-    def dstep(j):
+    def dstep(j, table=None):
         s = streams[j % 2]
         if world > 1:
             s.wait_stream(gstream)  # the slot's previous all-gather has read its words
-        ctx.verify_fixed_device(tid, 0, d_kidx.data_ptr(), d_sig.data_ptr(), d_blob.data_ptr(), L, n,
-                                d_verd[j % 2].data_ptr(), s.cuda_stream)
+        ctx.verify_fixed_device(tid if table is None else table, 0, d_kidx.data_ptr(), d_sig.data_ptr(),
+                                d_blob.data_ptr(), L, n, d_verd[j % 2].data_ptr(), s.cuda_stream)
         if world > 1:
             gstream.wait_stream(s)
             with torch.cuda.stream(gstream):
@@ -275,15 +277,73 @@ def main():
         for j in range(steps):
             dstep(j)
 
+    clk_before = clocks.read()
     drun(max(args.warmup, 2))
     elapsed = timed(drun, args.steps)
+    clk_after = clocks.read()
     value = world * n * args.steps / elapsed
-    for j, d in enumerate(d_verd):
-        if not np.array_equal(cb.bitmap_to_bools(d.cpu().numpy().view(np.uint8).tobytes(), n), ss.expected):
-            raise SystemExit(f"rank {rank}: device-path verdicts differ from OpenSSL")
-        if world > 1:
-            mine = d_gath[j].view(world, nwords)[rank]
-            assert torch.equal(mine, d), "all-gather lost this rank's verdict words"
+
+    def check_device(what):
+        for j, d in enumerate(d_verd):
+            if not np.array_equal(cb.bitmap_to_bools(d.cpu().numpy().view(np.uint8).tobytes(), n), ss.expected):
+                raise SystemExit(f"rank {rank}: {what}: device-path verdicts differ from OpenSSL")
+            if world > 1:
+                mine = d_gath[j].view(world, nwords)[rank]
+                assert torch.equal(mine, d), "all-gather lost this rank's verdict words"
+
+    check_device("headline")
+
+    # ---- the spread of the step: the same pipeline again, untimed by the
+    # contract, with an event after each batch on its stream: intervals between consecutive batch
+    # completions (median / min / max), and the GFX clock sampled by amdsmi while it runs
+    def drun_events(steps):
+        evs = []
+        for j in range(steps):
+            dstep(j)
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(streams[j % 2])
+            evs.append(e)
+        torch.cuda.synchronize()
+        return evs
+
+    spread_steps = max(args.steps, 200)
+    evs, clk_load = clocks.sample_during(lambda: drun_events(spread_steps))
+    done = sorted(evs[0].elapsed_time(e) for e in evs)
+    gaps = [b - a for a, b in zip(done, done[1:])]
+    step_spread = {"steps": spread_steps, "median_ms": statistics.median(gaps), "min_ms": min(gaps),
+                   "max_ms": max(gaps), "steady_ms_per_step": (done[-1] - done[0]) / (len(done) - 1),
+                   "first_steps_ms": [round(g, 4) for g in gaps[:5]],
+                   "timed_region_ms_per_step": elapsed / args.steps * 1e3}
+    gpu_clk = {"before_timed": clk_before, "after_timed": clk_after, "under_load": clk_load,
+               "note": clocks.why}
+
+    # ---- the client-count cliff: the key table's comb radix falls from 13 to
+    # 11 past ~5.9K keys and to 8 past ~21K keys per device ($CBFT_COMB_BUDGET_GB = 64, whole
+    # 256-key chunks; include/cbft_hipcrypto.h); the same headline loop at each radix
+    cliff = []
+    if args.extras:
+        budget = float(os.environ.get("CBFT_COMB_BUDGET_GB", "64")) * 1e9
+        for r in sorted({13, 11, 8} - {args.comb_radix} | {args.comb_radix}, reverse=True):
+            per_key = _comb_npos(r) * ((1 << (r - 1)) + 1) * 128
+            row = {"comb_radix": r, "additions_per_verify": _comb_npos(r) + 12,
+                   "table_mb_per_key": round(per_key / 1e6, 3),
+                   "table_gb_per_device_at_nkeys": round(args.nkeys * per_key / 1e9, 2),
+                   "max_keys_in_budget": int(budget // (256 * per_key)) * 256}
+            if r == args.comb_radix:
+                row["value"] = value
+            else:
+                tr = ctx.load_keys(ss.pk, radix=r)
+                try:
+                    def drun_r(steps, tr=tr):
+                        for j in range(steps):
+                            dstep(j, tr)
+
+                    drun_r(max(args.warmup, 2))
+                    row["value"] = world * n * args.steps / timed(drun_r, args.steps)
+                    check_device(f"comb radix {r}")
+                finally:
+                    ctx.unload_keys(tr)
+            cliff.append(row)
 
     # ---- kernel durations inside this same pipeline (per-batch HIP events on the launch streams)
     ctx.set_profiling(True, per_batch=True)
@@ -431,7 +491,9 @@ def main():
             parity["config4_bls"] = bls.pop("parity")
         if rsa:
             parity["rsa_2048_bench_sets"] = {"n": 2 * args.batch, "mismatch": 0}
-        detail = _write_detail({"parity": parity, "roofline": roofline, "mixed_config3": mixed, "bls_config4": bls,
+        detail = _write_detail({"step_spread": step_spread, "gpu_clocks": gpu_clk, "comb_radix_cliff": cliff,
+                                "comb_radix_cliff_fields": "comb radix, M verifies/s, MB per key, max keys in budget",
+                                "parity": parity, "roofline": roofline, "mixed_config3": mixed, "bls_config4": bls,
                                 "rsa_2048": rsa, "per_request_path": per_request, "single_process_multi_gpu": single})
         # the fused small-batch kernel in its default form ($CBFT_SMALL_WAVES: 3 -> small3, 2 -> small)
         small_name = "ed25519_small_kernel" if os.environ.get("CBFT_SMALL_WAVES") == "2" else "ed25519_small3_kernel"
@@ -460,6 +522,11 @@ def main():
             "parity": {"all_exact": True, "blocks": _parity_counts(parity), "detail": detail},
             "pageable_host_value": pageable,
             "single_process_multi_gpu": _brief(single, ("value", "devices", "open", "ms_per_step")),
+            "step_spread_ms": [round(step_spread[k], 4) for k in ("median_ms", "min_ms", "max_ms",
+                                                                   "steady_ms_per_step")],
+            "sclk_mhz": _clk_brief(gpu_clk),
+            "comb_radix_cliff": [[r["comb_radix"], round(r["value"] / 1e6, 1), r["table_mb_per_key"],
+                                  r["max_keys_in_budget"]] for r in cliff],
             "rsa_2048": _rsa_brief(rsa),
             "mixed_config3": _brief(mixed, ("value", "pipelined_pinned_value", "device_resident_value",
                                             "hash_kernel_ms", "hash_pmc", "exact_match", "n")),
@@ -477,6 +544,20 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def _clk_brief(clk: dict):
+    """[sclk before, after the timed region, median / min under load] (MHz) and mclk, or why not."""
+    b, a, ld = clk.get("before_timed"), clk.get("after_timed"), clk.get("under_load")
+    if not (b or a or ld):
+        return clk.get("note")
+    return [b and b["sclk_mhz"], a and a["sclk_mhz"], ld and ld["sclk_mhz_median"], ld and ld["sclk_mhz_min"],
+            (a or b or {}).get("mclk_mhz")]
+
+
+def _comb_npos(radix: int) -> int:
+    """Positions of a radix-2^radix comb over 253-bit scalars (ed25519_verify.h CombGeom)."""
+    return {8: 32, 9: 29, 10: 26, 11: 23, 12: 22, 13: 20, 14: 19, 15: 17}[radix]
 
 
 def _pmc_record(fname: str, kernel: str):

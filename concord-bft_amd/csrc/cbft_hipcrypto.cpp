@@ -740,10 +740,10 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   Ed25519Batch b{n, d_pk, d_kidx, KeyChunks{nullptr, 0}, d_sig, d_msg, d_off, d_len,
                  kt ? kt->nkeys : (uint32_t)n, fixed_len};
   Ed25519Work w{};
-  // a small (latency-bound) batch inverts per signature;
-  // one shared (variable-time) inversion per 2 signatures per lane from 16K: the inversion is now
-  // cheap, so more waves beat more sharing (64K: K = 2 55 us, 4 60, 8 74, 16 103, 32 162 us)
-  w.finish_batch = c->finish_batch ? c->finish_batch : (n >= 16384 ? 2 : 1);
+  // a small (latency-bound) batch inverts per signature; from 16K one inversion per block of
+  // 512 lanes x 2 signatures (the tree finish, K = -2); $CBFT_FINISH_BATCH = K > 0 selects one
+  // shared inversion per K signatures per lane (the round-4 finish: 64K: K = 2 55 us, 4 60, 8 74)
+  w.finish_batch = c->finish_batch ? c->finish_batch : (n >= 16384 ? -2 : 1);
   w.base_table = c->base_table.as<uint32_t>();
   w.h_soa = slot.h.as<uint32_t>();
   w.flags = slot.flags.as<uint8_t>();

@@ -117,7 +117,8 @@ struct Ed25519Work {
   const uint32_t* base_comb;   // comb table of B (key-table mode; the -A combs are in Batch::keys)
   CombLadder comb;             // their geometry
   int comb_lanes;              // lanes per signature of the comb ladder: 4 (quad) or 2 (pair)
-  int finish_batch;            // signatures per lane sharing one inversion in K4 (2/4/8/16; else 1)
+  int finish_batch;            // K4: K > 1 signatures per lane share one inversion (2/4/8/16/32);
+                               // -K: one inversion per 512-lane block, K signatures per lane (1/2/4)
   const uint8_t* aok;          // A decoded OK per signature (per-signature key mode)
   uint32_t* h_soa;             // 8 x n words
   uint8_t* flags;              // n bytes

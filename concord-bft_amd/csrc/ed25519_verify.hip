@@ -725,6 +725,136 @@ __global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519B
   }
 }
 
+// K4'' (tree): the same verdicts with ONE field inversion per block of FINISH_TREE_BLOCK lanes x K
+// signatures.  K4' shares an inversion among the K signatures of one lane, so a 64K batch still runs
+// 32,768 of them (one per lane, 512 waves each waiting on a ~15 K-instruction safegcd chain): 80 % of
+// the finish kernel's instructions and 14 % of the whole verify's.  Here the block shares it:
+//   leaf   l = prod of lane l's K Z's (entries of rejected signatures / Z = 0 count as 1),
+//   up     a product tree over the block's lanes in LDS (heap: root 1, leaves T..2T-1),
+//   root   one lane inverts the root (variable time: R' is public),
+//   down   each node's inverse becomes its children's: 1/L = inv * R, 1/R = inv * L (in place),
+//   lane   1/Z_j from the leaf's inverse and the lane's prefix products, then x = X/Z, y = Y/Z,
+//          encode, compare with R, ballot.
+// Per signature that is ~3.5 M + 2 M + an encode, against one inversion per K signatures: the
+// tree's 2 x log2(T) levels are a short serial chain (one product per level) and the kernel is
+// FINISH_TREE_BLOCK x K = 1,024 signatures per block (64 blocks at 64K).
+#define FINISH_TREE_BLOCK 512
+template <int K>
+__global__ void __launch_bounds__(FINISH_TREE_BLOCK) ed25519_finish_tree_kernel(const Ed25519Batch b,
+                                                                              const uint32_t* xyz_soa,
+                                                                              const uint8_t* flags, const uint8_t* aok,
+                                                                              uint64_t* verdict_words) {
+  constexpr uint32_t T = FINISH_TREE_BLOCK;
+  __shared__ uint32_t node[FE_LIMBS][2 * T];  // [limb][heap node]: lanes touch consecutive nodes
+  const uint32_t t = threadIdx.x;
+  const size_t base = (size_t)blockIdx.x * T * K;
+  fe pre[K];  // pre[j] = Z_0 * .. * Z_j of this lane
+  uint32_t okmask = 0;
+#pragma unroll
+  for (int j = 0; j < K; j++) {
+    const size_t i = base + (size_t)j * T + t;
+    fe Z;
+    fe_1(Z);
+    bool ok = false;
+    if (i < b.n) {
+      fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
+      ok = flags[i] && unit_aok(b, aok, batch_unit(b, i)) && !fe_iszero(Z);
+      if (!ok) fe_1(Z);
+    }
+    okmask |= (ok ? 1u : 0u) << j;
+    if (j == 0)
+      fe_copy(pre[0], Z);
+    else
+      fe_mul<false>(pre[j], pre[j - 1], Z);
+  }
+#pragma unroll
+  for (int k = 0; k < FE_LIMBS; k++) node[k][T + t] = pre[K - 1].v[k];
+  __syncthreads();
+#pragma nounroll
+  for (uint32_t m = T >> 1; m >= 1; m >>= 1) {  // up: node n = node 2n * node 2n+1
+    if (t < m) {
+      const uint32_t n = m + t;
+      fe l, r;
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        l.v[k] = node[k][2 * n];
+        r.v[k] = node[k][2 * n + 1];
+      }
+      fe_mul<false>(l, l, r);
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) node[k][n] = l.v[k];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {  // every leaf is non-zero, so is the root
+    fe r;
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) r.v[k] = node[k][1];
+    fe_invert_var(r, r);
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) node[k][1] = r.v[k];
+  }
+  __syncthreads();
+#pragma nounroll
+  for (uint32_t m = 1; m < T; m <<= 1) {  // down: the inverse of node n gives its children's
+    if (t < m) {
+      const uint32_t n = m + t;
+      fe inv, l, r;
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        inv.v[k] = node[k][n];
+        l.v[k] = node[k][2 * n];
+        r.v[k] = node[k][2 * n + 1];
+      }
+      fe li, ri;
+      fe_mul<false>(li, inv, r);
+      fe_mul<false>(ri, inv, l);
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        node[k][2 * n] = li.v[k];
+        node[k][2 * n + 1] = ri.v[k];
+      }
+    }
+    __syncthreads();
+  }
+  fe inv;  // 1 / pre[K-1]
+#pragma unroll
+  for (int k = 0; k < FE_LIMBS; k++) inv.v[k] = node[k][T + t];
+#pragma unroll
+  for (int j = K - 1; j >= 0; j--) {
+    const size_t i = base + (size_t)j * T + t;
+    const bool ok = (okmask >> j) & 1u;
+    fe zi;
+    if (j > 0)
+      fe_mul<false>(zi, inv, pre[j - 1]);
+    else
+      fe_copy(zi, inv);
+    bool verdict = false;
+    if (ok) {
+      fe Z, X, Y, x, y;
+      if (j > 0) {
+        fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
+        fe_mul<false>(inv, inv, Z);
+      }
+      fe_load_soa(X, xyz_soa, b.n, i);
+      fe_load_soa(Y, xyz_soa + 9 * b.n, b.n, i);
+      fe_mul<false>(x, X, zi);
+      fe_mul<false>(y, Y, zi);
+      uint32_t Rp[8], Rw[8];
+      fe_to_words(Rp, y);
+      Rp[7] ^= fe_isnegative(x) << 31;
+      load_words8(Rw, b.sig + i * 64);
+      uint32_t diff = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) diff |= Rp[k] ^ Rw[k];
+      verdict = diff == 0;
+    }  // (a rejected entry entered the product as 1: inv is already 1 / pre[j-1])
+    const uint64_t ballot = __ballot(verdict);
+    const size_t w0 = base + (size_t)j * T + (t & ~63u);  // this wave's first signature of step j
+    if ((t & 63u) == 0 && w0 < b.n) verdict_words[w0 >> 6] = ballot;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Wide fixed-base combs, four lanes per signature (key-table mode).
 //
@@ -1768,6 +1898,16 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   if (order && (e = hipEventRecord(order->done[1], stream)) != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[2], stream);
   switch (w.finish_batch) {
+#define CBFT_FINISH_TREE_CASE(K)                                                                              \
+  case -K:                                                                                                    \
+    hipLaunchKernelGGL(ed25519_finish_tree_kernel<K>,                                                         \
+                       dim3((unsigned)((b.n + (size_t)FINISH_TREE_BLOCK * K - 1) / ((size_t)FINISH_TREE_BLOCK * K))), \
+                       dim3(FINISH_TREE_BLOCK), 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words);     \
+    break;
+    CBFT_FINISH_TREE_CASE(1)
+    CBFT_FINISH_TREE_CASE(2)
+    CBFT_FINISH_TREE_CASE(4)
+#undef CBFT_FINISH_TREE_CASE
 #define CBFT_FINISH_CASE(K)                                                                                     \
   case K:                                                                                                       \
     hipLaunchKernelGGL(ed25519_finish_batch_kernel<K>, dim3((unsigned)((b.n + 64 * K - 1) / (64 * K))), dim3(64), \
