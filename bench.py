@@ -82,6 +82,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-runs", type=int, default=200)
     ap.add_argument("--inflight", type=int, default=4, help="host-path batches in flight")
+    ap.add_argument("--mixed-streams", type=int, default=4, help="config #3 device-resident streams")
+    ap.add_argument("--streams", type=int, default=2, help="headline (config #2) device-resident streams")
     ap.add_argument("--single-process-devices", default="",
                     help="also time one process over these devices (comma list, repeats allowed: cbft_open_devices); "
                          "with --gpus N > 1 rank 0 does this over all N GPUs (cbft_open_mask) by default")
@@ -255,23 +257,24 @@ def main():
 
     d_sig, d_blob = to_dev(ss.sig.reshape(-1), np.uint8), to_dev(ss.blob, np.uint8)
     d_kidx = to_dev(ss.key_idx.view(np.int32), np.int32)
-    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    nst = max(1, args.streams)
+    streams = [torch.cuda.Stream(device=dev) for _ in range(nst)]
     nwords = (n + 63) // 64
-    d_verd = [torch.zeros(nwords, dtype=torch.int64, device=dev) for _ in range(2)]
-    d_gath = [torch.zeros(world * nwords, dtype=torch.int64, device=dev) for _ in range(2)] if world > 1 else None
+    d_verd = [torch.zeros(nwords, dtype=torch.int64, device=dev) for _ in range(nst)]
+    d_gath = [torch.zeros(world * nwords, dtype=torch.int64, device=dev) for _ in range(nst)] if world > 1 else None
 
     assert np.array_equal(ss.off, np.arange(n, dtype=ss.off.dtype) * L), "config #2 blob is n x L bytes"
 
     def dstep(j, table=None):
-        s = streams[j % 2]
+        s = streams[j % nst]
         if world > 1:
             s.wait_stream(gstream)  # the slot's previous all-gather has read its words
         ctx.verify_fixed_device(tid if table is None else table, 0, d_kidx.data_ptr(), d_sig.data_ptr(),
-                                d_blob.data_ptr(), L, n, d_verd[j % 2].data_ptr(), s.cuda_stream)
+                                d_blob.data_ptr(), L, n, d_verd[j % nst].data_ptr(), s.cuda_stream)
         if world > 1:
             gstream.wait_stream(s)
             with torch.cuda.stream(gstream):
-                dist.all_gather_into_tensor(d_gath[j % 2], d_verd[j % 2])
+                dist.all_gather_into_tensor(d_gath[j % nst], d_verd[j % nst])
 
     def drun(steps):
         for j in range(steps):
@@ -301,7 +304,7 @@ def main():
         for j in range(steps):
             dstep(j)
             e = torch.cuda.Event(enable_timing=True)
-            e.record(streams[j % 2])
+            e.record(streams[j % nst])
             evs.append(e)
         torch.cuda.synchronize()
         return evs
@@ -841,12 +844,16 @@ def _mixed_device_resident(ctx, tid, ss, args):
 
     d_sig, d_blob = to_dev(ss.sig.reshape(-1), np.uint8), to_dev(ss.blob, np.uint8)
     d_off, d_len, d_k = to_dev(ss.off, np.int64), to_dev(ss.len, np.int32), to_dev(ss.key_idx, np.int32)
-    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
-    outs = [torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev) for _ in range(2)]
+    # more streams than the fixed-length headline's two: a batch's long-message tail (up to 33
+    # SHA-512 blocks on one lane) then runs under the next batches' short hashes and ladders
+    # (the library rotates over as many work slots, $CBFT_WORK_SLOTS)
+    ns = max(1, getattr(args, "mixed_streams", 4))
+    streams = [torch.cuda.Stream(device=dev) for _ in range(ns)]
+    outs = [torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev) for _ in range(ns)]
 
     def dstep(j):
         ctx.verify_device(tid, 0, d_k.data_ptr(), d_sig.data_ptr(), d_blob.data_ptr(), d_off.data_ptr(),
-                          d_len.data_ptr(), n, outs[j % 2].data_ptr(), streams[j % 2].cuda_stream)
+                          d_len.data_ptr(), n, outs[j % ns].data_ptr(), streams[j % ns].cuda_stream)
 
     for j in range(4):
         dstep(j)

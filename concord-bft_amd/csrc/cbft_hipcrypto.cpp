@@ -147,6 +147,8 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   if (!c) return CBFT_ENOMEM;
   c->device = device;
   if (const char* e = getenv("CBFT_FINISH_BATCH")) c->finish_batch = atoi(e);
+  if (const char* e = getenv("CBFT_WORK_SLOTS")) c->work_slots = std::max(1, std::min(CBFT_MAX_WORK_SLOTS, atoi(e)));
+  if (const char* e = getenv("CBFT_HASH_ORDER_EARLY")) c->hash_order_early = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER_MIN")) c->stage_order_min = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_SMALL_MAX")) c->small_max = (size_t)atoll(e);
@@ -712,7 +714,7 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   }
   // the fused small-batch kernel keeps everything in registers: no work slot to order against
   const bool small = kt && n <= c->small_max && !c->ladder_lanes;
-  WorkSlot& slot = c->slots[small ? 0 : c->next_slot++ % CBFT_WORK_SLOTS];
+  WorkSlot& slot = c->slots[small ? 0 : c->next_slot++ % (unsigned)c->work_slots];
   if (!small) {
     if (table_id == CBFT_NO_KEY_TABLE) {
       CBFT_HIP(slot.ps_tbl.reserve(n * cbft_ed25519_table_words_per_unit() * sizeof(uint32_t)));
@@ -788,6 +790,7 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     order.ladder = c->stage_order != 3;  // 3: hashes only (two batches' ladders may share the SIMDs)
     order.done[0] = c->stage_done[0];
     order.done[1] = c->stage_done[1];
+    order.hash_early = c->hash_order_early != 0;
   }
   hipEvent_t* evp = nullptr;
   if (c->profiling) evp = c->prof_mode == 2 ? &c->ring[(c->ring_n++ % CBFT_PROF_RING) * 4] : c->ev;

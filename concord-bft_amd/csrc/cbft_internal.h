@@ -100,13 +100,13 @@ struct BlsKeySet {
 };
 
 // Per-batch intermediate state of one in-flight verify (h, S<L flags, R' coordinates, the
-// per-signature key tables).  A context rotates over CBFT_WORK_SLOTS of them so that
-// consecutive device-path batches on different streams overlap (batch i's finish and batch
-// i+1's hash run together, each alone would leave the SIMDs half idle); a slot's `done` event
-// orders its reuse after its previous batch.
-#ifndef CBFT_WORK_SLOTS
-#define CBFT_WORK_SLOTS 2
-#endif
+// per-signature key tables).  A context rotates over work_slots (<= CBFT_MAX_WORK_SLOTS) of them
+// so that consecutive device-path batches on different streams overlap (batch i's finish and
+// batch i+1's hash run together, each alone would leave the SIMDs half idle); a slot's `done`
+// event orders its reuse after its previous batch.  With two streams two slots are enough (each
+// stream's order already serialises its own batches); callers with more streams in flight
+// (config #3's long-message tails) use more ($CBFT_WORK_SLOTS, default 4).
+#define CBFT_MAX_WORK_SLOTS 4
 struct WorkSlot {
   DevBuf h, flags, xyz, ps_tbl, ps_aok;
   DevBuf perm, buckets;  // hash order of a variable-length batch (counting sort by SHA-512 blocks)
@@ -169,7 +169,11 @@ struct cbft_ctx {
   hipStream_t build_stream = nullptr;  // key-table builds (appends), apart from the verify streams
   uint32_t next_table_id = 1;
   // per-batch work buffers
-  WorkSlot slots[CBFT_WORK_SLOTS];
+  WorkSlot slots[CBFT_MAX_WORK_SLOTS];
+  int work_slots = CBFT_MAX_WORK_SLOTS;
+  // the next batch's hash waits for this batch's SHORT-message hash only, not for the long tail
+  // hashing on the slot's aux stream ($CBFT_HASH_ORDER_EARLY, default 1)
+  int hash_order_early = 1;
   unsigned next_slot = 0;
   int finish_batch = 0;  // K4: signatures per lane sharing one inversion ($CBFT_FINISH_BATCH; 0 = by batch size)
   // Stage order across batches (any streams): batch i+1's hash starts after batch i's hash and

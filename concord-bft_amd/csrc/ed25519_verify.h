@@ -170,6 +170,7 @@ struct StageOrder {
   bool wait;
   bool hash;    // order the hashes
   bool ladder;  // order the ladders
+  bool hash_early;  // done[0] after the short-message hash, before the long tail's join
   hipEvent_t done[2];
 };
 hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& w, hipStream_t stream,

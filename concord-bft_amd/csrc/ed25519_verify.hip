@@ -1881,8 +1881,11 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   }
   hipLaunchKernelGGL(ed25519_hash_kernel, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
                      uniform_w, nshort_w, w.h_soa, w.flags);
+  // the next batch's hash may start behind this batch's short hashes while the long tail still
+  // runs on the aux stream (hash_early), or only after the whole hash stage
+  if (order && order->hash_early && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;
   if (nshort_w && (e = hipStreamWaitEvent(stream, w.join_ev, 0)) != hipSuccess) return e;
-  if (order && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;
+  if (order && !order->hash_early && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;
   if (order && order->wait && order->ladder && (e = hipStreamWaitEvent(stream, order->done[1], 0)) != hipSuccess)
     return e;
   if (ev) (void)hipEventRecord(ev[1], stream);

@@ -295,6 +295,48 @@ def test_device_path_two_streams_stage_order(monkeypatch, order):
         hip.close()
 
 
+@pytest.mark.parametrize("streams,slots,early", [(4, 4, "1"), (4, 4, "0"), (3, 2, "1"), (2, 4, "1")])
+def test_device_path_mixed_lengths_many_streams(monkeypatch, streams, slots, early):
+    # config #3's device-resident schedule: variable-length batches (sorted hash, long-message
+    # tail on the slot's aux stream) over several streams and work slots; with
+    # CBFT_HASH_ORDER_EARLY the next batch's hash waits only for this batch's short hashes.  Every
+    # batch keeps its own verdicts (different corruption per batch, a slot reused while the
+    # previous tail may still run).
+    monkeypatch.setenv("CBFT_WORK_SLOTS", str(slots))
+    monkeypatch.setenv("CBFT_HASH_ORDER_EARLY", early)
+    hip = _Hip()
+    n = 16384
+    nwords = (n + 63) // 64
+    base = sigsets.make_sigset(n, nkeys=256, msg_len=(64, 4096), seed=31, invalid_frac=0.05)
+    variants = []
+    for v in range(3):
+        sig = base.sig.copy()
+        bad = np.arange(v, n, 61 + 7 * v)
+        sig[bad, 40 + v] ^= 0x10
+        exp = base.expected.copy()
+        exp[bad] = False
+        variants.append((hip.to_dev(sig.reshape(-1)), exp))
+    try:
+        with cb.Context(device=0, max_batch=n) as c:
+            tid = c.load_keys(base.pk)
+            d_kidx = hip.to_dev(base.key_idx)
+            d_blob = hip.to_dev(base.blob)
+            d_off = hip.to_dev(base.off)
+            d_len = hip.to_dev(base.len)
+            ss = [hip.stream() for _ in range(streams)]
+            nb = 9
+            outs = [hip.to_dev(np.zeros(nwords, dtype=np.uint64)) for _ in range(nb)]
+            for b in range(nb):
+                c.verify_device(tid, 0, d_kidx, variants[b % 3][0], d_blob, d_off, d_len, n, outs[b], ss[b % streams])
+            hip.sync()
+            for b in range(nb):
+                got = _bools(hip.from_dev(outs[b], nwords * 8), n)
+                assert np.array_equal(got, variants[b % 3][1]), f"batch {b}"
+            c.unload_keys(tid)
+    finally:
+        hip.close()
+
+
 def test_per_batch_profiling_ring(golden):
     # cbft_set_profiling(ctx, 2): each verify keeps its own stage events; the average covers
     # exactly the batches since enabling, and verdicts are unchanged by the instrumentation

@@ -13,6 +13,7 @@ import workload  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--steps", type=int, default=40)
+ap.add_argument("--mixed-streams", type=int, default=4)
 args = ap.parse_args()
 import torch  # noqa: E402  (initialised first, as bench.py does)
 
@@ -21,4 +22,6 @@ ss = workload.make_sigset(65536, nkeys=4096, msg_len=(64, 4096), seed=0xBADC0DE,
 with cb.Context(device=0) as ctx:
     tid = ctx.load_keys(ss.pk)
     value, hash_ms = bench._mixed_device_resident(ctx, tid, ss, args)
-print(json.dumps({"device_resident_value": value, "hash_ms": hash_ms}))
+print(json.dumps({"device_resident_value": value, "hash_ms": hash_ms, "streams": args.mixed_streams,
+                  "work_slots": os.environ.get("CBFT_WORK_SLOTS", "default"),
+                  "hash_order_early": os.environ.get("CBFT_HASH_ORDER_EARLY", "default")}))
