@@ -396,7 +396,7 @@ def main():
     # multiplication (9 x 29-bit limbs, fe25519.h); the pair / quad combines are parallelisation
     # overhead and not counted.  Bound: the MAD64 pipe (half the INT32 issue rate).
     npos = {8: 32, 9: 29, 10: 26, 11: 23, 12: 22, 13: 20, 14: 19, 15: 17}[args.comb_radix] + \
-        {16: 16, 17: 15, 18: 15, 19: 14, 20: 13, 21: 13, 22: 12}[b_radix]
+        {16: 16, 17: 15, 18: 15, 19: 14, 20: 13, 21: 13, 22: 12, 23: 11, 24: 11, 25: 11, 26: 10}[b_radix]
     mads_per_unit = npos * 7 * 90
     achieved = mads_per_unit * n / (ladder_ms * 1e-3)
     h2d_bytes = 4 + 64 + L  # key index + R||S + message, per signature (fixed-length batch)

@@ -192,7 +192,7 @@ struct cbft_ctx {
   int sha_long = 1;             // their long messages on a second stream ($CBFT_SHA_LONG, 0 = off)
   int blocking_sync = 1;  // small batches' waiters sleep ($CBFT_BLOCKING_SYNC)
   int zero_copy = 1;  // fused small batches read pinned inputs and write verdicts in place ($CBFT_ZERO_COPY)
-  int b_radix = CBFT_COMB_B_RADIX;  // radix of B's comb table ($CBFT_B_RADIX, 16..22)
+  int b_radix = CBFT_COMB_B_RADIX;  // radix of B's comb table ($CBFT_B_RADIX, 16..26)
   int ladder_lanes = 0;             // comb ladder lanes per signature ($CBFT_LADDER_LANES 2 | 4; 0 = by batch)
   hipEvent_t stage_done[2] = {nullptr, nullptr};  // last hash, last ladder
   bool stage_used = false;

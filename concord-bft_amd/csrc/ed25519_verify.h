@@ -63,7 +63,7 @@ struct Ed25519Batch {
 // Messages longer than this verify false (SHA-512's 64 + len byte count must not wrap 32 bits).
 #define CBFT_MAX_MSG_LEN 0xFFFFFF00u
 
-// Geometry of a fixed-base comb table with signed radix-2^w digits (8 <= w <= 22):
+// Geometry of a fixed-base comb table with signed radix-2^w digits (8 <= w <= 26):
 // npos positions of entries() = 2^(w-1) + 1 affine niels points (e * 2^(w j) * P, e = 0 ..
 // 2^(w-1)), 32 words each.  npos is the least count whose top digit stays <= 2^(w-1) for every
 // scalar < L (tests/test_comb_recode.py).
@@ -75,8 +75,9 @@ struct CombGeom {
   __host__ __device__ size_t words_per_unit() const { return (size_t)npos * entries() * 32; }
 };
 inline int cbft_comb_npos(int w) {
-  static const int kPos[23] = {0, 0, 0, 0, 0, 0, 0, 0, 32, 29, 26, 23, 22, 20, 19, 17, 16, 15, 15, 14, 13, 13, 12};
-  return (w >= 8 && w <= 22) ? kPos[w] : 0;
+  static const int kPos[27] = {0,  0,  0,  0,  0,  0,  0,  0,  32, 29, 26, 23, 22, 20,
+                               19, 17, 16, 15, 15, 14, 13, 13, 12, 11, 11, 11, 10};
+  return (w >= 8 && w <= 26) ? kPos[w] : 0;
 }
 inline CombGeom cbft_comb_geom(int w) { return CombGeom{w, cbft_comb_npos(w)}; }
 
@@ -106,9 +107,11 @@ inline CombLadder cbft_comb_ladder(int wa, int wb) {
 // B's table: radix 2^22 by default (12 positions x 2,097,153 entries, 3.2 GB per context of the
 // 288 GB HBM), so a verify against a radix-2^13 key table is 20 + 12 = 32 additions: 16 per lane
 // of a pair, 8 per lane of a quad (radix 2^16: 16 positions, 67 MB, 36 additions; measured on
-// MI355X at 64K: pair ladder 104 us at 2^22 vs 112 us at 2^16).  $CBFT_B_RADIX selects 16..22.
+// MI355X at 64K: pair ladder 104 us at 2^22 vs 112 us at 2^16).  $CBFT_B_RADIX selects 16..26:
+// radix 2^26 is 10 positions (42.9 GB per context), so radix-2^13 keys + B = 30 additions, 15 per
+// lane of a pair.
 #define CBFT_COMB_B_RADIX 22
-#define CBFT_COMB_MAX_RADIX 22
+#define CBFT_COMB_MAX_RADIX 26
 
 // Device work buffers of one verify launch.
 struct Ed25519Work {

@@ -1141,7 +1141,7 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
   // thread index within the BLOCK-thread group the caller's sdig / stage belong to (a caller may
   // hand each wave of a bigger block its own arrays with BLOCK = 64)
   const uint32_t tid = threadIdx.x & (BLOCK - 1);
-  // Digits of this lane's additions (signed, up to +-2^21), kept in LDS ([step][thread]:
+  // Digits of this lane's additions (signed, up to +-2^25), kept in LDS ([step][thread]:
   // conflict-free) so the addition loop holds no digit registers.
   {
     uint32_t hs[8], ss[8];
@@ -1274,7 +1274,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
   size_t i = g >> 2;
   const bool live = i < b.n;
   if (!live) i = b.n - 1;  // tail quads compute a copy (all lanes stay active for the DPP)
-  // Digits of this lane's additions (signed, up to +-2^21), kept in LDS ([step][thread]:
+  // Digits of this lane's additions (signed, up to +-2^25), kept in LDS ([step][thread]:
   // conflict-free) so the addition loop holds no digit registers.
   __shared__ int32_t sdig[COMB_MAX_STEPS * CBFT_VERIFY_BLOCK];
   // Table entries are staged through LDS with global_load_lds (no VGPR destination): entry

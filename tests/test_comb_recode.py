@@ -11,8 +11,8 @@ import pytest
 
 L = 2**252 + 27742317777372353535851937790883648493
 NPOS = {8: 32, 9: 29, 10: 26, 11: 23, 12: 22, 13: 20, 14: 19, 15: 17, 16: 16, 17: 15, 18: 15, 19: 14, 20: 13,
-        21: 13, 22: 12}
-B_RADICES = (16, 22)  # B's table: CBFT_COMB_B_RADIX (22) and the $CBFT_B_RADIX=16 alternative
+        21: 13, 22: 12, 23: 11, 24: 11, 25: 11, 26: 10}
+B_RADICES = (16, 22, 24, 26)  # B's table: CBFT_COMB_B_RADIX (22) and $CBFT_B_RADIX alternatives
 
 
 def offset(w, npos):
@@ -49,7 +49,7 @@ def test_recode_sums_and_ranges(w):
         assert sum(d << (w * j) for j, d in enumerate(ds)) == s
         assert all(-half <= d <= half - 1 for d in ds[:-1])
         assert 0 <= ds[-1] <= half
-        assert -(1 << 21) <= min(ds) and max(ds) <= 1 << 21  # the ladder's digit storage (int32 LDS)
+        assert -(1 << 25) <= min(ds) and max(ds) <= 1 << 25  # the ladders' digits (int32 in LDS / registers)
 
 
 @pytest.mark.parametrize("w", sorted(NPOS))

@@ -69,11 +69,12 @@ def test_golden_key_table_radix(ctx, golden, radix):
         ctx.unload_keys(tid)
 
 
-@pytest.mark.parametrize("b_radix", [16, 17, 20])
+@pytest.mark.parametrize("b_radix", [16, 17, 20, 24, 26])
 @pytest.mark.parametrize("radix", [8, 13])
 def test_golden_base_table_radix(golden, monkeypatch, b_radix, radix):
     """B's comb radix ($CBFT_B_RADIX; the default 22 is covered above): the ladder's lane split
-    changes with it (radix-2^13 keys: 9 additions per lane at B radix 16, 9 at 17, 9 at 20, 8 at 22)."""
+    changes with it (radix-2^13 keys: 9 additions per lane at B radix 16, 9 at 17, 9 at 20, 8 at 22,
+    8 at 24, 8 at 26; radix 26 is a 42.9 GB table of 10 positions)."""
     monkeypatch.setenv("CBFT_B_RADIX", str(b_radix))
     keys = sorted({v.pk for v in golden})
     index = {k: i for i, k in enumerate(keys)}
@@ -84,6 +85,18 @@ def test_golden_base_table_radix(golden, monkeypatch, b_radix, radix):
                               [v.msg for v in golden]), n)
     exp = np.array([bool(v.verdict) for v in golden])
     assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
+
+
+@pytest.mark.parametrize("b_radix", [24, 26])
+def test_pair_ladder_wide_base_table(monkeypatch, b_radix):
+    """The pair ladder (batches from 32K) over B radix 2^24 / 2^26: 31 / 30 additions dealt to two
+    lanes (16 / 15 each), 10 % invalid signatures, verdicts equal to OpenSSL's."""
+    monkeypatch.setenv("CBFT_B_RADIX", str(b_radix))
+    ss = sigsets.make_sigset(40000, nkeys=64, msg_len=256, seed=0xB26 + b_radix, invalid_frac=0.1)
+    with cb.Context(device=0, max_batch=40000) as c:
+        tid = c.load_keys(ss.pk, radix=13)
+        got = _bools(c.verify_packed(tid, ss.key_idx, ss.sig, ss.blob, ss.off, ss.len), 40000)
+    assert np.array_equal(got, ss.expected), np.nonzero(got != ss.expected)[0][:10]
 
 
 def test_load_keys_bad_radix(ctx):
