@@ -149,6 +149,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   if (const char* e = getenv("CBFT_FINISH_BATCH")) c->finish_batch = atoi(e);
   if (const char* e = getenv("CBFT_WORK_SLOTS")) c->work_slots = std::max(1, std::min(CBFT_MAX_WORK_SLOTS, atoi(e)));
   if (const char* e = getenv("CBFT_HASH_ORDER_EARLY")) c->hash_order_early = atoi(e);
+  if (const char* e = getenv("CBFT_FINISH_TREE_BLOCK")) c->finish_tree_block = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER_MIN")) c->stage_order_min = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_SMALL_MAX")) c->small_max = (size_t)atoll(e);
@@ -746,6 +747,7 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   // 512 lanes x 2 signatures (the tree finish, K = -2); $CBFT_FINISH_BATCH = K > 0 selects one
   // shared inversion per K signatures per lane (the round-4 finish: 64K: K = 2 55 us, 4 60, 8 74)
   w.finish_batch = c->finish_batch ? c->finish_batch : (n >= 16384 ? -2 : 1);
+  w.finish_tree_block = c->finish_tree_block;
   w.base_table = c->base_table.as<uint32_t>();
   w.h_soa = slot.h.as<uint32_t>();
   w.flags = slot.flags.as<uint8_t>();

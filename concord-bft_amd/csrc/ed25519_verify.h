@@ -121,7 +121,8 @@ struct Ed25519Work {
   CombLadder comb;             // their geometry
   int comb_lanes;              // lanes per signature of the comb ladder: 4 (quad) or 2 (pair)
   int finish_batch;            // K4: K > 1 signatures per lane share one inversion (2/4/8/16/32);
-                               // -K: one inversion per 512-lane block, K signatures per lane (1/2/4)
+                               // -K: one inversion per block of finish_tree_block lanes, K per lane (1/2/4)
+  int finish_tree_block;       // 64 / 128 (default) / 256 / 512
   const uint8_t* aok;          // A decoded OK per signature (per-signature key mode)
   uint32_t* h_soa;             // 8 x n words
   uint8_t* flags;              // n bytes

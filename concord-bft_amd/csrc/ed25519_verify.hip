@@ -738,13 +738,15 @@ __global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519B
 // Per signature that is ~3.5 M + 2 M + an encode, against one inversion per K signatures: the
 // tree's 2 x log2(T) levels are a short serial chain (one product per level) and the kernel is
 // FINISH_TREE_BLOCK x K = 1,024 signatures per block (64 blocks at 64K).
-#define FINISH_TREE_BLOCK 512
-template <int K>
-__global__ void __launch_bounds__(FINISH_TREE_BLOCK) ed25519_finish_tree_kernel(const Ed25519Batch b,
-                                                                              const uint32_t* xyz_soa,
-                                                                              const uint8_t* flags, const uint8_t* aok,
-                                                                              uint64_t* verdict_words) {
-  constexpr uint32_t T = FINISH_TREE_BLOCK;
+//
+// Block size T: the tree's LDS is 72 T bytes.  It co-runs with the other stream's pair ladder,
+// whose 1,024 blocks of 36 KB exactly fill a 64K batch's LDS (4 per CU): a 512-lane tree block
+// (37 KB) on a CU pushes one ladder block into a second round (measured: ladder 113 -> 131 us in
+// the pipeline, 450 -> 422 M verifies/s), a 128-lane one (9 KB) fits beside four.
+template <int K, int T>
+__global__ void __launch_bounds__(T) ed25519_finish_tree_kernel(const Ed25519Batch b, const uint32_t* xyz_soa,
+                                                                const uint8_t* flags, const uint8_t* aok,
+                                                                uint64_t* verdict_words) {
   __shared__ uint32_t node[FE_LIMBS][2 * T];  // [limb][heap node]: lanes touch consecutive nodes
   const uint32_t t = threadIdx.x;
   const size_t base = (size_t)blockIdx.x * T * K;
@@ -1901,16 +1903,25 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   if (order && (e = hipEventRecord(order->done[1], stream)) != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[2], stream);
   switch (w.finish_batch) {
-#define CBFT_FINISH_TREE_CASE(K)                                                                              \
-  case -K:                                                                                                    \
-    hipLaunchKernelGGL(ed25519_finish_tree_kernel<K>,                                                         \
-                       dim3((unsigned)((b.n + (size_t)FINISH_TREE_BLOCK * K - 1) / ((size_t)FINISH_TREE_BLOCK * K))), \
-                       dim3(FINISH_TREE_BLOCK), 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words);     \
+#define CBFT_FINISH_TREE_LAUNCH(K, T)                                                                         \
+  hipLaunchKernelGGL((ed25519_finish_tree_kernel<K, T>), dim3((unsigned)((b.n + (size_t)(T) * K - 1) / ((size_t)(T) * K))), \
+                     dim3(T), 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words)
+#define CBFT_FINISH_TREE_CASE(K)                                       \
+  case -K:                                                             \
+    if (w.finish_tree_block == 512)                                    \
+      CBFT_FINISH_TREE_LAUNCH(K, 512);                                 \
+    else if (w.finish_tree_block == 256)                               \
+      CBFT_FINISH_TREE_LAUNCH(K, 256);                                 \
+    else if (w.finish_tree_block == 64)                                \
+      CBFT_FINISH_TREE_LAUNCH(K, 64);                                  \
+    else                                                               \
+      CBFT_FINISH_TREE_LAUNCH(K, 128);                                 \
     break;
     CBFT_FINISH_TREE_CASE(1)
     CBFT_FINISH_TREE_CASE(2)
     CBFT_FINISH_TREE_CASE(4)
 #undef CBFT_FINISH_TREE_CASE
+#undef CBFT_FINISH_TREE_LAUNCH
 #define CBFT_FINISH_CASE(K)                                                                                     \
   case K:                                                                                                       \
     hipLaunchKernelGGL(ed25519_finish_batch_kernel<K>, dim3((unsigned)((b.n + 64 * K - 1) / (64 * K))), dim3(64), \

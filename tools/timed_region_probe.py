@@ -1,0 +1,92 @@
+"""Where the contract's timed region spends its time (config #2 headline loop, inputs in HBM).
+
+bench.py times K steps between synchronizes; the same loop with an event after each batch shows a
+steadier per-step rate than the timed region's K-step average.  This probe repeats the timed region
+(K steps, host wall clock) and, in the same region, records a start event on the first stream and
+one event after each batch, so the region splits into: host enqueue time, start gap (host t0 ->
+first batch start is not observable; the start event is enqueued first), fill (start -> first
+completion), steady intervals and the tail after the last completion.  One JSON line per (K, rep).
+
+    python tools/timed_region_probe.py [--steps 20 200] [--reps 3] [--streams 2]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "concord-bft_amd"))
+import cbft_hipcrypto as cb  # noqa: E402
+import workload  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--steps", type=int, nargs="+", default=[20, 200])
+ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--streams", type=int, default=2)
+ap.add_argument("--warmup", type=int, default=5)
+ap.add_argument("--events", type=int, default=1, help="record per-batch events inside the region")
+args = ap.parse_args()
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+torch.cuda.set_device(0)
+dev = torch.device("cuda", 0)
+n, L = 65536, 256
+ss = workload.make_sigset(n, nkeys=4096, msg_len=L, seed=0xC0FFEE, threads=16)
+ctx = cb.Context(device=0, max_batch=n)
+tid = ctx.load_keys(ss.pk, radix=13)
+
+
+def to_dev(a, dtype):
+    return torch.from_numpy(np.ascontiguousarray(a).view(dtype)).to(dev)
+
+
+d_sig, d_blob = to_dev(ss.sig.reshape(-1), np.uint8), to_dev(ss.blob, np.uint8)
+d_kidx = to_dev(ss.key_idx.view(np.int32), np.int32)
+streams = [torch.cuda.Stream(device=dev) for _ in range(args.streams)]
+d_verd = [torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev) for _ in range(args.streams)]
+
+
+def dstep(j):
+    s = streams[j % args.streams]
+    ctx.verify_fixed_device(tid, 0, d_kidx.data_ptr(), d_sig.data_ptr(), d_blob.data_ptr(), L, n,
+                            d_verd[j % args.streams].data_ptr(), s.cuda_stream)
+
+
+for j in range(max(args.warmup, 2)):
+    dstep(j)
+torch.cuda.synchronize()
+for k in args.steps:
+    for rep in range(args.reps):
+        for j in range(max(args.warmup, 2)):
+            dstep(j)
+        torch.cuda.synchronize()
+        start = torch.cuda.Event(enable_timing=True)
+        evs = []
+        t0 = time.perf_counter()
+        start.record(streams[0])
+        for j in range(k):
+            dstep(j)
+            if args.events:
+                e = torch.cuda.Event(enable_timing=True)
+                e.record(streams[j % args.streams])
+                evs.append(e)
+        t_enq = time.perf_counter()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        rec = {"steps": k, "rep": rep, "host_ms_per_step": (t1 - t0) * 1e3 / k,
+               "enqueue_ms_per_step": (t_enq - t0) * 1e3 / k}
+        if evs:
+            done = sorted(start.elapsed_time(e) for e in evs)
+            gaps = [b - a for a, b in zip(done, done[1:])]
+            rec.update({"gpu_span_ms": done[-1], "first_done_ms": done[0],
+                        "steady_ms_per_step": (done[-1] - done[0]) / max(1, k - 1),
+                        "median_gap_ms": statistics.median(gaps) if gaps else None,
+                        "host_minus_gpu_ms": (t1 - t0) * 1e3 - done[-1]})
+        print(json.dumps({key: (round(v, 4) if isinstance(v, float) else v) for key, v in rec.items()}), flush=True)
+got = cb.bitmap_to_bools(d_verd[0].cpu().numpy().view(np.uint8).tobytes(), n)
+assert np.array_equal(got, ss.expected), "verdicts differ from OpenSSL"
+ctx.close()
