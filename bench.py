@@ -163,6 +163,7 @@ def main():
     cores, quota = _cpu_cores()
     cpu_threads = args.cpu_threads or cores
     clocks = gpu_clocks.Clocks(torch, dev.index)
+    clk_before = clocks.read()  # here, not between the warm-up and the timed region (no idle gap there)
 
     # ---- workload: this rank's static shard (weak scaling), signed by host OpenSSL
     n, L = args.batch, args.msg_len
@@ -280,7 +281,6 @@ def main():
         for j in range(steps):
             dstep(j)
 
-    clk_before = clocks.read()
     drun(max(args.warmup, 2))
     elapsed = timed(drun, args.steps)
     clk_after = clocks.read()
@@ -317,7 +317,7 @@ def main():
                    "max_ms": max(gaps), "steady_ms_per_step": (done[-1] - done[0]) / (len(done) - 1),
                    "first_steps_ms": [round(g, 4) for g in gaps[:5]],
                    "timed_region_ms_per_step": elapsed / args.steps * 1e3}
-    gpu_clk = {"before_timed": clk_before, "after_timed": clk_after, "under_load": clk_load,
+    gpu_clk = {"at_start": clk_before, "after_timed": clk_after, "under_load": clk_load,
                "note": clocks.why}
 
     # ---- the client-count cliff: the key table's comb radix falls from 13 to
@@ -550,8 +550,9 @@ def main():
 
 
 def _clk_brief(clk: dict):
-    """[sclk before, after the timed region, median / min under load] (MHz) and mclk, or why not."""
-    b, a, ld = clk.get("before_timed"), clk.get("after_timed"), clk.get("under_load")
+    """[sclk at the start of the run, after the timed region, median / min under load] (MHz) and mclk,
+    or why not."""
+    b, a, ld = clk.get("at_start"), clk.get("after_timed"), clk.get("under_load")
     if not (b or a or ld):
         return clk.get("note")
     return [b and b["sclk_mhz"], a and a["sclk_mhz"], ld and ld["sclk_mhz_median"], ld and ld["sclk_mhz_min"],
