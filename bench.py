@@ -820,7 +820,7 @@ def bench_mixed(ctx, args, cpu_threads):
         dres, hash_ms = _mixed_device_resident(ctx, tid, ss, args)
     finally:
         ctx.unload_keys(tid)
-    hk, hstat = _pmc_record("pmc_ed25519_mixed.json", "ed25519_hash_kernel")
+    hk, hstat = _pmc_record("pmc_ed25519_mixed.json", "ed25519_hash_kernel<0>")
     return {"config": f"config #3: {n} sigs, 4096 keys, msg 64-4096 B log-uniform, 10% invalid",
             "device_resident_value": dres, "hash_kernel_ms": hash_ms, "hash_pmc": _pmc_brief(hk, hstat),
             "value": n / (ms * 1e-3), "unit": "verifies/s (pageable host buffers, blocking call, PCIe included)",

@@ -150,6 +150,9 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   if (const char* e = getenv("CBFT_WORK_SLOTS")) c->work_slots = std::max(1, std::min(CBFT_MAX_WORK_SLOTS, atoi(e)));
   if (const char* e = getenv("CBFT_HASH_ORDER_EARLY")) c->hash_order_early = atoi(e);
   if (const char* e = getenv("CBFT_FINISH_TREE_BLOCK")) c->finish_tree_block = atoi(e);
+  if (const char* e = getenv("CBFT_SHA_LONG_GROUPS")) c->long_groups = std::max(0, std::min(1024, atoi(e)));
+  if (const char* e = getenv("CBFT_HASH_PRIO")) c->hash_prio = atoi(e);
+  if (const char* e = getenv("CBFT_HASH_LONG_PRIO")) c->long_prio = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER_MIN")) c->stage_order_min = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_SMALL_MAX")) c->small_max = (size_t)atoll(e);
@@ -748,6 +751,9 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   // shared inversion per K signatures per lane (the round-4 finish: 64K: K = 2 55 us, 4 60, 8 74)
   w.finish_batch = c->finish_batch ? c->finish_batch : (n >= 16384 ? -2 : 1);
   w.finish_tree_block = c->finish_tree_block;
+  w.long_groups = c->long_groups;
+  w.hash_prio = c->hash_prio;
+  w.long_prio = c->long_prio;
   w.base_table = c->base_table.as<uint32_t>();
   w.h_soa = slot.h.as<uint32_t>();
   w.flags = slot.flags.as<uint8_t>();

@@ -174,7 +174,10 @@ struct cbft_ctx {
   // the next batch's hash waits for this batch's SHORT-message hash only, not for the long tail
   // hashing on the slot's aux stream ($CBFT_HASH_ORDER_EARLY, default 1)
   int hash_order_early = 1;
-  int finish_tree_block = 128;  // lanes per tree-finish block ($CBFT_FINISH_TREE_BLOCK: 64/128/256/512)
+  int finish_tree_block = 128;
+  int long_groups = 0;  // $CBFT_SHA_LONG_GROUPS (0 = CBFT_SHA_LONG_GROUPS)
+  int hash_prio = 0;    // $CBFT_HASH_PRIO
+  int long_prio = 0;    // $CBFT_HASH_LONG_PRIO  // lanes per tree-finish block ($CBFT_FINISH_TREE_BLOCK: 64/128/256/512)
   unsigned next_slot = 0;
   int finish_batch = 0;  // K4: signatures per lane sharing one inversion ($CBFT_FINISH_BATCH; 0 = by batch size)
   // Stage order across batches (any streams): batch i+1's hash starts after batch i's hash and

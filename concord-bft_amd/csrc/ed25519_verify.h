@@ -138,6 +138,9 @@ struct Ed25519Work {
   // the rounds (ed25519_hash_long_kernel); null aux = off.
   hipStream_t aux;
   hipEvent_t fork_ev, join_ev;
+  int long_groups;  // cap of the long-message kernel's 64-signature groups (0 = CBFT_SHA_LONG_GROUPS)
+  int hash_prio;    // K1 waves at raised issue priority (s_setprio 2)
+  int long_prio;    // the long-message kernel's waves at s_setprio 3
 };
 // Block-count buckets of the hash sort: bucket min(nblocks, CBFT_SHA_BUCKETS - 1).
 #define CBFT_SHA_BUCKETS 256

@@ -387,7 +387,8 @@ __global__ void __launch_bounds__(256) ed25519_bucket_count_kernel(const Ed25519
   if (hist[threadIdx.x]) atomicAdd(&counts[threadIdx.x], hist[threadIdx.x]);
 }
 
-__global__ void __launch_bounds__(256) ed25519_bucket_scan_kernel(uint32_t* counts, uint32_t* cursors) {
+__global__ void __launch_bounds__(256) ed25519_bucket_scan_kernel(uint32_t* counts, uint32_t* cursors,
+                                                                  uint32_t long_groups) {
   __shared__ uint32_t v[CBFT_SHA_BUCKETS];
   const uint32_t t = threadIdx.x;
   v[t] = counts[t];
@@ -404,10 +405,10 @@ __global__ void __launch_bounds__(256) ed25519_bucket_scan_kernel(uint32_t* coun
   if (t == 0) cursors[CBFT_SHA_BUCKETS] = 0;
   // n_short: signatures below CBFT_SHA_LONG_BLOCKS blocks (the long ones follow them in the order;
   // with one bucket for all, 0 or n, which the identity order also satisfies), but at most
-  // CBFT_SHA_LONG_GROUPS x 64 positions for the long kernel: its blocks (83 KB of LDS each) must
+  // long_groups (CBFT_SHA_LONG_GROUPS by default) x 64 positions for the long kernel: its blocks (83 KB of LDS each) must
   // all be resident at once, or its last groups would run a second full chain after the others
   if (t == CBFT_SHA_LONG_BLOCKS) {
-    const uint32_t n = v[CBFT_SHA_BUCKETS - 1], cap = 64u * CBFT_SHA_LONG_GROUPS;
+    const uint32_t n = v[CBFT_SHA_BUCKETS - 1], cap = 64u * long_groups;
     const uint32_t ns = v[t] - c;
     cursors[CBFT_SHA_BUCKETS + 1] = n - ns > cap ? n - cap : ns;
   }
@@ -434,10 +435,14 @@ __global__ void __launch_bounds__(256) ed25519_bucket_scatter_kernel(const Ed255
 }
 
 // perm: the block-count order (nullable); uniform: its flag word (perm unused when set);
-// nshort (nullable): positions from *nshort on are ed25519_hash_long_kernel's
+// nshort (nullable): positions from *nshort on are ed25519_hash_long_kernel's.
+// PRIO > 0: the waves raise their issue priority (s_setprio) over the kernels they share SIMDs with
+// (the other batch's ladder): the hash stage is on each batch's dependency chain.
+template <int PRIO>
 __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const Ed25519Batch b, const uint32_t* perm,
                                                                           const uint32_t* uniform, const uint32_t* nshort,
                                                                           uint32_t* h_soa, uint8_t* flags) {
+  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= b.n || (nshort && g >= *nshort)) return;
   const size_t i = perm && !*uniform ? (size_t)perm[g] : g;
@@ -457,10 +462,12 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const E
 // lane).  Runs on a second stream beside ed25519_hash_kernel (which skips these positions); one
 // barrier per block, the same count in both waves (the group's most blocks).
 #define HASH_LONG_BLOCK 128
+template <int PRIO>
 __global__ void __launch_bounds__(HASH_LONG_BLOCK) ed25519_hash_long_kernel(const Ed25519Batch b, const uint32_t* perm,
                                                                             const uint32_t* uniform,
                                                                             const uint32_t* nshort, uint32_t* h_soa,
                                                                             uint8_t* flags) {
+  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   __shared__ uint64_t kwl[2][64 * KW_STRIDE];
   const size_t g0 = (size_t)*nshort + (size_t)blockIdx.x * 64;
   if (g0 >= b.n) return;  // the whole block
@@ -1618,6 +1625,10 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
 #ifndef CBFT_COMB2_MIN_WAVES
 #define CBFT_COMB2_MIN_WAVES 2
 #endif
+// CBFT_LADDER_FIRST_SET: each lane's first comb addition (from the identity) is a point set, 1 M
+#ifndef CBFT_LADDER_FIRST_SET
+#define CBFT_LADDER_FIRST_SET 1
+#endif
 
 __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
     ed25519_comb2_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* btbl,
@@ -1752,6 +1763,29 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
     }
   }
 #else
+    if (CBFT_LADDER_FIRST_SET && jj == 0) {
+      // The lane's first addition starts from the identity: O + (x, y) needs no product but T.
+      // With E = (y+x) - (y-x) = 2x and H = (y+x) + (y-x) = 2y (swapped for a negative digit,
+      // giving -x), P = (2E : 2H : 4 : E H) = (x : y : 1 : xy) scaled by 4 (XY = ZT holds):
+      // 1 M instead of the addition's 7 M.  The identity entry (1, 1, 0) gives (0 : 4 : 4 : 0).
+      fe ypx, ymx, E, H;
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        ypx.v[k] = neg ? ew[9 + k] : ew[k];
+        ymx.v[k] = neg ? ew[k] : ew[9 + k];
+      }
+      fe_sub(E, ypx, ymx);  // reduced
+      fe_add(H, ypx, ymx);
+      fe_carry(H);
+      fe_mul(P.T, E, H);
+      fe_add(P.X, E, E);
+      fe_carry(P.X);
+      fe_add(P.Y, H, H);
+      fe_carry(P.Y);
+      fe_0(P.Z);
+      P.Z.v[0] = 4;
+      continue;
+    }
     ge_p1p1 t;
     {
       // niels (y+x, y-x, 2dxy), negated by swapping y+x <-> y-x and C <-> -C (ge_add_mem)
@@ -1869,7 +1903,8 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   if (sorted) {
     const dim3 g256((unsigned)((b.n + 255) / 256)), b256(256);
     hipLaunchKernelGGL(ed25519_bucket_count_kernel, g256, b256, 0, stream, b, w.buckets);
-    hipLaunchKernelGGL(ed25519_bucket_scan_kernel, dim3(1), b256, 0, stream, w.buckets, w.buckets + CBFT_SHA_BUCKETS);
+    hipLaunchKernelGGL(ed25519_bucket_scan_kernel, dim3(1), b256, 0, stream, w.buckets, w.buckets + CBFT_SHA_BUCKETS,
+                       (uint32_t)(w.long_groups > 0 ? w.long_groups : CBFT_SHA_LONG_GROUPS));
     hipLaunchKernelGGL(ed25519_bucket_scatter_kernel, g256, b256, 0, stream, b, w.buckets + CBFT_SHA_BUCKETS, w.perm);
   }
   const uint32_t* uniform_w = sorted ? (const uint32_t*)(w.buckets + 2 * CBFT_SHA_BUCKETS) : nullptr;
@@ -1877,12 +1912,20 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   if (nshort_w) {  // the long messages on the second stream, beside the short ones
     if ((e = hipEventRecord(w.fork_ev, stream)) != hipSuccess || (e = hipStreamWaitEvent(w.aux, w.fork_ev, 0)) != hipSuccess)
       return e;
-    hipLaunchKernelGGL(ed25519_hash_long_kernel, dim3((unsigned)((b.n + 63) / 64)), dim3(HASH_LONG_BLOCK), 0, w.aux, b,
-                       (const uint32_t*)w.perm, uniform_w, nshort_w, w.h_soa, w.flags);
+    if (w.long_prio)
+      hipLaunchKernelGGL(ed25519_hash_long_kernel<3>, dim3((unsigned)((b.n + 63) / 64)), dim3(HASH_LONG_BLOCK), 0, w.aux, b,
+                         (const uint32_t*)w.perm, uniform_w, nshort_w, w.h_soa, w.flags);
+    else
+      hipLaunchKernelGGL(ed25519_hash_long_kernel<0>, dim3((unsigned)((b.n + 63) / 64)), dim3(HASH_LONG_BLOCK), 0, w.aux, b,
+                         (const uint32_t*)w.perm, uniform_w, nshort_w, w.h_soa, w.flags);
     if ((e = hipEventRecord(w.join_ev, w.aux)) != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(ed25519_hash_kernel, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
-                     uniform_w, nshort_w, w.h_soa, w.flags);
+  if (w.hash_prio)
+    hipLaunchKernelGGL(ed25519_hash_kernel<2>, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
+                       uniform_w, nshort_w, w.h_soa, w.flags);
+  else
+    hipLaunchKernelGGL(ed25519_hash_kernel<0>, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
+                       uniform_w, nshort_w, w.h_soa, w.flags);
   // the next batch's hash may start behind this batch's short hashes while the long tail still
   // runs on the aux stream (hash_early), or only after the whole hash stage
   if (order && order->hash_early && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;

@@ -373,6 +373,23 @@ def test_per_batch_profiling_ring(golden):
         assert lib.cbft_set_profiling(c.handle, 3) == -22
 
 
+@pytest.mark.parametrize("radix,b_radix", [(8, 22), (11, 22), (13, 16), (13, 22), (15, 22), (14, 24)])
+def test_pair_ladder_golden_geometries(golden, monkeypatch, radix, b_radix):
+    """The pair ladder over the golden set at several key / B comb geometries: each lane's first
+    addition is a point set from the identity (CBFT_LADDER_FIRST_SET), whichever table (a key
+    position or B) and digit sign (including the identity entry of a zero digit) it starts on."""
+    monkeypatch.setenv("CBFT_LADDER_LANES", "2")
+    monkeypatch.setenv("CBFT_B_RADIX", str(b_radix))
+    keys = sorted({v.pk for v in golden})
+    index = {k: i for i, k in enumerate(keys)}
+    with cb.Context(device=0) as c:
+        tid = c.load_keys(keys, radix=radix)
+        got = _bools(c.verify(tid, [index[v.pk] for v in golden], [v.sig for v in golden],
+                              [v.msg for v in golden]), len(golden))
+    exp = np.array([bool(v.verdict) for v in golden])
+    assert np.array_equal(got, exp), np.nonzero(got != exp)[0][:10]
+
+
 @pytest.mark.parametrize("lanes", ["2", "4"])
 def test_ladder_layouts_both_sizes(golden, monkeypatch, lanes):
     """Each comb-ladder layout ($CBFT_LADDER_LANES) at the sizes the default does not pick it for:
