@@ -1629,6 +1629,10 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
 #ifndef CBFT_LADDER_FIRST_SET
 #define CBFT_LADDER_FIRST_SET 1
 #endif
+// CBFT_LADDER_PHASED: both lanes of a pair walk the key positions, then B's (uniform table per step)
+#ifndef CBFT_LADDER_PHASED
+#define CBFT_LADDER_PHASED 1
+#endif
 
 __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
     ed25519_comb2_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* btbl,
@@ -1638,9 +1642,19 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
   size_t i = g >> 1;
   const bool live = i < b.n;
   if (!live) i = b.n - 1;  // tail pairs compute a copy (both lanes stay active for the DPP)
-  const uint32_t na = (uint32_t)cl.a.npos, ntot = na + (uint32_t)cl.b.npos;
+  const uint32_t na = (uint32_t)cl.a.npos, nb = (uint32_t)cl.b.npos;
+#if CBFT_LADDER_PHASED
+  // Phased split: each lane takes half of the key positions, then half of B's, so at every step
+  // both lanes of every pair read the same table (the step's table, radix and scalar are
+  // wave-uniform: scalar branches, no per-lane selects).  ceil(na/2) + ceil(nb/2) steps: the same
+  // 16 as ceil(32/2) at the default 20 + 12 positions.
+  const uint32_t naper = (na + 1u) >> 1, nbper = (nb + 1u) >> 1;
+  const uint32_t nper = naper + nbper;
+#else
+  const uint32_t ntot = na + nb;
   const uint32_t nper = (ntot + 1u) >> 1;
   const uint32_t first = q * nper;
+#endif
   __shared__ uint4 stage[COMB2_BLOCK / 64][2][7][64];  // per wave: two lane-linear 7 KB entry images
   __shared__ uint32_t sc[16][COMB2_BLOCK];              // h + offA (words 0..7), S + offB (8..15)
   {
@@ -1656,6 +1670,38 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
       sc[8 + k][threadIdx.x] = ss[k];
     }
   }
+  // chunk of w bits at bit offset `off` of the recoded scalar in sc[base..base+7]
+  auto chunk = [&](uint32_t base, uint32_t off, uint32_t w) -> uint32_t {
+    const uint32_t wi = off >> 5;
+    const uint32_t lo = sc[base + wi][threadIdx.x];
+    const uint32_t hi = wi < 7u ? sc[base + wi + 1u][threadIdx.x] : 0u;  // bits >= 256 read as 0
+    return (uint32_t)((((uint64_t)hi << 32) | lo) >> (off & 31u)) & ((1u << w) - 1u);
+  };
+#if CBFT_LADDER_PHASED
+  // signed digit of this lane's step jj (0 = the identity entry past the last position)
+  auto digit = [&](uint32_t jj) -> int {
+    if (jj >= nper) return 0;
+    const bool isA = jj < naper;  // uniform
+    const uint32_t pos = isA ? q * naper + jj : q * nbper + (jj - naper);
+    const uint32_t np = isA ? na : nb;
+    if (pos >= np) return 0;
+    const uint32_t w = isA ? (uint32_t)cl.a.w : (uint32_t)cl.b.w;
+    const uint32_t ch = chunk(isA ? 0u : 8u, pos * w, w);
+    const uint32_t half = 1u << (w - 1u);
+    // top digit in [0, 2^(w-1)]; only S >= L (flagged, rejected in K4) can exceed it
+    return pos == np - 1u ? (int)(ch < half ? ch : half) : (int)ch - (int)half;
+  };
+  const uint32_t* akey = b.keys.comb(batch_unit(b, i));
+  auto entry = [&](uint32_t jj, int d) {
+    const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+    if (jj < naper) {
+      const uint32_t pos = q * naper + jj;
+      return akey + ((size_t)(pos < na ? pos : 0u) * cl.a.entries() + ad) * COMB_STRIDE;
+    }
+    const uint32_t pos = jj < nper ? q * nbper + (jj - naper) : 0u;
+    return btbl + ((size_t)(pos < nb ? pos : 0u) * cl.b.entries() + ad) * COMB_STRIDE;
+  };
+#else
   // signed digit of this lane's step jj (0 = the identity entry past the last position)
   auto digit = [&](uint32_t jj) -> int {
     const uint32_t k = first + jj;
@@ -1664,10 +1710,7 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
     const uint32_t pos = isA ? k : k - na;
     const uint32_t w = isA ? (uint32_t)cl.a.w : (uint32_t)cl.b.w;
     const uint32_t top = (isA ? (uint32_t)cl.a.npos : (uint32_t)cl.b.npos) - 1u;
-    const uint32_t off = pos * w, wi = off >> 5, base = isA ? 0u : 8u;
-    const uint32_t lo = sc[base + wi][threadIdx.x];
-    const uint32_t hi = wi < 7u ? sc[base + wi + 1u][threadIdx.x] : 0u;  // bits >= 256 read as 0
-    const uint32_t ch = (uint32_t)((((uint64_t)hi << 32) | lo) >> (off & 31u)) & ((1u << w) - 1u);
+    const uint32_t ch = chunk(isA ? 0u : 8u, pos * w, w);
     const uint32_t half = 1u << (w - 1u);
     // top digit in [0, 2^(w-1)]; only S >= L (flagged, rejected in K4) can exceed it
     return pos == top ? (int)(ch < half ? ch : half) : (int)ch - (int)half;
@@ -1680,6 +1723,7 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
     const uint32_t pos = k < ntot ? k - na : 0u;
     return btbl + ((size_t)pos * cl.b.entries() + ad) * COMB_STRIDE;
   };
+#endif
   const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
   auto request = [&](uint32_t slot, const uint32_t* e) {
 #pragma unroll
