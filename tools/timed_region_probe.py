@@ -18,6 +18,7 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "concord-bft_amd"))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import cbft_hipcrypto as cb  # noqa: E402
 import workload  # noqa: E402
 
@@ -27,6 +28,7 @@ ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--streams", type=int, default=2)
 ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--events", type=int, default=1, help="record per-batch events inside the region")
+ap.add_argument("--ramp", type=int, default=0, help="after 2 s idle, N steps with events: mean step per 20-step window")
 args = ap.parse_args()
 
 import numpy as np  # noqa: E402
@@ -87,6 +89,27 @@ for k in args.steps:
                         "median_gap_ms": statistics.median(gaps) if gaps else None,
                         "host_minus_gpu_ms": (t1 - t0) * 1e3 - done[-1]})
         print(json.dumps({key: (round(v, 4) if isinstance(v, float) else v) for key, v in rec.items()}), flush=True)
+if args.ramp:
+    import gpu_clocks
+
+    clk = gpu_clocks.Clocks(torch, 0)
+    for idle in (2.0, 0.2, 0.02):
+        time.sleep(idle)
+        c0 = clk.read()
+        start = torch.cuda.Event(enable_timing=True)
+        evs = []
+        start.record(streams[0])
+        for j in range(args.ramp):
+            dstep(j)
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(streams[j % args.streams])
+            evs.append(e)
+        torch.cuda.synchronize()
+        c1 = clk.read()
+        done = sorted(start.elapsed_time(e) for e in evs)
+        win = [round((done[min(len(done) - 1, k + 20)] - done[k]) / 20, 4) for k in range(0, len(done) - 20, 20)]
+        print(json.dumps({"ramp_after_idle_s": idle, "first_done_ms": round(done[0], 4), "window20_ms_per_step": win,
+                          "sclk_before": c0 and c0["sclk_mhz"], "sclk_after": c1 and c1["sclk_mhz"]}), flush=True)
 got = cb.bitmap_to_bools(d_verd[0].cpu().numpy().view(np.uint8).tobytes(), n)
 assert np.array_equal(got, ss.expected), "verdicts differ from OpenSSL"
 ctx.close()
