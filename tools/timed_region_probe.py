@@ -90,12 +90,35 @@ for k in args.steps:
                         "host_minus_gpu_ms": (t1 - t0) * 1e3 - done[-1]})
         print(json.dumps({key: (round(v, 4) if isinstance(v, float) else v) for key, v in rec.items()}), flush=True)
 if args.ramp:
-    import gpu_clocks
+    import threading
 
-    clk = gpu_clocks.Clocks(torch, 0)
-    for idle in (2.0, 0.2, 0.02):
+    import amdsmi
+
+    amdsmi.amdsmi_init()
+    h = amdsmi.amdsmi_get_processor_handles()[0]
+    kinds = [k for k in ("SYS", "MEM", "SOC", "DF") if hasattr(amdsmi.AmdSmiClkType, k)]
+
+    def clocks():
+        out = {}
+        for k in kinds:
+            try:
+                out[k] = amdsmi.amdsmi_get_clock_info(h, getattr(amdsmi.AmdSmiClkType, k))["clk"]
+            except Exception:  # noqa: BLE001
+                out[k] = None
+        return out
+
+    for idle in (1.0, 0.02):
         time.sleep(idle)
-        c0 = clk.read()
+        samples, stop = [], threading.Event()
+
+        def loop():
+            t00 = time.perf_counter()
+            while not stop.is_set():
+                samples.append((round((time.perf_counter() - t00) * 1e3, 1), clocks()))
+                time.sleep(0.002)
+
+        th = threading.Thread(target=loop, daemon=True)
+        th.start()
         start = torch.cuda.Event(enable_timing=True)
         evs = []
         start.record(streams[0])
@@ -105,11 +128,13 @@ if args.ramp:
             e.record(streams[j % args.streams])
             evs.append(e)
         torch.cuda.synchronize()
-        c1 = clk.read()
+        stop.set()
+        th.join()
         done = sorted(start.elapsed_time(e) for e in evs)
         win = [round((done[min(len(done) - 1, k + 20)] - done[k]) / 20, 4) for k in range(0, len(done) - 20, 20)]
-        print(json.dumps({"ramp_after_idle_s": idle, "first_done_ms": round(done[0], 4), "window20_ms_per_step": win,
-                          "sclk_before": c0 and c0["sclk_mhz"], "sclk_after": c1 and c1["sclk_mhz"]}), flush=True)
+        print(json.dumps({"ramp_after_idle_s": idle, "streams": args.streams, "first_done_ms": round(done[0], 4),
+                          "window20_ms_per_step": win, "clock_samples_ms_mhz": samples[:: max(1, len(samples) // 12)]}),
+              flush=True)
 got = cb.bitmap_to_bools(d_verd[0].cpu().numpy().view(np.uint8).tobytes(), n)
 assert np.array_equal(got, ss.expected), "verdicts differ from OpenSSL"
 ctx.close()
