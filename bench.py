@@ -82,8 +82,8 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-runs", type=int, default=200)
     ap.add_argument("--inflight", type=int, default=4, help="host-path batches in flight")
-    ap.add_argument("--mixed-streams", type=int, default=4, help="config #3 device-resident streams")
-    ap.add_argument("--streams", type=int, default=2, help="headline (config #2) device-resident streams")
+    ap.add_argument("--mixed-streams", type=int, default=2, help="config #3 device-resident streams")
+    ap.add_argument("--streams", type=int, default=3, help="headline (config #2) device-resident streams")
     ap.add_argument("--single-process-devices", default="",
                     help="also time one process over these devices (comma list, repeats allowed: cbft_open_devices); "
                          "with --gpus N > 1 rank 0 does this over all N GPUs (cbft_open_mask) by default")
@@ -251,7 +251,8 @@ def main():
         check(outs[j], "pipelined batch")
 
     # ---- the headline: inputs resident in HBM, cbft_ed25519_verify_fixed_device (the device form
-    # of the fixed-length call; config #2's messages are all L bytes) alternating over two streams,
+    # of the fixed-length call; config #2's messages are all L bytes) rotating over --streams streams
+    # (default 3: each stream's hash -> ladder -> finish chain then covers three batches),
     # verdict words left in HBM; with N > 1 each rank's words are all-gathered over RCCL.
     def to_dev(a: np.ndarray, dtype):
         return torch.from_numpy(np.ascontiguousarray(a).view(dtype)).to(dev)
@@ -513,7 +514,7 @@ def main():
                                    "pcie_inclusive_value)",
                        "batch_per_gpu": n, "msg_len": L, "nkeys": args.nkeys, "comb_radix": args.comb_radix,
                        "b_comb_radix": b_radix, "ladder_lanes_per_signature": lanes,
-                       "inputs": "HBM (cbft_ed25519_verify_fixed_device, two streams); verdict words stay in HBM",
+                       "inputs": f"HBM (cbft_ed25519_verify_fixed_device, {nst} streams); verdict words stay in HBM",
                        "pcie_inclusive_inputs": "pinned host memory (cbft_host_alloc) -> GPU each step; bitmap -> host",
                        "inflight_batches": depth,
                        "parallelism": f"static shard x{world}" + (", RCCL all-gather of verdict bitmaps"
@@ -833,7 +834,7 @@ def bench_mixed(ctx, args, cpu_threads):
 
 
 def _mixed_device_resident(ctx, tid, ss, args):
-    """Config #3 with its inputs already in HBM (cbft_ed25519_verify_batch_device, two streams):
+    """Config #3 with its inputs already in HBM (cbft_ed25519_verify_batch_device, --mixed-streams):
     the GPU's own rate on the variable-length batch, and the hash kernel's isolated duration."""
     import torch
 

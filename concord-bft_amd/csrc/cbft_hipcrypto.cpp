@@ -747,8 +747,10 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
                  kt ? kt->nkeys : (uint32_t)n, fixed_len};
   Ed25519Work w{};
   // a small (latency-bound) batch inverts per signature; from 16K one inversion per block of
-  // 512 lanes x 2 signatures (the tree finish, K = -2); $CBFT_FINISH_BATCH = K > 0 selects one
-  // shared inversion per K signatures per lane (the round-4 finish: 64K: K = 2 55 us, 4 60, 8 74)
+  // 64 lanes x 2 signatures (the tree finish, K = -2, $CBFT_FINISH_TREE_BLOCK lanes); $CBFT_FINISH_BATCH
+  // = K > 0 selects one shared inversion per K signatures per lane on every lane (the round-4
+  // finish).  Headline A/B, 200 steps: K = 2 450 M/s, tree 512 x 2 422, 128 x 2
+  // 454-459, 64 x 2 465-470, 64 x 1 384-387
   w.finish_batch = c->finish_batch ? c->finish_batch : (n >= 16384 ? -2 : 1);
   w.finish_tree_block = c->finish_tree_block;
   w.long_groups = c->long_groups;

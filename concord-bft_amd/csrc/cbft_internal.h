@@ -174,7 +174,7 @@ struct cbft_ctx {
   // the next batch's hash waits for this batch's SHORT-message hash only, not for the long tail
   // hashing on the slot's aux stream ($CBFT_HASH_ORDER_EARLY, default 1)
   int hash_order_early = 1;
-  int finish_tree_block = 128;
+  int finish_tree_block = 64;  // lanes per tree-finish block ($CBFT_FINISH_TREE_BLOCK: 64/128/256/512)
   int long_groups = 0;  // $CBFT_SHA_LONG_GROUPS (0 = CBFT_SHA_LONG_GROUPS)
   int hash_prio = 0;    // $CBFT_HASH_PRIO
   int long_prio = 0;    // $CBFT_HASH_LONG_PRIO  // lanes per tree-finish block ($CBFT_FINISH_TREE_BLOCK: 64/128/256/512)
