@@ -82,7 +82,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-runs", type=int, default=200)
     ap.add_argument("--inflight", type=int, default=4, help="host-path batches in flight")
-    ap.add_argument("--mixed-streams", type=int, default=2, help="config #3 device-resident streams")
+    ap.add_argument("--mixed-streams", type=int, default=4, help="config #3 device-resident streams")
     ap.add_argument("--streams", type=int, default=3, help="headline (config #2) device-resident streams")
     ap.add_argument("--single-process-devices", default="",
                     help="also time one process over these devices (comma list, repeats allowed: cbft_open_devices); "
@@ -398,14 +398,18 @@ def main():
     # overhead and not counted.  Bound: the MAD64 pipe (half the INT32 issue rate).
     npos = {8: 32, 9: 29, 10: 26, 11: 23, 12: 22, 13: 20, 14: 19, 15: 17}[args.comb_radix] + \
         {16: 16, 17: 15, 18: 15, 19: 14, 20: 13, 21: 13, 22: 12, 23: 11, 24: 11, 25: 11, 26: 10}[b_radix]
-    mads_per_unit = npos * 7 * 90
+    # each pair-ladder lane's first addition starts from the identity and is a point set (1 M, not
+    # 7: CBFT_LADDER_FIRST_SET in ed25519_verify.hip), so a verify is (npos - 2) x 7 + 2 x 1 M
+    first_sets = 2 if lanes == 2 else 0
+    mads_per_unit = ((npos - first_sets) * 7 + first_sets) * 90
     achieved = mads_per_unit * n / (ladder_ms * 1e-3)
     h2d_bytes = 4 + 64 + L  # key index + R||S + message, per signature (fixed-length batch)
     roofline = {"bound": "valu_mad64", "achieved": achieved / 1e12, "peak": MAD64_PEAK / 1e12, "unit": "T MAD64/s",
                 "frac": achieved / MAD64_PEAK, "traffic": traffic,
                 "kernel": kname, "kernel_ms": ladder_ms, "units_per_launch": n,
                 "ops_per_unit": mads_per_unit,
-                "achieved_basis": f"{npos} comb additions x 7 field mults x 90 v_mad_u64_u32 per verify x units / "
+                "achieved_basis": f"{npos} comb positions: {npos - first_sets} additions x 7 field mults + {first_sets} first "
+                                  f"point sets x 1, x 90 v_mad_u64_u32 per verify x units / "
                                   f"mean ladder launch ({pipe_batches} launches, HIP events on the launch streams, "
                                   f"inside the timed pipeline)",
                 "issue_frac": (slot_ops / (ladder_ms * 1e-3) / INT32_PEAK) if slot_ops else None,

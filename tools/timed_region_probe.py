@@ -29,6 +29,8 @@ ap.add_argument("--streams", type=int, default=2)
 ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--events", type=int, default=1, help="record per-batch events inside the region")
 ap.add_argument("--ramp", type=int, default=0, help="after 2 s idle, N steps with events: mean step per 20-step window")
+ap.add_argument("--distinct", type=int, default=1,
+                help="distinct batches cycled over the steps (1 = the same batch every step, as bench.py)")
 args = ap.parse_args()
 
 import numpy as np  # noqa: E402
@@ -37,23 +39,27 @@ import torch  # noqa: E402
 torch.cuda.set_device(0)
 dev = torch.device("cuda", 0)
 n, L = 65536, 256
-ss = workload.make_sigset(n, nkeys=4096, msg_len=L, seed=0xC0FFEE, threads=16)
+sets = [workload.make_sigset(n, nkeys=4096, msg_len=L, seed=0xC0FFEE + 7919 * k, threads=16) for k in range(args.distinct)]
+ss = sets[0]
 ctx = cb.Context(device=0, max_batch=n)
 tid = ctx.load_keys(ss.pk, radix=13)
+for t in sets[1:]:
+    assert np.array_equal(t.pk, ss.pk), "same key set"
 
 
 def to_dev(a, dtype):
     return torch.from_numpy(np.ascontiguousarray(a).view(dtype)).to(dev)
 
 
-d_sig, d_blob = to_dev(ss.sig.reshape(-1), np.uint8), to_dev(ss.blob, np.uint8)
-d_kidx = to_dev(ss.key_idx.view(np.int32), np.int32)
+dsets = [(to_dev(t.sig.reshape(-1), np.uint8), to_dev(t.blob, np.uint8), to_dev(t.key_idx.view(np.int32), np.int32))
+         for t in sets]
 streams = [torch.cuda.Stream(device=dev) for _ in range(args.streams)]
 d_verd = [torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev) for _ in range(args.streams)]
 
 
 def dstep(j):
     s = streams[j % args.streams]
+    d_sig, d_blob, d_kidx = dsets[j % len(dsets)]
     ctx.verify_fixed_device(tid, 0, d_kidx.data_ptr(), d_sig.data_ptr(), d_blob.data_ptr(), L, n,
                             d_verd[j % args.streams].data_ptr(), s.cuda_stream)
 
@@ -132,9 +138,16 @@ if args.ramp:
         th.join()
         done = sorted(start.elapsed_time(e) for e in evs)
         win = [round((done[min(len(done) - 1, k + 20)] - done[k]) / 20, 4) for k in range(0, len(done) - 20, 20)]
-        print(json.dumps({"ramp_after_idle_s": idle, "streams": args.streams, "first_done_ms": round(done[0], 4),
+        print(json.dumps({"ramp_after_idle_s": idle, "streams": args.streams, "distinct": args.distinct, "first_done_ms": round(done[0], 4),
                           "window20_ms_per_step": win, "clock_samples_ms_mhz": samples[:: max(1, len(samples) // 12)]}),
               flush=True)
-got = cb.bitmap_to_bools(d_verd[0].cpu().numpy().view(np.uint8).tobytes(), n)
-assert np.array_equal(got, ss.expected), "verdicts differ from OpenSSL"
+torch.cuda.synchronize()
+for j in range(len(dsets)):  # one more pass, each set's verdicts checked
+    s0 = streams[0]
+    d_sig, d_blob, d_kidx = dsets[j]
+    ctx.verify_fixed_device(tid, 0, d_kidx.data_ptr(), d_sig.data_ptr(), d_blob.data_ptr(), L, n, d_verd[0].data_ptr(),
+                            s0.cuda_stream)
+    torch.cuda.synchronize()
+    got = cb.bitmap_to_bools(d_verd[0].cpu().numpy().view(np.uint8).tobytes(), n)
+    assert np.array_equal(got, sets[j].expected), f"set {j}: verdicts differ from OpenSSL"
 ctx.close()
