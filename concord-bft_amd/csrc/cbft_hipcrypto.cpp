@@ -150,6 +150,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   if (const char* e = getenv("CBFT_WORK_SLOTS")) c->work_slots = std::max(1, std::min(CBFT_MAX_WORK_SLOTS, atoi(e)));
   if (const char* e = getenv("CBFT_HASH_ORDER_EARLY")) c->hash_order_early = atoi(e);
   if (const char* e = getenv("CBFT_FINISH_TREE_BLOCK")) c->finish_tree_block = atoi(e);
+  if (const char* e = getenv("CBFT_FINISH_SPLIT")) c->finish_split = atoi(e);
   if (const char* e = getenv("CBFT_SHA_LONG_GROUPS")) c->long_groups = std::max(0, std::min(1024, atoi(e)));
   if (const char* e = getenv("CBFT_HASH_PRIO")) c->hash_prio = atoi(e);
   if (const char* e = getenv("CBFT_HASH_LONG_PRIO")) c->long_prio = atoi(e);
@@ -753,6 +754,11 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   // 454-459, 64 x 2 465-470, 64 x 1 384-387
   w.finish_batch = c->finish_batch ? c->finish_batch : (n >= 16384 ? -2 : 1);
   w.finish_tree_block = c->finish_tree_block;
+  if (c->finish_split && w.finish_batch < 0 && !small) {
+    // blocks x 9 limbs x 2T nodes: at most 18 n / K + 18 T words (T <= 128 in the split form)
+    CBFT_HIP(slot.tree.reserve((18 * n + 18 * 128) * sizeof(uint32_t)));
+    w.tree = slot.tree.as<uint32_t>();
+  }
   w.long_groups = c->long_groups;
   w.hash_prio = c->hash_prio;
   w.long_prio = c->long_prio;

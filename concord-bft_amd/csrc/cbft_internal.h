@@ -110,6 +110,7 @@ struct BlsKeySet {
 struct WorkSlot {
   DevBuf h, flags, xyz, ps_tbl, ps_aok;
   DevBuf perm, buckets;  // hash order of a variable-length batch (counting sort by SHA-512 blocks)
+  DevBuf tree;           // the split tree finish's block trees
   hipStream_t aux = nullptr;                        // long-message hash stream (ed25519_hash_long_kernel)
   hipEvent_t fork = nullptr, join = nullptr;
   hipEvent_t done = nullptr;
@@ -174,6 +175,7 @@ struct cbft_ctx {
   // the next batch's hash waits for this batch's SHORT-message hash only, not for the long tail
   // hashing on the slot's aux stream ($CBFT_HASH_ORDER_EARLY, default 1)
   int hash_order_early = 1;
+  int finish_split = 0;        // the split tree finish ($CBFT_FINISH_SPLIT)
   int finish_tree_block = 64;  // lanes per tree-finish block ($CBFT_FINISH_TREE_BLOCK: 64/128/256/512)
   int long_groups = 0;  // $CBFT_SHA_LONG_GROUPS (0 = CBFT_SHA_LONG_GROUPS)
   int hash_prio = 0;    // $CBFT_HASH_PRIO

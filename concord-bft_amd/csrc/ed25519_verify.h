@@ -122,7 +122,9 @@ struct Ed25519Work {
   int comb_lanes;              // lanes per signature of the comb ladder: 4 (quad) or 2 (pair)
   int finish_batch;            // K4: K > 1 signatures per lane share one inversion (2/4/8/16/32);
                                // -K: one inversion per block of finish_tree_block lanes, K per lane (1/2/4)
-  int finish_tree_block;       // 64 / 128 (default) / 256 / 512
+  int finish_tree_block;       // 64 (default) / 128 / 256 / 512
+  uint32_t* tree;              // non-null: the split tree finish (up / root inversions / down), its
+                               // block trees here (9 x 2T words per block)
   const uint8_t* aok;          // A decoded OK per signature (per-signature key mode)
   uint32_t* h_soa;             // 8 x n words
   uint8_t* flags;              // n bytes

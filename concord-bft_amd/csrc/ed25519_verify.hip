@@ -750,13 +750,21 @@ __global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519B
 // whose 1,024 blocks of 36 KB exactly fill a 64K batch's LDS (4 per CU): a 512-lane tree block
 // (37 KB) on a CU pushes one ladder block into a second round (measured: ladder 113 -> 131 us in
 // the pipeline, 450 -> 422 M verifies/s), a 128-lane one (9 KB) fits beside four.
-template <int K, int T>
+//
+// M (the split form, $CBFT_FINISH_SPLIT): one inversion per BLOCK still costs a whole wave's time
+// for one lane's safegcd chain (~60 % of the kernel's instructions at 64 lanes per block).  M = 1
+// runs the leaves and the up-sweep and stores the block's tree ([limb][node], 72 T bytes) to
+// `tree`; ed25519_finish_root_kernel then inverts every block's root with ONE LANE PER ROOT (512
+// roots at 64K: 8 waves); M = 2 loads the tree back and runs the down-sweep and the lanes.  M = 0
+// is the one-launch form (the root inverted by lane 0 of its own block).
+template <int K, int T, int M>
 __global__ void __launch_bounds__(T) ed25519_finish_tree_kernel(const Ed25519Batch b, const uint32_t* xyz_soa,
                                                                 const uint8_t* flags, const uint8_t* aok,
-                                                                uint64_t* verdict_words) {
+                                                                uint64_t* verdict_words, uint32_t* tree) {
   __shared__ uint32_t node[FE_LIMBS][2 * T];  // [limb][heap node]: lanes touch consecutive nodes
   const uint32_t t = threadIdx.x;
   const size_t base = (size_t)blockIdx.x * T * K;
+  uint32_t* tb = tree ? tree + (size_t)blockIdx.x * FE_LIMBS * 2 * T : nullptr;  // this block's nodes
   fe pre[K];  // pre[j] = Z_0 * .. * Z_j of this lane
   uint32_t okmask = 0;
 #pragma unroll
@@ -773,29 +781,45 @@ __global__ void __launch_bounds__(T) ed25519_finish_tree_kernel(const Ed25519Bat
     okmask |= (ok ? 1u : 0u) << j;
     if (j == 0)
       fe_copy(pre[0], Z);
-    else
+    else if (M != 2 || j < K - 1)  // the down pass needs the prefixes below the leaf only
       fe_mul<false>(pre[j], pre[j - 1], Z);
   }
+  if (M != 2) {
 #pragma unroll
-  for (int k = 0; k < FE_LIMBS; k++) node[k][T + t] = pre[K - 1].v[k];
-  __syncthreads();
-#pragma nounroll
-  for (uint32_t m = T >> 1; m >= 1; m >>= 1) {  // up: node n = node 2n * node 2n+1
-    if (t < m) {
-      const uint32_t n = m + t;
-      fe l, r;
-#pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) {
-        l.v[k] = node[k][2 * n];
-        r.v[k] = node[k][2 * n + 1];
-      }
-      fe_mul<false>(l, l, r);
-#pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) node[k][n] = l.v[k];
-    }
+    for (int k = 0; k < FE_LIMBS; k++) node[k][T + t] = pre[K - 1].v[k];
     __syncthreads();
+#pragma nounroll
+    for (uint32_t m = T >> 1; m >= 1; m >>= 1) {  // up: node n = node 2n * node 2n+1
+      if (t < m) {
+        const uint32_t n = m + t;
+        fe l, r;
+#pragma unroll
+        for (int k = 0; k < FE_LIMBS; k++) {
+          l.v[k] = node[k][2 * n];
+          r.v[k] = node[k][2 * n + 1];
+        }
+        fe_mul<false>(l, l, r);
+#pragma unroll
+        for (int k = 0; k < FE_LIMBS; k++) node[k][n] = l.v[k];
+      }
+      __syncthreads();
+    }
   }
-  if (t == 0) {  // every leaf is non-zero, so is the root
+  if (M == 1) {  // the tree to HBM; the root kernel inverts node 1
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) {
+      tb[k * 2 * T + t] = node[k][t];
+      tb[k * 2 * T + T + t] = node[k][T + t];
+    }
+    return;
+  }
+  if (M == 2) {  // the tree back, its root inverted
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) {
+      node[k][t] = tb[k * 2 * T + t];
+      node[k][T + t] = tb[k * 2 * T + T + t];
+    }
+  } else if (t == 0) {  // every leaf is non-zero, so is the root
     fe r;
 #pragma unroll
     for (int k = 0; k < FE_LIMBS; k++) r.v[k] = node[k][1];
@@ -862,6 +886,20 @@ __global__ void __launch_bounds__(T) ed25519_finish_tree_kernel(const Ed25519Bat
     const size_t w0 = base + (size_t)j * T + (t & ~63u);  // this wave's first signature of step j
     if ((t & 63u) == 0 && w0 < b.n) verdict_words[w0 >> 6] = ballot;
   }
+}
+
+// The split tree finish's middle step: lane i inverts block i's root (node 1 of its stored tree).
+template <int T>
+__global__ void __launch_bounds__(64) ed25519_finish_root_kernel(uint32_t* tree, uint32_t nblocks) {
+  const uint32_t bi = blockIdx.x * 64 + threadIdx.x;
+  if (bi >= nblocks) return;
+  uint32_t* tb = tree + (size_t)bi * FE_LIMBS * 2 * T;
+  fe r;
+#pragma unroll
+  for (int k = 0; k < FE_LIMBS; k++) r.v[k] = tb[k * 2 * T + 1];
+  fe_invert_var(r, r);
+#pragma unroll
+  for (int k = 0; k < FE_LIMBS; k++) tb[k * 2 * T + 1] = r.v[k];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1991,11 +2029,24 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   if (ev) (void)hipEventRecord(ev[2], stream);
   switch (w.finish_batch) {
 #define CBFT_FINISH_TREE_LAUNCH(K, T)                                                                         \
-  hipLaunchKernelGGL((ed25519_finish_tree_kernel<K, T>), dim3((unsigned)((b.n + (size_t)(T) * K - 1) / ((size_t)(T) * K))), \
-                     dim3(T), 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words)
+  hipLaunchKernelGGL((ed25519_finish_tree_kernel<K, T, 0>), dim3((unsigned)((b.n + (size_t)(T) * K - 1) / ((size_t)(T) * K))), \
+                     dim3(T), 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words, (uint32_t*)nullptr)
+#define CBFT_FINISH_SPLIT_LAUNCH(K, T)                                                                        \
+  do {                                                                                                        \
+    const unsigned nb = (unsigned)((b.n + (size_t)(T) * K - 1) / ((size_t)(T) * K));                          \
+    hipLaunchKernelGGL((ed25519_finish_tree_kernel<K, T, 1>), dim3(nb), dim3(T), 0, stream, b, w.xyz_soa, w.flags,   \
+                       w.aok, w.verdict_words, w.tree);                                                       \
+    hipLaunchKernelGGL((ed25519_finish_root_kernel<T>), dim3((nb + 63) / 64), dim3(64), 0, stream, w.tree, nb);     \
+    hipLaunchKernelGGL((ed25519_finish_tree_kernel<K, T, 2>), dim3(nb), dim3(T), 0, stream, b, w.xyz_soa, w.flags,   \
+                       w.aok, w.verdict_words, w.tree);                                                       \
+  } while (0)
 #define CBFT_FINISH_TREE_CASE(K)                                       \
   case -K:                                                             \
-    if (w.finish_tree_block == 512)                                    \
+    if (w.tree && w.finish_tree_block == 128)                          \
+      CBFT_FINISH_SPLIT_LAUNCH(K, 128);                                \
+    else if (w.tree)                                                   \
+      CBFT_FINISH_SPLIT_LAUNCH(K, 64);                                 \
+    else if (w.finish_tree_block == 512)                               \
       CBFT_FINISH_TREE_LAUNCH(K, 512);                                 \
     else if (w.finish_tree_block == 256)                               \
       CBFT_FINISH_TREE_LAUNCH(K, 256);                                 \
@@ -2008,6 +2059,7 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
     CBFT_FINISH_TREE_CASE(2)
     CBFT_FINISH_TREE_CASE(4)
 #undef CBFT_FINISH_TREE_CASE
+#undef CBFT_FINISH_SPLIT_LAUNCH
 #undef CBFT_FINISH_TREE_LAUNCH
 #define CBFT_FINISH_CASE(K)                                                                                     \
   case K:                                                                                                       \
