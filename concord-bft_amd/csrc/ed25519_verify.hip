@@ -1170,6 +1170,11 @@ __device__ __forceinline__ void add256(uint32_t* s, const uint32_t* off) {
 #ifndef CBFT_COMB_MIN_WAVES
 #define CBFT_COMB_MIN_WAVES 4
 #endif
+// CBFT_QUAD_FIRST_SET: each lane's first addition of the quad comb sum (from the identity) is a
+// point set, 1 M instead of 7 M (the quad ladder of batches < 32K and the fused small kernels)
+#ifndef CBFT_QUAD_FIRST_SET
+#define CBFT_QUAD_FIRST_SET 1
+#endif
 
 // Lane q's quarter of the comb sum [h](-A) + [S]B of signature i (h = h_in, 8 LE words): its
 // nper mixed additions from the key's and B's comb tables, entries staged through LDS one
@@ -1278,6 +1283,25 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
 #if !CBFT_LADDER_NOFETCH  // (probe builds only: compute without the table traffic, wrong verdicts)
       request(entry(jj + DEPTH, dn), slot);
 #endif
+    }
+    if (CBFT_QUAD_FIRST_SET && jj == 0) {  // O + entry as a point set (see the pair ladder): 1 M
+      fe ypx, ymx, E, H;
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        ypx.v[k] = neg ? ew[9 + k] : ew[k];
+        ymx.v[k] = neg ? ew[k] : ew[9 + k];
+      }
+      fe_sub(E, ypx, ymx);
+      fe_add(H, ypx, ymx);
+      fe_carry(H);
+      fe_mul(P.T, E, H);
+      fe_add(P.X, E, E);
+      fe_carry(P.X);
+      fe_add(P.Y, H, H);
+      fe_carry(P.Y);
+      fe_0(P.Z);
+      P.Z.v[0] = 4;
+      continue;
     }
     ge_p1p1 t;
     {
