@@ -155,6 +155,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   if (const char* e = getenv("CBFT_HASH_PRIO")) c->hash_prio = atoi(e);
   if (const char* e = getenv("CBFT_HASH_LONG_PRIO")) c->long_prio = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e);
+  if (const char* e = getenv("CBFT_STAGE_ORDER_VAR")) c->stage_order_var = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER_MIN")) c->stage_order_min = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_SMALL_MAX")) c->small_max = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_SHA_SORT_MIN")) c->sha_sort_min = (size_t)atoll(e);
@@ -796,14 +797,15 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   // Small batches are latency-bound single waves per stage: ordering them only serialises
   // concurrent callers' batches (the per-request coalescer keeps several in flight), so they run
   // unordered ($CBFT_STAGE_ORDER_MIN, default 4,096 signatures).
-  const bool ordered = c->stage_order && n >= c->stage_order_min && !w.small;
+  const int so = sort ? c->stage_order_var : c->stage_order;
+  const bool ordered = so && n >= c->stage_order_min && !w.small;
   StageOrder order{};
   if (ordered) {
     for (hipEvent_t& e : c->stage_done)
       if (!e) CBFT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     order.wait = c->stage_used;
-    order.hash = c->stage_order != 2;    // 2: ladders only
-    order.ladder = c->stage_order != 3;  // 3: hashes only (two batches' ladders may share the SIMDs)
+    order.hash = so != 2;    // 2: ladders only
+    order.ladder = so != 3;  // 3: hashes only (two batches' ladders may share the SIMDs)
     order.done[0] = c->stage_done[0];
     order.done[1] = c->stage_done[1];
     order.hash_early = c->hash_order_early != 0;

@@ -187,6 +187,10 @@ struct cbft_ctx {
   // ladder-to-ladder instead of two streams marching in phase (both finishes together, 7/8 of
   // the SIMDs idle).  $CBFT_STAGE_ORDER: 0 off, 1 hash + ladder, 2 ladder only.
   int stage_order = 1;
+  // the same for variable-length (block-count sorted) batches: 2 = ladders only, so consecutive
+  // batches' hash stages (whose long-message tails set their latency) overlap ($CBFT_STAGE_ORDER_VAR;
+  // config #3 A/B: 1 -> 219, 2 -> 228-231 M/s)
+  int stage_order_var = 2;
   size_t stage_order_min = 4096;  // smaller batches run unordered ($CBFT_STAGE_ORDER_MIN)
   // key-table batches up to this size run as one fused launch (ed25519_small_kernel;
   // $CBFT_SMALL_MAX, 0 = never): the per-request coalescer's batches
