@@ -176,7 +176,7 @@ struct cbft_ctx {
   // hashing on the slot's aux stream ($CBFT_HASH_ORDER_EARLY, default 1)
   int hash_order_early = 1;
   int finish_split = 0;        // the split tree finish ($CBFT_FINISH_SPLIT)
-  int finish_tree_block = 64;  // lanes per tree-finish block ($CBFT_FINISH_TREE_BLOCK: 64/128/256/512)
+  int finish_tree_block = 64;  // lanes per tree-finish block ($CBFT_FINISH_TREE_BLOCK: 64/128/256/512; 0 = wave butterflies)
   int long_groups = 0;  // $CBFT_SHA_LONG_GROUPS (0 = CBFT_SHA_LONG_GROUPS)
   int hash_prio = 0;    // $CBFT_HASH_PRIO
   int long_prio = 0;    // $CBFT_HASH_LONG_PRIO  // lanes per tree-finish block ($CBFT_FINISH_TREE_BLOCK: 64/128/256/512)

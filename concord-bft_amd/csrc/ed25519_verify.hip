@@ -902,6 +902,125 @@ __global__ void __launch_bounds__(64) ed25519_finish_root_kernel(uint32_t* tree,
   for (int k = 0; k < FE_LIMBS; k++) tb[k * 2 * T + 1] = r.v[k];
 }
 
+// K4 (wave tree): one inversion per 4-wave block (256 lanes x K signatures).  Each wave reduces
+// its 64 leaves with a butterfly (xor 1, 2, .., 32 partners: every lane ends with the wave's
+// product, keeping the six partial products it saw); the four wave products meet in LDS, lanes
+// 0..3 of wave 0 invert them (one safegcd chain's latency for four roots), and each lane walks its
+// butterfly back: 1/G_(d-1)(i) = 1/G_d(i) * G_(d-1)(i ^ 2^d).  Per lane 12 M of tree (the LDS tree:
+// 18 M), a quarter of the root inversions of the 64-lane tree, and 144 B of LDS per block, so it
+// sits beside the other stream's ladder blocks.
+#define FINISH_WAVE_BLOCK 256
+template <int CTRL>
+__device__ __forceinline__ void fe_dpp_w(fe& r, const fe& a) {
+#pragma unroll
+  for (int k = 0; k < FE_LIMBS; k++) r.v[k] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a.v[k], CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ void fe_xor_lane(fe& r, const fe& a, uint32_t m) {
+  if (m == 1) {
+    fe_dpp_w<0xB1>(r, a);  // quad_perm [1, 0, 3, 2]
+  } else if (m == 2) {
+    fe_dpp_w<0x4E>(r, a);  // quad_perm [2, 3, 0, 1]
+  } else {
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) r.v[k] = (uint32_t)__shfl_xor((int)a.v[k], (int)m, 64);
+  }
+}
+template <int K>
+__global__ void __launch_bounds__(FINISH_WAVE_BLOCK) ed25519_finish_wave_kernel(const Ed25519Batch b,
+                                                                              const uint32_t* xyz_soa,
+                                                                              const uint8_t* flags, const uint8_t* aok,
+                                                                              uint64_t* verdict_words) {
+  constexpr uint32_t T = FINISH_WAVE_BLOCK;
+  __shared__ uint32_t roots[T / 64][FE_LIMBS];
+  const uint32_t t = threadIdx.x, wv = t >> 6;
+  const size_t base = (size_t)blockIdx.x * T * K;
+  fe pre[K];  // pre[j] = Z_0 * .. * Z_j of this lane
+  uint32_t okmask = 0;
+#pragma unroll
+  for (int j = 0; j < K; j++) {
+    const size_t i = base + (size_t)j * T + t;
+    fe Z;
+    fe_1(Z);
+    bool ok = false;
+    if (i < b.n) {
+      fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
+      ok = flags[i] && unit_aok(b, aok, batch_unit(b, i)) && !fe_iszero(Z);
+      if (!ok) fe_1(Z);
+    }
+    okmask |= (ok ? 1u : 0u) << j;
+    if (j == 0)
+      fe_copy(pre[0], Z);
+    else
+      fe_mul<false>(pre[j], pre[j - 1], Z);
+  }
+  fe G[6];  // G[d] = this lane's group product before butterfly level d (G[0] = the leaf)
+  fe v;
+  fe_copy(v, pre[K - 1]);
+#pragma unroll
+  for (int d = 0; d < 6; d++) {
+    fe_copy(G[d], v);
+    fe p;
+    fe_xor_lane(p, v, 1u << d);
+    fe_mul<false>(v, v, p);
+  }
+  if ((t & 63u) == 0) {
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) roots[wv][k] = v.v[k];
+  }
+  __syncthreads();
+  if (t < T / 64) {  // every leaf is non-zero, so is every wave product
+    fe r;
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) r.v[k] = roots[t][k];
+    fe_invert_var(r, r);
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) roots[t][k] = r.v[k];
+  }
+  __syncthreads();
+  fe inv;  // 1 / (the wave's product), then down the butterfly to 1 / leaf
+#pragma unroll
+  for (int k = 0; k < FE_LIMBS; k++) inv.v[k] = roots[wv][k];
+#pragma unroll
+  for (int d = 5; d >= 0; d--) {
+    fe p;
+    fe_xor_lane(p, G[d], 1u << d);
+    fe_mul<false>(inv, inv, p);
+  }
+#pragma unroll
+  for (int j = K - 1; j >= 0; j--) {
+    const size_t i = base + (size_t)j * T + t;
+    const bool ok = (okmask >> j) & 1u;
+    fe zi;
+    if (j > 0)
+      fe_mul<false>(zi, inv, pre[j - 1]);
+    else
+      fe_copy(zi, inv);
+    bool verdict = false;
+    if (ok) {
+      fe Z, X, Y, x, y;
+      if (j > 0) {
+        fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
+        fe_mul<false>(inv, inv, Z);
+      }
+      fe_load_soa(X, xyz_soa, b.n, i);
+      fe_load_soa(Y, xyz_soa + 9 * b.n, b.n, i);
+      fe_mul<false>(x, X, zi);
+      fe_mul<false>(y, Y, zi);
+      uint32_t Rp[8], Rw[8];
+      fe_to_words(Rp, y);
+      Rp[7] ^= fe_isnegative(x) << 31;
+      load_words8(Rw, b.sig + i * 64);
+      uint32_t diff = 0;
+#pragma unroll
+      for (int k = 0; k < 8; k++) diff |= Rp[k] ^ Rw[k];
+      verdict = diff == 0;
+    }  // (a rejected entry entered the product as 1: inv is already 1 / pre[j-1])
+    const uint64_t ballot = __ballot(verdict);
+    const size_t w0 = base + (size_t)j * T + (t & ~63u);
+    if ((t & 63u) == 0 && w0 < b.n) verdict_words[w0 >> 6] = ballot;
+  }
+}
+
 // ---------------------------------------------------------------------------------------
 // Wide fixed-base combs, four lanes per signature (key-table mode).
 //
@@ -2066,7 +2185,11 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   } while (0)
 #define CBFT_FINISH_TREE_CASE(K)                                       \
   case -K:                                                             \
-    if (w.tree && w.finish_tree_block == 128)                          \
+    if (w.finish_tree_block == 0)                                      \
+      hipLaunchKernelGGL((ed25519_finish_wave_kernel<K>),              \
+                         dim3((unsigned)((b.n + (size_t)FINISH_WAVE_BLOCK * K - 1) / ((size_t)FINISH_WAVE_BLOCK * K))), \
+                         dim3(FINISH_WAVE_BLOCK), 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words); \
+    else if (w.tree && w.finish_tree_block == 128)                          \
       CBFT_FINISH_SPLIT_LAUNCH(K, 128);                                \
     else if (w.tree)                                                   \
       CBFT_FINISH_SPLIT_LAUNCH(K, 64);                                 \

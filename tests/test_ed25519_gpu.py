@@ -216,12 +216,14 @@ def test_fresh_context_without_presizing(golden):
 @pytest.mark.parametrize("k,tree_block,split", [(1, 64, 0), (2, 64, 0), (4, 64, 0), (8, 64, 0), (16, 64, 0),
                                                 (32, 64, 0), (-1, 128, 0), (-2, 128, 0), (-4, 128, 0), (-2, 64, 0),
                                                 (-2, 256, 0), (-1, 512, 0), (-2, 512, 0), (-1, 64, 1), (-2, 64, 1),
-                                                (-4, 64, 1), (-2, 128, 1)])
+                                                (-4, 64, 1), (-2, 128, 1), (-1, 0, 0), (-2, 0, 0),
+                                                (-4, 0, 0)])
 def test_finish_inversion_batching(golden, monkeypatch, k, tree_block, split):
     # K4' shares one inversion among K signatures per lane (Montgomery's trick); rejected items
     # (S >= L, undecodable A) enter the product as 1.  K < 0: the tree finish (one inversion per
     # block of tree_block lanes, |K| signatures per lane: 64 .. 2,048 signatures per block; split:
-    # the block trees go through HBM and one lane per block root inverts them).  Every K
+    # the block trees go through HBM and one lane per block root inverts them; tree_block 0: the
+    # wave-butterfly tree, four waves per inversion).  Every K
     # must give the golden verdicts, including the ragged last block (1,145 vectors is not a
     # multiple of 64 K).
     monkeypatch.setenv("CBFT_FINISH_BATCH", str(k))
