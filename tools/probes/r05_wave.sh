@@ -17,3 +17,11 @@ for rep in 1 2; do
     python3 -c "import json;d=json.load(open('$out/t${tb}_20_$rep.json'));print('tree $tb rep $rep 20 steps', round(d['value']/1e6,1), round(d['ms_per_step'],4))"
   done
 done
+for rep in 1 2; do
+  for cfg in "2 1" "2 0" "3 0" "3 1"; do
+    set -- $cfg
+    CBFT_STAGE_ORDER=$2 timeout -k 10 200 python -u bench.py --gpus 1 --steps 20 --warmup 5 --streams $1 \
+      --no-extras --no-cpu --latency-runs 0 > $out/st$1_so$2_$rep.json 2> $out/st$1_so$2_$rep.err || exit 1
+    python3 -c "import json;d=json.load(open('$out/st$1_so$2_$rep.json'));print('20 steps: streams $1 order $2 rep $rep', round(d['value']/1e6,1), round(d['ms_per_step'],4), d.get('sclk_mhz'))"
+  done
+done
