@@ -156,6 +156,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   if (const char* e = getenv("CBFT_HASH_LONG_PRIO")) c->long_prio = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER_VAR")) c->stage_order_var = atoi(e);
+  if (const char* e = getenv("CBFT_ORDER_MAX_STREAMS")) c->order_max_streams = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER_MIN")) c->stage_order_min = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_SMALL_MAX")) c->small_max = (size_t)atoll(e);
   if (const char* e = getenv("CBFT_SHA_SORT_MIN")) c->sha_sort_min = (size_t)atoll(e);
@@ -798,7 +799,17 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   // concurrent callers' batches (the per-request coalescer keeps several in flight), so they run
   // unordered ($CBFT_STAGE_ORDER_MIN, default 4,096 signatures).
   const int so = sort ? c->stage_order_var : c->stage_order;
-  const bool ordered = so && n >= c->stage_order_min && !w.small;
+  bool ordered = so && n >= c->stage_order_min && !w.small;
+  if (ordered) {  // how many streams do the recent big batches use?
+    c->recent_streams[c->recent_n++ % 4] = s;
+    unsigned distinct = 0;
+    for (unsigned a = 0; a < 4 && a < c->recent_n; a++) {
+      bool seen = false;
+      for (unsigned q = 0; q < a; q++) seen = seen || c->recent_streams[q] == c->recent_streams[a];
+      distinct += seen ? 0u : 1u;
+    }
+    if ((int)distinct > c->order_max_streams) ordered = false;
+  }
   StageOrder order{};
   if (ordered) {
     for (hipEvent_t& e : c->stage_done)

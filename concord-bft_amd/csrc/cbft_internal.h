@@ -191,6 +191,12 @@ struct cbft_ctx {
   // batches' hash stages (whose long-message tails set their latency) overlap ($CBFT_STAGE_ORDER_VAR;
   // config #3 A/B: 1 -> 219, 2 -> 228-231 M/s)
   int stage_order_var = 2;
+  // streams of the last ordered-size batches: with three or more distinct streams in flight each
+  // stream's hash -> ladder -> finish chain already covers three batches, and the order only
+  // serialises them (headline at 20 steps, 3 streams: unordered 461-493 vs ordered 451-471 M/s)
+  hipStream_t recent_streams[4] = {};
+  unsigned recent_n = 0;
+  int order_max_streams = 2;  // order only while at most this many streams are in use ($CBFT_ORDER_MAX_STREAMS)
   size_t stage_order_min = 4096;  // smaller batches run unordered ($CBFT_STAGE_ORDER_MIN)
   // key-table batches up to this size run as one fused launch (ed25519_small_kernel;
   // $CBFT_SMALL_MAX, 0 = never): the per-request coalescer's batches
