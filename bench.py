@@ -426,6 +426,12 @@ def main():
                 "pmc": _pmc_brief(lrec, lstat),
                 "stage_ms_pipelined": {k: round(v, 4) for k, v in pipe_stage.items()},
                 "stage_ms_isolated": {k: round(statistics.median(v), 4) for k, v in iso.items()},
+                # the same work over the ladder's duration when it runs alone (one batch at a time):
+                # inside the pipeline the batches' kernels share the SIMDs (from three streams two
+                # ladders co-run), which stretches every launch while the step gets shorter
+                "frac_isolated": mads_per_unit * n / (statistics.median(iso["ladder"]) * 1e-3) / MAD64_PEAK,
+                # the ladder's work per step over the whole step time (ms_per_step)
+                "frac_of_step": mads_per_unit * n / (elapsed / args.steps) / MAD64_PEAK,
                 "pcie": {"bound": "pcie_h2d", "of": "pcie_inclusive_value",
                          "achieved": pcie_value / world * h2d_bytes / 1e9, "peak": PCIE_PEAK / 1e9,
                          "measured_copy_rate": h2d_rate / 1e9, "unit": "GB/s",
