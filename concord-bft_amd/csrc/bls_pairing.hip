@@ -51,10 +51,12 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
                                                                       int do_verify, int parsed, uint8_t* valid,
                                                                       uint32_t* sig, uint32_t* ids) {
   __shared__ PairXchg xc;
+  __shared__ FeMail fm;  // WAVES = 2: the final exponentiation's helper wave (CBFT_P36_FE2)
   const uint32_t j = blockIdx.x;
   if (j >= k) return;  // whole blocks exit together
   const int wave = threadIdx.x >> 6;
   const P36 g = p36_lane();
+  if (WAVES == 2 && threadIdx.x == 0) femail_init(fm);
   const uint8_t* sh = shares + 37 * (size_t)j;
   const uint32_t id = ((uint32_t)sh[0] << 24) | ((uint32_t)sh[1] << 16) | ((uint32_t)sh[2] << 8) | sh[3];
   const bool id_ok = id >= 1 && id <= n;
@@ -120,15 +122,19 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
     p36_miller<1>(f, &P, l, g);
   }
   __syncthreads();
-  if (wave != 0) return;
   bool good = xc.ok != 0;
+  if (CBFT_P36_FE2 && wave == 1) {
+    if (do_verify && good && key_ok) p36_fe2_helper(fm, g);
+    return;
+  }
+  if (wave != 0) return;
   if (do_verify) {
     good = good && key_ok;
     if (good) {
       fp f1;
       xchg_get(f1, xc, g);
       p36_mul(f, f, f1, g);
-      good = p36_is_one_after_final_exp(f, g);
+      good = CBFT_P36_FE2 ? p36_is_one_after_final_exp_lead(f, fm, g) : p36_is_one_after_final_exp(f, g);
     }
   }
   if (g.lane == 0) valid[j] = good ? 1 : 0;
@@ -153,9 +159,11 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
                                                                   uint8_t* result, const uint32_t* H_in,
                                                                   const uint32_t* sig_aff) {
   __shared__ PairXchg xc[3];  // the values of waves 1, 2, 3
+  __shared__ FeMail fm;       // wave 1 helps wave 0's final exponentiation (CBFT_P36_FE2)
   if (blockIdx.x != 0) return;
   const int wave = threadIdx.x >> 6;
   const P36 g = p36_lane();
+  if (threadIdx.x == 0) femail_init(fm);
   BLS_PHASE(wave == 0 ? 0 : 1);
   fp f;
   if (wave < 2) {
@@ -194,8 +202,12 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
   }
   if (wave > 0) xchg_put(xc[wave - 1], f, g);
   __syncthreads();
-  if (wave != 0) return;
   bool good = xc[1].ok != 0 && pk_ok[0] != 0;
+  if (CBFT_P36_FE2 && wave == 1) {
+    if (good) p36_fe2_helper(fm, g);
+    return;
+  }
+  if (wave != 0) return;
   if (good) {
 #pragma nounroll
     for (int w = 0; w < 3; w++) {
@@ -204,7 +216,7 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
       p36_mul(f, f, f1, g);
     }
     BLS_PHASE(6);
-    good = p36_is_one_after_final_exp(f, g);
+    good = CBFT_P36_FE2 ? p36_is_one_after_final_exp_lead(f, fm, g) : p36_is_one_after_final_exp(f, g);
     BLS_PHASE(11);
   }
   if (g.lane == 0) result[0] = good ? 1 : 0;
@@ -239,6 +251,7 @@ __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uin
   __shared__ uint32_t lines[BN_ATE_LINES * BN_ABC_WORDS];
   __shared__ int progress;
   __shared__ int usable;
+  __shared__ FeMail fm;  // wave 2 helps wave 1's final exponentiation (CBFT_P36_FE2)
   if (blockIdx.x != 0) return;
   const int wave = threadIdx.x >> 6;
   const P36 g = p36_lane();
@@ -246,6 +259,7 @@ __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uin
     progress = 0;
     usable = 0;
     xc.ok = 0;
+    femail_init(fm);
   }
   __syncthreads();
   fp f;
@@ -299,13 +313,17 @@ __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uin
     if (g.lane == 0) xc.ok = ok ? 1 : 0;
   }
   __syncthreads();
-  if (wave != 1) return;
   bool good = xc.ok != 0 && usable != 0;
+  if (CBFT_P36_FE2 && wave == 2) {
+    if (good) p36_fe2_helper(fm, g);
+    return;
+  }
+  if (wave != 1) return;
   if (good) {
     fp f1;
     xchg_get(f1, xc, g);
     p36_mul(f, f, f1, g);
-    good = p36_is_one_after_final_exp(f, g);
+    good = CBFT_P36_FE2 ? p36_is_one_after_final_exp_lead(f, fm, g) : p36_is_one_after_final_exp(f, g);
   }
   BLS_PHASE(11);
   if (g.lane == 0) result[0] = good ? 1 : 0;

@@ -215,10 +215,16 @@ __device__ __forceinline__ void p36_coef(fp& m, fp& o, const uint32_t* c, int h)
 
 // f <- f * (yP + s w + mu w^3), s = -lambda xP, for one precomputed line:
 //   s = 0: f_k yP;  s = 1: -xP (f_{k-1} lambda) (xi for k = 0);  s = 2: f_{k-3} mu (xi for k < 3)
-__device__ __forceinline__ void p36_line1(fp& f, const uint32_t* ln, const g1a& P, const P36& g) {
-  fp om, oo, cm, co;
-  p36_fetch(om, oo, f, g.s == 1 ? (g.k + 5) % 6 : (g.k + 3) % 6, g);
+// this lane's (my, other) components of the line coefficient it multiplies by (lambda for s < 2,
+// mu for s = 2): the line's global-memory read, separable from the line so that it can be issued
+// one line ahead (p36_miller, CBFT_P36_PREFETCH)
+__device__ __forceinline__ void p36_line_coef(fp& cm, fp& co, const uint32_t* ln, const P36& g) {
   p36_coef(cm, co, ln + (g.s == 2 ? 18 : 0), g.h);
+}
+
+__device__ __forceinline__ void p36_line1c(fp& f, const fp& cm, const fp& co, const g1a& P, const P36& g) {
+  fp om, oo;
+  p36_fetch(om, oo, f, g.s == 1 ? (g.k + 5) % 6 : (g.k + 3) % 6, g);
   const fp u = g.h ? oo : om, v = g.h ? om : oo;
   fp X1 = g.s == 0 ? f : u;
   fp Y1 = g.s == 0 ? P.y : cm;
@@ -234,6 +240,12 @@ __device__ __forceinline__ void p36_line1(fp& f, const uint32_t* ln, const g1a& 
   p36_xi(w, T, g);
   fp_sel(T, w, wrap);
   p36_sum3(f, T, g);
+}
+
+__device__ __forceinline__ void p36_line1(fp& f, const uint32_t* ln, const g1a& P, const P36& g) {
+  fp cm, co;
+  p36_line_coef(cm, co, ln, g);
+  p36_line1c(f, cm, co, P, g);
 }
 
 // f <- f * (A yP + B xP w + C w^3) for an unnormalised line (bn254_g2wave.h, 54 words):
@@ -436,12 +448,50 @@ __device__ __forceinline__ void p36_final_exp(fp& r, const fp& f, const P36& g) 
 // two waves may run one pair each and multiply their f.  All 64 lanes of the wave call it.
 // progress (nullable, LDS): lines are still being produced by another wave of the block
 // (g2w_lines_abc); line k is read once progress > k.
+// CBFT_P36_PREFETCH = 1 (A/B only): normalised lines from global memory are read one line ahead
+// (each pair's next coefficients load while the current line and the next squaring run) instead
+// of right before their use.  Measured equal or 1-2 % slower (profiles/r05_ab/bls_line_prefetch.txt):
+// the line tables are L2-resident and the load latency is not what a lone wave waits on.
+#ifndef CBFT_P36_PREFETCH
+#define CBFT_P36_PREFETCH 0
+#endif
 template <int NP, bool ABC = false>
 __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* const* lines, const P36& g,
                                            const volatile int* progress = nullptr) {
   constexpr int W = ABC ? 54 : BN_LINE_WORDS;  // ABC: unnormalised lines (bn254_g2wave.h)
   p36_one(f, g);
   int k = 0;
+  if (CBFT_P36_PREFETCH && !ABC && !progress) {
+    fp cm[NP], co[NP];
+#pragma unroll
+    for (int j = 0; j < NP; j++) p36_line_coef(cm[j], co[j], lines[j], g);
+    auto pline = [&](int j) {
+      fp nm, no;
+      if (k + 1 < BN_ATE_LINES) p36_line_coef(nm, no, lines[j] + (k + 1) * W, g);
+      p36_line1c(f, cm[j], co[j], P[j], g);
+      cm[j] = nm;
+      co[j] = no;
+    };
+#pragma nounroll
+    for (int i = BN_ATE_DBL - 1; i >= 0; i--) {
+      p36_sqr(f, f, g);
+#pragma unroll
+      for (int j = 0; j < NP; j++) pline(j);
+      k++;
+      if (bn_ate_bit(i)) {
+#pragma unroll
+        for (int j = 0; j < NP; j++) pline(j);
+        k++;
+      }
+    }
+    p36_conj(f, f, g);
+    for (int t = 0; t < 2; t++) {
+#pragma unroll
+      for (int j = 0; j < NP; j++) pline(j);
+      k++;
+    }
+    return;
+  }
   auto line = [&](int j) {
     if (progress) {
       while (*progress <= k) __builtin_amdgcn_s_sleep(2);
@@ -484,11 +534,26 @@ __device__ __forceinline__ void p36_miller_part(fp& f, const g1a& P, const uint3
   int k = 0;
   const int hi = TOP ? BN_ATE_DBL - 1 : P36_MILLER_SPLIT - 1, lo = TOP ? P36_MILLER_SPLIT : 0;
   for (int i = BN_ATE_DBL - 1; i > hi; i--) k += bn_ate_bit(i) ? 2 : 1;
+  // lines read one ahead (CBFT_P36_PREFETCH; the top part's last read is a bottom line, unused)
+  fp cm, co;
+  if (CBFT_P36_PREFETCH) p36_line_coef(cm, co, lines + k * BN_LINE_WORDS, g);
+  auto line = [&]() {
+    if (CBFT_P36_PREFETCH) {
+      fp nm, no;
+      if (k + 1 < BN_ATE_LINES) p36_line_coef(nm, no, lines + (k + 1) * BN_LINE_WORDS, g);
+      p36_line1c(f, cm, co, P, g);
+      cm = nm;
+      co = no;
+      k++;
+    } else {
+      p36_line1(f, lines + (k++) * BN_LINE_WORDS, P, g);
+    }
+  };
 #pragma nounroll
   for (int i = hi; i >= lo; i--) {
     p36_sqr(f, f, g);
-    p36_line1(f, lines + (k++) * BN_LINE_WORDS, P, g);
-    if (bn_ate_bit(i)) p36_line1(f, lines + (k++) * BN_LINE_WORDS, P, g);
+    line();
+    if (bn_ate_bit(i)) line();
   }
   if (TOP) {
 #pragma nounroll
@@ -496,8 +561,8 @@ __device__ __forceinline__ void p36_miller_part(fp& f, const g1a& P, const uint3
   }
   p36_conj(f, f, g);
   if (!TOP) {
-    p36_line1(f, lines + (k++) * BN_LINE_WORDS, P, g);
-    p36_line1(f, lines + (k++) * BN_LINE_WORDS, P, g);
+    line();
+    line();
   }
 }
 
@@ -505,6 +570,123 @@ __device__ __forceinline__ void p36_miller_part(fp& f, const g1a& P, const uint3
 __device__ __forceinline__ bool p36_is_one_after_final_exp(const fp& f, const P36& g) {
   fp e;
   p36_final_exp(e, f, g);
+  fp want;
+  p36_one(want, g);
+  const bool mine = f_eq(e, want);
+  bool all = true;
+#pragma unroll
+  for (int q = 0; q < 12; q++) all = all && (__shfl((int)mine, q) != 0);
+  return all;
+}
+
+// ---- the final exponentiation on two waves of a block (CBFT_P36_FE2) ----
+// The hard part's three u-powers a = gg^u, b = a^u, c = b^u are one serial chain; everything
+// else p36_final_exp derives from gg, a and b (a^12, a^18, b^6, b^18, b^30, gg^2 and two of the
+// Frobenius terms) runs on a helper wave while the lead wave is still raising to u, so the lead's
+// tail after c is c^36 and six products instead of 16 squarings and 17 products.  Same GT element
+// as p36_final_exp (products reassociated; f_eq compares canonical forms).  Values pass through
+// an LDS mailbox: the writer's owning lanes store, release-fence, then lane 0 raises the slot's
+// flag; the reader spins on the flag (s_sleep) and acquire-fences.
+#ifndef CBFT_P36_FE2
+#define CBFT_P36_FE2 1
+#endif
+struct FeMail {
+  enum { GG = 0, A = 1, B = 2, X = 3, Y = 4, Z = 5, SLOTS = 6 };
+  uint32_t v[SLOTS][36][BN_LIMBS];
+  int flag[SLOTS];
+};
+__device__ __forceinline__ void femail_init(FeMail& m) {  // one thread; a barrier before any use
+  for (int i = 0; i < FeMail::SLOTS; i++) m.flag[i] = 0;
+}
+__device__ __forceinline__ void femail_write(FeMail& m, int slot, const fp& x, const P36& g) {
+  if (g.own)
+#pragma unroll
+    for (int i = 0; i < BN_LIMBS; i++) m.v[slot][g.e][i] = x.v[i];
+}
+__device__ __forceinline__ void femail_raise(FeMail& m, int slot, const P36& g) {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (g.lane == 0) *(volatile int*)&m.flag[slot] = 1;
+}
+__device__ __forceinline__ void femail_wait(const FeMail& m, int slot) {
+  while (*(const volatile int*)&m.flag[slot] == 0) __builtin_amdgcn_s_sleep(2);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ void femail_read(fp& x, const FeMail& m, int slot, const P36& g) {
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) x.v[i] = m.v[slot][g.e][i];  // shadows read the slot they mirror
+}
+
+// lead wave: r = final_exp(f), with p36_fe2_helper running on another wave of the block
+__device__ __forceinline__ void p36_final_exp_lead(fp& r, const fp& f, FeMail& m, const P36& g) {
+  fp t, gg;
+  p36_inv(t, f, g);
+  P36_PHASE(8);
+  p36_conj(gg, f, g);
+  p36_mul(gg, gg, t, g);
+  p36_frob<2>(t, gg, g);
+  p36_mul(gg, t, gg, g);
+  femail_write(m, FeMail::GG, gg, g);
+  femail_raise(m, FeMail::GG, g);
+  P36_PHASE(9);
+  fp a, b, c;
+  p36_pow_u(a, gg, g);
+  femail_write(m, FeMail::A, a, g);
+  femail_raise(m, FeMail::A, g);
+  p36_pow_u(b, a, g);
+  femail_write(m, FeMail::B, b, g);
+  femail_raise(m, FeMail::B, g);
+  p36_pow_u(c, b, g);
+  P36_PHASE(10);
+  fp c36, X, Y, Z, t0, t1;
+  p36_pow_small(c36, c, 36, g);
+  femail_wait(m, FeMail::Z);  // X, Y, Z raised together
+  femail_read(X, m, FeMail::X, g);
+  femail_read(Y, m, FeMail::Y, g);
+  femail_read(Z, m, FeMail::Z, g);
+  p36_mul(t0, c36, X, g);  // c^36 b^30 a^18 gg^2
+  p36_conj(t0, t0, g);
+  p36_mul(t1, c36, Y, g);  // c^36 b^18 a^12
+  p36_conj(t1, t1, g);
+  p36_mul(t1, t1, gg, g);
+  p36_frob<1>(t1, t1, g);
+  p36_mul(t0, t0, t1, g);
+  p36_mul(r, t0, Z, g);  // Z = frob2(b^6 gg) frob3(gg)
+}
+
+// helper wave: X = b^30 a^18 gg^2, Y = b^18 a^12, Z = frob2(b^6 gg) frob3(gg) from the lead's gg, a, b
+__device__ __forceinline__ void p36_fe2_helper(FeMail& m, const P36& g) {
+  fp gg, g2, t3, a, a12, a18, P1, b, b6, b18, b30, t2, X, Y, Z;
+  femail_wait(m, FeMail::GG);
+  femail_read(gg, m, FeMail::GG, g);
+  p36_cyc_sqr(g2, gg, g);
+  p36_frob<3>(t3, gg, g);
+  femail_wait(m, FeMail::A);
+  femail_read(a, m, FeMail::A, g);
+  p36_pow_small(a12, a, 12, g);
+  p36_pow_small(a18, a, 18, g);
+  p36_mul(P1, a18, g2, g);
+  femail_wait(m, FeMail::B);
+  femail_read(b, m, FeMail::B, g);
+  p36_pow_small(b6, b, 6, g);
+  p36_pow_small(b18, b6, 3, g);
+  p36_mul(b30, b18, b6, g);
+  p36_mul(b30, b30, b6, g);
+  p36_mul(t2, b6, gg, g);
+  p36_frob<2>(t2, t2, g);
+  p36_mul(X, b30, P1, g);
+  p36_mul(Y, b18, a12, g);
+  p36_mul(Z, t2, t3, g);
+  femail_write(m, FeMail::X, X, g);
+  femail_write(m, FeMail::Y, Y, g);
+  femail_write(m, FeMail::Z, Z, g);
+  femail_raise(m, FeMail::Z, g);
+}
+
+// final_exp(f) == 1 by the lead wave (every lane of it gets the verdict); another wave of the block
+// must run p36_fe2_helper on the same mailbox (initialised, then a barrier, before either starts)
+__device__ __forceinline__ bool p36_is_one_after_final_exp_lead(const fp& f, FeMail& m, const P36& g) {
+  fp e;
+  p36_final_exp_lead(e, f, m, g);
   fp want;
   p36_one(want, g);
   const bool mine = f_eq(e, want);
