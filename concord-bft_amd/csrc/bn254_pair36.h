@@ -343,6 +343,18 @@ __device__ __forceinline__ void p36_frob(fp& r, const fp& x, const P36& g) {
 // N on the wave (one p36_mul), N^-1 by the Fp6 tower on every lane (variable-time Fp inversion:
 // x is a Miller value of public inputs), then conj(x) N^-1 on the wave.  Half the one-lane tower
 // work of inverting in Fp12 directly.
+//
+// CBFT_P36_INV_LANES: the Fp6 inversion's Fp2 products spread over lanes (fp6_inv's formulas): six
+// lanes form c0^2, c1 c2, c2^2, c0 c1, c1^2, c0 c2 at once, three lanes c2 t1, c1 t2, c0 t0, and
+// each lane its own t_(k/2) N^-1 -- 3 Fp2 products on the critical path between the gathers and
+// the one Fp2 inversion instead of 12.
+#ifndef CBFT_P36_INV_LANES
+#define CBFT_P36_INV_LANES 1
+#endif
+__device__ __forceinline__ void fp2_shfl(fp2& r, const fp2& x, int src) {
+  fp_shfl(r.a, x.a, src);
+  fp_shfl(r.b, x.b, src);
+}
 __device__ __noinline__ void p36_inv(fp& r, const fp& x, const P36& g) {
   fp xc, n;
   p36_conj(xc, x, g);
@@ -354,10 +366,55 @@ __device__ __noinline__ void p36_inv(fp& r, const fp& x, const P36& g) {
   fp_shfl(t.c1.b, n, p36_src(2, 1, 0));
   fp_shfl(t.c2.a, n, p36_src(4, 0, 0));
   fp_shfl(t.c2.b, n, p36_src(4, 1, 0));
-  fp6_inv<true>(t, t);
-  fp2 pick = t.c0;
-  p12_sel2(pick, t.c1, g.k == 2);
-  p12_sel2(pick, t.c2, g.k == 4);
+  fp2 pick;
+  if (CBFT_P36_INV_LANES) {
+    const int j = g.lane;
+    // lane j < 6: (c0 c0, c1 c2, c2 c2, c0 c1, c1 c1, c0 c2)[j]
+    fp2 X = t.c0, Y = t.c0, R, R0, R1, R2, R3, R4, R5;
+    p12_sel2(X, t.c1, j == 1 || j == 4);
+    p12_sel2(X, t.c2, j == 2);
+    p12_sel2(Y, t.c2, j == 1 || j == 2 || j == 5);
+    p12_sel2(Y, t.c1, j == 3 || j == 4);
+    fp2_mul(R, X, Y);
+    fp2_shfl(R0, R, 0);
+    fp2_shfl(R1, R, 1);
+    fp2_shfl(R2, R, 2);
+    fp2_shfl(R3, R, 3);
+    fp2_shfl(R4, R, 4);
+    fp2_shfl(R5, R, 5);
+    fp2 t0, t1, t2, u;
+    fp2_mul_xi(u, R1);  // t0 = c0^2 - xi c1 c2
+    fp2_sub(t0, R0, u);
+    fp2_mul_xi(u, R2);  // t1 = xi c2^2 - c0 c1
+    fp2_sub(t1, u, R3);
+    fp2_sub(t2, R4, R5);  // t2 = c1^2 - c0 c2
+    // lane j < 3: (c2 t1, c1 t2, c0 t0)[j]; N = c0 t0 + xi (c2 t1 + c1 t2)
+    X = t.c2;
+    Y = t1;
+    p12_sel2(X, t.c1, j == 1);
+    p12_sel2(Y, t2, j == 1);
+    p12_sel2(X, t.c0, j == 2);
+    p12_sel2(Y, t0, j == 2);
+    fp2_mul(R, X, Y);
+    fp2_shfl(R0, R, 0);
+    fp2_shfl(R1, R, 1);
+    fp2_shfl(R2, R, 2);
+    fp2 nn;
+    fp2_add(u, R0, R1);
+    fp2_mul_xi(u, u);
+    fp2_add(nn, R2, u);
+    fp2_inv<true>(nn, nn);
+    // this lane's coefficient of the inverse: t_(k/2) N^-1 (k odd: unused)
+    fp2 tk = t0;
+    p12_sel2(tk, t1, g.k == 2 || g.k == 3);
+    p12_sel2(tk, t2, g.k >= 4);
+    fp2_mul(pick, tk, nn);
+  } else {
+    fp6_inv<true>(t, t);
+    pick = t.c0;
+    p12_sel2(pick, t.c1, g.k == 2);
+    p12_sel2(pick, t.c2, g.k == 4);
+  }
   fp ninv = g.h ? pick.b : pick.a;
   if (g.k & 1) f_zero(ninv);
   p36_mul(r, xc, ninv, g);
@@ -402,6 +459,14 @@ __device__ uint64_t g_bls_phase[16];
 #endif
 #define P36_PHASE(name) BLS_STAMP(name)
 
+// CBFT_P36_FE_VEC: the hard part's tail as a vectorial addition chain (gg^d = y0 y1^2 y2^6 y3^12
+// y4^18 y5^30 y6^36 with y0 = gg^(p + p^2 + p^3), y1 = 1/gg, y2 = b^(p^2), y3 = a^-p, y4 = 1/(a b^p),
+// y5 = 1/b, y6 = 1/(c c^p): 4 squarings, 13 products, 7 Frobenius maps) instead of raising c, b, a
+// to 36, 30, 18, 12, 6 separately (16 squarings, 17 products, 3 maps).  The same exponent d, so
+// the same GT element.
+#ifndef CBFT_P36_FE_VEC
+#define CBFT_P36_FE_VEC 1
+#endif
 __device__ __forceinline__ void p36_final_exp(fp& r, const fp& f, const P36& g) {
   fp t, gg;
   p36_inv(t, f, g);
@@ -411,11 +476,45 @@ __device__ __forceinline__ void p36_final_exp(fp& r, const fp& f, const P36& g) 
   p36_frob<2>(t, gg, g);
   p36_mul(gg, t, gg, g);
   P36_PHASE(9);
-  fp a, b, c, c36, b6, b18, b30, a12, a18, g2;
+  fp a, b, c;
   p36_pow_u(a, gg, g);
   p36_pow_u(b, a, g);
   p36_pow_u(c, b, g);
   P36_PHASE(10);
+  if (CBFT_P36_FE_VEC) {
+    fp y0, y1, y2, y3, y4, y5, y6, u, T0, T1;
+    p36_frob<1>(y0, gg, g);
+    p36_frob<2>(u, gg, g);
+    p36_mul(y0, y0, u, g);
+    p36_frob<3>(u, gg, g);
+    p36_mul(y0, y0, u, g);
+    p36_conj(y1, gg, g);
+    p36_frob<2>(y2, b, g);
+    p36_frob<1>(y3, a, g);
+    p36_conj(y3, y3, g);
+    p36_frob<1>(y4, b, g);
+    p36_mul(y4, y4, a, g);
+    p36_conj(y4, y4, g);
+    p36_conj(y5, b, g);
+    p36_frob<1>(y6, c, g);
+    p36_mul(y6, y6, c, g);
+    p36_conj(y6, y6, g);
+    p36_cyc_sqr(T0, y6, g);  // y6^2 y4 y5
+    p36_mul(T0, T0, y4, g);
+    p36_mul(T0, T0, y5, g);
+    p36_mul(T1, y3, y5, g);  // y6^2 y5^2 y4 y3
+    p36_mul(T1, T1, T0, g);
+    p36_mul(T0, T0, y2, g);  // y6^2 y5 y4 y2
+    p36_cyc_sqr(T1, T1, g);
+    p36_mul(T1, T1, T0, g);  // y6^6 y5^5 y4^3 y3^2 y2
+    p36_cyc_sqr(T1, T1, g);
+    p36_mul(T0, T1, y1, g);
+    p36_mul(T1, T1, y0, g);
+    p36_cyc_sqr(T0, T0, g);  // y6^24 y5^20 y4^12 y3^8 y2^4 y1^2
+    p36_mul(r, T0, T1, g);
+    return;
+  }
+  fp c36, b6, b18, b30, a12, a18, g2;
   p36_pow_small(c36, c, 36, g);
   p36_pow_small(b6, b, 6, g);
   p36_pow_small(b18, b6, 3, g);
