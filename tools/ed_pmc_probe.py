@@ -21,10 +21,11 @@ import workload  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--mode", choices=("headline", "small", "mixed"), required=True)
 ap.add_argument("--reps", type=int, default=0)
+ap.add_argument("--nkeys", type=int, default=0, help="client keys (default: 4,096; 1,024 for small)")
 a = ap.parse_args()
 n = 1024 if a.mode == "small" else 65536
 msg_len = (64, 4096) if a.mode == "mixed" else 256
-ss = workload.make_sigset(n, nkeys=4096 if a.mode != "small" else 1024, msg_len=msg_len, seed=0xC0FFEE,
+ss = workload.make_sigset(n, nkeys=a.nkeys or (4096 if a.mode != "small" else 1024), msg_len=msg_len, seed=0xC0FFEE,
                           invalid_frac=0.10 if a.mode == "mixed" else 0.0, threads=16)
 reps = a.reps or (20 if a.mode == "small" else 3)
 with cb.Context(device=0, max_batch=65536) as ctx:

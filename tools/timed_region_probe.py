@@ -29,6 +29,7 @@ ap.add_argument("--streams", type=int, default=2)
 ap.add_argument("--warmup", type=int, default=5)
 ap.add_argument("--events", type=int, default=1, help="record per-batch events inside the region")
 ap.add_argument("--ramp", type=int, default=0, help="after 2 s idle, N steps with events: mean step per 20-step window")
+ap.add_argument("--nkeys", type=int, default=4096, help="client keys (key-table footprint 10.5 MB each at radix 13)")
 ap.add_argument("--distinct", type=int, default=1,
                 help="distinct batches cycled over the steps (1 = the same batch every step, as bench.py)")
 args = ap.parse_args()
@@ -39,7 +40,7 @@ import torch  # noqa: E402
 torch.cuda.set_device(0)
 dev = torch.device("cuda", 0)
 n, L = 65536, 256
-sets = [workload.make_sigset(n, nkeys=4096, msg_len=L, seed=0xC0FFEE + 7919 * k, threads=16) for k in range(args.distinct)]
+sets = [workload.make_sigset(n, nkeys=args.nkeys, msg_len=L, seed=0xC0FFEE + 7919 * k, threads=16) for k in range(args.distinct)]
 ss = sets[0]
 ctx = cb.Context(device=0, max_batch=n)
 tid = ctx.load_keys(ss.pk, radix=13)
@@ -138,7 +139,7 @@ if args.ramp:
         th.join()
         done = sorted(start.elapsed_time(e) for e in evs)
         win = [round((done[min(len(done) - 1, k + 20)] - done[k]) / 20, 4) for k in range(0, len(done) - 20, 20)]
-        print(json.dumps({"ramp_after_idle_s": idle, "streams": args.streams, "distinct": args.distinct, "first_done_ms": round(done[0], 4),
+        print(json.dumps({"ramp_after_idle_s": idle, "streams": args.streams, "distinct": args.distinct, "nkeys": args.nkeys, "first_done_ms": round(done[0], 4),
                           "window20_ms_per_step": win, "clock_samples_ms_mhz": samples[:: max(1, len(samples) // 12)]}),
               flush=True)
 torch.cuda.synchronize()
