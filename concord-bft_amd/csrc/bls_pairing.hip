@@ -234,7 +234,7 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
 #endif
 }
 
-// Multisig verify in one 3-wave block (BlsMultisigVerifier: e(H, sum vk_i) e(-sigma, g2) == 1):
+// Multisig verify in one block (BlsMultisigVerifier: e(H, sum vk_i) e(-sigma, g2) == 1):
 //   wave 0  PK = sum of the key-sum partials (bls_g2_sum_kernel), to affine, then its 70
 //           unnormalised lines (bn254_g2wave.h) into LDS, publishing each as it lands;
 //   wave 1  H = g1_map(msg), then the (H, PK) Miller loop, reading each line as soon as wave 0
@@ -242,28 +242,38 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
 //   wave 2  decompress sigma, the (-sigma, g2) Miller loop over the precomputed generator lines.
 // Wave 1 joins the two Miller values and runs the final exponentiation.  Every wave reaches the
 // end: wave 0 publishes "all lines" even when PK is unusable (bad key, infinity).
-#define MS_BLOCK 192
+// CBFT_MS_SPLIT = 1 (A/B only): five waves, each Miller loop split in two (p36_miller_part, as
+// bls_verify_kernel): waves 1 / 2 the top / bottom of (H, PK) (the bottom trails the line
+// computation, the top needs only its first lines), waves 3 / 4 those of (-sigma, g2); wave 1
+// joins the four values, wave 3 helps its final exponentiation.  Measured 1.018 against 0.926 ms
+// (profiles/r05_ab/bls_multisig_split.txt): the fifth wave shares a SIMD with the line
+// computation, which sets the pace of the (H, PK) loop, and the 320-thread block caps VGPRs at 256.
+#ifndef CBFT_MS_SPLIT
+#define CBFT_MS_SPLIT 0
+#endif
+#define MS_BLOCK (CBFT_MS_SPLIT ? 320 : 192)
 __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uint32_t* parts, uint32_t count,
                                                                        const uint8_t* msg, uint32_t len,
                                                                        const uint8_t* sig33, const uint32_t* gen_lines,
                                                                        uint8_t* pk_ok, uint8_t* result) {
-  __shared__ PairXchg xc;
+  __shared__ PairXchg xc[CBFT_MS_SPLIT ? 3 : 1];  // split: the values of waves 2, 3, 4
   __shared__ uint32_t lines[BN_ATE_LINES * BN_ABC_WORDS];
   __shared__ int progress;
   __shared__ int usable;
-  __shared__ FeMail fm;  // wave 2 helps wave 1's final exponentiation (CBFT_P36_FE2)
+  __shared__ FeMail fm;  // the final exponentiation's helper: wave 3 (split) or wave 2
   if (blockIdx.x != 0) return;
   const int wave = threadIdx.x >> 6;
   const P36 g = p36_lane();
   if (threadIdx.x == 0) {
     progress = 0;
     usable = 0;
-    xc.ok = 0;
+    for (int w = 0; w < (CBFT_MS_SPLIT ? 3 : 1); w++) xc[w].ok = 0;
     femail_init(fm);
   }
   __syncthreads();
   fp f;
   BLS_PHASE(wave == 0 ? 0 : wave == 1 ? 4 : 6);
+  const int lead = 1, helper = CBFT_MS_SPLIT ? 3 : 2;
   if (wave == 0) {
     g2j acc;
     fp2_one(acc.X);
@@ -288,8 +298,17 @@ __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uin
     if (ok) g2r_lines_abc(lines, s, &progress);
     BLS_PHASE(3);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    if (g.lane == 0) progress = BN_ATE_LINES + 1;  // release the consumer whatever happened
-  } else if (wave == 1) {
+    if (g.lane == 0) progress = BN_ATE_LINES + 1;  // release the consumers whatever happened
+  } else if (CBFT_MS_SPLIT && wave <= 2) {
+    g1a P;
+    g1_map_row(P, msg, len);
+    BLS_PHASE(wave == 1 ? 5 : 14);
+    if (wave == 1)
+      p36_miller_part<true, true>(f, P, lines, g, &progress);
+    else
+      p36_miller_part<false, true>(f, P, lines, g, &progress);
+    BLS_PHASE(wave == 1 ? 12 : 15);
+  } else if (!CBFT_MS_SPLIT && wave == 1) {
     g1a P;
     g1_map_row(P, msg, len);
     BLS_PHASE(5);
@@ -302,27 +321,36 @@ __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uin
     if (ok && !s.inf) {
       g1a P = s;
       f_neg(P.y, s.y);
-      const uint32_t* l[1] = {gen_lines};
       BLS_PHASE(13);
-      p36_miller<1>(f, &P, l, g);
+      if (!CBFT_MS_SPLIT) {
+        const uint32_t* l[1] = {gen_lines};
+        p36_miller<1>(f, &P, l, g);
+      } else if (wave == 3) {
+        p36_miller_part<true>(f, P, gen_lines, g);
+      } else {
+        p36_miller_part<false>(f, P, gen_lines, g);
+      }
     } else {
       p36_one(f, g);
     }
     BLS_PHASE(7);
-    xchg_put(xc, f, g);
-    if (g.lane == 0) xc.ok = ok ? 1 : 0;
+    if (g.lane == 0) xc[CBFT_MS_SPLIT ? wave - 2 : 0].ok = ok ? 1 : 0;
   }
+  if (wave >= 2) xchg_put(xc[CBFT_MS_SPLIT ? wave - 2 : 0], f, g);
   __syncthreads();
-  bool good = xc.ok != 0 && usable != 0;
-  if (CBFT_P36_FE2 && wave == 2) {
+  bool good = xc[CBFT_MS_SPLIT ? 1 : 0].ok != 0 && usable != 0;  // sigma decoded (wave 3 / 2), PK usable
+  if (CBFT_P36_FE2 && wave == helper) {
     if (good) p36_fe2_helper(fm, g);
     return;
   }
-  if (wave != 1) return;
+  if (wave != lead) return;
   if (good) {
-    fp f1;
-    xchg_get(f1, xc, g);
-    p36_mul(f, f, f1, g);
+#pragma nounroll
+    for (int w = 0; w < (CBFT_MS_SPLIT ? 3 : 1); w++) {
+      fp f1;
+      xchg_get(f1, xc[w], g);
+      p36_mul(f, f, f1, g);
+    }
     good = CBFT_P36_FE2 ? p36_is_one_after_final_exp_lead(f, fm, g) : p36_is_one_after_final_exp(f, g);
   }
   BLS_PHASE(11);

@@ -627,26 +627,36 @@ __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* 
 // the product), conjugation applied to both.  With s = 40 both parts cost 209 Fp multiplications
 // per lane (sqr 2, line 3) against 320 for the whole loop on one wave.
 #define P36_MILLER_SPLIT 40
-template <bool TOP>
-__device__ __forceinline__ void p36_miller_part(fp& f, const g1a& P, const uint32_t* lines, const P36& g) {
+// ABC: unnormalised lines (54 words, bn254_g2wave.h) read once progress > k (nullable: all present)
+template <bool TOP, bool ABC = false>
+__device__ __forceinline__ void p36_miller_part(fp& f, const g1a& P, const uint32_t* lines, const P36& g,
+                                                const volatile int* progress = nullptr) {
+  constexpr int W = ABC ? 54 : BN_LINE_WORDS;
   p36_one(f, g);
   int k = 0;
   const int hi = TOP ? BN_ATE_DBL - 1 : P36_MILLER_SPLIT - 1, lo = TOP ? P36_MILLER_SPLIT : 0;
   for (int i = BN_ATE_DBL - 1; i > hi; i--) k += bn_ate_bit(i) ? 2 : 1;
   // lines read one ahead (CBFT_P36_PREFETCH; the top part's last read is a bottom line, unused)
+  constexpr bool PF = CBFT_P36_PREFETCH && !ABC;
   fp cm, co;
-  if (CBFT_P36_PREFETCH) p36_line_coef(cm, co, lines + k * BN_LINE_WORDS, g);
+  if (PF) p36_line_coef(cm, co, lines + k * W, g);
   auto line = [&]() {
-    if (CBFT_P36_PREFETCH) {
+    if (progress) {
+      while (*progress <= k) __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    }
+    if (ABC) {
+      p36_line_abc(f, lines + k * W, P, g);
+    } else if (PF) {
       fp nm, no;
-      if (k + 1 < BN_ATE_LINES) p36_line_coef(nm, no, lines + (k + 1) * BN_LINE_WORDS, g);
+      if (k + 1 < BN_ATE_LINES) p36_line_coef(nm, no, lines + (k + 1) * W, g);
       p36_line1c(f, cm, co, P, g);
       cm = nm;
       co = no;
-      k++;
     } else {
-      p36_line1(f, lines + (k++) * BN_LINE_WORDS, P, g);
+      p36_line1(f, lines + k * W, P, g);
     }
+    k++;
   };
 #pragma nounroll
   for (int i = hi; i >= lo; i--) {
