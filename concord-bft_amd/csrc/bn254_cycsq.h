@@ -75,6 +75,20 @@ constexpr int cs_bitlen(uint32_t x) {
   return n;
 }
 
+// ---- lane-role selects ----------------------------------------------------------------------
+// A lane condition (h, diag, s == 2, ...) as an all-ones / zero mask that LLVM cannot see through:
+// with the plain ternaries it merged the limb-wise selects of one condition into ONE divergent
+// branch around both limb loops (exec-mask save / restore, both sides issued anyway: ~40 % of the
+// p36_sqr operand code); with an opaque mask every select is one v_bfi_b32.
+BN_HD uint32_t cs_mask(bool c) {
+  uint32_t m = c ? ~0u : 0u;
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+v"(m));
+#endif
+  return m;
+}
+BN_HD uint32_t cs_sel(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }  // m ? a : b
+
 // ---- carry passes -------------------------------------------------------------------------
 // limbs 0..7 non-negative (as uint32, any size): -> [0, 2^29), carries into the top limb
 // (two's complement, so a signed top limb stays signed).  Sequential, 3 instructions a limb.
@@ -142,10 +156,11 @@ BN_HD void cs_pre(fp& R, const fp& a, const fp& t, int s) {
 // >= Wo_i, so non-negative) or Wo (h = 1), then carried (value < 8q).  f_mul(U, V): product
 // columns < 9 2^60 + 9 2^58 + 2^35 < 2^64, result T < 64 q^2 / 2^261 + q < 1.3 q, normalised.
 BN_HD void cs_operands(fp& U, fp& V, const fp& Wm, const fp& Wo, int h) {
+  const uint32_t mh = cs_mask(h != 0);
 #pragma unroll
   for (int i = 0; i < BN_LIMBS; i++) {
-    U.v[i] = Wm.v[i] + (h ? Wm.v[i] : Wo.v[i]);
-    V.v[i] = h ? Wo.v[i] : Wm.v[i] - Wo.v[i] + CsConst::Q4R.v[i];
+    U.v[i] = Wm.v[i] + cs_sel(mh, Wm.v[i], Wo.v[i]);
+    V.v[i] = cs_sel(mh, Wo.v[i], Wm.v[i] - Wo.v[i] + CsConst::Q4R.v[i]);
   }
   cs_carry(V);
 }
@@ -245,18 +260,19 @@ struct SqConst {
 };
 BN_HD void sq_operands(fp& U1, fp& V1, fp& U2, fp& V2, const fp& xm, const fp& xo, const fp& zm, const fp& zo,
                        bool diag, int h) {
+  const uint32_t mh = cs_mask(h != 0), md = cs_mask(diag);
 #pragma unroll
   for (int i = 0; i < BN_LIMBS; i++) {
-    const uint32_t du1 = xm.v[i] + (h ? xm.v[i] : xo.v[i]);
-    const uint32_t dv1 = h ? xo.v[i] : xm.v[i] - xo.v[i] + SqConst::Q2R.v[i];
-    const uint32_t du2 = zm.v[i] + (h ? zm.v[i] : zo.v[i]);
-    const uint32_t dv2 = h ? zo.v[i] : zm.v[i] - zo.v[i] + SqConst::Q2R.v[i];
-    const uint32_t cu1 = (h ? xo.v[i] : xm.v[i]) << 1;
-    const uint32_t cu2 = (h ? xm.v[i] : xo.v[i]) << 1;
-    U1.v[i] = diag ? du1 : cu1;
-    V1.v[i] = diag ? dv1 : zm.v[i];
-    U2.v[i] = diag ? du2 : cu2;
-    V2.v[i] = diag ? dv2 : zo.v[i];
+    const uint32_t du1 = xm.v[i] + cs_sel(mh, xm.v[i], xo.v[i]);
+    const uint32_t dv1 = cs_sel(mh, xo.v[i], xm.v[i] - xo.v[i] + SqConst::Q2R.v[i]);
+    const uint32_t du2 = zm.v[i] + cs_sel(mh, zm.v[i], zo.v[i]);
+    const uint32_t dv2 = cs_sel(mh, zo.v[i], zm.v[i] - zo.v[i] + SqConst::Q2R.v[i]);
+    const uint32_t cu1 = cs_sel(mh, xo.v[i], xm.v[i]) << 1;
+    const uint32_t cu2 = cs_sel(mh, xm.v[i], xo.v[i]) << 1;
+    U1.v[i] = cs_sel(md, du1, cu1);
+    V1.v[i] = cs_sel(md, dv1, zm.v[i]);
+    U2.v[i] = cs_sel(md, du2, cu2);
+    V2.v[i] = cs_sel(md, dv2, zo.v[i]);
   }
   cs_carry(V1);
   cs_carry(V2);

@@ -70,6 +70,17 @@ BN_HD void f_one(Fe<F>& r) {
 // word-serial REDC, m_k = c_k * (-q^-1) mod 2^29, then m_k q added into columns k..k+8.  The
 // only serial dependency is column k -> m_k -> column k+1 (about 4 instructions per step);
 // the 9 mads of each step are independent.  Columns stay < 2^62.2 + carries.
+// A modulus limb that is a power of two (p's limb 3 is 2^25) is passed to its mad as an opaque
+// SGPR: LLVM would otherwise strength-reduce m_k * 2^25 + c into a 64-bit shift plus a 64-bit add,
+// two half-rate instructions where the mad is one.
+template <class F>
+BN_HD uint32_t bn_qlimb(int i) {
+  uint32_t q = F::Q[i];
+#if defined(__HIP_DEVICE_COMPILE__)
+  if ((q & (q - 1u)) == 0u) asm("" : "+s"(q));
+#endif
+  return q;
+}
 template <class F>
 BN_HD void f_redc(Fe<F>& r, uint64_t* c) {
 #pragma unroll
@@ -78,7 +89,7 @@ BN_HD void f_redc(Fe<F>& r, uint64_t* c) {
     c[k] = bn_mad(mk, F::Q[0], c[k]);  // low 29 bits become 0
     c[k + 1] = bn_mad(mk, F::Q[1], c[k + 1]) + (c[k] >> 29);
 #pragma unroll
-    for (int i = 2; i < BN_LIMBS; i++) c[k + i] = bn_mad(mk, F::Q[i], c[k + i]);
+    for (int i = 2; i < BN_LIMBS; i++) c[k + i] = bn_mad(mk, bn_qlimb<F>(i), c[k + i]);
   }
   uint64_t acc = 0;
 #pragma unroll

@@ -178,7 +178,8 @@ __device__ __forceinline__ void p36_sqr(fp& r, const fp& a, const P36& g) {
 // (one component each), then P = x^2 + xi y^2 (even k) or Q = (x + y)^2 - x^2 - y^2 (odd k)
 __device__ __forceinline__ void p36_cyc_sqr(fp& r, const fp& a, const P36& g) {
   // lazy form (bn254_cycsq.h): 4 gathers of 9 limbs, one Fp multiplication, one reduction
-  const int sx = (g.k == 0 || g.k == 3) ? 0 : ((g.k == 1 || g.k == 4) ? 2 : 1);
+  const int k3 = g.k >= 3 ? g.k - 3 : g.k;  // sx = 0, 2, 1 for k mod 3 = 0, 1, 2 (arithmetic, no branch)
+  const int sx = k3 == 0 ? 0 : 3 - k3;
   const bool odd = (g.k & 1) != 0;
   fp t, R, Wm, Wo, U, V, T, X2, Y2, G3, v, vo, Z3;
   fp_shfl(t, a, p36_src(g.k < 3 ? g.k + 3 : g.k - 3, g.h, g.s));
