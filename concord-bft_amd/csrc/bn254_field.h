@@ -122,6 +122,28 @@ BN_HD void f_mul(Fe<F>& r, const Fe<F>& a, const Fe<F>& b) {
   f_redc(r, c);
 }
 
+// r = (a b + c d) 2^-261 mod q: both products' columns in one set of accumulators and ONE
+// f_redc (half the reductions of two f_mul and a sum).  a, b normalised (< 2q); c may have limbs
+// up to 2^30 (a redundant negation, value < 4q), d normalised.  Columns < 9 2^58 + 9 2^59 < 2^62.6
+// (+ the REDC terms, < 2^63.1); the value ab + cd < 12 q^2 < q 2^261, so the result is < 2q.
+template <class F>
+BN_HD void f_mul_sum2(Fe<F>& r, const Fe<F>& a, const Fe<F>& b, const Fe<F>& c, const Fe<F>& d) {
+  uint64_t t[2 * BN_LIMBS];
+#pragma unroll
+  for (int k = 0; k < 2 * BN_LIMBS; k++) t[k] = 0;
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+#pragma unroll
+    for (int j = 0; j < BN_LIMBS; j++) t[i + j] = bn_mad(a.v[i], b.v[j], t[i + j]);
+  }
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) {
+#pragma unroll
+    for (int j = 0; j < BN_LIMBS; j++) t[i + j] = bn_mad(c.v[i], d.v[j], t[i + j]);
+  }
+  f_redc(r, t);
+}
+
 template <class F>
 BN_HD void f_sqr(Fe<F>& r, const Fe<F>& a) {
   uint32_t a2[BN_LIMBS];

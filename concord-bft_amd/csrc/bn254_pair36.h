@@ -223,19 +223,49 @@ __device__ __forceinline__ void p36_line_coef(fp& cm, fp& co, const uint32_t* ln
   p36_coef(cm, co, ln + (g.s == 2 ? 18 : 0), g.h);
 }
 
+// CBFT_P36_LINE_MERGE: a line's component C = u c_m +- v c_o (the Fp2 product's component h) as
+// ONE two-product reduction (f_mul_sum2) with v negated beforehand (4q - v, redundant limbs, on
+// the h = 0 lanes) instead of two f_mul and f_addsub; s = 0 lanes zero their second product.
+#ifndef CBFT_P36_LINE_MERGE
+#define CBFT_P36_LINE_MERGE 1
+#endif
+struct P36Const {
+  static constexpr CsLimbs Q4N = cs_redundant(4, 1 << 29);  // 4q, low limbs in [2^29, 2^30): 4q - v >= 0 limb-wise
+};
+// v' = -v (as 4q - v) where neg, else v
+__device__ __forceinline__ void p36_cneg4(fp& r, const fp& v, bool neg) {
+  const uint32_t m = cs_mask(neg);
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) r.v[i] = cs_sel(m, P36Const::Q4N.v[i] - v.v[i], v.v[i]);
+}
+
 __device__ __forceinline__ void p36_line1c(fp& f, const fp& cm, const fp& co, const g1a& P, const P36& g) {
   fp om, oo;
   p36_fetch(om, oo, f, g.s == 1 ? (g.k + 5) % 6 : (g.k + 3) % 6, g);
   const fp u = g.h ? oo : om, v = g.h ? om : oo;
   fp X1 = g.s == 0 ? f : u;
   fp Y1 = g.s == 0 ? P.y : cm;
-  fp P1, P2, P3, C;
+  fp P3, C;
+#if CBFT_P36_LINE_MERGE
+  fp vn, cz;
+  p36_cneg4(vn, v, g.h == 0);
+  const uint32_t mz = cs_mask(g.s != 0);
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) cz.v[i] = co.v[i] & mz;
+  f_mul_sum2(C, X1, Y1, vn, cz);  // s = 0: f_k yP; else u c_m +- v c_o
+  f_mul(P3, C, P.x);
+  f_neg(P3, P3);
+  fp T = C;
+  fp_sel(T, P3, g.s == 1);
+#else
+  fp P1, P2;
   f_mul(P1, X1, Y1);
   f_mul(P2, v, co);
   f_addsub(C, P1, P2, g.h != 0);
   f_mul(P3, C, P.x);
   f_neg(P3, P3);
   fp T = g.s == 0 ? P1 : (g.s == 1 ? P3 : C);
+#endif
   const bool wrap = (g.s == 1 && g.k == 0) || (g.s == 2 && g.k < 3);
   fp w;
   p36_xi(w, T, g);
@@ -257,10 +287,17 @@ __device__ __forceinline__ void p36_line_abc(fp& f, const uint32_t* ln, const g1
   p36_fetch(om, oo, f, g.s == 0 ? g.k : (g.s == 1 ? (g.k + 5) % 6 : (g.k + 3) % 6), g);
   p36_coef(cm, co, ln + 18 * g.s, g.h);
   const fp u = g.h ? oo : om, v = g.h ? om : oo;
-  fp P1, P2, P3, C;
+  fp P3, C;
+#if CBFT_P36_LINE_MERGE
+  fp vn;
+  p36_cneg4(vn, v, g.h == 0);
+  f_mul_sum2(C, u, cm, vn, co);
+#else
+  fp P1, P2;
   f_mul(P1, u, cm);
   f_mul(P2, v, co);
   f_addsub(C, P1, P2, g.h != 0);
+#endif
   f_mul(P3, C, g.s == 0 ? P.y : P.x);
   fp T = g.s == 2 ? C : P3;
   const bool wrap = (g.s == 1 && g.k == 0) || (g.s == 2 && g.k < 3);
