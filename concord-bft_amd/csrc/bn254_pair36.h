@@ -120,8 +120,24 @@ __device__ __forceinline__ void p36_xi(fp& r, const fp& z, const P36& g) {
   p12_cxi(r, z, zo, g.h);
 }
 
+struct P36Const {
+  static constexpr CsLimbs Q4N = cs_redundant(4, 1 << 29);  // 4q, low limbs in [2^29, 2^30): 4q - v >= 0 limb-wise
+};
+// v' = -v (as 4q - v) where neg, else v
+__device__ __forceinline__ void p36_cneg4(fp& r, const fp& v, bool neg) {
+  const uint32_t m = cs_mask(neg);
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) r.v[i] = cs_sel(m, P36Const::Q4N.v[i] - v.v[i], v.v[i]);
+}
+
 // r = a * b: sub-lane s forms the terms i = 2s, 2s + 1 of c_k = sum_i a_i b_{k-i} (xi on wrap);
 // lazy sums and one reduction (bn254_cycsq.h: cm_terms, cm_xi, cm_sum3)
+// CBFT_P36_MUL_MERGE: each term's Fp2-product component u b_m +- v b_o as ONE two-product
+// reduction (f_mul_sum2, v negated beforehand on the h = 0 lanes, as the lines): two reductions
+// per lane instead of four; cm_terms then only sums (h = 1, zero second terms).
+#ifndef CBFT_P36_MUL_MERGE
+#define CBFT_P36_MUL_MERGE 1
+#endif
 __device__ __forceinline__ void p36_mul(fp& r, const fp& a, const fp& b, const P36& g) {
   fp T[4];
   bool wrap[2];
@@ -135,11 +151,18 @@ __device__ __forceinline__ void p36_mul(fp& r, const fp& a, const fp& b, const P
     p36_fetch(am, ao, a, i, g);
     p36_fetch(bm, bo, b, j, g);
     const fp u = g.h ? ao : am, v = g.h ? am : ao;
-    f_mul(T[2 * t], u, bm);
-    f_mul(T[2 * t + 1], v, bo);
+    if (CBFT_P36_MUL_MERGE) {
+      fp vn;
+      p36_cneg4(vn, v, g.h == 0);
+      f_mul_sum2(T[2 * t], u, bm, vn, bo);
+      f_zero(T[2 * t + 1]);
+    } else {
+      f_mul(T[2 * t], u, bm);
+      f_mul(T[2 * t + 1], v, bo);
+    }
   }
   fp acc, accw, ao, z, z0, z1, z2;
-  cm_terms(acc, accw, T[0], T[1], T[2], T[3], g.h, wrap[0], wrap[1]);
+  cm_terms(acc, accw, T[0], T[1], T[2], T[3], CBFT_P36_MUL_MERGE ? 1 : g.h, wrap[0], wrap[1]);
   fp_swap_h(ao, accw, g);
   cm_xi(z, acc, accw, ao, g.h);
   p36_gather3(z0, z1, z2, z, g);
@@ -229,16 +252,6 @@ __device__ __forceinline__ void p36_line_coef(fp& cm, fp& co, const uint32_t* ln
 #ifndef CBFT_P36_LINE_MERGE
 #define CBFT_P36_LINE_MERGE 1
 #endif
-struct P36Const {
-  static constexpr CsLimbs Q4N = cs_redundant(4, 1 << 29);  // 4q, low limbs in [2^29, 2^30): 4q - v >= 0 limb-wise
-};
-// v' = -v (as 4q - v) where neg, else v
-__device__ __forceinline__ void p36_cneg4(fp& r, const fp& v, bool neg) {
-  const uint32_t m = cs_mask(neg);
-#pragma unroll
-  for (int i = 0; i < BN_LIMBS; i++) r.v[i] = cs_sel(m, P36Const::Q4N.v[i] - v.v[i], v.v[i]);
-}
-
 __device__ __forceinline__ void p36_line1c(fp& f, const fp& cm, const fp& co, const g1a& P, const P36& g) {
   fp om, oo;
   p36_fetch(om, oo, f, g.s == 1 ? (g.k + 5) % 6 : (g.k + 3) % 6, g);
