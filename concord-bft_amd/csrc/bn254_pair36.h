@@ -252,6 +252,13 @@ __device__ __forceinline__ void p36_line_coef(fp& cm, fp& co, const uint32_t* ln
 #ifndef CBFT_P36_LINE_MERGE
 #define CBFT_P36_LINE_MERGE 1
 #endif
+// P: the G1 point with its x NEGATED (p36_neg_x), so the s = 1 term -xP (f_{k-1} lambda) is one
+// product; the Miller loops negate once, before their first line.
+__device__ __forceinline__ g1a p36_neg_x(const g1a& P) {
+  g1a n = P;
+  f_neg(n.x, P.x);
+  return n;
+}
 __device__ __forceinline__ void p36_line1c(fp& f, const fp& cm, const fp& co, const g1a& P, const P36& g) {
   fp om, oo;
   p36_fetch(om, oo, f, g.s == 1 ? (g.k + 5) % 6 : (g.k + 3) % 6, g);
@@ -266,8 +273,7 @@ __device__ __forceinline__ void p36_line1c(fp& f, const fp& cm, const fp& co, co
 #pragma unroll
   for (int i = 0; i < BN_LIMBS; i++) cz.v[i] = co.v[i] & mz;
   f_mul_sum2(C, X1, Y1, vn, cz);  // s = 0: f_k yP; else u c_m +- v c_o
-  f_mul(P3, C, P.x);
-  f_neg(P3, P3);
+  f_mul(P3, C, P.x);              // P.x holds -xP (p36_line1: the caller negates once per loop)
   fp T = C;
   fp_sel(T, P3, g.s == 1);
 #else
@@ -275,8 +281,7 @@ __device__ __forceinline__ void p36_line1c(fp& f, const fp& cm, const fp& co, co
   f_mul(P1, X1, Y1);
   f_mul(P2, v, co);
   f_addsub(C, P1, P2, g.h != 0);
-  f_mul(P3, C, P.x);
-  f_neg(P3, P3);
+  f_mul(P3, C, P.x);  // P.x holds -xP
   fp T = g.s == 0 ? P1 : (g.s == 1 ? P3 : C);
 #endif
   const bool wrap = (g.s == 1 && g.k == 0) || (g.s == 2 && g.k < 3);
@@ -611,6 +616,9 @@ __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* 
   constexpr int W = ABC ? 54 : BN_LINE_WORDS;  // ABC: unnormalised lines (bn254_g2wave.h)
   p36_one(f, g);
   int k = 0;
+  g1a Pn[NP];  // normalised lines take -xP (p36_line1c)
+#pragma unroll
+  for (int j = 0; j < NP; j++) Pn[j] = ABC ? P[j] : p36_neg_x(P[j]);
   if (CBFT_P36_PREFETCH && !ABC && !progress) {
     fp cm[NP], co[NP];
 #pragma unroll
@@ -618,7 +626,7 @@ __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* 
     auto pline = [&](int j) {
       fp nm, no;
       if (k + 1 < BN_ATE_LINES) p36_line_coef(nm, no, lines[j] + (k + 1) * W, g);
-      p36_line1c(f, cm[j], co[j], P[j], g);
+      p36_line1c(f, cm[j], co[j], Pn[j], g);
       cm[j] = nm;
       co[j] = no;
     };
@@ -650,7 +658,7 @@ __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* 
     if (ABC)
       p36_line_abc(f, lines[j] + k * W, P[j], g);
     else
-      p36_line1(f, lines[j] + k * W, P[j], g);
+      p36_line1(f, lines[j] + k * W, Pn[j], g);
   };
 #pragma nounroll
   for (int i = BN_ATE_DBL - 1; i >= 0; i--) {
@@ -689,6 +697,7 @@ __device__ __forceinline__ void p36_miller_part(fp& f, const g1a& P, const uint3
   for (int i = BN_ATE_DBL - 1; i > hi; i--) k += bn_ate_bit(i) ? 2 : 1;
   // lines read one ahead (CBFT_P36_PREFETCH; the top part's last read is a bottom line, unused)
   constexpr bool PF = CBFT_P36_PREFETCH && !ABC;
+  const g1a Pn = ABC ? P : p36_neg_x(P);  // normalised lines take -xP (p36_line1c)
   fp cm, co;
   if (PF) p36_line_coef(cm, co, lines + k * W, g);
   auto line = [&]() {
@@ -701,11 +710,11 @@ __device__ __forceinline__ void p36_miller_part(fp& f, const g1a& P, const uint3
     } else if (PF) {
       fp nm, no;
       if (k + 1 < BN_ATE_LINES) p36_line_coef(nm, no, lines + (k + 1) * W, g);
-      p36_line1c(f, cm, co, P, g);
+      p36_line1c(f, cm, co, Pn, g);
       cm = nm;
       co = no;
     } else {
-      p36_line1(f, lines + k * W, P, g);
+      p36_line1(f, lines + k * W, Pn, g);
     }
     k++;
   };
