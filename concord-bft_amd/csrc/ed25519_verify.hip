@@ -1815,10 +1815,34 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
 #define CBFT_LADDER_PHASED 1
 #endif
 
+// CBFT_LADDER_PRIO (A/B only): the two waves a SIMD holds at 64K run nearly one after the other
+// under the oldest-first issue arbitration (CBFT_LADDER_STAMPS: ~a quarter of the waves end by
+// ~60 us, half at 120-140 us), so the second runs its tail alone; a priority that falls with
+// progress (3, 2, 1, 0 by quarter of the steps) keeps the lagging wave ahead.  Isolated ladder
+// 109 -> 105 us, but the pipelined headline loses (494-506 vs 511-516 M/s at 200 steps: the
+// co-running finish and hash kernels are starved), profiles/r05_ab/ladder_wave_ends_prio.txt.
+#ifndef CBFT_LADDER_PRIO
+#define CBFT_LADDER_PRIO 0
+#endif
+// CBFT_LADDER_STAMPS (probe builds only): per-wave wall-clock stamps of the pair ladder (start,
+// first entry landed, end; 10 ns ticks) stored per wave; the last wave of a launch folds them and
+// prints the spread of the end times (launches must not overlap).
+#ifndef CBFT_LADDER_STAMPS
+#define CBFT_LADDER_STAMPS 0
+#endif
+#if CBFT_LADDER_STAMPS
+__device__ unsigned long long g_lw[3 * 8192];  // per wave: start, first entry landed, end
+__device__ unsigned int g_lcount;
+__device__ unsigned int g_lhist[32];
+#endif
 __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
     ed25519_comb2_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* btbl,
                                 const CombLadder cl, uint32_t* xyz_soa) {
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+#if CBFT_LADDER_STAMPS
+  const uint64_t st0 = wall_clock64();
+  uint64_t st1 = st0;
+#endif
   const uint32_t q = threadIdx.x & 1u;
   size_t i = g >> 1;
   const bool live = i < b.n;
@@ -1920,12 +1944,28 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
 #pragma nounroll
   for (uint32_t jj = 0; jj < nper; jj++) {
     const uint32_t slot = jj & 1u;
+#if CBFT_LADDER_PRIO
+    {  // issue priority falls with progress: a SIMD's lagging wave outranks its leading one
+      const uint32_t qtr = (jj * 4u) / nper;  // wave-uniform
+      if (qtr == 0)
+        __builtin_amdgcn_s_setprio(3);
+      else if (qtr == 1)
+        __builtin_amdgcn_s_setprio(2);
+      else if (qtr == 2)
+        __builtin_amdgcn_s_setprio(1);
+      else
+        __builtin_amdgcn_s_setprio(0);
+    }
+#endif
     if (jj + 1u < nper)
       asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // entry jj landed; jj + 1 may still fly
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // The stage is read with asm ds_reads: the compiler would otherwise see LDS reads after
     // global_load_lds writes and wait for ALL of them (vmcnt(0)), serialising the two stages.
+#if CBFT_LADDER_STAMPS
+    if (jj == 0) st1 = wall_clock64();
+#endif
     uint32_t ew[28];
     {
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -2050,6 +2090,48 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
     fe_store_soa(xyz_soa + 9 * b.n, b.n, i, P.Y);
     fe_store_soa(xyz_soa + 18 * b.n, b.n, i, P.Z);
   }
+#if CBFT_LADDER_STAMPS
+  {
+    const unsigned wid = (unsigned)(g >> 6), waves = (unsigned)((gridDim.x * (size_t)blockDim.x) >> 6);
+    if ((threadIdx.x & 63u) == 0 && wid < 8192u) {
+      g_lw[3 * wid] = st0;
+      g_lw[3 * wid + 1] = st1;
+      g_lw[3 * wid + 2] = wall_clock64();
+    }
+    __threadfence();
+    unsigned last = 0;
+    if ((threadIdx.x & 63u) == 0) last = atomicAdd(&g_lcount, 1u) == waves - 1u;
+    last = __shfl(last, 0);
+    if (last && waves <= 8192u) {  // the last wave: every lane folds waves ln, ln + 64, ...
+      __threadfence();
+      const unsigned ln2 = threadIdx.x & 63u;
+      unsigned long long mn0 = ~0ull, mx0 = 0, sdur = 0, swait = 0;
+      for (unsigned w = ln2; w < waves; w += 64) mn0 = min(mn0, g_lw[3 * w]);
+      for (int o = 32; o; o >>= 1) mn0 = min(mn0, (unsigned long long)__shfl_xor((long long)mn0, o));
+      for (unsigned w = ln2; w < waves; w += 64) {
+        const unsigned long long t0 = g_lw[3 * w], t1 = g_lw[3 * w + 1], t2 = g_lw[3 * w + 2];
+        mx0 = max(mx0, t2);
+        sdur += t2 - t0;
+        swait += t1 - t0;
+        const unsigned bk = (unsigned)((t2 - mn0) / 500u);  // 5 us buckets of the END time
+        atomicAdd(&g_lhist[bk < 31u ? bk : 31u], 1u);
+      }
+      for (int o = 32; o; o >>= 1) {
+        mx0 = max(mx0, (unsigned long long)__shfl_xor((long long)mx0, o));
+        sdur += (unsigned long long)__shfl_xor((long long)sdur, o);
+        swait += (unsigned long long)__shfl_xor((long long)swait, o);
+      }
+      __threadfence();
+      if (ln2 == 0) {
+        printf("comb2 ladder %u waves: last end %.1f us, mean wave %.1f, mean first-entry wait %.1f; ends per 5 us: ",
+               waves, (mx0 - mn0) * 0.01, sdur * 0.01 / waves, swait * 0.01 / waves);
+        for (int k = 0; k < 32; k++) printf("%u ", atomicExch(&g_lhist[k], 0u));
+        printf("\n");
+        atomicExch(&g_lcount, 0u);
+      }
+    }
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------------------
