@@ -154,6 +154,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   if (const char* e = getenv("CBFT_SHA_LONG_GROUPS")) c->long_groups = std::max(0, std::min(1024, atoi(e)));
   if (const char* e = getenv("CBFT_HASH_PRIO")) c->hash_prio = atoi(e);
   if (const char* e = getenv("CBFT_HASH_LONG_PRIO")) c->long_prio = atoi(e);
+  if (const char* e = getenv("CBFT_LADDER_PREFETCH")) c->ladder_prefetch = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e);
   if (const char* e = getenv("CBFT_STAGE_ORDER_VAR")) c->stage_order_var = atoi(e);
   if (const char* e = getenv("CBFT_ORDER_MAX_STREAMS")) c->order_max_streams = atoi(e);
@@ -764,6 +765,7 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   w.long_groups = c->long_groups;
   w.hash_prio = c->hash_prio;
   w.long_prio = c->long_prio;
+  w.ladder_prefetch = c->ladder_prefetch;
   w.base_table = c->base_table.as<uint32_t>();
   w.h_soa = slot.h.as<uint32_t>();
   w.flags = slot.flags.as<uint8_t>();

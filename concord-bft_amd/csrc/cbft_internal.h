@@ -179,6 +179,7 @@ struct cbft_ctx {
   int finish_tree_block = 64;  // lanes per tree-finish block ($CBFT_FINISH_TREE_BLOCK: 64/128/256/512; 0 = wave butterflies)
   int long_groups = 0;  // $CBFT_SHA_LONG_GROUPS (0 = CBFT_SHA_LONG_GROUPS)
   int hash_prio = 0;    // $CBFT_HASH_PRIO
+  int ladder_prefetch = 0;  // $CBFT_LADDER_PREFETCH
   int long_prio = 0;    // $CBFT_HASH_LONG_PRIO  // lanes per tree-finish block ($CBFT_FINISH_TREE_BLOCK: 64/128/256/512)
   unsigned next_slot = 0;
   int finish_batch = 0;  // K4: signatures per lane sharing one inversion ($CBFT_FINISH_BATCH; 0 = by batch size)

@@ -143,6 +143,7 @@ struct Ed25519Work {
   int long_groups;  // cap of the long-message kernel's 64-signature groups (0 = CBFT_SHA_LONG_GROUPS)
   int hash_prio;    // K1 waves at raised issue priority (s_setprio 2)
   int long_prio;    // the long-message kernel's waves at s_setprio 3
+  int ladder_prefetch;  // K1 touches the pair ladder's first key-table entries (L2 / MALL warm-up)
 };
 // Block-count buckets of the hash sort: bucket min(nblocks, CBFT_SHA_BUCKETS - 1).
 #define CBFT_SHA_BUCKETS 256

@@ -438,10 +438,49 @@ __global__ void __launch_bounds__(256) ed25519_bucket_scatter_kernel(const Ed255
 // nshort (nullable): positions from *nshort on are ed25519_hash_long_kernel's.
 // PRIO > 0: the waves raise their issue priority (s_setprio) over the kernels they share SIMDs with
 // (the other batch's ladder): the hash stage is on each batch's dependency chain.
+#define COMB_STRIDE 32  // words per comb entry (defined with the comb kernels below)
+__device__ __forceinline__ void add256(uint32_t* s, const uint32_t* off);
+// Touch the pair ladder's first key-table entries of signature i (steps 0 and 1 of both lanes,
+// the phased split's key positions 0, 1, naper, naper + 1): one word of each 128-byte entry, so
+// the ladder's 2,048 waves, which all start together, find them in L2 / MALL instead of opening
+// with a cold ~29 MB burst (CBFT_LADDER_STAMPS: ~9 us of every wave's ~100).  The words are
+// discarded.  $CBFT_LADDER_PREFETCH=1 (A/B only): isolated ladder 108.7 -> 108.2 us for +4 us of
+// hash, headline within noise (profiles/r05_ab/ladder_entry_prefetch.txt): the first-entry wait is
+// the burst itself, not cold lines.
+__device__ __forceinline__ void ladder_entry_prefetch(const Ed25519Batch& b, size_t i, const uint32_t* hw,
+                                                      const CombLadder& cl) {
+  uint32_t s[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) s[k] = hw[k];
+  add256(s, cl.offA);
+  const uint32_t na = (uint32_t)cl.a.npos, naper = (na + 1u) >> 1, w = (uint32_t)cl.a.w;
+  const uint32_t half = 1u << (w - 1u), ents = (uint32_t)cl.a.entries();
+  const uint32_t* akey = b.keys.comb(batch_unit(b, i));
+  uint32_t acc = 0;
+#pragma unroll
+  for (int t = 0; t < 4; t++) {
+    const uint32_t pos = (t >> 1) * naper + (t & 1);
+    if (pos >= na) continue;
+    const uint32_t off = pos * w, wi = off >> 5;
+    uint32_t lo = 0, hi = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {  // s[wi], s[wi + 1] without dynamic register indexing
+      lo = (uint32_t)k == wi ? s[k] : lo;
+      hi = (uint32_t)k == wi + 1u ? s[k] : hi;
+    }
+    const uint32_t ch = (uint32_t)((((uint64_t)hi << 32) | lo) >> (off & 31u)) & ((1u << w) - 1u);
+    const int d = pos == na - 1u ? (int)(ch < half ? ch : half) : (int)ch - (int)half;
+    const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+    acc += akey[((size_t)pos * ents + ad) * COMB_STRIDE];
+  }
+  asm volatile("" ::"v"(acc));  // keep the loads
+}
+
 template <int PRIO>
 __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const Ed25519Batch b, const uint32_t* perm,
                                                                           const uint32_t* uniform, const uint32_t* nshort,
-                                                                          uint32_t* h_soa, uint8_t* flags) {
+                                                                          uint32_t* h_soa, uint8_t* flags,
+                                                                          const CombLadder cl, int prefetch) {
   if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= b.n || (nshort && g >= *nshort)) return;
@@ -452,6 +491,7 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const E
 #pragma unroll
   for (int k = 0; k < 8; k++) h_soa[k * b.n + i] = hw[k];
   flags[i] = flag ? 1 : 0;
+  if (prefetch) ladder_entry_prefetch(b, i, hw, cl);
 }
 
 // K1 for the sorted order's tail (messages of >= CBFT_SHA_LONG_BLOCKS blocks): 64 signatures per
@@ -2227,12 +2267,13 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
                          (const uint32_t*)w.perm, uniform_w, nshort_w, w.h_soa, w.flags);
     if ((e = hipEventRecord(w.join_ev, w.aux)) != hipSuccess) return e;
   }
+  const int pf = comb && w.comb_lanes == 2 && b.key_idx && w.ladder_prefetch ? 1 : 0;
   if (w.hash_prio)
     hipLaunchKernelGGL(ed25519_hash_kernel<2>, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
-                       uniform_w, nshort_w, w.h_soa, w.flags);
+                       uniform_w, nshort_w, w.h_soa, w.flags, w.comb, pf);
   else
     hipLaunchKernelGGL(ed25519_hash_kernel<0>, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
-                       uniform_w, nshort_w, w.h_soa, w.flags);
+                       uniform_w, nshort_w, w.h_soa, w.flags, w.comb, pf);
   // the next batch's hash may start behind this batch's short hashes while the long tail still
   // runs on the aux stream (hash_early), or only after the whole hash stage
   if (order && order->hash_early && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;
