@@ -1864,6 +1864,9 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
 #ifndef CBFT_LADDER_PRIO
 #define CBFT_LADDER_PRIO 0
 #endif
+#ifndef CBFT_LADDER_NOPPAD
+#define CBFT_LADDER_NOPPAD 0
+#endif
 // CBFT_LADDER_STAMPS (probe builds only): per-wave wall-clock stamps of the pair ladder (start,
 // first entry landed, end; 10 ns ticks) stored per wave; the last wave of a launch folds them and
 // prints the spread of the end times (launches must not overlap).
@@ -1996,6 +1999,11 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
       else
         __builtin_amdgcn_s_setprio(0);
     }
+#endif
+#if CBFT_LADDER_NOPPAD  // probe builds: pad each step with N 4-byte s_nop (instruction-fetch sensitivity)
+#define CBFT_STR2(x) #x
+#define CBFT_STR(x) CBFT_STR2(x)
+    asm volatile(".rept " CBFT_STR(CBFT_LADDER_NOPPAD) "\n\ts_nop 0\n\t.endr" ::: "memory");
 #endif
     if (jj + 1u < nper)
       asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // entry jj landed; jj + 1 may still fly
