@@ -1860,7 +1860,8 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
 // ~60 us, half at 120-140 us), so the second runs its tail alone; a priority that falls with
 // progress (3, 2, 1, 0 by quarter of the steps) keeps the lagging wave ahead.  Isolated ladder
 // 109 -> 105 us, but the pipelined headline loses (494-506 vs 511-516 M/s at 200 steps: the
-// co-running finish and hash kernels are starved), profiles/r05_ab/ladder_wave_ends_prio.txt.
+// co-running finish and hash kernels are starved), profiles/r05_ab/ladder_wave_ends_prio.txt;
+// = 2 (priority 1 for the first half only): isolated -1.7 %, pipelined 503-505 vs 511-513 M/s.
 #ifndef CBFT_LADDER_PRIO
 #define CBFT_LADDER_PRIO 0
 #endif
@@ -1987,7 +1988,11 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
 #pragma nounroll
   for (uint32_t jj = 0; jj < nper; jj++) {
     const uint32_t slot = jj & 1u;
-#if CBFT_LADDER_PRIO
+#if CBFT_LADDER_PRIO == 2
+    // two levels: the first half of the steps at priority 1, the rest at 0
+    if (jj == 0) __builtin_amdgcn_s_setprio(1);
+    if (jj == (nper >> 1)) __builtin_amdgcn_s_setprio(0);
+#elif CBFT_LADDER_PRIO
     {  // issue priority falls with progress: a SIMD's lagging wave outranks its leading one
       const uint32_t qtr = (jj * 4u) / nper;  // wave-uniform
       if (qtr == 0)
