@@ -232,12 +232,10 @@ static int bls_combine_range(cbft_ctx* c, const uint8_t* shares37, uint32_t k, u
   CBFT_HIP(c->bls_lambda.reserve((size_t)k * 8 * 4));
   CBFT_HIP(c->bls_partial.reserve((size_t)(2 * k + 16) * BLS_JAC_WORDS * 4));  // row MSM levels
   CBFT_HIP(c->bls_out.reserve(BLS_JAC_WORDS * 4));
-  // every share decoded? (the parse kernel wrote valid = decodable && id in range)
+  // every share decoded? (the parse kernel wrote valid = decodable && id in range).  Checked after
+  // the combine, in the same synchronisation: the combine only reads the shares valid marks, and its
+  // result is discarded when any share failed to decode (one host round trip instead of two).
   std::vector<uint8_t> v(k);
-  CBFT_HIP(hipMemcpyAsync(v.data(), c->bls_valid.p, k, hipMemcpyDeviceToHost, c->stream));
-  CBFT_HIP(hipStreamSynchronize(c->stream));
-  for (uint32_t j = 0; j < k; j++)
-    if (!v[j]) return CBFT_EINVAL;
   if (!multisig && !c->bls_inv.p) {  // inverses of 1..2048 mod r, once per context
     CBFT_HIP(c->bls_inv.reserve((size_t)BLS_INV_TABLE * 9 * 4));
     CBFT_HIP(cbft_bls_launch_inv_table(c->bls_inv.as<uint32_t>(), c->stream));
@@ -247,11 +245,13 @@ static int bls_combine_range(cbft_ctx* c, const uint8_t* shares37, uint32_t k, u
                                    c->bls_partial.as<uint32_t>(),
                                    c->bls_out.as<uint8_t>(), nullptr,
                                    out_part ? c->bls_out.as<uint32_t>() : nullptr, c->stream));
-  if (out_part)
-    CBFT_HIP(hipMemcpyAsync(out_part, c->bls_out.p, CBFT_BLS_G1_PARTIAL_BYTES, hipMemcpyDeviceToHost, c->stream));
-  else
-    CBFT_HIP(hipMemcpyAsync(out33, c->bls_out.p, 33, hipMemcpyDeviceToHost, c->stream));
+  std::vector<uint8_t> res(out_part ? CBFT_BLS_G1_PARTIAL_BYTES : 33);
+  CBFT_HIP(hipMemcpyAsync(res.data(), c->bls_out.p, res.size(), hipMemcpyDeviceToHost, c->stream));
+  CBFT_HIP(hipMemcpyAsync(v.data(), c->bls_valid.p, k, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipStreamSynchronize(c->stream));
+  for (uint32_t j = 0; j < k; j++)
+    if (!v[j]) return CBFT_EINVAL;  // outputs untouched
+  std::memcpy(out_part ? out_part : out33, res.data(), res.size());
   return CBFT_OK;
 }
 
@@ -388,7 +388,7 @@ int cbft_bls_combine_threshold(cbft_ctx* c, uint32_t id, const uint8_t* msg, uin
     return CBFT_OK;
   };
   std::vector<uint8_t> v(k ? k : 1, 0);
-  uint8_t ok = 0;
+  uint8_t ok = 0, sig33[33] = {0};
   bool done = false;
   if (optimistic && k) {
     CBFT_HIP(cbft_bls_launch_and(c->bls_first.as<uint8_t>(), c->bls_valid.as<uint8_t>(), c->bls_use.as<uint8_t>(), k,
@@ -397,6 +397,7 @@ int cbft_bls_combine_threshold(cbft_ctx* c, uint32_t id, const uint8_t* msg, uin
     if (rc) return rc;
     CBFT_HIP(hipMemcpyAsync(v.data(), c->bls_valid.p, k, hipMemcpyDeviceToHost, c->stream));
     CBFT_HIP(hipMemcpyAsync(&ok, c->bls_flag.p, 1, hipMemcpyDeviceToHost, c->stream));
+    CBFT_HIP(hipMemcpyAsync(sig33, c->bls_out.p, 33, hipMemcpyDeviceToHost, c->stream));
     CBFT_HIP(hipStreamSynchronize(c->stream));
     bool all_parsed = true;
     for (uint32_t j = 0; j < k; j++) all_parsed = all_parsed && (v[j] || !first[j]);
@@ -414,12 +415,13 @@ int cbft_bls_combine_threshold(cbft_ctx* c, uint32_t id, const uint8_t* msg, uin
     if (rc) return rc;
     if (k) CBFT_HIP(hipMemcpyAsync(v.data(), c->bls_valid.p, k, hipMemcpyDeviceToHost, c->stream));
     CBFT_HIP(hipMemcpyAsync(&ok, c->bls_flag.p, 1, hipMemcpyDeviceToHost, c->stream));
+    CBFT_HIP(hipMemcpyAsync(sig33, c->bls_out.p, 33, hipMemcpyDeviceToHost, c->stream));
     CBFT_HIP(hipStreamSynchronize(c->stream));
     if (k) std::memset(bad_bitmap, 0, (k + 7) / 8);
     for (uint32_t j = 0; j < k; j++)
       if (first[j] && !v[j]) bad_bitmap[j >> 3] |= (uint8_t)(1u << (j & 7));
   }
-  CBFT_HIP(hipMemcpy(out_sig33, c->bls_out.p, 33, hipMemcpyDeviceToHost));
+  std::memcpy(out_sig33, sig33, 33);  // copied back with the verdicts, before the last synchronisation
   *out_ok = ok ? 1 : 0;
   return CBFT_OK;
 }
