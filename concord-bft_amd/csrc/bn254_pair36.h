@@ -297,6 +297,68 @@ __device__ __forceinline__ void p36_line1(fp& f, const uint32_t* ln, const g1a& 
   p36_line1c(f, cm, co, P, g);
 }
 
+// CBFT_P36_LAMBDA_X: the Miller loops first form lambda' = -xP lambda for every normalised line
+// they will read (p36_lambda_x: 140 Fp products per pair over the wave's 64 lanes, into LDS); a
+// line's s = 1 term -xP (f_{k-1} lambda) = f_{k-1} lambda' is then the same two-product reduction
+// as the s = 2 term, and no lane multiplies by xP inside the loop (two products per lane per line
+// instead of three).
+#ifndef CBFT_P36_LAMBDA_X
+#define CBFT_P36_LAMBDA_X 1
+#endif
+// lx[(j (k1 - k0) + k - k0) 18 + 9 c + i] = limb i of component c of lambda'_k of pair j, k in [k0, k1);
+// Pn[j].x holds -xP_j.  The whole wave calls it.
+template <int NP>
+__device__ __forceinline__ void p36_lambda_x(uint32_t* lx, const g1a* Pn, const uint32_t* const* lines, int k0, int k1,
+                                             const P36& g) {
+  const int nl = k1 - k0, total = NP * nl * 2;
+#pragma nounroll
+  for (int base = 0; base < total; base += 64) {
+    const int item = base + g.lane;
+    const bool on = item < total;
+    const int it = on ? item : 0;
+    const int j = it / (2 * nl), r = it - j * 2 * nl, kk = r >> 1, c = r & 1;
+    const uint32_t* src = lines[0];
+    fp x = Pn[0].x;
+#pragma unroll
+    for (int q = 1; q < NP; q++) {
+      if (j == q) src = lines[q];
+      fp_sel(x, Pn[q].x, j == q);
+    }
+    fp l, prod;
+#pragma unroll
+    for (int i = 0; i < BN_LIMBS; i++) l.v[i] = src[(k0 + kk) * BN_LINE_WORDS + 9 * c + i];
+    f_mul(prod, l, x);
+    if (on)
+#pragma unroll
+      for (int i = 0; i < BN_LIMBS; i++) lx[(j * nl + kk) * 18 + 9 * c + i] = prod.v[i];
+  }
+}
+
+// the normalised line k with lambda' from p36_lambda_x (lxk: its 18 words) and mu from the table
+__device__ __forceinline__ void p36_line_lx(fp& f, const uint32_t* lxk, const uint32_t* ln, const g1a& P, const P36& g) {
+  fp om, oo;
+  p36_fetch(om, oo, f, g.s == 1 ? (g.k + 5) % 6 : (g.k + 3) % 6, g);
+  fp lm, lo, mm, mo;
+  p36_coef(lm, lo, lxk, g.h);
+  p36_coef(mm, mo, ln + 18, g.h);
+  const fp u = g.h ? oo : om, v = g.h ? om : oo;
+  fp X1 = g.s == 0 ? f : u;
+  fp Y1 = g.s == 0 ? P.y : (g.s == 1 ? lm : mm);
+  fp cz = g.s == 1 ? lo : mo;
+  const uint32_t mz = cs_mask(g.s != 0);
+#pragma unroll
+  for (int i = 0; i < BN_LIMBS; i++) cz.v[i] &= mz;
+  fp vn;
+  p36_cneg4(vn, v, g.h == 0);
+  fp T;
+  f_mul_sum2(T, X1, Y1, vn, cz);  // s = 0: f_k yP; s = 1: f_{k-1} lambda'; s = 2: f_{k-3} mu
+  const bool wrap = (g.s == 1 && g.k == 0) || (g.s == 2 && g.k < 3);
+  fp w;
+  p36_xi(w, T, g);
+  fp_sel(T, w, wrap);
+  p36_sum3(f, T, g);
+}
+
 // f <- f * (A yP + B xP w + C w^3) for an unnormalised line (bn254_g2wave.h, 54 words):
 //   s = 0: yP (f_k A);  s = 1: xP (f_{k-1} B) (xi for k = 0);  s = 2: f_{k-3} C (xi for k < 3)
 // Three multiplications per lane, as p36_line1.
@@ -610,15 +672,39 @@ __device__ __forceinline__ void p36_final_exp(fp& r, const fp& f, const P36& g) 
 #ifndef CBFT_P36_PREFETCH
 #define CBFT_P36_PREFETCH 0
 #endif
+// lx (nullable, LDS, NP x 70 x 18 words, normalised lines only): room for p36_lambda_x
 template <int NP, bool ABC = false>
 __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* const* lines, const P36& g,
-                                           const volatile int* progress = nullptr) {
+                                           const volatile int* progress = nullptr, uint32_t* lx = nullptr) {
   constexpr int W = ABC ? 54 : BN_LINE_WORDS;  // ABC: unnormalised lines (bn254_g2wave.h)
   p36_one(f, g);
   int k = 0;
   g1a Pn[NP];  // normalised lines take -xP (p36_line1c)
 #pragma unroll
   for (int j = 0; j < NP; j++) Pn[j] = ABC ? P[j] : p36_neg_x(P[j]);
+  if (CBFT_P36_LAMBDA_X && !ABC && !progress && lx) {
+    p36_lambda_x<NP>(lx, Pn, lines, 0, BN_ATE_LINES, g);
+    auto lline = [&](int j) { p36_line_lx(f, lx + (j * BN_ATE_LINES + k) * 18, lines[j] + k * W, P[j], g); };
+#pragma nounroll
+    for (int i = BN_ATE_DBL - 1; i >= 0; i--) {
+      p36_sqr(f, f, g);
+#pragma unroll
+      for (int j = 0; j < NP; j++) lline(j);
+      k++;
+      if (bn_ate_bit(i)) {
+#pragma unroll
+        for (int j = 0; j < NP; j++) lline(j);
+        k++;
+      }
+    }
+    p36_conj(f, f, g);
+    for (int t = 0; t < 2; t++) {
+#pragma unroll
+      for (int j = 0; j < NP; j++) lline(j);
+      k++;
+    }
+    return;
+  }
   if (CBFT_P36_PREFETCH && !ABC && !progress) {
     fp cm[NP], co[NP];
 #pragma unroll
@@ -687,14 +773,44 @@ __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* 
 // per lane (sqr 2, line 3) against 320 for the whole loop on one wave.
 #define P36_MILLER_SPLIT 40
 // ABC: unnormalised lines (54 words, bn254_g2wave.h) read once progress > k (nullable: all present)
+// lx (nullable, LDS, up to 70 x 18 words, normalised lines only): room for p36_lambda_x
 template <bool TOP, bool ABC = false>
 __device__ __forceinline__ void p36_miller_part(fp& f, const g1a& P, const uint32_t* lines, const P36& g,
-                                                const volatile int* progress = nullptr) {
+                                                const volatile int* progress = nullptr, uint32_t* lx = nullptr) {
   constexpr int W = ABC ? 54 : BN_LINE_WORDS;
   p36_one(f, g);
   int k = 0;
   const int hi = TOP ? BN_ATE_DBL - 1 : P36_MILLER_SPLIT - 1, lo = TOP ? P36_MILLER_SPLIT : 0;
   for (int i = BN_ATE_DBL - 1; i > hi; i--) k += bn_ate_bit(i) ? 2 : 1;
+  if (CBFT_P36_LAMBDA_X && !ABC && !progress && lx) {
+    int k1 = k;  // this part's lines: [k, k1)
+    for (int i = hi; i >= lo; i--) k1 += bn_ate_bit(i) ? 2 : 1;
+    if (!TOP) k1 += 2;  // the two Frobenius lines
+    const int k0 = k;
+    const g1a Pn = p36_neg_x(P);
+    const uint32_t* l1[1] = {lines};
+    p36_lambda_x<1>(lx, &Pn, l1, k0, k1, g);
+    auto lline = [&]() {
+      p36_line_lx(f, lx + (k - k0) * 18, lines + k * W, P, g);
+      k++;
+    };
+#pragma nounroll
+    for (int i = hi; i >= lo; i--) {
+      p36_sqr(f, f, g);
+      lline();
+      if (bn_ate_bit(i)) lline();
+    }
+    if (TOP) {
+#pragma nounroll
+      for (int t = 0; t < P36_MILLER_SPLIT; t++) p36_sqr(f, f, g);
+    }
+    p36_conj(f, f, g);
+    if (!TOP) {
+      lline();
+      lline();
+    }
+    return;
+  }
   // lines read one ahead (CBFT_P36_PREFETCH; the top part's last read is a bottom line, unused)
   constexpr bool PF = CBFT_P36_PREFETCH && !ABC;
   const g1a Pn = ABC ? P : p36_neg_x(P);  // normalised lines take -xP (p36_line1c)
@@ -867,8 +983,9 @@ __device__ __forceinline__ bool p36_is_one_after_final_exp_lead(const fp& f, FeM
 
 // prod_{j < NP} e(P_j, Q_j) == 1 on one wave
 template <int NP>
-__device__ __forceinline__ bool p36_pairing_check(const g1a* P, const uint32_t* const* lines, const P36& g) {
+__device__ __forceinline__ bool p36_pairing_check(const g1a* P, const uint32_t* const* lines, const P36& g,
+                                                  uint32_t* lx = nullptr) {
   fp f;
-  p36_miller<NP>(f, P, lines, g);
+  p36_miller<NP>(f, P, lines, g, nullptr, lx);
   return p36_is_one_after_final_exp(f, g);
 }
