@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
                                                                       uint32_t* sig, uint32_t* ids) {
   __shared__ PairXchg xc;
   __shared__ FeMail fm;  // WAVES = 2: the final exponentiation's helper wave (CBFT_P36_FE2)
-  __shared__ uint32_t lxs[2 * BN_ATE_LINES * 18];  // lambda' (p36_lambda_x): two pairs, or one per wave
+  __shared__ uint32_t lxs[2 * BN_ATE_LINES * P36_LX_WORDS];  // lambda' (p36_lambda_x): two pairs, or one per wave
   const uint32_t j = blockIdx.x;
   if (j >= k) return;  // whole blocks exit together
   const int wave = threadIdx.x >> 6;
@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
       g1a P = s;
       f_neg(P.y, s.y);
       const uint32_t* l[1] = {gen_lines};
-      p36_miller<1>(f, &P, l, g, nullptr, lxs + BN_ATE_LINES * 18);
+      p36_miller<1>(f, &P, l, g, nullptr, lxs + BN_ATE_LINES * P36_LX_WORDS);
     } else {
       p36_one(f, g);  // e(O, g2) = 1: an infinite sigma checks against e(H, vk) alone
     }
@@ -161,7 +161,7 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
                                                                   const uint32_t* sig_aff) {
   __shared__ PairXchg xc[3];  // the values of waves 1, 2, 3
   __shared__ FeMail fm;       // wave 1 helps wave 0's final exponentiation (CBFT_P36_FE2)
-  __shared__ uint32_t lxv[4 * BN_ATE_LINES * 18];  // lambda' of each wave's Miller part
+  __shared__ uint32_t lxv[4 * BN_ATE_LINES * P36_LX_WORDS];  // lambda' of each wave's Miller part
   if (blockIdx.x != 0) return;
   const int wave = threadIdx.x >> 6;
   const P36 g = p36_lane();
@@ -179,7 +179,7 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
     if (wave == 0)
       p36_miller_part<true>(f, P, pk_lines, g, nullptr, lxv);
     else
-      p36_miller_part<false>(f, P, pk_lines, g, nullptr, lxv + BN_ATE_LINES * 18);
+      p36_miller_part<false>(f, P, pk_lines, g, nullptr, lxv + BN_ATE_LINES * P36_LX_WORDS);
     BLS_PHASE(wave == 0 ? 5 : 13);
   } else {
     g1a s;
@@ -193,9 +193,9 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
       g1a P = s;
       f_neg(P.y, s.y);
       if (wave == 2)
-        p36_miller_part<true>(f, P, gen_lines, g, nullptr, lxv + 2 * BN_ATE_LINES * 18);
+        p36_miller_part<true>(f, P, gen_lines, g, nullptr, lxv + 2 * BN_ATE_LINES * P36_LX_WORDS);
       else
-        p36_miller_part<false>(f, P, gen_lines, g, nullptr, lxv + 3 * BN_ATE_LINES * 18);
+        p36_miller_part<false>(f, P, gen_lines, g, nullptr, lxv + 3 * BN_ATE_LINES * P36_LX_WORDS);
     } else {
       p36_one(f, g);  // e(O, g2) = 1
     }

@@ -305,18 +305,25 @@ __device__ __forceinline__ void p36_line1(fp& f, const uint32_t* ln, const g1a& 
 #ifndef CBFT_P36_LAMBDA_X
 #define CBFT_P36_LAMBDA_X 1
 #endif
-// lx[(j (k1 - k0) + k - k0) 18 + 9 c + i] = limb i of component c of lambda'_k of pair j, k in [k0, k1);
-// Pn[j].x holds -xP_j.  The whole wave calls it.
+// CBFT_P36_XI_PRE: the record also holds xi lambda' and xi mu, so the lanes whose term wraps (s = 1,
+// k = 0; s = 2, k < 3) read pre-twisted coefficients and no lane applies xi after the product.
+#ifndef CBFT_P36_XI_PRE
+#define CBFT_P36_XI_PRE 1
+#endif
+#define P36_LX_WORDS (CBFT_P36_XI_PRE ? 54 : 18)  // per line: lambda' | xi lambda' | xi mu (9-limb components)
+// lx[(j (k1 - k0) + k - k0) P36_LX_WORDS + ...] for pair j's line k in [k0, k1): lambda' = -xP lambda
+// (components 0, 1), then (CBFT_P36_XI_PRE) xi lambda', xi mu; Pn[j].x holds -xP_j.  One lane per
+// (pair, line); the whole wave calls it.
 template <int NP>
 __device__ __forceinline__ void p36_lambda_x(uint32_t* lx, const g1a* Pn, const uint32_t* const* lines, int k0, int k1,
                                              const P36& g) {
-  const int nl = k1 - k0, total = NP * nl * 2;
+  const int nl = k1 - k0, total = NP * nl;
 #pragma nounroll
   for (int base = 0; base < total; base += 64) {
     const int item = base + g.lane;
     const bool on = item < total;
     const int it = on ? item : 0;
-    const int j = it / (2 * nl), r = it - j * 2 * nl, kk = r >> 1, c = r & 1;
+    const int j = it / nl, kk = it - j * nl;
     const uint32_t* src = lines[0];
     fp x = Pn[0].x;
 #pragma unroll
@@ -324,27 +331,58 @@ __device__ __forceinline__ void p36_lambda_x(uint32_t* lx, const g1a* Pn, const 
       if (j == q) src = lines[q];
       fp_sel(x, Pn[q].x, j == q);
     }
-    fp l, prod;
+    src += (k0 + kk) * BN_LINE_WORDS;
+    fp2 l, r;
 #pragma unroll
-    for (int i = 0; i < BN_LIMBS; i++) l.v[i] = src[(k0 + kk) * BN_LINE_WORDS + 9 * c + i];
-    f_mul(prod, l, x);
+    for (int i = 0; i < BN_LIMBS; i++) {
+      l.a.v[i] = src[i];
+      l.b.v[i] = src[9 + i];
+    }
+    f_mul(r.a, l.a, x);
+    f_mul(r.b, l.b, x);
+    uint32_t* dst = lx + (j * nl + kk) * P36_LX_WORDS;
     if (on)
 #pragma unroll
-      for (int i = 0; i < BN_LIMBS; i++) lx[(j * nl + kk) * 18 + 9 * c + i] = prod.v[i];
+      for (int i = 0; i < BN_LIMBS; i++) {
+        dst[i] = r.a.v[i];
+        dst[9 + i] = r.b.v[i];
+      }
+    if (CBFT_P36_XI_PRE) {
+      fp2 m, t;
+#pragma unroll
+      for (int i = 0; i < BN_LIMBS; i++) {
+        m.a.v[i] = src[18 + i];
+        m.b.v[i] = src[27 + i];
+      }
+      fp2_mul_xi(t, r);
+      fp2_mul_xi(m, m);
+      if (on)
+#pragma unroll
+        for (int i = 0; i < BN_LIMBS; i++) {
+          dst[18 + i] = t.a.v[i];
+          dst[27 + i] = t.b.v[i];
+          dst[36 + i] = m.a.v[i];
+          dst[45 + i] = m.b.v[i];
+        }
+    }
   }
 }
 
-// the normalised line k with lambda' from p36_lambda_x (lxk: its 18 words) and mu from the table
+// the normalised line k with lambda' from p36_lambda_x (lxk: its record) and mu from the table
 __device__ __forceinline__ void p36_line_lx(fp& f, const uint32_t* lxk, const uint32_t* ln, const g1a& P, const P36& g) {
   fp om, oo;
   p36_fetch(om, oo, f, g.s == 1 ? (g.k + 5) % 6 : (g.k + 3) % 6, g);
+  const bool wrap = (g.s == 1 && g.k == 0) || (g.s == 2 && g.k < 3);
   fp lm, lo, mm, mo;
-  p36_coef(lm, lo, lxk, g.h);
+  // s = 1: lambda' (xi lambda' on wrap); s = 2 on wrap: xi mu (CBFT_P36_XI_PRE); else mu from the table
+  const int off = CBFT_P36_XI_PRE ? (g.s == 2 ? 36 : (wrap ? 18 : 0)) : 0;
+  p36_coef(lm, lo, lxk + off, g.h);
   p36_coef(mm, mo, ln + 18, g.h);
+  const bool use_lds = g.s == 1 || (CBFT_P36_XI_PRE && wrap);
   const fp u = g.h ? oo : om, v = g.h ? om : oo;
   fp X1 = g.s == 0 ? f : u;
-  fp Y1 = g.s == 0 ? P.y : (g.s == 1 ? lm : mm);
-  fp cz = g.s == 1 ? lo : mo;
+  fp Y1 = g.s == 0 ? P.y : (use_lds ? lm : mm);
+  fp cz = use_lds ? lo : mo;
   const uint32_t mz = cs_mask(g.s != 0);
 #pragma unroll
   for (int i = 0; i < BN_LIMBS; i++) cz.v[i] &= mz;
@@ -352,10 +390,11 @@ __device__ __forceinline__ void p36_line_lx(fp& f, const uint32_t* lxk, const ui
   p36_cneg4(vn, v, g.h == 0);
   fp T;
   f_mul_sum2(T, X1, Y1, vn, cz);  // s = 0: f_k yP; s = 1: f_{k-1} lambda'; s = 2: f_{k-3} mu
-  const bool wrap = (g.s == 1 && g.k == 0) || (g.s == 2 && g.k < 3);
-  fp w;
-  p36_xi(w, T, g);
-  fp_sel(T, w, wrap);
+  if (!CBFT_P36_XI_PRE) {
+    fp w;
+    p36_xi(w, T, g);
+    fp_sel(T, w, wrap);
+  }
   p36_sum3(f, T, g);
 }
 
@@ -672,7 +711,7 @@ __device__ __forceinline__ void p36_final_exp(fp& r, const fp& f, const P36& g) 
 #ifndef CBFT_P36_PREFETCH
 #define CBFT_P36_PREFETCH 0
 #endif
-// lx (nullable, LDS, NP x 70 x 18 words, normalised lines only): room for p36_lambda_x
+// lx (nullable, LDS, NP x 70 x P36_LX_WORDS words, normalised lines only): room for p36_lambda_x
 template <int NP, bool ABC = false>
 __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* const* lines, const P36& g,
                                            const volatile int* progress = nullptr, uint32_t* lx = nullptr) {
@@ -684,7 +723,7 @@ __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* 
   for (int j = 0; j < NP; j++) Pn[j] = ABC ? P[j] : p36_neg_x(P[j]);
   if (CBFT_P36_LAMBDA_X && !ABC && !progress && lx) {
     p36_lambda_x<NP>(lx, Pn, lines, 0, BN_ATE_LINES, g);
-    auto lline = [&](int j) { p36_line_lx(f, lx + (j * BN_ATE_LINES + k) * 18, lines[j] + k * W, P[j], g); };
+    auto lline = [&](int j) { p36_line_lx(f, lx + (j * BN_ATE_LINES + k) * P36_LX_WORDS, lines[j] + k * W, P[j], g); };
 #pragma nounroll
     for (int i = BN_ATE_DBL - 1; i >= 0; i--) {
       p36_sqr(f, f, g);
@@ -773,7 +812,7 @@ __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* 
 // per lane (sqr 2, line 3) against 320 for the whole loop on one wave.
 #define P36_MILLER_SPLIT 40
 // ABC: unnormalised lines (54 words, bn254_g2wave.h) read once progress > k (nullable: all present)
-// lx (nullable, LDS, up to 70 x 18 words, normalised lines only): room for p36_lambda_x
+// lx (nullable, LDS, up to 70 x P36_LX_WORDS words, normalised lines only): room for p36_lambda_x
 template <bool TOP, bool ABC = false>
 __device__ __forceinline__ void p36_miller_part(fp& f, const g1a& P, const uint32_t* lines, const P36& g,
                                                 const volatile int* progress = nullptr, uint32_t* lx = nullptr) {
@@ -791,7 +830,7 @@ __device__ __forceinline__ void p36_miller_part(fp& f, const g1a& P, const uint3
     const uint32_t* l1[1] = {lines};
     p36_lambda_x<1>(lx, &Pn, l1, k0, k1, g);
     auto lline = [&]() {
-      p36_line_lx(f, lx + (k - k0) * 18, lines + k * W, P, g);
+      p36_line_lx(f, lx + (k - k0) * P36_LX_WORDS, lines + k * W, P, g);
       k++;
     };
 #pragma nounroll
