@@ -106,7 +106,7 @@ struct BlsKeySet {
 // event orders its reuse after its previous batch.  With two streams two slots are enough (each
 // stream's order already serialises its own batches); callers with more streams in flight
 // (config #3's long-message tails) use more ($CBFT_WORK_SLOTS, default 4).
-#define CBFT_MAX_WORK_SLOTS 4
+#define CBFT_MAX_WORK_SLOTS 8
 struct WorkSlot {
   DevBuf h, flags, xyz, ps_tbl, ps_aok;
   DevBuf perm, buckets;  // hash order of a variable-length batch (counting sort by SHA-512 blocks)
@@ -171,7 +171,7 @@ struct cbft_ctx {
   uint32_t next_table_id = 1;
   // per-batch work buffers
   WorkSlot slots[CBFT_MAX_WORK_SLOTS];
-  int work_slots = CBFT_MAX_WORK_SLOTS;
+  int work_slots = 4;  // $CBFT_WORK_SLOTS (1 .. CBFT_MAX_WORK_SLOTS)
   // the next batch's hash waits for this batch's SHORT-message hash only, not for the long tail
   // hashing on the slot's aux stream ($CBFT_HASH_ORDER_EARLY, default 1)
   int hash_order_early = 1;

@@ -21,7 +21,7 @@ torch.cuda.set_device(0)
 ss = workload.make_sigset(65536, nkeys=4096, msg_len=(64, 4096), seed=0xBADC0DE, invalid_frac=0.10, threads=16)
 with cb.Context(device=0) as ctx:
     tid = ctx.load_keys(ss.pk)
-    value, hash_ms = bench._mixed_device_resident(ctx, tid, ss, args)
+    value, hash_ms, _steps = bench._mixed_device_resident(ctx, tid, ss, args)
 print(json.dumps({"device_resident_value": value, "hash_ms": hash_ms, "streams": args.mixed_streams,
                   "work_slots": os.environ.get("CBFT_WORK_SLOTS", "default"),
                   "hash_order_early": os.environ.get("CBFT_HASH_ORDER_EARLY", "default")}))
