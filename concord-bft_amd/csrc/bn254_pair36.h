@@ -106,11 +106,24 @@ __device__ __forceinline__ void p36_fetch(fp& m, fp& o, const fp& x, int k2, con
 }
 
 // r = sum over the three sub-lanes of component (k, h) of part, in the order 0, 1, 2
+// CBFT_P36_SUM3_LAZY: one limb-wise three-term sum (< 6q), one carry pass and fp_reduce64 instead of
+// two reduced additions (each with its own conditional 2q subtraction and wave vote)
+#ifndef CBFT_P36_SUM3_LAZY
+#define CBFT_P36_SUM3_LAZY 1
+#endif
 __device__ __forceinline__ void p36_sum3(fp& r, const fp& part, const P36& g) {
   fp q0, q1, q2;
   p36_gather3(q0, q1, q2, part, g);
-  f_add(r, q0, q1);
-  f_add(r, r, q2);
+  if (CBFT_P36_SUM3_LAZY) {
+    fp x;
+#pragma unroll
+    for (int i = 0; i < BN_LIMBS; i++) x.v[i] = q0.v[i] + q1.v[i] + q2.v[i];  // inputs < 2q, normalised
+    cs_carry(x);
+    fp_reduce64(r, x);
+  } else {
+    f_add(r, q0, q1);
+    f_add(r, r, q2);
+  }
 }
 
 // my component of xi * z, z held componentwise by this lane and its partner (same k, s)
