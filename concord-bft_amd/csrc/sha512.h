@@ -43,11 +43,20 @@ __device__ __forceinline__ uint64_t rotr64(uint64_t x) {
 // gfx950 v_bitop3_b32: any 3-input boolean function in one instruction; the truth table is
 // indexed by (S0, S1, S2) with S0 <-> 0xf0, S1 <-> 0xcc, S2 <-> 0xaa (0x96 = xor3, 0xe8 = majority,
 // 0xca = S0 ? S1 : S2).  The compiler does not form it from a ^ b ^ c by itself.
+#ifndef CBFT_SHA_PAIR_PIN
+#define CBFT_SHA_PAIR_PIN 1
+#endif
 template <uint32_t T>
 __device__ __forceinline__ uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
   const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, T);
   const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), T);
-  return ((uint64_t)hi << 32) | lo;
+  uint64_t r = ((uint64_t)hi << 32) | lo;
+#if CBFT_SHA_PAIR_PIN && defined(__HIP_DEVICE_COMPILE__)
+  // one 64-bit value in a register pair: otherwise LLVM splits the following 64-bit adds into
+  // zero-extended halves (~6 v_mov + 4 extra v_lshl_add_u64 per 16 rounds' schedule words)
+  asm("" : "+v"(r));
+#endif
+  return r;
 }
 // x >> N (64-bit, N < 32) as v_alignbit_b32 + v_lshrrev_b32
 template <int N>
