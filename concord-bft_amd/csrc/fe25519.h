@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "fe25519_asm.h"
 #include "safegcd30.h"
 
 #define FE_LIMBS 9
@@ -352,9 +353,51 @@ FE_INLINE void fe_mul2(fe& r1, const fe& a1, const fe& b1, fe& r2, const fe& a2,
   r2 = o2;
 }
 
+// CBFT_FE_ONEASM: a whole multiply / square (fe25519_asm.h, generated by tools/gen/fe25519_asm.py:
+// the same mads in the same order as the column-per-statement form) as ONE asm statement.  The
+// compiler puts an s_nop between an asm statement and an instruction right after it that reads
+// its results, since it cannot see inside the text: 17 per multiply with a statement per column,
+// 1 with one statement.  The accumulator is pinned to v[20:21] so the text can split its digits.
+#ifndef CBFT_FE_ONEASM
+#define CBFT_FE_ONEASM 1
+#endif
+#define CBFT_FE_ASM_OUT                                                                                \
+  [acc] "=&{v[20:21]}"(acc), [cc] "=s"(cc), [o0] "=&v"(o.v[0]), [o1] "=&v"(o.v[1]), [o2] "=&v"(o.v[2]), \
+      [o3] "=&v"(o.v[3]), [o4] "=&v"(o.v[4]), [o5] "=&v"(o.v[5]), [o6] "=&v"(o.v[6]), [o7] "=&v"(o.v[7]), \
+      [o8] "=&v"(o.v[8]), [h0] "=&v"(h[0]), [h1] "=&v"(h[1]), [h2] "=&v"(h[2]), [h3] "=&v"(h[3]),      \
+      [h4] "=&v"(h[4]), [h5] "=&v"(h[5]), [h6] "=&v"(h[6]), [h7] "=&v"(h[7]), [h8] "=&v"(h[8])
+#define CBFT_FE_ASM_IN9(N, X)                                                                     \
+  [N##0] "v"(X[0]), [N##1] "v"(X[1]), [N##2] "v"(X[2]), [N##3] "v"(X[3]), [N##4] "v"(X[4]),    \
+      [N##5] "v"(X[5]), [N##6] "v"(X[6]), [N##7] "v"(X[7]), [N##8] "v"(X[8])
+FE_INLINE void fe_oneasm_final(fe& r, fe& o, uint64_t acc) {
+  // acc < 2^34.2: carry of weight 2^261 == 1216
+  uint64_t w = acc * 1216ull + (uint64_t)o.v[0];
+  o.v[0] = (uint32_t)w & FE_MASK;
+  o.v[1] += (uint32_t)(w >> 29);
+  r = o;
+}
+FE_INLINE void fe_mul_oneasm(fe& r, const fe& a, const fe& b) {
+  fe o;
+  uint32_t h[9];
+  uint64_t acc, cc;
+  asm(CBFT_FE_MUL_ASM : CBFT_FE_ASM_OUT : CBFT_FE_ASM_IN9(a, a.v), CBFT_FE_ASM_IN9(b, b.v), [k1216] "v"(1216u));
+  fe_oneasm_final(r, o, acc);
+}
+FE_INLINE void fe_sq_oneasm(fe& r, const fe& a, const uint32_t* a2) {
+  fe o;
+  uint32_t h[9];
+  uint64_t acc, cc;
+  asm(CBFT_FE_SQ_ASM : CBFT_FE_ASM_OUT : CBFT_FE_ASM_IN9(a, a.v), CBFT_FE_ASM_IN9(d, a2), [k1216] "v"(1216u));
+  fe_oneasm_final(r, o, acc);
+}
+
 template <bool C = CBFT_FE_CHAIN>
 FE_INLINE void fe_mul(fe& r, const fe& a, const fe& b) {
 #if CBFT_FE_ASMCOL
+  if (C && CBFT_FE_ONEASM) {
+    fe_mul_oneasm(r, a, b);
+    return;
+  }
   if (C) {
     fe o;
     uint32_t h[9];
@@ -402,6 +445,10 @@ FE_INLINE void fe_sq(fe& r, const fe& a) {
 #pragma unroll
   for (int i = 0; i < FE_LIMBS; i++) a2[i] = a.v[i] << 1;
 #if CBFT_FE_ASMCOL
+  if (C && CBFT_FE_ONEASM) {
+    fe_sq_oneasm(r, a, a2);
+    return;
+  }
   if (C) {
     uint32_t h[9];
     uint64_t t = 0;
