@@ -11,20 +11,25 @@ WORLD_SIZE differs from --gpus exits non-zero.
 A step = one batch of `--batch` (default 65,536) synthetic signed 256-byte messages per GPU,
 4,096 keys, BASELINE config #2: the key tables resident on the GPU and, as the bench contract
 defines `value`, the batch (signatures, key indices, messages) already resident in HBM when the
-timed region starts.  Batches go through cbft_ed25519_verify_fixed_device alternating over two
-streams, verdict words left in HBM.  When N > 1 each rank verifies its own static shard (weak
-scaling) and the per-rank verdict words are all-gathered over RCCL (the only cross-GPU traffic
-north_star prescribes).  value = signatures verified by all ranks / max-over-ranks wall time.
+timed region starts.  Each GPU holds `--distinct` (default 8) different signed batches with 1 %
+planted invalid signatures and the steps cycle through them over three streams
+(cbft_ed25519_verify_fixed_device); each step writes its own verdict words, and after the region
+every step's words are compared with the OpenSSL verdicts of the batch it verified.  When N > 1
+each rank verifies its own static shard (weak scaling) and each step's verdict words are
+all-gathered over RCCL (the only cross-GPU traffic north_star prescribes); the rank path is
+concord-bft_amd/cbft_multigpu.py, which the gloo CPU tests drive.  value = signatures verified by
+all ranks / max-over-ranks wall time.  Config #5 (1,048,576 signatures sharded over the ranks, one
+all-gather) is timed beside it as `flood_config5`.
 
 SURVEY.md §8(d) also quotes config #2 with the host -> device copy inside the step: that rate
-(`pcie_inclusive_value`: pinned host batch -> cbft_ed25519_verify_fixed_async, batch i+1's copy
-under batch i's kernels, bitmap back on the host) is timed the same way and reported beside it,
-with its PCIe bound.
+(`pcie_inclusive_value`: pinned host batches -> cbft_ed25519_verify_fixed_async, batch i+1's copy
+under batch i's kernels, bitmap back on the host) is timed the same way over the same distinct
+batches, every step's bitmap checked, and reported beside it with its PCIe bound.
 
 Verdicts are checked bit-exact against the host OpenSSL before any number is printed.  Also
 reported: the roofline of the dominant kernel (INT32 VALU, SURVEY.md §8(d) algorithmic ops) with
 the PCIe host->device bound of the PCIe-inclusive rate beside it,
-the host-CPU OpenSSL baseline on every core this process may use (rank 0, N = 1), p50 latency at
+the host-CPU OpenSSL baseline on every core this process may use (rank 0, every N), p50 latency at
 batch 1K, and the config #3 / #4 / RSA side measurements.
 """
 from __future__ import annotations
@@ -44,6 +49,7 @@ for p in (os.path.join(ROOT, "concord-bft_amd"), os.path.join(ROOT, "tools")):
     sys.path.insert(0, p)
 
 import cbft_hipcrypto as cb  # noqa: E402  (ctypes binding; the library loads at the first Context)
+import cbft_multigpu as mg  # noqa: E402  (the rank path: timing, per-step verdicts + all-gathers, flood plan)
 import gpu_clocks  # noqa: E402  (sclk / mclk through amdsmi, best effort)
 import parity_gate  # noqa: E402  (golden-data verdict gate, run before anything is timed)
 import tree_hash  # noqa: E402  (csrc stamp: PMC records are attached only to the tree they describe)
@@ -74,6 +80,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--msg-len", type=int, default=256)
+    ap.add_argument("--distinct", type=int, default=8,
+                    help="distinct signed batches per GPU cycled through the timed loops (8 x 21 MB of inputs)")
+    ap.add_argument("--invalid-frac", type=float, default=0.01,
+                    help="planted invalid signatures per batch (R / S / message bit flips, S + L, wrong key)")
+    ap.add_argument("--flood", type=int, default=1 << 20,
+                    help="config #5: total signatures sharded over the ranks (0 = skip)")
+    ap.add_argument("--flood-reps", type=int, default=5)
     ap.add_argument("--nkeys", type=int, default=4096)
     ap.add_argument("--comb-radix", type=int, default=13,
                     help="radix 2^r of the per-key comb tables (8..15; 13 = 10.5 MB per key, 43 GB at 4,096 keys; "
@@ -168,152 +181,204 @@ def main():
     clocks = gpu_clocks.Clocks(torch, dev.index)
     clk_before = clocks.read()  # here, not between the warm-up and the timed region (no idle gap there)
 
-    # ---- workload: this rank's static shard (weak scaling), signed by host OpenSSL
+    # ---- workload: this rank's static shard (weak scaling).  --distinct batches (default 8), each its
+    # own set of n OpenSSL-signed L-byte messages over the same 4,096 keys with --invalid-frac
+    # (default 1 %) planted bad signatures (a flipped bit of R, S or M, S + L, the wrong key: every one
+    # runs the whole hash -> ladder -> finish pipeline).  The timed loops cycle through the batches,
+    # each step writes its own verdict words, and after each timed region every step's words are
+    # compared with the OpenSSL verdicts of the batch it verified (a stale or skipped launch leaves
+    # zero words, which 99 % valid batches cannot match).
     n, L = args.batch, args.msg_len
-    ss = workload.make_sigset(n, nkeys=args.nkeys, msg_len=L, seed=0xC0FFEE + rank, threads=min(cpu_threads, 64))
+    nb = max(1, args.distinct)
+    nwords = (n + 63) // 64
+    gen_t0 = time.perf_counter()
+    sets = [workload.make_sigset(n, nkeys=args.nkeys, msg_len=L, seed=0xC0FFEE + rank + 7919 * b,
+                                 invalid_frac=args.invalid_frac, threads=min(cpu_threads, 64)) for b in range(nb)]
+    gen_s = time.perf_counter() - gen_t0
+    ss = sets[0]
+    invalid = [int((~s.expected).sum()) for s in sets]
     ctx = cb.Context(device=dev.index, max_batch=n)
     # parity first: every golden verdict class (Ed25519 edge cases through both key modes, the
     # RELIC key fixture, RSA accepts and rejects); any mismatch exits non-zero before timing
     parity = parity_gate.run(ctx, rsa=args.extras, relic=args.extras)
-
-    # the batch as a caller builds it: in one pinned host block (cbft_host_alloc) laid out as
-    # cbft_ed25519_batch_layout says, so each step's host -> device transfer is one DMA
-    blk, h_kidx, h_sig, b_raw = ctx.batch_views(n, L)
-    h_kidx[:] = ss.key_idx
-    h_sig[:] = ss.sig
-    b_raw[:] = ss.blob[: n * L]
-    depth = max(1, args.inflight)
-    outs = [np.zeros(n // 8 + 1, dtype=np.uint8) for _ in range(depth)]
-    nbytes = (n + 7) // 8
+    # the OpenSSL verdict words of every batch on this device (and, N > 1, every rank's)
+    exp_rows = torch.from_numpy(np.stack([mg.bools_to_words(s.expected) for s in sets])).to(dev)
+    all_exp = mg.all_gather_rows(exp_rows, world, dist) if world > 1 else None
     gstream = torch.cuda.Stream(device=dev) if world > 1 else None
-    gathered = [torch.zeros(world * nbytes, dtype=torch.uint8, device=dev) for _ in range(depth)] \
-        if world > 1 else None
 
-    def gather(j):  # RCCL all-gather of this rank's verdict bitmap (every rank gets all bitmaps)
-        with torch.cuda.stream(gstream):
-            mine = torch.from_numpy(outs[j][:nbytes]).to(dev, non_blocking=True)
-            dist.all_gather_into_tensor(gathered[j], mine)
+    def verdicts(steps):  # per-step verdict words (+ their all-gathers when N > 1)
+        return mg.StepVerdicts(nwords, steps, world, rank, dist, dev, gstream)
 
-    def run(steps: int):
-        tickets = []
-        for st in range(steps):
-            tickets.append(ctx.verify_async(tid, h_kidx, h_sig, b_raw, outs[st % depth], msg_len=L, n=n))
-            if world > 1 and st >= depth - 1:
-                ctx.wait(tickets[st - depth + 1])
-                gather((st - depth + 1) % depth)
-        for st in range(max(0, steps - depth), steps):
-            ctx.wait(tickets[st])
-            if world > 1:
-                gather(st % depth)
+    def require_exact(ver, what, steps=None):
+        bad = ver.mismatches(exp_rows, lambda j: j % nb, steps, all_exp)
+        if world > 1:
+            bad = mg.sum_over_ranks(bad, dist, dev)
+        if bad:
+            raise SystemExit(f"rank {rank}: {what}: {bad} verdict words differ from OpenSSL's")
 
-    def check(out, what):
-        got = cb.bitmap_to_bools(out[:nbytes].tobytes(), n)
-        if not np.array_equal(got, ss.expected):
-            raise SystemExit(f"rank {rank}: {what}: GPU verdicts differ from OpenSSL on "
-                             f"{int((got != ss.expected).sum())} signatures")
-
+    def sync_all():
+        torch.cuda.synchronize()
+        if gstream is not None:
+            gstream.synchronize()
 
     def timed(fn, steps):
         """Contract timing: barrier + synchronize on both sides, max over ranks."""
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        fn(steps)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el], dtype=torch.float64, device=dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return el
+        return mg.timed_region(fn, steps, dist if world > 1 else None, sync_all, dev)
+
+    # the batches as a caller builds them: each in one pinned host block (cbft_host_alloc) laid out as
+    # cbft_ed25519_batch_layout says, so each step's host -> device transfer is one DMA
+    blocks = []
+    for s in sets:
+        blk, h_kidx, h_sig, b_raw = ctx.batch_views(n, L)
+        h_kidx[:] = s.key_idx
+        h_sig[:] = s.sig
+        b_raw[:] = s.blob[: n * L]
+        blocks.append((blk, h_kidx, h_sig, b_raw))
+    depth = max(1, args.inflight)
+
+    def run(steps, bitmaps, ver=None):
+        """Host-buffer pipeline: step st verifies batch st % nb into bitmaps[st % len(bitmaps)],
+        `depth` batches in flight; ver (N > 1: the gather, and the post-region check) takes each
+        step's bitmap once cbft_wait has delivered it."""
+        tickets = []
+
+        def done(st):
+            ctx.wait(tickets[st])
+            if ver is not None:
+                ver.after_host_step(st, bitmaps[st % len(bitmaps)])
+
+        for st in range(steps):
+            _, h_kidx, h_sig, b_raw = blocks[st % nb]
+            tickets.append(ctx.verify_async(tid, h_kidx, h_sig, b_raw, bitmaps[st % len(bitmaps)], msg_len=L, n=n))
+            if st >= depth - 1:
+                done(st - depth + 1)
+        for st in range(max(0, steps - depth + 1), steps):
+            done(st)
+
+    def host_mismatch(bitmaps, steps):
+        bad = 0
+        for st in range(steps):
+            got = cb.bitmap_to_bools(bitmaps[st][: (n + 7) // 8].tobytes(), n)
+            bad += int((got != sets[st % nb].expected).sum())
+        return bad
 
     # ---- the headline: inputs resident in HBM, cbft_ed25519_verify_fixed_device (the device form
     # of the fixed-length call; config #2's messages are all L bytes) rotating over --streams streams
-    # (default 3: each stream's hash -> ladder -> finish chain then covers three batches),
-    # verdict words left in HBM; with N > 1 each rank's words are all-gathered over RCCL.
+    # (default 3: each stream's hash -> ladder -> finish chain then covers three batches) and over
+    # the nb distinct batches; verdict words left in HBM (a buffer per step); with N > 1 each step's
+    # words are all-gathered over RCCL on the gather stream.
     def to_dev(a: np.ndarray, dtype):
         return torch.from_numpy(np.ascontiguousarray(a).view(dtype)).to(dev)
 
-    d_sig, d_blob = to_dev(ss.sig.reshape(-1), np.uint8), to_dev(ss.blob, np.uint8)
-    d_kidx = to_dev(ss.key_idx.view(np.int32), np.int32)
+    for s in sets:
+        assert np.array_equal(s.off, np.arange(n, dtype=s.off.dtype) * L), "config #2 blob is n x L bytes"
+    dsets = [(to_dev(s.sig.reshape(-1), np.uint8), to_dev(s.blob, np.uint8), to_dev(s.key_idx.view(np.int32), np.int32))
+             for s in sets]
     nst = max(1, args.streams)
     streams = [torch.cuda.Stream(device=dev) for _ in range(nst)]
-    nwords = (n + 63) // 64
-    d_verd = [torch.zeros(nwords, dtype=torch.int64, device=dev) for _ in range(nst)]
-    d_gath = [torch.zeros(world * nwords, dtype=torch.int64, device=dev) for _ in range(nst)] if world > 1 else None
 
-    assert np.array_equal(ss.off, np.arange(n, dtype=ss.off.dtype) * L), "config #2 blob is n x L bytes"
-
-    def dstep(j, table=None):
+    def dstep(j, ver, table=None):
         s = streams[j % nst]
-        if world > 1:
-            s.wait_stream(gstream)  # the slot's previous all-gather has read its words
+        d_sig, d_blob, d_kidx = dsets[j % nb]
         ctx.verify_fixed_device(tid if table is None else table, 0, d_kidx.data_ptr(), d_sig.data_ptr(),
-                                d_blob.data_ptr(), L, n, d_verd[j % nst].data_ptr(), s.cuda_stream)
-        if world > 1:
-            gstream.wait_stream(s)
-            with torch.cuda.stream(gstream):
-                dist.all_gather_into_tensor(d_gath[j % nst], d_verd[j % nst])
+                                d_blob.data_ptr(), L, n, ver.words_ptr(j), s.cuda_stream)
+        ver.after_step(j, s)
 
-    def drun(steps):
-        for j in range(steps):
-            dstep(j)
+    def drun_with(ver, table=None):
+        def go(steps):
+            for j in range(steps):
+                dstep(j, ver, table)
+        return go
 
     def headline():
-        """warm-up + the contract's timed region + the verdict check (every stream's words)."""
-        drun(max(args.warmup, 2))
-        el = timed(drun, args.steps)
-        return el, clocks.read()
+        """warm-up + the contract's timed region; every step's words checked after it."""
+        drun_with(verdicts(max(args.warmup, 2)))(max(args.warmup, 2))
+        ver = verdicts(args.steps)
+        el = timed(drun_with(ver), args.steps)
+        clk = clocks.read()
+        require_exact(ver, "headline (device-resident)")
+        return el, clk
 
     t_keys = time.perf_counter()
     tid = ctx.load_keys(ss.pk, radix=args.comb_radix)  # key tables resident, like SigManager's verifiers
     key_load_ms = (time.perf_counter() - t_keys) * 1e3
     if args.headline_first:  # (an A/B option: measured slower, the GFX clock runs lower after the build)
         elapsed, clk_after = headline()
-    # ---- the host pipeline's parity gate (the device path's verdicts are checked after its timed
-    # region, every stream's words; the golden gate above ran before anything was timed)
-    run(1)
-    check(outs[0], "host pipeline")
-    parity["config2_headline"] = {"n": n, "invalid": int((~ss.expected).sum()), "mismatch": 0,
-                                  "reference": "host OpenSSL EVP_DigestVerify(ED25519)"}
-    if world > 1:
-        torch.cuda.synchronize()
-        mine = gathered[0].view(world, nbytes)[rank].cpu().numpy()
-        assert np.array_equal(mine, outs[0][:nbytes]), "all-gather lost this rank's bitmap"
-    for o in outs:
-        o[:] = 0
+    # ---- the host pipeline's first check: one pass over every batch, before anything else is timed
+    first = [np.zeros(nwords * 8, dtype=np.uint8) for _ in range(nb)]
+    run(nb, first)
+    if host_mismatch(first, nb):
+        raise SystemExit(f"rank {rank}: host pipeline: GPU verdicts differ from OpenSSL on "
+                         f"{host_mismatch(first, nb)} signatures")
     # ---- PCIe-inclusive rate (SURVEY.md §8(d) config #2 as written: sig + msg copied from pinned
     # host memory each step, bitmap back to the host).  Reported beside `value`, never as it: the
     # contract's value has its inputs resident in HBM when the timed region starts.
-    run(args.warmup)
-    pcie_elapsed = timed(run, args.steps)
+    run(args.warmup, [np.zeros(nwords * 8, dtype=np.uint8) for _ in range(depth)])
+    bitmaps = [np.zeros(nwords * 8, dtype=np.uint8) for _ in range(max(1, args.steps))]
+    hver = verdicts(args.steps) if world > 1 else None
+    pcie_elapsed = timed(lambda k: run(k, bitmaps, hver), args.steps)
     pcie_value = world * n * args.steps / pcie_elapsed
-    for j in range(min(depth, args.steps)):  # every in-flight slot produced the exact verdicts
-        check(outs[j], "pipelined batch")
+    if host_mismatch(bitmaps, args.steps):  # every step's bitmap, against its own batch
+        raise SystemExit(f"rank {rank}: PCIe-inclusive leg: GPU verdicts differ from OpenSSL")
+    if hver is not None:
+        require_exact(hver, "PCIe-inclusive leg (all-gathered bitmaps)")
     if not args.headline_first:
         elapsed, clk_after = headline()
     value = world * n * args.steps / elapsed
-    def check_device(what):
-        for j, d in enumerate(d_verd):
-            if not np.array_equal(cb.bitmap_to_bools(d.cpu().numpy().view(np.uint8).tobytes(), n), ss.expected):
-                raise SystemExit(f"rank {rank}: {what}: device-path verdicts differ from OpenSSL")
-            if world > 1:
-                mine = d_gath[j].view(world, nwords)[rank]
-                assert torch.equal(mine, d), "all-gather lost this rank's verdict words"
+    parity["config2_headline"] = {"batches": nb, "n": n * nb, "invalid": int(sum(invalid)), "mismatch": 0,
+                                  "steps_checked": args.steps,
+                                  "reference": "host OpenSSL EVP_DigestVerify(ED25519), each step's verdict words "
+                                               "against the batch it verified (device and PCIe legs)"}
 
-    check_device("headline")
+    # ---- SURVEY.md §8(d) config #5: 1,048,576 signatures (--flood) statically sharded over the ranks
+    # (131,072 per GPU at N = 8), each rank's shard as calls of `n` over the distinct batches on the
+    # headline's streams, then ONE all-gather of the shard's verdict words (16 KiB per GPU at 8);
+    # a fixed total, so this is the strong-scaling figure beside the weak-scaling `value`
+    flood = None
+    if args.flood:
+        total = args.flood
+        plan = mg.flood_plan(total, world, rank, n)
+        sw = mg.shard_size(total, world) // 64
+        fwords = torch.zeros(sw, dtype=torch.int64, device=dev)
+        fexp = torch.from_numpy(mg.flood_expected(plan, [s.expected for s in sets], sw, lambda c: c % nb)).to(dev)
+        cur = torch.cuda.current_stream(dev)
+        fout = {}
+
+        def flood_run(reps):
+            for _ in range(reps):
+                for c, (o, m) in enumerate(plan):
+                    s = streams[c % nst]
+                    s.wait_stream(cur)  # the previous flood's gather has read the words
+                    d_sig, d_blob, d_kidx = dsets[c % nb]
+                    ctx.verify_fixed_device(tid, 0, d_kidx.data_ptr(), d_sig.data_ptr(), d_blob.data_ptr(), L, m,
+                                            fwords.data_ptr() + (o // 64) * 8, s.cuda_stream)
+                for s in streams:
+                    cur.wait_stream(s)
+                fout["g"] = mg.gather_verdicts(fwords, total, world, dist) if world > 1 else fwords
+
+        flood_run(1)
+        reps = max(1, args.flood_reps)
+        fel = timed(flood_run, reps)
+        bad = int((fwords != fexp).sum().item())
+        if world > 1:
+            want = mg.all_gather_rows(fexp, world, dist).view(-1)[: (total + 63) // 64]
+            bad = mg.sum_over_ranks(bad + int((fout["g"] != want).sum().item()), dist, dev)
+        if bad:
+            raise SystemExit(f"rank {rank}: config #5 flood: {bad} verdict words differ from OpenSSL's")
+        flood = {"total_signatures": total, "per_rank": mg.shard_size(total, world), "calls_per_rank": len(plan),
+                 "reps": reps, "ms_per_flood": fel / reps * 1e3, "value": total * reps / fel, "mismatch": 0,
+                 "gather_bytes_per_rank": sw * 8 if world > 1 else 0,
+                 "scaling": "strong (fixed total over the ranks)"}
+        parity["config5_flood"] = {"n": total, "mismatch": 0}
 
 
     # ---- the spread of the step (VERDICT r4 item 5): the same pipeline again, untimed by the
     # contract, with an event after each batch on its stream: intervals between consecutive batch
     # completions (median / min / max), and the GFX clock sampled by amdsmi while it runs
-    def drun_events(steps):
+    def drun_events(steps, ver):
         evs = []
         for j in range(steps):
-            dstep(j)
+            dstep(j, ver)
             e = torch.cuda.Event(enable_timing=True)
             e.record(streams[j % nst])
             evs.append(e)
@@ -321,7 +386,10 @@ def main():
         return evs
 
     spread_steps = max(args.steps, 200)
-    evs, clk_load = clocks.sample_during(lambda: drun_events(spread_steps))
+    sver = verdicts(spread_steps)
+    evs, clk_load = clocks.sample_during(lambda: drun_events(spread_steps, sver))
+    require_exact(sver, "step-spread run")
+    del sver
     done = sorted(evs[0].elapsed_time(e) for e in evs)
     gaps = [b - a for a, b in zip(done, done[1:])]
     step_spread = {"steps": spread_steps, "median_ms": statistics.median(gaps), "min_ms": min(gaps),
@@ -348,32 +416,34 @@ def main():
             else:
                 tr = ctx.load_keys(ss.pk, radix=r)
                 try:
-                    def drun_r(steps, tr=tr):
-                        for j in range(steps):
-                            dstep(j, tr)
-
-                    drun_r(max(args.warmup, 2))
-                    row["value"] = world * n * args.steps / timed(drun_r, args.steps)
-                    check_device(f"comb radix {r}")
+                    drun_with(verdicts(max(args.warmup, 2)), tr)(max(args.warmup, 2))
+                    rver = verdicts(args.steps)
+                    row["value"] = world * n * args.steps / timed(drun_with(rver, tr), args.steps)
+                    require_exact(rver, f"comb radix {r}")
                 finally:
                     ctx.unload_keys(tr)
             cliff.append(row)
 
     # ---- kernel durations inside this same pipeline (per-batch HIP events on the launch streams)
     ctx.set_profiling(True, per_batch=True)
-    drun(args.steps)
+    pver = verdicts(args.steps)
+    drun_with(pver)(args.steps)
     torch.cuda.synchronize()
     pipe_stage, pipe_batches = ctx.stage_times_avg_ms()
     ctx.set_profiling(False)
+    require_exact(pver, "profiled pipeline")
     ladder_ms = pipe_stage["ladder"]
     ctx.set_profiling(True)
     iso = {"hash": [], "ladder": [], "finish": []}
-    for _ in range(5):
-        dstep(0)  # one batch at a time: kernel durations without overlap
+    iver = verdicts(5)
+    for j in range(5):
+        dstep(j, iver)  # one batch at a time: kernel durations without overlap
         for k, v in ctx.stage_times_ms().items():
             iso[k].append(v)
     ctx.set_profiling(False)
-    del d_sig, d_blob, d_kidx
+    torch.cuda.synchronize()
+    require_exact(iver, "isolated batches")
+    del dsets, pver, iver
 
     # ---- PCIe host -> device copy rate of this box (pinned, 256 MiB), for the PCIe bound
     src = torch.empty(256 << 20, dtype=torch.uint8).pin_memory()
@@ -454,7 +524,7 @@ def main():
     out = None
     if rank == 0:
         cpu = None
-        if not args.no_cpu and world == 1:
+        if not args.no_cpu:  # every N (north_star: "in the same run"), after every timed region
             kc = workload.cpu_lib().cbft_cpu_keys_new(workload._p(ss.pk), ss.pk.shape[0])
             try:
                 workload.cpu_verify(ss, threads=cpu_threads, keycache=kc)  # warm-up batch
@@ -469,8 +539,10 @@ def main():
             cpu = {"value": n / statistics.median(ts), "unit": "verifies/s", "cores": cpu_threads,
                    "kind": "reference",
                    "sample": f"OpenSSL {_openssl_version()} EVP_DigestVerify(ED25519), EVP_PKEY cached per key, "
-                             f"{cpu_threads} pthreads = every CPU this process may use ({quota}), static "
-                             f"ranges; median of 5 batches of the same {n} x {L} B set after 1 warm-up batch"}
+                             f"{cpu_threads} pthreads = every CPU this process may use ({quota}"
+                             + (f"; rank 0 bound to NUMA node {numa}" if numa is not None else "") +
+                             f"), static ranges; median of 5 passes over batch 0 ({n} x {L} B, "
+                             f"{invalid[0]} invalid) after 1 warm-up pass"}
         # p50 end-to-end latency at batch 1K: the caller's (pageable) host arrays -> one blocking
         # cbft_ed25519_verify_batch -> bitmap on host (what a C++ SigManager::verifySigBatch call
         # costs); the Python-list form (messages packed by the binding each call) beside it
@@ -515,7 +587,7 @@ def main():
             parity["config4_bls"] = bls.pop("parity")
         if rsa:
             parity["rsa_2048_bench_sets"] = {"n": 2 * args.batch, "mismatch": 0}
-        detail = _write_detail({"step_spread": step_spread, "gpu_clocks": gpu_clk, "comb_radix_cliff": cliff,
+        detail = _write_detail({"workload_gen_s": gen_s, "flood_config5": flood, "step_spread": step_spread, "gpu_clocks": gpu_clk, "comb_radix_cliff": cliff,
                                 "comb_radix_cliff_fields": "comb radix, M verifies/s, MB per key, max keys in budget",
                                 "parity": parity, "roofline": roofline, "mixed_config3": mixed, "bls_config4": bls,
                                 "rsa_2048": rsa, "per_request_path": per_request, "single_process_multi_gpu": single})
@@ -535,6 +607,11 @@ def main():
                        "batch_per_gpu": n, "msg_len": L, "nkeys": args.nkeys, "comb_radix": args.comb_radix,
                        "b_comb_radix": b_radix, "ladder_lanes_per_signature": lanes,
                        "inputs": f"HBM (cbft_ed25519_verify_fixed_device, {nst} streams); verdict words stay in HBM",
+                       "batches": f"{nb} distinct signed batches per GPU cycled through every timed loop, "
+                                  f"{args.invalid_frac:.0%} planted invalid ({invalid}); every step's verdicts "
+                                  f"checked against OpenSSL after the region",
+                       "config5": "flood_config5: --flood total (1,048,576) sharded over the ranks, 131,072 per "
+                                  "GPU at N = 8 (= --batch 131072 per rank), one RCCL all-gather of verdict words",
                        "pcie_inclusive_inputs": "pinned host memory (cbft_host_alloc) -> GPU each step; bitmap -> host",
                        "inflight_batches": depth,
                        "parallelism": f"static shard x{world}" + (", RCCL all-gather of verdict bitmaps"
@@ -544,6 +621,7 @@ def main():
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,
             "verdicts": "bit-exact vs host OpenSSL (checked before and after timing)",
             "parity": {"all_exact": True, "blocks": _parity_counts(parity), "detail": detail},
+            "flood_config5": _brief(flood, ("value", "ms_per_flood", "per_rank", "calls_per_rank", "mismatch")),
             "pageable_host_value": pageable,
             "single_process_multi_gpu": _brief(single, ("value", "devices", "open", "ms_per_step")),
             "step_spread_ms": [round(step_spread[k], 4) for k in ("median_ms", "min_ms", "max_ms",
@@ -564,7 +642,8 @@ def main():
             "p50_latency_ms_batch1k": lat,
         }
         print(json.dumps(out), flush=True)
-    ctx.host_free(blk)
+    for blk in blocks:
+        ctx.host_free(blk[0])
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

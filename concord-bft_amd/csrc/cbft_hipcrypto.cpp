@@ -96,9 +96,11 @@ static int reserve_slot(WorkSlot& w, size_t n) {
   return CBFT_OK;
 }
 
+// Only the slots launches rotate over (slot 0 also serves small batches): the rest of the
+// CBFT_MAX_WORK_SLOTS array stays unallocated.
 static int reserve_work(cbft_ctx* c, size_t n) {
-  for (WorkSlot& w : c->slots) {
-    int rc = reserve_slot(w, n);
+  for (int k = 0; k < c->work_slots; k++) {
+    int rc = reserve_slot(c->slots[k], n);
     if (rc) return rc;
   }
   CBFT_HIP(c->verdicts.reserve(((n + 63) / 64) * sizeof(uint64_t)));
@@ -309,7 +311,7 @@ void cbft_close(cbft_ctx* c) {
     b->release();
   c->hstage.release();
   for (WorkSlot& w : c->slots) {
-    for (DevBuf* b : {&w.h, &w.flags, &w.xyz, &w.ps_tbl, &w.ps_aok, &w.perm, &w.buckets}) b->release();
+    for (DevBuf* b : {&w.h, &w.flags, &w.xyz, &w.ps_tbl, &w.ps_aok, &w.perm, &w.buckets, &w.tree}) b->release();
     if (w.done) (void)hipEventDestroy(w.done);
     if (w.fork) (void)hipEventDestroy(w.fork);
     if (w.join) (void)hipEventDestroy(w.join);

@@ -634,7 +634,15 @@ struct Fe25519S30 {
                                    0x3fffffff, 0x3fffffff, 0x3fffffff, 0x00007fff};
   static constexpr uint32_t PINV30 = 0x179435e5u;
 };
-FE_INLINE void fe_invert_var(fe& r, const fe& z) {
+// UNIFORM: z is the same in every lane of the wave (a finish block's tree root): the chain runs on
+// the scalar unit (safegcd30.h sg_inv30_var_uniform), every lane receives the inverse.
+template <bool UNIFORM = false>
+FE_INLINE void fe_invert_var(fe& r, const fe& z0) {
+  fe z = z0;
+  if (UNIFORM) {
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) z.v[k] = __builtin_amdgcn_readfirstlane(z0.v[k]);
+  }
   uint32_t w[8];
   fe_to_words(w, z);  // canonical, [0, p)
   Sg30 x;

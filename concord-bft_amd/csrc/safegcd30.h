@@ -157,6 +157,19 @@ SG_HD void sg_inv30_var(Sg30& x) {
   x = d;
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// The same inversion of a value every lane of the wave holds (a finish block's shared tree root, a
+// pairing check's norm): the limbs are taken from the first active lane, so the whole chain is
+// wave-uniform and compiles to scalar (SALU) code -- one scalar instruction stream with scalar
+// branches instead of one lane's VALU stream under an exec mask.
+template <class M>
+__device__ __forceinline__ void sg_inv30_var_uniform(Sg30& x) {
+#pragma unroll
+  for (int j = 0; j < 9; j++) x.v[j] = __builtin_amdgcn_readfirstlane(x.v[j]);
+  sg_inv30_var<M>(x);
+}
+#endif
+
 // value of 9 29-bit limbs (< 2^261, < p here) <-> 9 signed-30 limbs
 SG_HD void sg_from_limbs29(Sg30& x, const uint32_t* c) {
 #pragma unroll

@@ -314,9 +314,13 @@ PreProcessBatchValidation checkPreProcessBatchReqMsgCorrectness(const char* body
     const size_t k = owner[j];
     const PreProcessRequestMsgHeader& h = elems[k].h;
     out.outcome[k] = PreProcessOutcome::Invalid;
-    out.error[k] = "Signature verification failed for: clientId: " + std::to_string(bh.clientId) +
-                   ", reqSeqNum: " + std::to_string(h.reqSeqNum) + ", requestLength: " +
-                   std::to_string(h.requestLength) + ", reqSignatureLength: " + std::to_string(h.reqSignatureLength);
+    // the reference's text: "Signature verification failed for: " << KVLOG(header->clientId, ...),
+    // KVARGS naming each argument by its source text and KvLog opening with a space
+    // (PreProcessRequestMsg.cpp:108-109, util/include/kvstream.h, util/include/macros.h)
+    out.error[k] = "Signature verification failed for:  header->clientId: " + std::to_string(bh.clientId) +
+                   ", header->reqSeqNum: " + std::to_string(h.reqSeqNum) + ", header->requestLength: " +
+                   std::to_string(h.requestLength) +
+                   ", header->reqSignatureLength: " + std::to_string(h.reqSignatureLength);
     out.invalid++;
   }
   out.valid = out.ignored == 0 && out.invalid == 0;

@@ -490,7 +490,14 @@ static int testPreProcessBatch(SigManager& sm, const ReplicasInfo& ri, SignerOf 
     CHECK(!v.valid && v.invalid == 4 && v.ignored == 0);
     CHECK(v.outcome == ref);
     for (int k = 0; k < n; k++) CHECK((v.outcome[k] == PreProcessOutcome::Invalid) == (k == 3 || k == 17 || k == 30 || k == 47));
-    CHECK(v.error[17].find("Signature verification failed") != std::string::npos);
+    {  // the whole text, as PreProcessRequestMsg::validate builds it with KVLOG
+      PreProcessRequestMsgHeader h17;
+      std::memcpy(&h17, e2[17].data(), sizeof h17);
+      const std::string want = "Signature verification failed for:  header->clientId: " + std::to_string(client) +
+                               ", header->reqSeqNum: 517, header->requestLength: " + std::to_string(reqs[17].size()) +
+                               ", header->reqSignatureLength: " + std::to_string(h17.reqSignatureLength);
+      CHECK(v.error[17] == want);
+    }
     CHECK(c2.externalVerified - c1.externalVerified == c1.externalVerified - c0.externalVerified);
     CHECK(c2.externalFailed - c1.externalFailed == c1.externalFailed - c0.externalFailed);
     CHECK(c2.externalFailed - c1.externalFailed == 4);

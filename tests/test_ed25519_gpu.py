@@ -520,6 +520,39 @@ def test_fixed_device_path(n):
         hip.close()
 
 
+@pytest.mark.parametrize("streams", [3, 2])
+def test_fixed_device_64k_streams_planted_invalid(streams):
+    """The headline's exact schedule: cbft_ed25519_verify_fixed_device at 64K,
+    distinct signed batches with 1 % planted invalid signatures (R / S / message bit flips, S + L,
+    wrong key) cycled over three (and two) streams, a verdict buffer per step pre-filled with a
+    pattern no batch can produce; every step's words equal its own batch's OpenSSL verdicts."""
+    hip = _Hip()
+    n, L, nb, steps = 65536, 256, 3, 9
+    nwords = n // 64
+    sets = [sigsets.make_sigset(n, nkeys=512, msg_len=L, seed=77 + b, invalid_frac=0.01) for b in range(nb)]
+    assert all(int((~s.expected).sum()) > 300 for s in sets)
+    for s in sets[1:]:
+        assert np.array_equal(s.pk, sets[0].pk)
+    try:
+        with cb.Context(device=0, max_batch=n) as c:
+            tid = c.load_keys(sets[0].pk)
+            dev = [(hip.to_dev(s.key_idx), hip.to_dev(s.sig.reshape(-1)), hip.to_dev(s.blob)) for s in sets]
+            ss = [hip.stream() for _ in range(streams)]
+            fill = np.full(nwords, 0x5A5A5A5A5A5A5A5A, dtype=np.uint64)
+            outs = [hip.to_dev(fill) for _ in range(steps)]
+            for j in range(steps):
+                d_kidx, d_sig, d_blob = dev[j % nb]
+                c.verify_fixed_device(tid, 0, d_kidx, d_sig, d_blob, L, n, outs[j], ss[j % streams])
+            hip.sync()
+            for j in range(steps):
+                got = _bools(hip.from_dev(outs[j], nwords * 8), n)
+                bad = np.nonzero(got != sets[j % nb].expected)[0]
+                assert bad.size == 0, f"step {j} (batch {j % nb}): {bad.size} mismatches, first {bad[:8]}"
+            c.unload_keys(tid)
+    finally:
+        hip.close()
+
+
 @pytest.mark.parametrize("n", [1, 100, 257, 5000])
 def test_hash_block_count_sort(golden, n, monkeypatch):
     """Variable-length batches hash in order of their SHA-512 block count (a counting sort into a

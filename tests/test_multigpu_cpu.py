@@ -77,3 +77,131 @@ def test_gloo_world2_gather_matches_single_process():
         got = res[r][: len(want)]
         assert got == want
     assert 0 < ss.expected.sum() < n
+
+
+# ---------------------------------------------------------------------------------------------
+# bench.py's N > 1 branch, function for function (VERDICT r5 item 5): the contract timing
+# (mg.timed_region), each step's verdict words and their all-gather (mg.StepVerdicts, device and
+# host-buffer forms), the post-region check against every rank's OpenSSL verdicts
+# (StepVerdicts.mismatches + all_gather_rows + sum_over_ranks) and the config #5 flood
+# (flood_plan / flood_expected / gather_verdicts).  The host OpenSSL stands in for the GPU; the
+# collectives are the same calls bench.py makes, over gloo.
+# ---------------------------------------------------------------------------------------------
+def _bench_rank_worker(rank, world, port, result_q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import workload
+
+    try:
+        n, nb, steps = 320, 3, 7
+        nwords = (n + 63) // 64
+        sets = [workload.make_sigset(n, nkeys=8, msg_len=256, seed=0xC0FFEE + rank + 7919 * b, invalid_frac=0.05,
+                                     threads=2) for b in range(nb)]
+        words = [torch.from_numpy(mg.bools_to_words(s.expected)) for s in sets]
+        exp_rows = torch.stack(words)
+        all_exp = mg.all_gather_rows(exp_rows, world, dist)
+        assert all_exp.shape == (world, nb, nwords)
+        assert torch.equal(all_exp[rank], exp_rows)
+
+        def verify_words(b):  # the "launch": OpenSSL verdict words of batch b
+            return torch.from_numpy(mg.bools_to_words(workload.cpu_verify(sets[b], threads=2).astype(bool)))
+
+        # device form: after_step all-gathers each step's row
+        ver = mg.StepVerdicts(nwords, steps, world, rank, dist, "cpu", stream=None)
+
+        def drun(k):
+            for j in range(k):
+                ver.local[j].copy_(verify_words(j % nb))
+                ver.after_step(j, None)
+
+        el = mg.timed_region(drun, steps, dist, None, "cpu")
+        assert el > 0
+        assert mg.sum_over_ranks(ver.mismatches(exp_rows, lambda j: j % nb, None, all_exp), dist, "cpu") == 0
+        # the gathered rows hold every rank's words
+        for j in range(steps):
+            for r in range(world):
+                assert torch.equal(ver.gathered[j, r], all_exp[r, j % nb])
+        # a stale step (zero words) is caught on every rank
+        ver.local[3].zero_()
+        bad = mg.sum_over_ranks(ver.mismatches(exp_rows, lambda j: j % nb, None, all_exp), dist, "cpu")
+        assert bad > 0
+
+        # host-buffer form: bitmaps from the host, moved into the rows and gathered
+        hver = mg.StepVerdicts(nwords, steps, world, rank, dist, "cpu", stream=None)
+        for j in range(steps):
+            bm = np.zeros(nwords * 8, dtype=np.uint8)
+            bm[:] = verify_words(j % nb).numpy().view(np.uint8)
+            hver.after_host_step(j, bm)
+        assert mg.sum_over_ranks(hver.mismatches(exp_rows, lambda j: j % nb, None, all_exp), dist, "cpu") == 0
+
+        # config #5 flood: total over the ranks in calls of at most n, one gather
+        total = 2 * n * world + 128
+        plan = mg.flood_plan(total, world, rank, n)
+        sw = mg.shard_size(total, world) // 64
+        fwords = torch.zeros(sw, dtype=torch.int64)
+        for c, (o, m) in enumerate(plan):
+            v = workload.cpu_verify(sets[c % nb], threads=2).astype(bool)[:m]
+            w = torch.from_numpy(mg.bools_to_words(v))
+            fwords[o // 64:o // 64 + w.numel()] = w  # chunk offsets are multiples of 64
+        fexp = torch.from_numpy(mg.flood_expected(plan, [s.expected for s in sets], sw, lambda c: c % nb))
+        assert torch.equal(fwords, fexp)
+        g = mg.gather_verdicts(fwords, total, world, dist)
+        want = mg.all_gather_rows(fexp, world, dist).view(-1)[: (total + 63) // 64]
+        assert torch.equal(g, want)
+        result_q.put((rank, "ok", [(o, m) for o, m in plan]))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+
+        result_q.put((rank, "fail: " + traceback.format_exc(), None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_gloo_world2_bench_rank_path():
+    import multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_rank_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in procs:
+        r, status, plan = q.get(timeout=240)
+        res[r] = (status, plan)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        assert res[r][0] == "ok", res[r][0]
+    # the two ranks' flood chunks tile the total
+    n = 320
+    total = 2 * n * 2 + 128
+    spans = []
+    for r in range(2):
+        lo, _ = mg.shard_bounds(total, 2, r)
+        spans += [(lo + o, lo + o + m) for o, m in res[r][1]]
+    spans.sort()
+    assert spans[0][0] == 0 and spans[-1][1] == total
+    assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+
+
+def test_flood_plan_config5_geometry():
+    """SURVEY.md §8(d) config #5: 1,048,576 over 8 ranks = 131,072 per GPU = two 64K calls."""
+    for world, calls in ((1, 16), (2, 8), (4, 4), (8, 2)):
+        plan = mg.flood_plan(1 << 20, world, world - 1, 65536)
+        assert len(plan) == calls and all(m == 65536 for _, m in plan)
+        assert mg.shard_size(1 << 20, world) == (1 << 20) // world
+    assert mg.shard_size(1 << 20, 8) // 64 * 8 == 16384  # 16 KiB of verdict words per GPU
+
+
+def test_bools_to_words_layout():
+    v = np.zeros(130, dtype=bool)
+    v[[0, 63, 64, 129]] = True
+    w = mg.bools_to_words(v).view(np.uint64)
+    assert w.tolist() == [1 | (1 << 63), 1, 2]
