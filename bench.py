@@ -461,8 +461,8 @@ def main():
 
     # ---- roofline: the dominant kernel (INT32 VALU) + the PCIe bound of the whole step
     # the ladder layout the library picks (cbft_hipcrypto.cpp): two lanes per signature from 32K
-    lanes = int(os.environ.get("CBFT_LADDER_LANES", "0")) or (2 if n >= 32768 else 4)
-    b_radix = int(os.environ.get("CBFT_B_RADIX", "22"))
+    lanes = 2 if n >= 32768 else 4
+    b_radix = 22  # CBFT_COMB_B_RADIX (ed25519_verify.h)
     kname = "ed25519_comb2_ladder_kernel" if lanes == 2 else "ed25519_comb_ladder_kernel"
     # PMC record of the headline workload (tools/ed_pmc_probe.py --mode headline under
     # tools/pmc_passes.sh): attached only while it was collected on this csrc tree
@@ -479,7 +479,7 @@ def main():
     npos = {8: 32, 9: 29, 10: 26, 11: 23, 12: 22, 13: 20, 14: 19, 15: 17}[args.comb_radix] + \
         {16: 16, 17: 15, 18: 15, 19: 14, 20: 13, 21: 13, 22: 12, 23: 11, 24: 11, 25: 11, 26: 10}[b_radix]
     # each pair-ladder lane's first addition starts from the identity and is a point set (1 M, not
-    # 7: CBFT_LADDER_FIRST_SET in ed25519_verify.hip), so a verify is (npos - 2) x 7 + 2 x 1 M
+    # 7: ed25519_comb2_ladder_kernel), so a verify is (npos - 2) x 7 + 2 x 1 M
     first_sets = 2 if lanes == 2 else 0
     mads_per_unit = ((npos - first_sets) * 7 + first_sets) * 90
     achieved = mads_per_unit * n / (ladder_ms * 1e-3)
@@ -591,8 +591,7 @@ def main():
                                 "comb_radix_cliff_fields": "comb radix, M verifies/s, MB per key, max keys in budget",
                                 "parity": parity, "roofline": roofline, "mixed_config3": mixed, "bls_config4": bls,
                                 "rsa_2048": rsa, "per_request_path": per_request, "single_process_multi_gpu": single})
-        # the fused small-batch kernel in its default form ($CBFT_SMALL_WAVES: 3 -> small3, 2 -> small)
-        small_name = "ed25519_small_kernel" if os.environ.get("CBFT_SMALL_WAVES") == "2" else "ed25519_small3_kernel"
+        small_name = "ed25519_small3_kernel"  # the fused small-batch kernel
         small_k, small_stat = _pmc_record("pmc_ed25519_small.json", small_name)
         # The line: the contract's keys first, then side measurements, and LAST what the driver's
         # stdout tail must keep: the second half of the metric (p50 @ 1K), the
@@ -947,7 +946,7 @@ def _mixed_device_resident(ctx, tid, ss, args):
     d_off, d_len, d_k = to_dev(ss.off, np.int64), to_dev(ss.len, np.int32), to_dev(ss.key_idx, np.int32)
     # more streams than the fixed-length headline's two: a batch's long-message tail (up to 33
     # SHA-512 blocks on one lane) then runs under the next batches' short hashes and ladders
-    # (the library rotates over as many work slots, $CBFT_WORK_SLOTS)
+    # (the library rotates over as many work slots, CBFT_OPT_WORK_SLOTS, default 4)
     ns = max(1, getattr(args, "mixed_streams", 4))
     streams = [torch.cuda.Stream(device=dev) for _ in range(ns)]
     outs = [torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev) for _ in range(ns)]
@@ -1050,10 +1049,8 @@ def bench_rsa(ctx, args, cpu_threads):
             kms = statistics.median(kms)
             nbits = e.bit_length()
             products = 1 + (nbits - 1) + bin(e).count("1") + 1  # CONV + squarings + multiplies + REDC
-            # v_mad_u64_u32 per verify of the running kernel's schedule: lane-pair radix-2^28 (74 rows x
-            # 2 x 74 columns) or, with CBFT_RSA_KERNEL=fios, 32-bit FIOS (64 rows x 2 x 64 columns)
-            fios = os.environ.get("CBFT_RSA_KERNEL") == "fios"
-            macs = products * (64 * 128 if fios else 74 * 148)
+            # v_mad_u64_u32 per verify of the lane-pair radix-2^28 schedule (74 rows x 2 x 74 columns)
+            macs = products * 74 * 148
             ts = []
             workload.cpu_lib().cbft_cpu_rsa_verify(kc, workload._p(kidx_a), workload._p(sig_a), workload._p(blob),
                                                    workload._p(offs), workload._p(lens), n, workload._p(cpu_v),
@@ -1071,7 +1068,7 @@ def bench_rsa(ctx, args, cpu_threads):
                              "peak": MAD64_PEAK / 1e12, "unit": "T MAC/s",
                              "frac": macs * n / (kms * 1e-3) / MAD64_PEAK, "macs_per_verify": macs,
                              "frac_of_measured_mad_rate": macs * n / (kms * 1e-3) / MAD64_MEASURED,
-                             "kernel": "rsa_verify_kernel" if fios else "rsa_verify_pair_kernel"},
+                             "kernel": "rsa_verify_pair_kernel"},
                 "cpu_baseline": {"value": cpu_value, "unit": "verifies/s", "cores": cpu_threads,
                                  "kind": "reference",
                                  "sample": f"OpenSSL {_openssl_version()} EVP_DigestVerify(RSA PKCS#1 v1.5, "

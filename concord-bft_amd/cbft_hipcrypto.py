@@ -36,6 +36,7 @@ ABI = [
      [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_size_t]),
     ("cbft_device_of", ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ("cbft_close", None, [ctypes.c_void_p]),
+    ("cbft_set_option", ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]),
     ("cbft_host_alloc", ctypes.c_int, [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
     ("cbft_host_free", ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p]),
     ("cbft_ed25519_verify_batch_async", ctypes.c_int,
@@ -117,6 +118,16 @@ ABI = [
       ctypes.POINTER(ctypes.c_int)]),
 ]
 
+# cbft_set_option options (include/cbft_hipcrypto.h, "tuning")
+OPT_LADDER_LANES = 1
+OPT_B_RADIX = 2
+OPT_WORK_SLOTS = 3
+OPT_SMALL_MAX = 4
+OPT_SHA_SORT_MIN = 5
+OPT_STAGE_ORDER = 6
+OPT_HASH_ORDER_EARLY = 7
+OPT_FINISH_K = 8
+
 BLS_G1_PARTIAL_BYTES = 108
 BLS_G2_PARTIAL_BYTES = 220
 
@@ -140,6 +151,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
         raise RuntimeError(f"{path} is missing: run `make lib` (or __graft_entry__.build())")
     lib = ctypes.CDLL(path)
     for name, res, args in ABI:
+        if os.environ.get("CBFT_LIB") and not hasattr(lib, name):
+            continue  # an older A/B build ($CBFT_LIB) without a later entry point
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -191,6 +204,11 @@ class Context:
         else:
             _check(self.lib.cbft_open(ctypes.byref(self.handle), device, max_batch), f"cbft_open(device={device})")
         self.device = device
+
+    def set_option(self, option: int, value: int):
+        """cbft_set_option: a per-context geometry / scheduling switch (OPT_*)."""
+        _check(self.lib.cbft_set_option(self.handle, option, int(value)), f"cbft_set_option({option}, {value})")
+        return self
 
     def devices(self) -> List[int]:
         out = (ctypes.c_int * 32)()

@@ -9,10 +9,9 @@
 #define BLS_G2A_WORDS 37     // affine G2 (x.a, x.b, y.a, y.b, inf flag) of a decoded key
 
 size_t cbft_bls_lines_words_per_key();
-// d_scratch: cbft_bls_keys_scratch_words(nkeys) words (line normalisation, freed after the call)
-size_t cbft_bls_keys_scratch_words(uint32_t nkeys);
+// decode + subgroup-check nkeys G2 keys (d_ok, d_aff) and build their Miller-loop lines (d_lines)
 hipError_t cbft_bls_launch_keys(const uint8_t* d_keys65, uint32_t nkeys, uint32_t* d_lines, uint8_t* d_ok,
-                                uint32_t* d_aff, uint32_t* d_scratch, hipStream_t s);
+                                uint32_t* d_aff, hipStream_t s);
 hipError_t cbft_bls_launch_gen_lines(uint32_t* d_lines, hipStream_t s);
 hipError_t cbft_bls_launch_hash(const uint8_t* d_msg, uint32_t len, uint32_t* d_H, hipStream_t s);
 // H = g1_map(msg) when d_H is non-null, beside the decoding of k shares (lane per share):
@@ -44,9 +43,8 @@ hipError_t cbft_bls_launch_g1_parts(const uint32_t* d_parts, uint32_t count, uin
 // BLS_G2_PART_WORDS) or compressed (d_out65)
 hipError_t cbft_bls_launch_g2_sum(const uint32_t* d_aff, const uint8_t* d_key_ok, uint32_t n, const uint8_t* d_bitmap,
                                   uint32_t lo_id, uint32_t hi_id, uint8_t* d_ok, uint8_t* d_out65, uint32_t* d_out_part,
-                                  uint32_t* d_tmp,
-                                  hipStream_t s);
-// scratch words cbft_bls_launch_g2_sum needs for the wave form's intermediate partials
+                                  uint32_t* d_tmp, hipStream_t s);
+// scratch words (d_tmp, required) cbft_bls_launch_g2_sum needs for its intermediate partials
 size_t cbft_bls_g2_sum_tmp_words();
 // H = g1_map(msg) (-> d_H when non-null) and e(H, PK) e(-sigma, g2) == 1 in one launch
 // multisig verify in one launch: PK = sum of count key-sum partials, its lines streamed from one
@@ -61,9 +59,7 @@ hipError_t cbft_bls_launch_verify(const uint8_t* d_msg, uint32_t len, uint32_t* 
                                   const uint32_t* d_pk_lines, const uint8_t* d_pk_ok,
                                   const uint32_t* d_gen_lines, uint8_t* d_result, hipStream_t s,
                                   const uint32_t* d_H_in = nullptr, const uint32_t* d_sig_aff = nullptr);
-hipError_t cbft_bls_launch_sign(const uint8_t* d_msg, uint32_t len, const uint32_t* d_sk, uint32_t id,
-                                uint8_t* d_out37, hipStream_t s);
-// the same signature on row-parallel Fp (bls_msm_row.hip): d_H = g1_map(msg) from
+// sigma = sk * g1_map(msg) as a 37-byte share on row-parallel Fp (bls_msm_row.hip): d_H = g1_map(msg) from
 // cbft_bls_launch_hash first, or nullptr (the kernel hashes); constant operation sequence in the
 // secret scalar
 hipError_t cbft_bls_launch_sign_row(const uint32_t* d_H, const uint32_t* d_sk, const uint8_t* d_msg, uint32_t len,
@@ -73,4 +69,3 @@ hipError_t cbft_bls_launch_sign_row(const uint32_t* d_H, const uint32_t* d_sk, c
 size_t cbft_bls_pub_table_words();
 hipError_t cbft_bls_launch_pub_table(uint32_t* d_tbl, hipStream_t s);
 hipError_t cbft_bls_launch_pubkey_row(const uint32_t* d_tbl, const uint32_t* d_sk, uint8_t* d_out65, hipStream_t s);
-hipError_t cbft_bls_launch_pubkey(const uint32_t* d_sk, uint8_t* d_out65, hipStream_t s);

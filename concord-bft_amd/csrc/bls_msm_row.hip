@@ -22,20 +22,6 @@
 
 using RCtx = RowCtx<uint32_t, uint64_t>;
 
-#ifndef CBFT_BLS_PHASES
-#define CBFT_BLS_PHASES 0
-#endif
-#if CBFT_BLS_PHASES  // probe builds: block 0's phase timestamps, printed at its end
-__device__ uint64_t g_msm_phase[4];
-#define MSM_STAMP(s)                                                                      \
-  do {                                                                                    \
-    if (blockIdx.x == 0 && threadIdx.x == 0) g_msm_phase[(s)] = wall_clock64();           \
-  } while (0)
-#else
-#define MSM_STAMP(s) \
-  do {               \
-  } while (0)
-#endif
 using RPt = G1R<uint32_t>;
 
 // row point <- 9-limb words (one-lane limbs at p[0..8]: lane i of every row takes p[i])
@@ -86,7 +72,6 @@ __global__ void __launch_bounds__(MSM_ROW_BLOCK) bls_msm_row_kernel(const uint32
   __shared__ int xinf;
   const uint32_t j = blockIdx.x;
   if (j >= k) return;
-  MSM_STAMP(0);
   const int wave = threadIdx.x >> 6;
   const uint32_t tag = 0;
   const RCtx c(tag);
@@ -117,7 +102,6 @@ __global__ void __launch_bounds__(MSM_ROW_BLOCK) bls_msm_row_kernel(const uint32
     g1r_dbl(T[5], T[2], c);
     g1r_add(T[6], T[5], T[0], c);
     g1r_dbl(T[7], T[3], c);
-    MSM_STAMP(1);
 #pragma nounroll
     for (int w = 32; w >= 0; w--) {
       if (!inf) {
@@ -147,7 +131,6 @@ __global__ void __launch_bounds__(MSM_ROW_BLOCK) bls_msm_row_kernel(const uint32
       acc.X = c.mul(acc.X, rf_from_fe(beta, tag));
     }
   }
-  MSM_STAMP(2);
   // wave 1 hands its half to wave 0
   if (wave == 1) {
     const uint32_t l = __lane_id();
@@ -167,12 +150,6 @@ __global__ void __launch_bounds__(MSM_ROW_BLOCK) bls_msm_row_kernel(const uint32
   h.Z = xch[32 + rl];
   rpt_accum(acc, inf, h, xinf != 0, c);
   rpt_store(out + BLS_JAC_WORDS * (size_t)j, acc, inf, c);
-#if CBFT_BLS_PHASES
-  if (j == 0 && threadIdx.x == 0)
-    printf("bls_msm_row block 0 (us): table %.1f chain %.1f joined+stored %.1f\n",
-           (g_msm_phase[1] - g_msm_phase[0]) * 0.01, (g_msm_phase[2] - g_msm_phase[1]) * 0.01,
-           (wall_clock64() - g_msm_phase[0]) * 0.01);
-#endif
 }
 
 // sum of m points -> one Jacobian partial per block of 16 waves.  affine: points are parsed shares
@@ -323,13 +300,6 @@ __global__ void __launch_bounds__(128) bls_sign_row_kernel(const uint32_t* H, co
                                                            uint32_t len, uint32_t id, uint8_t* out37) {
   __shared__ uint32_t xch[3 * 16];
   const int wave = threadIdx.x >> 6;
-#if CBFT_BLS_PHASES  // probe builds: phase times of each wave (10 ns ticks), printed by lane 0
-  uint64_t ph[6];
-#define SIGN_STAMP(k) ph[k] = wall_clock64()
-#else
-#define SIGN_STAMP(k)
-#endif
-  SIGN_STAMP(0);
   const uint32_t tag = 0;
   const RCtx c(tag);
   g1a h;
@@ -387,7 +357,6 @@ __global__ void __launch_bounds__(128) bls_sign_row_kernel(const uint32_t* H, co
   g1r_dbl(P2, P, c);
 #pragma unroll
   for (int m = 1; m < 8; m++) g1r_add(T[m], T[m - 1], P2, c);  // unrolled: T stays in registers
-  SIGN_STAMP(1);
   auto pick = [&](int w, RPt& e) {  // +-T[(|d_w| - 1) / 2] by selects over all entries
     const uint32_t nib = (u[w >> 3] >> (4 * (w & 7))) & 15u;  // d = 2 nib - 15
     const uint32_t dn = nib < 8u ? 1u : 0u;                    // d < 0
@@ -419,7 +388,6 @@ __global__ void __launch_bounds__(128) bls_sign_row_kernel(const uint32_t* H, co
     g1r_add(t, acc, e, c);
     acc = t;
   }
-  SIGN_STAMP(2);
   bool inf = false;
   {  // undo the odd fix: acc - base when k was even (computed always, kept by a select)
     RPt nb, t;
@@ -449,13 +417,7 @@ __global__ void __launch_bounds__(128) bls_sign_row_kernel(const uint32_t* H, co
     if (l == 0) xinf = inf ? 1 : 0;
   }
   __syncthreads();
-#if CBFT_BLS_PHASES
-  if (__lane_id() == 0)
-    printf("sign wave %d (us): table %.1f windows %.1f to-exchange %.1f\n", wave, (ph[1] - ph[0]) * 0.01,
-           (ph[2] - ph[1]) * 0.01, (wall_clock64() - ph[2]) * 0.01);
-#endif
   if (wave != 0) return;
-  SIGN_STAMP(3);
   {
     RPt o;
     const uint32_t rl = __lane_id() & 15u;
@@ -502,9 +464,6 @@ __global__ void __launch_bounds__(128) bls_sign_row_kernel(const uint32_t* H, co
     out37[3] = (uint8_t)id;
     g1_compress(out37 + 4, a);
   }
-#if CBFT_BLS_PHASES
-  if (__lane_id() == 0) printf("sign finish (us): %.1f\n", (wall_clock64() - ph[3]) * 0.01);
-#endif
 }
 
 // H = g1_map(msg) into d_H (bls_hash_kernel), then the row-parallel signature

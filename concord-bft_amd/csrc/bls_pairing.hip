@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
                                                                       int do_verify, int parsed, uint8_t* valid,
                                                                       uint32_t* sig, uint32_t* ids) {
   __shared__ PairXchg xc;
-  __shared__ FeMail fm;  // WAVES = 2: the final exponentiation's helper wave (CBFT_P36_FE2)
+  __shared__ FeMail fm;  // WAVES = 2: the final exponentiation's helper wave
   __shared__ uint32_t lxs[2 * BN_ATE_LINES * P36_LX_WORDS];  // lambda' (p36_lambda_x): two pairs, or one per wave
   const uint32_t j = blockIdx.x;
   if (j >= k) return;  // whole blocks exit together
@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
   }
   __syncthreads();
   bool good = xc.ok != 0;
-  if (CBFT_P36_FE2 && wave == 1) {
+  if (wave == 1) {
     if (do_verify && good && key_ok) p36_fe2_helper(fm, g);
     return;
   }
@@ -135,17 +135,11 @@ __global__ void __launch_bounds__(64 * WAVES) bls_share_verify_kernel(const uint
       fp f1;
       xchg_get(f1, xc, g);
       p36_mul(f, f, f1, g);
-      good = CBFT_P36_FE2 ? p36_is_one_after_final_exp_lead(f, fm, g) : p36_is_one_after_final_exp(f, g);
+      good = p36_is_one_after_final_exp_lead(f, fm, g);
     }
   }
   if (g.lane == 0) valid[j] = good ? 1 : 0;
 }
-
-// H = g1_map(msg) on wave 0 (also stored to H_out when non-null), sigma from 33 bytes on wave 1:
-// e(H, PK) * e(-sigma, g2) == 1 for a combined signature.  One block of two waves.
-// CBFT_BLS_PHASES (probe builds only): phase timestamps (bn254_pair36.h: BLS_STAMP), printed
-// by lane 0 of wave 0 at the end in 10 ns wall-clock ticks.
-#define BLS_PHASE(slot) BLS_STAMP(slot)
 
 // H = g1_map(msg), sigma from 33 bytes: e(H, PK) * e(-sigma, g2) == 1 for a combined signature,
 // in one block of FOUR waves: each pair's Miller loop is split in two (p36_miller_part: top part
@@ -160,13 +154,12 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
                                                                   uint8_t* result, const uint32_t* H_in,
                                                                   const uint32_t* sig_aff) {
   __shared__ PairXchg xc[3];  // the values of waves 1, 2, 3
-  __shared__ FeMail fm;       // wave 1 helps wave 0's final exponentiation (CBFT_P36_FE2)
+  __shared__ FeMail fm;       // wave 1 helps wave 0's final exponentiation
   __shared__ uint32_t lxv[4 * BN_ATE_LINES * P36_LX_WORDS];  // lambda' of each wave's Miller part
   if (blockIdx.x != 0) return;
   const int wave = threadIdx.x >> 6;
   const P36 g = p36_lane();
   if (threadIdx.x == 0) femail_init(fm);
-  BLS_PHASE(wave == 0 ? 0 : 1);
   fp f;
   if (wave < 2) {
     g1a P;
@@ -174,13 +167,11 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
       g1a_load(P, H_in);  // hashed by an earlier kernel of the same call
     else
       g1_map_row(P, msg, len);
-    BLS_PHASE(wave == 0 ? 4 : 12);
     if (wave == 0 && g.lane == 0 && H_out) g1a_store(H_out, P);
     if (wave == 0)
       p36_miller_part<true>(f, P, pk_lines, g, nullptr, lxv);
     else
       p36_miller_part<false>(f, P, pk_lines, g, nullptr, lxv + BN_ATE_LINES * P36_LX_WORDS);
-    BLS_PHASE(wave == 0 ? 5 : 13);
   } else {
     g1a s;
     bool ok = true;
@@ -188,7 +179,6 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
       g1a_load(s, sig_aff);  // the combine's own point: decompressing its 33 bytes gives it back
     else
       ok = g1_decompress_row(s, sig33);
-    BLS_PHASE(wave == 2 ? 2 : 14);
     if (ok && !s.inf) {
       g1a P = s;
       f_neg(P.y, s.y);
@@ -199,13 +189,12 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
     } else {
       p36_one(f, g);  // e(O, g2) = 1
     }
-    BLS_PHASE(wave == 2 ? 3 : 15);
     if (g.lane == 0) xc[wave - 1].ok = ok ? 1 : 0;
   }
   if (wave > 0) xchg_put(xc[wave - 1], f, g);
   __syncthreads();
   bool good = xc[1].ok != 0 && pk_ok[0] != 0;
-  if (CBFT_P36_FE2 && wave == 1) {
+  if (wave == 1) {
     if (good) p36_fe2_helper(fm, g);
     return;
   }
@@ -217,23 +206,9 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
       xchg_get(f1, xc[w], g);
       p36_mul(f, f, f1, g);
     }
-    BLS_PHASE(6);
-    good = CBFT_P36_FE2 ? p36_is_one_after_final_exp_lead(f, fm, g) : p36_is_one_after_final_exp(f, g);
-    BLS_PHASE(11);
+    good = p36_is_one_after_final_exp_lead(f, fm, g);
   }
   if (g.lane == 0) result[0] = good ? 1 : 0;
-#if CBFT_BLS_PHASES
-  if (g.lane == 0) {
-    const uint64_t t0 = g_bls_phase[0];
-    printf("bls_verify phases (us from start): sigma decoded %.1f/%.1f miller top %.1f bottom %.1f | H %.1f/%.1f "
-           "miller top %.1f bottom %.1f | joined %.1f fe_inv %.1f fe_easy %.1f fe_pow_u %.1f fe_done %.1f\n",
-           (g_bls_phase[2] - t0) * 0.01, (g_bls_phase[14] - t0) * 0.01, (g_bls_phase[3] - t0) * 0.01,
-           (g_bls_phase[15] - t0) * 0.01, (g_bls_phase[4] - t0) * 0.01, (g_bls_phase[12] - t0) * 0.01,
-           (g_bls_phase[5] - t0) * 0.01, (g_bls_phase[13] - t0) * 0.01, (g_bls_phase[6] - t0) * 0.01,
-           (g_bls_phase[8] - t0) * 0.01, (g_bls_phase[9] - t0) * 0.01, (g_bls_phase[10] - t0) * 0.01,
-           (g_bls_phase[11] - t0) * 0.01);
-  }
-#endif
 }
 
 // Multisig verify in one block (BlsMultisigVerifier: e(H, sum vk_i) e(-sigma, g2) == 1):
@@ -242,40 +217,32 @@ __global__ void __launch_bounds__(VERIFY_BLOCK) bls_verify_kernel(const uint8_t*
 //   wave 1  H = g1_map(msg), then the (H, PK) Miller loop, reading each line as soon as wave 0
 //           has published it (the loop trails the line computation instead of following it);
 //   wave 2  decompress sigma, the (-sigma, g2) Miller loop over the precomputed generator lines.
-// Wave 1 joins the two Miller values and runs the final exponentiation.  Every wave reaches the
-// end: wave 0 publishes "all lines" even when PK is unusable (bad key, infinity).
-// CBFT_MS_SPLIT = 1 (A/B only): five waves, each Miller loop split in two (p36_miller_part, as
-// bls_verify_kernel): waves 1 / 2 the top / bottom of (H, PK) (the bottom trails the line
-// computation, the top needs only its first lines), waves 3 / 4 those of (-sigma, g2); wave 1
-// joins the four values, wave 3 helps its final exponentiation.  Measured 1.018 against 0.926 ms
-// (profiles/r05_ab/bls_multisig_split.txt): the fifth wave shares a SIMD with the line
-// computation, which sets the pace of the (H, PK) loop, and the 320-thread block caps VGPRs at 256.
-#ifndef CBFT_MS_SPLIT
-#define CBFT_MS_SPLIT 0
-#endif
-#define MS_BLOCK (CBFT_MS_SPLIT ? 320 : 192)
+// Wave 1 joins the two Miller values and runs the final exponentiation, wave 2 helps it.  Every
+// wave reaches the end: wave 0 publishes "all lines" even when PK is unusable (bad key, infinity).
+// (Five waves with each Miller loop split in two, as bls_verify_kernel, measured 1.018 against
+// 0.926 ms: the fifth wave shares a SIMD with the line computation that paces the (H, PK) loop.)
+#define MS_BLOCK 192
 __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uint32_t* parts, uint32_t count,
                                                                        const uint8_t* msg, uint32_t len,
                                                                        const uint8_t* sig33, const uint32_t* gen_lines,
                                                                        uint8_t* pk_ok, uint8_t* result) {
-  __shared__ PairXchg xc[CBFT_MS_SPLIT ? 3 : 1];  // split: the values of waves 2, 3, 4
+  __shared__ PairXchg xc[1];  // wave 2's value
   __shared__ uint32_t lines[BN_ATE_LINES * BN_ABC_WORDS];
   __shared__ int progress;
   __shared__ int usable;
-  __shared__ FeMail fm;  // the final exponentiation's helper: wave 3 (split) or wave 2
+  __shared__ FeMail fm;  // the final exponentiation's helper: wave 2
   if (blockIdx.x != 0) return;
   const int wave = threadIdx.x >> 6;
   const P36 g = p36_lane();
   if (threadIdx.x == 0) {
     progress = 0;
     usable = 0;
-    for (int w = 0; w < (CBFT_MS_SPLIT ? 3 : 1); w++) xc[w].ok = 0;
+    xc[0].ok = 0;
     femail_init(fm);
   }
   __syncthreads();
   fp f;
-  BLS_PHASE(wave == 0 ? 0 : wave == 1 ? 4 : 6);
-  const int lead = 1, helper = CBFT_MS_SPLIT ? 3 : 2;
+  const int lead = 1, helper = 2;
   if (wave == 0) {
     g2j acc;
     fp2_one(acc.X);
@@ -288,88 +255,51 @@ __global__ void __launch_bounds__(MS_BLOCK) bls_verify_multisig_kernel(const uin
       bad |= parts[55 * (size_t)b + 54] != 0;
       g2_add_j(acc, acc, o);
     }
-    BLS_PHASE(1);
     g2a s;
     g2_to_affine<true>(s, acc);  // public point: variable-time inversion
-    BLS_PHASE(2);
     const bool ok = !bad && !s.inf;
     if (g.lane == 0) {
       pk_ok[0] = ok ? 1 : 0;
       usable = ok ? 1 : 0;
     }
     if (ok) g2r_lines_abc(lines, s, &progress);
-    BLS_PHASE(3);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     if (g.lane == 0) progress = BN_ATE_LINES + 1;  // release the consumers whatever happened
-  } else if (CBFT_MS_SPLIT && wave <= 2) {
+  } else if (wave == 1) {
     g1a P;
     g1_map_row(P, msg, len);
-    BLS_PHASE(wave == 1 ? 5 : 14);
-    if (wave == 1)
-      p36_miller_part<true, true>(f, P, lines, g, &progress);
-    else
-      p36_miller_part<false, true>(f, P, lines, g, &progress);
-    BLS_PHASE(wave == 1 ? 12 : 15);
-  } else if (!CBFT_MS_SPLIT && wave == 1) {
-    g1a P;
-    g1_map_row(P, msg, len);
-    BLS_PHASE(5);
     const uint32_t* l[1] = {lines};
     p36_miller<1, true>(f, &P, l, g, &progress);
-    BLS_PHASE(12);
   } else {
     g1a s;
     const bool ok = g1_decompress_row(s, sig33);
     if (ok && !s.inf) {
       g1a P = s;
       f_neg(P.y, s.y);
-      BLS_PHASE(13);
       // (no lambda' here: this loop finishes before the (H, PK) loop that trails the line
       // computation, and forming it measured 12 us slower overall)
-      if (!CBFT_MS_SPLIT) {
-        const uint32_t* l[1] = {gen_lines};
-        p36_miller<1>(f, &P, l, g);
-      } else if (wave == 3) {
-        p36_miller_part<true>(f, P, gen_lines, g);
-      } else {
-        p36_miller_part<false>(f, P, gen_lines, g);
-      }
+      const uint32_t* l[1] = {gen_lines};
+      p36_miller<1>(f, &P, l, g);
     } else {
       p36_one(f, g);
     }
-    BLS_PHASE(7);
-    if (g.lane == 0) xc[CBFT_MS_SPLIT ? wave - 2 : 0].ok = ok ? 1 : 0;
+    if (g.lane == 0) xc[0].ok = ok ? 1 : 0;
   }
-  if (wave >= 2) xchg_put(xc[CBFT_MS_SPLIT ? wave - 2 : 0], f, g);
+  if (wave == 2) xchg_put(xc[0], f, g);
   __syncthreads();
-  bool good = xc[CBFT_MS_SPLIT ? 1 : 0].ok != 0 && usable != 0;  // sigma decoded (wave 3 / 2), PK usable
-  if (CBFT_P36_FE2 && wave == helper) {
+  bool good = xc[0].ok != 0 && usable != 0;  // sigma decoded (wave 2), PK usable
+  if (wave == helper) {
     if (good) p36_fe2_helper(fm, g);
     return;
   }
   if (wave != lead) return;
   if (good) {
-#pragma nounroll
-    for (int w = 0; w < (CBFT_MS_SPLIT ? 3 : 1); w++) {
-      fp f1;
-      xchg_get(f1, xc[w], g);
-      p36_mul(f, f, f1, g);
-    }
-    good = CBFT_P36_FE2 ? p36_is_one_after_final_exp_lead(f, fm, g) : p36_is_one_after_final_exp(f, g);
+    fp f1;
+    xchg_get(f1, xc[0], g);
+    p36_mul(f, f, f1, g);
+    good = p36_is_one_after_final_exp_lead(f, fm, g);
   }
-  BLS_PHASE(11);
   if (g.lane == 0) result[0] = good ? 1 : 0;
-#if CBFT_BLS_PHASES
-  if (g.lane == 0) {
-    const uint64_t t0 = g_bls_phase[0];
-    printf("bls_verify_multisig phases (us from start): key sum %.1f affine %.1f lines %.1f | H %.1f miller %.1f | "
-           "sigma %.1f miller %.1f | fe_inv %.1f fe_easy %.1f fe_pow_u %.1f fe_done %.1f\n",
-           (g_bls_phase[1] - t0) * 0.01, (g_bls_phase[2] - t0) * 0.01, (g_bls_phase[3] - t0) * 0.01,
-           (g_bls_phase[5] - t0) * 0.01, (g_bls_phase[12] - t0) * 0.01, (g_bls_phase[13] - t0) * 0.01,
-           (g_bls_phase[7] - t0) * 0.01, (g_bls_phase[8] - t0) * 0.01, (g_bls_phase[9] - t0) * 0.01,
-           (g_bls_phase[10] - t0) * 0.01, (g_bls_phase[11] - t0) * 0.01);
-  }
-#endif
 }
 
 // H = g1_map(msg) (block 0, when H is non-null) beside the decoding of k shares, one DPP row per
@@ -411,11 +341,7 @@ hipError_t cbft_bls_launch_share_verify(const uint8_t* d_shares, uint32_t k, uin
                                         const uint32_t* d_gen_lines, int do_verify, int parsed, uint8_t* d_valid,
                                         uint32_t* d_sig, uint32_t* d_ids, hipStream_t s) {
   if (!k) return hipSuccess;
-  static const int forced = [] {  // $CBFT_BLS_SHARE_WAVES: 1 or 2 forces the form (A/B), else by k
-    const char* e = getenv("CBFT_BLS_SHARE_WAVES");
-    return e ? atoi(e) : 0;
-  }();
-  const bool two = forced ? forced == 2 : 2 * (size_t)k <= SIMDS;
+  const bool two = 2 * (size_t)k <= SIMDS;  // two waves per share while they all fit one per SIMD
   if (do_verify && two)
     hipLaunchKernelGGL(bls_share_verify_kernel<2>, dim3(k), dim3(128), 0, s, d_shares, k, n, d_H, d_vk_lines,
                        d_vk_ok, d_gen_lines, do_verify, parsed, d_valid, d_sig, d_ids);

@@ -43,10 +43,6 @@ struct RowCtx {
 };
 
 // one round: row r multiplies a[r] * b[r] (r < N <= 4); every row receives all N products
-// (CBFT_ROW_GATHER_BPERMUTE=1: by ds_bpermute, the round-3 form, kept for A/B)
-#ifndef CBFT_ROW_GATHER_BPERMUTE
-#define CBFT_ROW_GATHER_BPERMUTE 0
-#endif
 template <int N, class U, class W>
 RF_HD void g1r_round(U* o, const U* a, const U* b, const RowCtx<U, W>& c) {
   U ua = a[0], ub = b[0];
@@ -61,17 +57,10 @@ RF_HD void g1r_round(U* o, const U* a, const U* b, const RowCtx<U, W>& c) {
     o[0] = p;
     return;
   }
-#if CBFT_ROW_GATHER_BPERMUTE
-  o[0] = rl_from_row<0>(p);
-  if (N > 1) o[1] = rl_from_row<1>(p);
-  if (N > 2) o[2] = rl_from_row<2>(p);
-  if (N > 3) o[3] = rl_from_row<3>(p);
-#else
   U r[4];
   rl_all_rows(p, r);  // lane swaps (row_lanes.h), not the LDS crossbar
 #pragma unroll
   for (int k = 0; k < N; k++) o[k] = r[k];
-#endif
 }
 
 // r = 2p, a = 0 (dbl-2009-l with D = 4XB taken as one product: (X + B)^2 - A - C = 2XB)

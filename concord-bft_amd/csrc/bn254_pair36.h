@@ -6,10 +6,8 @@
 // e_k, lanes 36..63 shadow lanes 0..27) and the products an Fp12 operation needs are dealt out
 // to the sub-lanes, then summed.  The other component of a lane's coefficient sits in the partner
 // lane (lane ^ 1): a DPP quad_perm move; the coefficient fetches and the sub-lane sums are
-// ds_bpermute gathers.
-//   CBFT_P36_ROWS = 1 (A/B only): sub-lane s in DPP row s (lane 16 s + 2 k + h, row positions
-//   12..15 shadow 8..11, row 3 shadows row 0), the sub-lane sum one rl_all_rows permlane gather.
-//   Measured 1.3 % (verify) to 2 % (multisig verify) slower than the bpermute sums.
+// ds_bpermute gathers.  (Sub-lane s in DPP row s, the sub-lane sum one permlane gather, measured
+// 1.3 % (verify) to 2 % (multisig verify) slower than the bpermute sums.)
 //   op          Fp mults per lane   (bn254_pair12.h)
 //   mul         4                   12    6 split products per component, 2 per sub-lane
 //   sqr         2                    8    even k: two diagonal squares on s = 0, one cross
@@ -26,10 +24,6 @@
 #include "bn254_pair12.h"
 #include "row_lanes.h"
 
-#ifndef CBFT_P36_ROWS
-#define CBFT_P36_ROWS 0
-#endif
-
 struct P36 {
   int k;     // coefficient 0..5
   int h;     // component: 0 = real, 1 = imaginary
@@ -42,17 +36,10 @@ struct P36 {
 __device__ __forceinline__ P36 p36_lane() {
   P36 g;
   g.lane = threadIdx.x & 63;
-#if CBFT_P36_ROWS
-  const int r = g.lane >> 4, q = g.lane & 15;
-  const int c = q < 12 ? q : q - 4;
-  g.s = r < 3 ? r : 0;
-  g.own = r < 3 && q < 12;
-#else
   const int e = g.lane < 36 ? g.lane : g.lane - 36;
   const int c = e % 12;
   g.s = e / 12;
   g.own = g.lane < 36;
-#endif
   g.k = c >> 1;
   g.h = c & 1;
   g.e = 12 * g.s + c;
@@ -60,42 +47,22 @@ __device__ __forceinline__ P36 p36_lane() {
 }
 
 __device__ __forceinline__ int p36_src(int k2, int h2, int s2) {
-  return (CBFT_P36_ROWS ? 16 : 12) * s2 + 2 * k2 + h2;
+  return 12 * s2 + 2 * k2 + h2;
 }
 
 // (q0, q1, q2) = part of sub-lanes 0, 1, 2 of this lane's component
 __device__ __forceinline__ void p36_gather3(fp& q0, fp& q1, fp& q2, const fp& part, const P36& g) {
-#if CBFT_P36_ROWS
-  (void)g;
-#pragma unroll
-  for (int i = 0; i < BN_LIMBS; i++) {
-    uint32_t r[4];
-    rl_all_rows(part.v[i], r);
-    q0.v[i] = r[0];
-    q1.v[i] = r[1];
-    q2.v[i] = r[2];
-  }
-#else
   fp_shfl(q0, part, p36_src(g.k, g.h, 0));
   fp_shfl(q1, part, p36_src(g.k, g.h, 1));
   fp_shfl(q2, part, p36_src(g.k, g.h, 2));
-#endif
 }
 
-// r = x of the partner lane (same k and s, the other component h): lane ^ 1 in both layouts,
-// shadows included, as a DPP quad_perm [1, 0, 3, 2] move instead of a ds_bpermute (CBFT_P36_DPP = 0:
-// the bpermute form)
-#ifndef CBFT_P36_DPP
-#define CBFT_P36_DPP 1
-#endif
+// r = x of the partner lane (same k and s, the other component h): lane ^ 1, shadows included, as a
+// DPP quad_perm [1, 0, 3, 2] move instead of a ds_bpermute
 __device__ __forceinline__ void fp_swap_h(fp& r, const fp& x, const P36& g) {
-#if CBFT_P36_DPP
   (void)g;
 #pragma unroll
   for (int i = 0; i < BN_LIMBS; i++) r.v[i] = (uint32_t)__builtin_amdgcn_mov_dpp((int)x.v[i], 0xB1, 0xF, 0xF, false);
-#else
-  fp_shfl(r, x, g.lane ^ 1);
-#endif
 }
 
 // (my component, the other component) of coefficient k2 of x.  The partner lane fetches the same
@@ -105,25 +72,17 @@ __device__ __forceinline__ void p36_fetch(fp& m, fp& o, const fp& x, int k2, con
   fp_swap_h(o, m, g);
 }
 
-// r = sum over the three sub-lanes of component (k, h) of part, in the order 0, 1, 2
-// CBFT_P36_SUM3_LAZY: one limb-wise three-term sum (< 6q), one carry pass and fp_reduce64 instead of
-// two reduced additions (each with its own conditional 2q subtraction and wave vote)
-#ifndef CBFT_P36_SUM3_LAZY
-#define CBFT_P36_SUM3_LAZY 1
-#endif
+// r = sum over the three sub-lanes of component (k, h) of part, in the order 0, 1, 2: one limb-wise
+// three-term sum (< 6q), one carry pass and fp_reduce64 (two reduced additions would each pay their
+// own conditional 2q subtraction and wave vote)
 __device__ __forceinline__ void p36_sum3(fp& r, const fp& part, const P36& g) {
   fp q0, q1, q2;
   p36_gather3(q0, q1, q2, part, g);
-  if (CBFT_P36_SUM3_LAZY) {
-    fp x;
+  fp x;
 #pragma unroll
-    for (int i = 0; i < BN_LIMBS; i++) x.v[i] = q0.v[i] + q1.v[i] + q2.v[i];  // inputs < 2q, normalised
-    cs_carry(x);
-    fp_reduce64(r, x);
-  } else {
-    f_add(r, q0, q1);
-    f_add(r, r, q2);
-  }
+  for (int i = 0; i < BN_LIMBS; i++) x.v[i] = q0.v[i] + q1.v[i] + q2.v[i];  // inputs < 2q, normalised
+  cs_carry(x);
+  fp_reduce64(r, x);
 }
 
 // my component of xi * z, z held componentwise by this lane and its partner (same k, s)
@@ -144,13 +103,10 @@ __device__ __forceinline__ void p36_cneg4(fp& r, const fp& v, bool neg) {
 }
 
 // r = a * b: sub-lane s forms the terms i = 2s, 2s + 1 of c_k = sum_i a_i b_{k-i} (xi on wrap);
-// lazy sums and one reduction (bn254_cycsq.h: cm_terms, cm_xi, cm_sum3)
-// CBFT_P36_MUL_MERGE: each term's Fp2-product component u b_m +- v b_o as ONE two-product
-// reduction (f_mul_sum2, v negated beforehand on the h = 0 lanes, as the lines): two reductions
-// per lane instead of four; cm_terms then only sums (h = 1, zero second terms).
-#ifndef CBFT_P36_MUL_MERGE
-#define CBFT_P36_MUL_MERGE 1
-#endif
+// lazy sums and one reduction (bn254_cycsq.h: cm_terms, cm_xi, cm_sum3).  Each term's Fp2-product
+// component u b_m +- v b_o is ONE two-product reduction (f_mul_sum2, v negated beforehand on the
+// h = 0 lanes, as the lines): two reductions per lane instead of four; cm_terms then only sums
+// (h = 1, zero second terms).
 __device__ __forceinline__ void p36_mul(fp& r, const fp& a, const fp& b, const P36& g) {
   fp T[4];
   bool wrap[2];
@@ -164,18 +120,13 @@ __device__ __forceinline__ void p36_mul(fp& r, const fp& a, const fp& b, const P
     p36_fetch(am, ao, a, i, g);
     p36_fetch(bm, bo, b, j, g);
     const fp u = g.h ? ao : am, v = g.h ? am : ao;
-    if (CBFT_P36_MUL_MERGE) {
-      fp vn;
-      p36_cneg4(vn, v, g.h == 0);
-      f_mul_sum2(T[2 * t], u, bm, vn, bo);
-      f_zero(T[2 * t + 1]);
-    } else {
-      f_mul(T[2 * t], u, bm);
-      f_mul(T[2 * t + 1], v, bo);
-    }
+    fp vn;
+    p36_cneg4(vn, v, g.h == 0);
+    f_mul_sum2(T[2 * t], u, bm, vn, bo);
+    f_zero(T[2 * t + 1]);
   }
   fp acc, accw, ao, z, z0, z1, z2;
-  cm_terms(acc, accw, T[0], T[1], T[2], T[3], CBFT_P36_MUL_MERGE ? 1 : g.h, wrap[0], wrap[1]);
+  cm_terms(acc, accw, T[0], T[1], T[2], T[3], 1, wrap[0], wrap[1]);
   fp_swap_h(ao, accw, g);
   cm_xi(z, acc, accw, ao, g.h);
   p36_gather3(z0, z1, z2, z, g);
@@ -226,16 +177,10 @@ __device__ __forceinline__ void p36_cyc_sqr(fp& r, const fp& a, const P36& g) {
   cs_operands(U, V, Wm, Wo, g.h);
   f_mul(T, U, V);
   // (x+y)^2_h (odd k) | y^2_h' (even k: the partner's sub-lane 1)
-#if CBFT_P36_ROWS
-  p36_gather3(X2, Y2, Z3, T, g);
-  fp_swap_h(G3, Y2, g);
-  if (odd) G3 = Z3;
-#else
   fp_shfl(X2, T, p36_src(g.k, g.h, 0));
   fp_shfl(Y2, T, p36_src(g.k, g.h, 1));
   fp_shfl(G3, T, odd ? p36_src(g.k, g.h, 2) : p36_src(g.k, 1 - g.h, 1));
   (void)Z3;
-#endif
   cs_combine(v, X2, Y2, G3, g.k, g.h);
   fp_swap_h(vo, v, g);
   cs_finish(r, v, vo, a, g.k, g.h);
@@ -253,18 +198,14 @@ __device__ __forceinline__ void p36_coef(fp& m, fp& o, const uint32_t* c, int h)
 // f <- f * (yP + s w + mu w^3), s = -lambda xP, for one precomputed line:
 //   s = 0: f_k yP;  s = 1: -xP (f_{k-1} lambda) (xi for k = 0);  s = 2: f_{k-3} mu (xi for k < 3)
 // this lane's (my, other) components of the line coefficient it multiplies by (lambda for s < 2,
-// mu for s = 2): the line's global-memory read, separable from the line so that it can be issued
-// one line ahead (p36_miller, CBFT_P36_PREFETCH)
+// mu for s = 2): the line's global-memory read
 __device__ __forceinline__ void p36_line_coef(fp& cm, fp& co, const uint32_t* ln, const P36& g) {
   p36_coef(cm, co, ln + (g.s == 2 ? 18 : 0), g.h);
 }
 
-// CBFT_P36_LINE_MERGE: a line's component C = u c_m +- v c_o (the Fp2 product's component h) as
-// ONE two-product reduction (f_mul_sum2) with v negated beforehand (4q - v, redundant limbs, on
-// the h = 0 lanes) instead of two f_mul and f_addsub; s = 0 lanes zero their second product.
-#ifndef CBFT_P36_LINE_MERGE
-#define CBFT_P36_LINE_MERGE 1
-#endif
+// A line's component C = u c_m +- v c_o (the Fp2 product's component h) is ONE two-product
+// reduction (f_mul_sum2) with v negated beforehand (4q - v, redundant limbs, on the h = 0 lanes)
+// instead of two f_mul and f_addsub; s = 0 lanes zero their second product.
 // P: the G1 point with its x NEGATED (p36_neg_x), so the s = 1 term -xP (f_{k-1} lambda) is one
 // product; the Miller loops negate once, before their first line.
 __device__ __forceinline__ g1a p36_neg_x(const g1a& P) {
@@ -279,7 +220,6 @@ __device__ __forceinline__ void p36_line1c(fp& f, const fp& cm, const fp& co, co
   fp X1 = g.s == 0 ? f : u;
   fp Y1 = g.s == 0 ? P.y : cm;
   fp P3, C;
-#if CBFT_P36_LINE_MERGE
   fp vn, cz;
   p36_cneg4(vn, v, g.h == 0);
   const uint32_t mz = cs_mask(g.s != 0);
@@ -289,14 +229,6 @@ __device__ __forceinline__ void p36_line1c(fp& f, const fp& cm, const fp& co, co
   f_mul(P3, C, P.x);              // P.x holds -xP (p36_line1: the caller negates once per loop)
   fp T = C;
   fp_sel(T, P3, g.s == 1);
-#else
-  fp P1, P2;
-  f_mul(P1, X1, Y1);
-  f_mul(P2, v, co);
-  f_addsub(C, P1, P2, g.h != 0);
-  f_mul(P3, C, P.x);  // P.x holds -xP
-  fp T = g.s == 0 ? P1 : (g.s == 1 ? P3 : C);
-#endif
   const bool wrap = (g.s == 1 && g.k == 0) || (g.s == 2 && g.k < 3);
   fp w;
   p36_xi(w, T, g);
@@ -310,23 +242,17 @@ __device__ __forceinline__ void p36_line1(fp& f, const uint32_t* ln, const g1a& 
   p36_line1c(f, cm, co, P, g);
 }
 
-// CBFT_P36_LAMBDA_X: the Miller loops first form lambda' = -xP lambda for every normalised line
-// they will read (p36_lambda_x: 140 Fp products per pair over the wave's 64 lanes, into LDS); a
-// line's s = 1 term -xP (f_{k-1} lambda) = f_{k-1} lambda' is then the same two-product reduction
-// as the s = 2 term, and no lane multiplies by xP inside the loop (two products per lane per line
-// instead of three).
-#ifndef CBFT_P36_LAMBDA_X
-#define CBFT_P36_LAMBDA_X 1
-#endif
-// CBFT_P36_XI_PRE: the record also holds xi lambda' and xi mu, so the lanes whose term wraps (s = 1,
-// k = 0; s = 2, k < 3) read pre-twisted coefficients and no lane applies xi after the product.
-#ifndef CBFT_P36_XI_PRE
-#define CBFT_P36_XI_PRE 1
-#endif
-#define P36_LX_WORDS (CBFT_P36_XI_PRE ? 54 : 18)  // per line: lambda' | xi lambda' | xi mu (9-limb components)
+// Lambda records: with LDS room (lx) the Miller loops first form lambda' = -xP lambda for every
+// normalised line they will read (p36_lambda_x: 140 Fp products per pair over the wave's 64 lanes,
+// into LDS); a line's s = 1 term -xP (f_{k-1} lambda) = f_{k-1} lambda' is then the same two-product
+// reduction as the s = 2 term, and no lane multiplies by xP inside the loop (two products per lane
+// per line instead of three).  The record also holds xi lambda' and xi mu, so the lanes whose term
+// wraps (s = 1, k = 0; s = 2, k < 3) read pre-twisted coefficients and no lane applies xi after the
+// product.
+#define P36_LX_WORDS 54  // per line: lambda' | xi lambda' | xi mu (9-limb components)
 // lx[(j (k1 - k0) + k - k0) P36_LX_WORDS + ...] for pair j's line k in [k0, k1): lambda' = -xP lambda
-// (components 0, 1), then (CBFT_P36_XI_PRE) xi lambda', xi mu; Pn[j].x holds -xP_j.  One lane per
-// (pair, line); the whole wave calls it.
+// (components 0, 1), then xi lambda', xi mu; Pn[j].x holds -xP_j.  One lane per (pair, line); the
+// whole wave calls it.
 template <int NP>
 __device__ __forceinline__ void p36_lambda_x(uint32_t* lx, const g1a* Pn, const uint32_t* const* lines, int k0, int k1,
                                              const P36& g) {
@@ -360,7 +286,7 @@ __device__ __forceinline__ void p36_lambda_x(uint32_t* lx, const g1a* Pn, const 
         dst[i] = r.a.v[i];
         dst[9 + i] = r.b.v[i];
       }
-    if (CBFT_P36_XI_PRE) {
+    {
       fp2 m, t;
 #pragma unroll
       for (int i = 0; i < BN_LIMBS; i++) {
@@ -387,11 +313,11 @@ __device__ __forceinline__ void p36_line_lx(fp& f, const uint32_t* lxk, const ui
   p36_fetch(om, oo, f, g.s == 1 ? (g.k + 5) % 6 : (g.k + 3) % 6, g);
   const bool wrap = (g.s == 1 && g.k == 0) || (g.s == 2 && g.k < 3);
   fp lm, lo, mm, mo;
-  // s = 1: lambda' (xi lambda' on wrap); s = 2 on wrap: xi mu (CBFT_P36_XI_PRE); else mu from the table
-  const int off = CBFT_P36_XI_PRE ? (g.s == 2 ? 36 : (wrap ? 18 : 0)) : 0;
+  // s = 1: lambda' (xi lambda' on wrap); s = 2 on wrap: xi mu; else mu from the table
+  const int off = g.s == 2 ? 36 : (wrap ? 18 : 0);
   p36_coef(lm, lo, lxk + off, g.h);
   p36_coef(mm, mo, ln + 18, g.h);
-  const bool use_lds = g.s == 1 || (CBFT_P36_XI_PRE && wrap);
+  const bool use_lds = g.s == 1 || wrap;
   const fp u = g.h ? oo : om, v = g.h ? om : oo;
   fp X1 = g.s == 0 ? f : u;
   fp Y1 = g.s == 0 ? P.y : (use_lds ? lm : mm);
@@ -403,11 +329,6 @@ __device__ __forceinline__ void p36_line_lx(fp& f, const uint32_t* lxk, const ui
   p36_cneg4(vn, v, g.h == 0);
   fp T;
   f_mul_sum2(T, X1, Y1, vn, cz);  // s = 0: f_k yP; s = 1: f_{k-1} lambda'; s = 2: f_{k-3} mu
-  if (!CBFT_P36_XI_PRE) {
-    fp w;
-    p36_xi(w, T, g);
-    fp_sel(T, w, wrap);
-  }
   p36_sum3(f, T, g);
 }
 
@@ -420,16 +341,9 @@ __device__ __forceinline__ void p36_line_abc(fp& f, const uint32_t* ln, const g1
   p36_coef(cm, co, ln + 18 * g.s, g.h);
   const fp u = g.h ? oo : om, v = g.h ? om : oo;
   fp P3, C;
-#if CBFT_P36_LINE_MERGE
   fp vn;
   p36_cneg4(vn, v, g.h == 0);
   f_mul_sum2(C, u, cm, vn, co);
-#else
-  fp P1, P2;
-  f_mul(P1, u, cm);
-  f_mul(P2, v, co);
-  f_addsub(C, P1, P2, g.h != 0);
-#endif
   f_mul(P3, C, g.s == 0 ? P.y : P.x);
   fp T = g.s == 2 ? C : P3;
   const bool wrap = (g.s == 1 && g.k == 0) || (g.s == 2 && g.k < 3);
@@ -514,13 +428,10 @@ __device__ __forceinline__ void p36_frob(fp& r, const fp& x, const P36& g) {
 // x is a Miller value of public inputs), then conj(x) N^-1 on the wave.  Half the one-lane tower
 // work of inverting in Fp12 directly.
 //
-// CBFT_P36_INV_LANES: the Fp6 inversion's Fp2 products spread over lanes (fp6_inv's formulas): six
-// lanes form c0^2, c1 c2, c2^2, c0 c1, c1^2, c0 c2 at once, three lanes c2 t1, c1 t2, c0 t0, and
-// each lane its own t_(k/2) N^-1 -- 3 Fp2 products on the critical path between the gathers and
-// the one Fp2 inversion instead of 12.
-#ifndef CBFT_P36_INV_LANES
-#define CBFT_P36_INV_LANES 1
-#endif
+// The Fp6 inversion's Fp2 products are spread over lanes (fp6_inv's formulas): six lanes form c0^2,
+// c1 c2, c2^2, c0 c1, c1^2, c0 c2 at once, three lanes c2 t1, c1 t2, c0 t0, and each lane its own
+// t_(k/2) N^-1 -- 3 Fp2 products on the critical path between the gathers and the one Fp2
+// inversion instead of 12.
 __device__ __forceinline__ void fp2_shfl(fp2& r, const fp2& x, int src) {
   fp_shfl(r.a, x.a, src);
   fp_shfl(r.b, x.b, src);
@@ -537,7 +448,7 @@ __device__ __noinline__ void p36_inv(fp& r, const fp& x, const P36& g) {
   fp_shfl(t.c2.a, n, p36_src(4, 0, 0));
   fp_shfl(t.c2.b, n, p36_src(4, 1, 0));
   fp2 pick;
-  if (CBFT_P36_INV_LANES) {
+  {
     const int j = g.lane;
     // lane j < 6: (c0 c0, c1 c2, c2 c2, c0 c1, c1 c1, c0 c2)[j]
     fp2 X = t.c0, Y = t.c0, R, R0, R1, R2, R3, R4, R5;
@@ -579,11 +490,6 @@ __device__ __noinline__ void p36_inv(fp& r, const fp& x, const P36& g) {
     p12_sel2(tk, t1, g.k == 2 || g.k == 3);
     p12_sel2(tk, t2, g.k >= 4);
     fp2_mul(pick, tk, nn);
-  } else {
-    fp6_inv<true>(t, t);
-    pick = t.c0;
-    p12_sel2(pick, t.c1, g.k == 2);
-    p12_sel2(pick, t.c2, g.k == 4);
   }
   fp ninv = g.h ? pick.b : pick.a;
   if (g.k & 1) f_zero(ninv);
@@ -612,46 +518,23 @@ __device__ __forceinline__ void p36_pow_small(fp& r, const fp& x, uint32_t e, co
   r = acc;
 }
 
-#ifndef CBFT_BLS_PHASES
-#define CBFT_BLS_PHASES 0
-#endif
-// phase timestamps (probe builds): slot -> 10 ns wall-clock tick, printed once by the kernel
-#if CBFT_BLS_PHASES
-__device__ uint64_t g_bls_phase[16];
-#define BLS_STAMP(slot)                                                 \
-  do {                                                                  \
-    if ((threadIdx.x & 63) == 0) g_bls_phase[(slot)] = wall_clock64(); \
-  } while (0)
-#else
-#define BLS_STAMP(slot) \
-  do {                  \
-  } while (0)
-#endif
-#define P36_PHASE(name) BLS_STAMP(name)
-
-// CBFT_P36_FE_VEC: the hard part's tail as a vectorial addition chain (gg^d = y0 y1^2 y2^6 y3^12
+// The hard part's tail as a vectorial addition chain (gg^d = y0 y1^2 y2^6 y3^12
 // y4^18 y5^30 y6^36 with y0 = gg^(p + p^2 + p^3), y1 = 1/gg, y2 = b^(p^2), y3 = a^-p, y4 = 1/(a b^p),
 // y5 = 1/b, y6 = 1/(c c^p): 4 squarings, 13 products, 7 Frobenius maps) instead of raising c, b, a
 // to 36, 30, 18, 12, 6 separately (16 squarings, 17 products, 3 maps).  The same exponent d, so
 // the same GT element.
-#ifndef CBFT_P36_FE_VEC
-#define CBFT_P36_FE_VEC 1
-#endif
 __device__ __forceinline__ void p36_final_exp(fp& r, const fp& f, const P36& g) {
   fp t, gg;
   p36_inv(t, f, g);
-  P36_PHASE(8);
   p36_conj(gg, f, g);
   p36_mul(gg, gg, t, g);
   p36_frob<2>(t, gg, g);
   p36_mul(gg, t, gg, g);
-  P36_PHASE(9);
   fp a, b, c;
   p36_pow_u(a, gg, g);
   p36_pow_u(b, a, g);
   p36_pow_u(c, b, g);
-  P36_PHASE(10);
-  if (CBFT_P36_FE_VEC) {
+  {
     fp y0, y1, y2, y3, y4, y5, y6, u, T0, T1;
     p36_frob<1>(y0, gg, g);
     p36_frob<2>(u, gg, g);
@@ -682,33 +565,7 @@ __device__ __forceinline__ void p36_final_exp(fp& r, const fp& f, const P36& g) 
     p36_mul(T1, T1, y0, g);
     p36_cyc_sqr(T0, T0, g);  // y6^24 y5^20 y4^12 y3^8 y2^4 y1^2
     p36_mul(r, T0, T1, g);
-    return;
   }
-  fp c36, b6, b18, b30, a12, a18, g2;
-  p36_pow_small(c36, c, 36, g);
-  p36_pow_small(b6, b, 6, g);
-  p36_pow_small(b18, b6, 3, g);
-  p36_mul(b30, b18, b6, g);
-  p36_mul(b30, b30, b6, g);
-  p36_pow_small(a12, a, 12, g);
-  p36_pow_small(a18, a, 18, g);
-  p36_cyc_sqr(g2, gg, g);
-  fp t0, t1, t2, t3;
-  p36_mul(t0, c36, b30, g);
-  p36_mul(t0, t0, a18, g);
-  p36_mul(t0, t0, g2, g);
-  p36_conj(t0, t0, g);
-  p36_mul(t1, c36, b18, g);
-  p36_mul(t1, t1, a12, g);
-  p36_conj(t1, t1, g);
-  p36_mul(t1, t1, gg, g);
-  p36_mul(t2, b6, gg, g);
-  p36_frob<1>(t1, t1, g);
-  p36_frob<2>(t2, t2, g);
-  p36_frob<3>(t3, gg, g);
-  p36_mul(t0, t0, t1, g);
-  p36_mul(t0, t0, t2, g);
-  p36_mul(r, t0, t3, g);
 }
 
 // f = prod_{j < NP} of the Miller values of (P_j, Q_j) (lines of Q_j precomputed, normalised or
@@ -716,14 +573,9 @@ __device__ __forceinline__ void p36_final_exp(fp& r, const fp& f, const P36& g) 
 // Miller values of disjoint pair sets multiply (the loop squares and conjugates a product), so
 // two waves may run one pair each and multiply their f.  All 64 lanes of the wave call it.
 // progress (nullable, LDS): lines are still being produced by another wave of the block
-// (g2w_lines_abc); line k is read once progress > k.
-// CBFT_P36_PREFETCH = 1 (A/B only): normalised lines from global memory are read one line ahead
-// (each pair's next coefficients load while the current line and the next squaring run) instead
-// of right before their use.  Measured equal or 1-2 % slower (profiles/r05_ab/bls_line_prefetch.txt):
-// the line tables are L2-resident and the load latency is not what a lone wave waits on.
-#ifndef CBFT_P36_PREFETCH
-#define CBFT_P36_PREFETCH 0
-#endif
+// (g2w_lines_abc); line k is read once progress > k.  (Reading each line's coefficients one line
+// ahead measured equal or 1-2 % slower: the line tables are L2-resident and the load latency is not
+// what a lone wave waits on.)
 // lx (nullable, LDS, NP x 70 x P36_LX_WORDS words, normalised lines only): room for p36_lambda_x
 template <int NP, bool ABC = false>
 __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* const* lines, const P36& g,
@@ -734,7 +586,7 @@ __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* 
   g1a Pn[NP];  // normalised lines take -xP (p36_line1c)
 #pragma unroll
   for (int j = 0; j < NP; j++) Pn[j] = ABC ? P[j] : p36_neg_x(P[j]);
-  if (CBFT_P36_LAMBDA_X && !ABC && !progress && lx) {
+  if (!ABC && !progress && lx) {
     p36_lambda_x<NP>(lx, Pn, lines, 0, BN_ATE_LINES, g);
     auto lline = [&](int j) { p36_line_lx(f, lx + (j * BN_ATE_LINES + k) * P36_LX_WORDS, lines[j] + k * W, P[j], g); };
 #pragma nounroll
@@ -753,37 +605,6 @@ __device__ __forceinline__ void p36_miller(fp& f, const g1a* P, const uint32_t* 
     for (int t = 0; t < 2; t++) {
 #pragma unroll
       for (int j = 0; j < NP; j++) lline(j);
-      k++;
-    }
-    return;
-  }
-  if (CBFT_P36_PREFETCH && !ABC && !progress) {
-    fp cm[NP], co[NP];
-#pragma unroll
-    for (int j = 0; j < NP; j++) p36_line_coef(cm[j], co[j], lines[j], g);
-    auto pline = [&](int j) {
-      fp nm, no;
-      if (k + 1 < BN_ATE_LINES) p36_line_coef(nm, no, lines[j] + (k + 1) * W, g);
-      p36_line1c(f, cm[j], co[j], Pn[j], g);
-      cm[j] = nm;
-      co[j] = no;
-    };
-#pragma nounroll
-    for (int i = BN_ATE_DBL - 1; i >= 0; i--) {
-      p36_sqr(f, f, g);
-#pragma unroll
-      for (int j = 0; j < NP; j++) pline(j);
-      k++;
-      if (bn_ate_bit(i)) {
-#pragma unroll
-        for (int j = 0; j < NP; j++) pline(j);
-        k++;
-      }
-    }
-    p36_conj(f, f, g);
-    for (int t = 0; t < 2; t++) {
-#pragma unroll
-      for (int j = 0; j < NP; j++) pline(j);
       k++;
     }
     return;
@@ -834,7 +655,7 @@ __device__ __forceinline__ void p36_miller_part(fp& f, const g1a& P, const uint3
   int k = 0;
   const int hi = TOP ? BN_ATE_DBL - 1 : P36_MILLER_SPLIT - 1, lo = TOP ? P36_MILLER_SPLIT : 0;
   for (int i = BN_ATE_DBL - 1; i > hi; i--) k += bn_ate_bit(i) ? 2 : 1;
-  if (CBFT_P36_LAMBDA_X && !ABC && !progress && lx) {
+  if (!ABC && !progress && lx) {
     int k1 = k;  // this part's lines: [k, k1)
     for (int i = hi; i >= lo; i--) k1 += bn_ate_bit(i) ? 2 : 1;
     if (!TOP) k1 += 2;  // the two Frobenius lines
@@ -863,27 +684,16 @@ __device__ __forceinline__ void p36_miller_part(fp& f, const g1a& P, const uint3
     }
     return;
   }
-  // lines read one ahead (CBFT_P36_PREFETCH; the top part's last read is a bottom line, unused)
-  constexpr bool PF = CBFT_P36_PREFETCH && !ABC;
   const g1a Pn = ABC ? P : p36_neg_x(P);  // normalised lines take -xP (p36_line1c)
-  fp cm, co;
-  if (PF) p36_line_coef(cm, co, lines + k * W, g);
   auto line = [&]() {
     if (progress) {
       while (*progress <= k) __builtin_amdgcn_s_sleep(2);
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
-    if (ABC) {
+    if (ABC)
       p36_line_abc(f, lines + k * W, P, g);
-    } else if (PF) {
-      fp nm, no;
-      if (k + 1 < BN_ATE_LINES) p36_line_coef(nm, no, lines + (k + 1) * W, g);
-      p36_line1c(f, cm, co, Pn, g);
-      cm = nm;
-      co = no;
-    } else {
+    else
       p36_line1(f, lines + k * W, Pn, g);
-    }
     k++;
   };
 #pragma nounroll
@@ -916,7 +726,7 @@ __device__ __forceinline__ bool p36_is_one_after_final_exp(const fp& f, const P3
   return all;
 }
 
-// ---- the final exponentiation on two waves of a block (CBFT_P36_FE2) ----
+// ---- the final exponentiation on two waves of a block ----
 // The hard part's three u-powers a = gg^u, b = a^u, c = b^u are one serial chain; everything
 // else p36_final_exp derives from gg, a and b (a^12, a^18, b^6, b^18, b^30, gg^2 and two of the
 // Frobenius terms) runs on a helper wave while the lead wave is still raising to u, so the lead's
@@ -924,9 +734,6 @@ __device__ __forceinline__ bool p36_is_one_after_final_exp(const fp& f, const P3
 // as p36_final_exp (products reassociated; f_eq compares canonical forms).  Values pass through
 // an LDS mailbox: the writer's owning lanes store, release-fence, then lane 0 raises the slot's
 // flag; the reader spins on the flag (s_sleep) and acquire-fences.
-#ifndef CBFT_P36_FE2
-#define CBFT_P36_FE2 1
-#endif
 struct FeMail {
   enum { GG = 0, A = 1, B = 2, X = 3, Y = 4, Z = 5, SLOTS = 6 };
   uint32_t v[SLOTS][36][BN_LIMBS];
@@ -957,14 +764,12 @@ __device__ __forceinline__ void femail_read(fp& x, const FeMail& m, int slot, co
 __device__ __forceinline__ void p36_final_exp_lead(fp& r, const fp& f, FeMail& m, const P36& g) {
   fp t, gg;
   p36_inv(t, f, g);
-  P36_PHASE(8);
   p36_conj(gg, f, g);
   p36_mul(gg, gg, t, g);
   p36_frob<2>(t, gg, g);
   p36_mul(gg, t, gg, g);
   femail_write(m, FeMail::GG, gg, g);
   femail_raise(m, FeMail::GG, g);
-  P36_PHASE(9);
   fp a, b, c;
   p36_pow_u(a, gg, g);
   femail_write(m, FeMail::A, a, g);
@@ -973,7 +778,6 @@ __device__ __forceinline__ void p36_final_exp_lead(fp& r, const fp& f, FeMail& m
   femail_write(m, FeMail::B, b, g);
   femail_raise(m, FeMail::B, g);
   p36_pow_u(c, b, g);
-  P36_PHASE(10);
   fp c36, X, Y, Z, t0, t1;
   p36_pow_small(c36, c, 36, g);
   femail_wait(m, FeMail::Z);  // X, Y, Z raised together

@@ -74,13 +74,9 @@ int cbft_bls_load_keys(cbft_ctx* c, const uint8_t* pk65, const uint8_t* vks65, u
   CBFT_HIP(hipMemcpyAsync(ks.keys65.p, pk65, 65, hipMemcpyHostToDevice, c->stream));
   if (n)
     CBFT_HIP(hipMemcpyAsync(ks.keys65.as<uint8_t>() + 65, vks65, (size_t)n * 65, hipMemcpyHostToDevice, c->stream));
-  DevBuf scratch;
-  CBFT_HIP(scratch.reserve(cbft_bls_keys_scratch_words((uint32_t)nk) * 4));
-  hipError_t e = cbft_bls_launch_keys(ks.keys65.as<uint8_t>(), (uint32_t)nk, ks.lines.as<uint32_t>(),
-                                      ks.ok.as<uint8_t>(), ks.aff.as<uint32_t>(), scratch.as<uint32_t>(), c->stream);
-  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-  scratch.release();
-  CBFT_HIP(e);
+  CBFT_HIP(cbft_bls_launch_keys(ks.keys65.as<uint8_t>(), (uint32_t)nk, ks.lines.as<uint32_t>(), ks.ok.as<uint8_t>(),
+                                ks.aff.as<uint32_t>(), c->stream));
+  CBFT_HIP(hipStreamSynchronize(c->stream));
   uint32_t id = c->next_bls_id++;
   c->bls_sets.emplace(id, std::move(ks));
   *out_id = id;
@@ -572,22 +568,13 @@ int cbft_bls_public_key(cbft_ctx* c, const uint8_t* sk32, uint8_t* out65) {
   CBFT_HIP(c->bls_out.reserve(65));
   wipe.on_device = true;
   CBFT_HIP(hipMemcpyAsync(c->bls_lambda.p, w, sizeof(w), hipMemcpyHostToDevice, c->stream));
-  // fixed-base comb of g2 on row-parallel Fp (its 64 x 8 table built once per context, ~10 ms),
-  // unless $CBFT_BLS_PUBKEY=lane (the one-lane Montgomery ladder, 17 ms: the A/B reference)
-  static const bool lane = [] {
-    const char* e = getenv("CBFT_BLS_PUBKEY");
-    return e && strcmp(e, "lane") == 0;
-  }();
-  if (lane) {
-    CBFT_HIP(cbft_bls_launch_pubkey(c->bls_lambda.as<uint32_t>(), c->bls_out.as<uint8_t>(), c->stream));
-  } else {
-    if (!c->bls_pub_tbl.p) {
-      CBFT_HIP(c->bls_pub_tbl.reserve(cbft_bls_pub_table_words() * sizeof(uint32_t)));
-      CBFT_HIP(cbft_bls_launch_pub_table(c->bls_pub_tbl.as<uint32_t>(), c->stream));
-    }
-    CBFT_HIP(cbft_bls_launch_pubkey_row(c->bls_pub_tbl.as<uint32_t>(), c->bls_lambda.as<uint32_t>(),
-                                        c->bls_out.as<uint8_t>(), c->stream));
+  // fixed-base comb of g2 on row-parallel Fp (its 64 x 8 table built once per context, ~10 ms)
+  if (!c->bls_pub_tbl.p) {
+    CBFT_HIP(c->bls_pub_tbl.reserve(cbft_bls_pub_table_words() * sizeof(uint32_t)));
+    CBFT_HIP(cbft_bls_launch_pub_table(c->bls_pub_tbl.as<uint32_t>(), c->stream));
   }
+  CBFT_HIP(cbft_bls_launch_pubkey_row(c->bls_pub_tbl.as<uint32_t>(), c->bls_lambda.as<uint32_t>(),
+                                      c->bls_out.as<uint8_t>(), c->stream));
   CBFT_HIP(hipMemcpyAsync(out65, c->bls_out.p, 65, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipMemsetAsync(c->bls_lambda.p, 0, sizeof(w), c->stream));  // the secret scalar leaves the device
   CBFT_HIP(hipStreamSynchronize(c->stream));
@@ -635,17 +622,8 @@ int cbft_bls_sign(cbft_ctx* c, const uint8_t* sk32, uint32_t id, const uint8_t* 
   CBFT_HIP(hipMemcpyAsync(c->bls_msg.p, in.data(), in.size(), hipMemcpyHostToDevice, c->stream));
   const uint32_t* d_sk = c->bls_msg.as<uint32_t>();
   const uint8_t* d_msg = c->bls_msg.as<uint8_t>() + msg_at;
-  // row-parallel GLV signature (0.4-0.5 ms) unless $CBFT_BLS_SIGN=lane (the one-lane Montgomery
-  // ladder, 4.4 ms: kept as the A/B reference)
-  static const bool lane = [] {
-    const char* e = getenv("CBFT_BLS_SIGN");
-    return e && strcmp(e, "lane") == 0;
-  }();
-  if (lane) {
-    CBFT_HIP(cbft_bls_launch_sign(d_msg, len, d_sk, id, c->bls_out.as<uint8_t>(), c->stream));
-  } else {  // the hash to G1 inside the signing kernel (H = nullptr)
-    CBFT_HIP(cbft_bls_launch_sign_row(nullptr, d_sk, d_msg, len, id, c->bls_out.as<uint8_t>(), c->stream));
-  }
+  // row-parallel GLV signature (0.4-0.5 ms), the hash to G1 inside the signing kernel (H = nullptr)
+  CBFT_HIP(cbft_bls_launch_sign_row(nullptr, d_sk, d_msg, len, id, c->bls_out.as<uint8_t>(), c->stream));
   CBFT_HIP(hipMemcpyAsync(out37, c->bls_out.p, 37, hipMemcpyDeviceToHost, c->stream));
   CBFT_HIP(hipMemsetAsync(c->bls_msg.p, 0, sizeof(w), c->stream));  // the secret scalar leaves the device
   CBFT_HIP(hipStreamSynchronize(c->stream));

@@ -83,6 +83,23 @@ static hipError_t build_comb(const uint8_t* d_pk, size_t nunits, int negate, con
 
 static int collect_locked(HostSlot& s);
 
+// Comb table of B at radix c->b_radix (the "key" is B's encoding, not negated); synchronous.
+static int build_base_comb(cbft_ctx* c) {
+  static const uint8_t kB[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                                 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
+                                 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
+  const CombGeom gb = cbft_comb_geom(c->b_radix);
+  DevBuf enc;
+  if (c->base_comb.reserve(gb.words_per_unit() * 4) != hipSuccess || enc.reserve(32) != hipSuccess) {
+    enc.release();
+    return CBFT_ENOMEM;
+  }
+  const bool ok = hipMemcpy(enc.p, kB, 32, hipMemcpyHostToDevice) == hipSuccess &&
+                  build_comb(enc.as<uint8_t>(), 1, 0, gb, c->base_comb.as<uint32_t>(), nullptr, c->stream) == hipSuccess;
+  enc.release();
+  return ok ? CBFT_OK : CBFT_EIO;
+}
+
 // A multi-GPU context runs BLS, RSA and profiling calls on its first device.
 cbft_ctx* cbft_dev0(cbft_ctx* c) { return (c && !c->kids.empty()) ? c->kids[0] : c; }
 
@@ -148,34 +165,6 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   cbft_ctx* c = new (std::nothrow) cbft_ctx();
   if (!c) return CBFT_ENOMEM;
   c->device = device;
-  if (const char* e = getenv("CBFT_FINISH_BATCH")) c->finish_batch = atoi(e);
-  if (const char* e = getenv("CBFT_WORK_SLOTS")) c->work_slots = std::max(1, std::min(CBFT_MAX_WORK_SLOTS, atoi(e)));
-  if (const char* e = getenv("CBFT_HASH_ORDER_EARLY")) c->hash_order_early = atoi(e);
-  if (const char* e = getenv("CBFT_FINISH_TREE_BLOCK")) c->finish_tree_block = atoi(e);
-  if (const char* e = getenv("CBFT_FINISH_SPLIT")) c->finish_split = atoi(e);
-  if (const char* e = getenv("CBFT_SHA_LONG_GROUPS")) c->long_groups = std::max(0, std::min(1024, atoi(e)));
-  if (const char* e = getenv("CBFT_HASH_PRIO")) c->hash_prio = atoi(e);
-  if (const char* e = getenv("CBFT_HASH_LONG_PRIO")) c->long_prio = atoi(e);
-  if (const char* e = getenv("CBFT_LADDER_PREFETCH")) c->ladder_prefetch = atoi(e);
-  if (const char* e = getenv("CBFT_STAGE_ORDER")) c->stage_order = atoi(e);
-  if (const char* e = getenv("CBFT_STAGE_ORDER_VAR")) c->stage_order_var = atoi(e);
-  if (const char* e = getenv("CBFT_ORDER_MAX_STREAMS")) c->order_max_streams = atoi(e);
-  if (const char* e = getenv("CBFT_STAGE_ORDER_MIN")) c->stage_order_min = (size_t)atoll(e);
-  if (const char* e = getenv("CBFT_SMALL_MAX")) c->small_max = (size_t)atoll(e);
-  if (const char* e = getenv("CBFT_SHA_SORT_MIN")) c->sha_sort_min = (size_t)atoll(e);
-  if (const char* e = getenv("CBFT_SHA_LONG")) c->sha_long = atoi(e);
-  if (const char* e = getenv("CBFT_SMALL_WAVES")) c->small_waves = atoi(e) == 3 ? 3 : 2;
-  if (const char* e = getenv("CBFT_ZERO_COPY")) c->zero_copy = atoi(e);
-  if (const char* e = getenv("CBFT_BLOCKING_SYNC")) c->blocking_sync = atoi(e);
-  if (const char* e = getenv("CBFT_SMALL_STREAMS")) c->nsmall = std::max(1, std::min(CBFT_SMALL_STREAMS, atoi(e)));
-  if (const char* e = getenv("CBFT_LADDER_LANES")) {
-    const int l = atoi(e);
-    if (l == 2 || l == 4) c->ladder_lanes = l;
-  }
-  if (const char* e = getenv("CBFT_B_RADIX")) {
-    const int r = atoi(e);
-    if (r >= 16 && r <= CBFT_COMB_MAX_RADIX) c->b_radix = r;
-  }
   int rc = CBFT_OK;
   do {
     if (hipSetDevice(device) != hipSuccess) {
@@ -199,25 +188,7 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
       rc = CBFT_EIO;
       break;
     }
-    {  // comb table of B (the "key" is B's encoding, not negated)
-      static const uint8_t kB[32] = {0x58, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
-                                     0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66,
-                                     0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66, 0x66};
-      const CombGeom gb = cbft_comb_geom(c->b_radix);
-      DevBuf enc;
-      if (c->base_comb.reserve(gb.words_per_unit() * 4) != hipSuccess || enc.reserve(32) != hipSuccess) {
-        enc.release();
-        rc = CBFT_ENOMEM;
-        break;
-      }
-      bool okb = hipMemcpy(enc.p, kB, 32, hipMemcpyHostToDevice) == hipSuccess &&
-                 build_comb(enc.as<uint8_t>(), 1, 0, gb, c->base_comb.as<uint32_t>(), nullptr, c->stream) == hipSuccess;
-      enc.release();
-      if (!okb) {
-        rc = CBFT_EIO;
-        break;
-      }
-    }
+    if ((rc = build_base_comb(c)) != CBFT_OK) break;
     if (max_batch) rc = reserve_work(c, max_batch);
   } while (0);
   if (rc != CBFT_OK) {
@@ -227,6 +198,66 @@ int cbft_open(cbft_ctx** out, int device, size_t max_batch) {
   }
   *out = c;
   return CBFT_OK;
+}
+
+int cbft_set_option(cbft_ctx* c, int option, int64_t v) {
+  if (!c) return CBFT_EINVAL;
+  if (!c->kids.empty()) {
+    for (cbft_ctx* k : c->kids) {
+      const int rc = cbft_set_option(k, option, v);
+      if (rc) return rc;
+    }
+    return CBFT_OK;
+  }
+  std::lock_guard<std::mutex> g(c->mu);
+  switch (option) {
+    case CBFT_OPT_LADDER_LANES:
+      if (v != 0 && v != 2 && v != 4) return CBFT_EINVAL;
+      c->ladder_lanes = (int)v;
+      return CBFT_OK;
+    case CBFT_OPT_B_RADIX: {
+      if (v < 16 || v > CBFT_COMB_MAX_RADIX) return CBFT_EINVAL;
+      if (v == c->b_radix) return CBFT_OK;
+      CBFT_HIP(hipSetDevice(c->device));
+      CBFT_HIP(hipDeviceSynchronize());  // batches in flight read the old table
+      c->base_comb.release();
+      const int old = c->b_radix;
+      c->b_radix = (int)v;
+      const int rc = build_base_comb(c);
+      if (rc) {  // back to the old radix (the context stays usable)
+        c->b_radix = old;
+        c->base_comb.release();
+        (void)build_base_comb(c);
+      }
+      return rc;
+    }
+    case CBFT_OPT_WORK_SLOTS:
+      if (v < 1 || v > CBFT_MAX_WORK_SLOTS) return CBFT_EINVAL;
+      c->work_slots = (int)v;
+      return CBFT_OK;
+    case CBFT_OPT_SMALL_MAX:
+      if (v < 0) return CBFT_EINVAL;
+      c->small_max = (size_t)v;
+      return CBFT_OK;
+    case CBFT_OPT_SHA_SORT_MIN:
+      if (v < 0) return CBFT_EINVAL;
+      c->sha_sort_min = (size_t)v;
+      return CBFT_OK;
+    case CBFT_OPT_STAGE_ORDER:
+      if (v < 0 || v > 2) return CBFT_EINVAL;
+      c->stage_order = (int)v;
+      return CBFT_OK;
+    case CBFT_OPT_HASH_ORDER_EARLY:
+      if (v < 0 || v > 1) return CBFT_EINVAL;
+      c->hash_order_early = (int)v;
+      return CBFT_OK;
+    case CBFT_OPT_FINISH_K:
+      if (v < 0 || v > 2) return CBFT_EINVAL;
+      c->finish_k = (int)v;
+      return CBFT_OK;
+    default:
+      return CBFT_EINVAL;
+  }
 }
 
 int cbft_open_devices(cbft_ctx** out, const int* devices, int ndevices, size_t max_batch) {
@@ -311,7 +342,7 @@ void cbft_close(cbft_ctx* c) {
     b->release();
   c->hstage.release();
   for (WorkSlot& w : c->slots) {
-    for (DevBuf* b : {&w.h, &w.flags, &w.xyz, &w.ps_tbl, &w.ps_aok, &w.perm, &w.buckets, &w.tree}) b->release();
+    for (DevBuf* b : {&w.h, &w.flags, &w.xyz, &w.ps_tbl, &w.ps_aok, &w.perm, &w.buckets}) b->release();
     if (w.done) (void)hipEventDestroy(w.done);
     if (w.fork) (void)hipEventDestroy(w.fork);
     if (w.join) (void)hipEventDestroy(w.join);
@@ -733,7 +764,7 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     // the slot's previous batch (maybe on another stream) must be done with its buffers
     if (slot.used) CBFT_HIP(hipStreamWaitEvent(s, slot.done, 0));
   }
-  // variable-length batches from $CBFT_SHA_SORT_MIN signatures (default 4,096; 0 = never) hash
+  // variable-length batches from sha_sort_min signatures (default 4,096; 0 = never) hash
   // in order of their SHA-512 block count (SURVEY.md §7 hard part ii)
   const bool sort = !small && d_off && !uniform_blocks && c->sha_sort_min && n >= c->sha_sort_min;
   if (sort) {
@@ -742,7 +773,7 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
       CBFT_HIP(slot.buckets.reserve((2 * CBFT_SHA_BUCKETS + 2) * sizeof(uint32_t)));
       CBFT_HIP(hipMemsetAsync(slot.buckets.p, 0, (2 * CBFT_SHA_BUCKETS + 2) * sizeof(uint32_t), s));  // counts start at 0
     }
-    if (c->sha_long && !slot.aux) {
+    if (!slot.aux) {  // the long-message hash stream
       CBFT_HIP(hipStreamCreateWithFlags(&slot.aux, hipStreamNonBlocking));
       CBFT_HIP(hipEventCreateWithFlags(&slot.fork, hipEventDisableTiming));
       CBFT_HIP(hipEventCreateWithFlags(&slot.join, hipEventDisableTiming));
@@ -752,22 +783,9 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   Ed25519Batch b{n, d_pk, d_kidx, KeyChunks{nullptr, 0}, d_sig, d_msg, d_off, d_len,
                  kt ? kt->nkeys : (uint32_t)n, fixed_len};
   Ed25519Work w{};
-  // a small (latency-bound) batch inverts per signature; from 16K one inversion per block of
-  // 64 lanes x 2 signatures (the tree finish, K = -2, $CBFT_FINISH_TREE_BLOCK lanes); $CBFT_FINISH_BATCH
-  // = K > 0 selects one shared inversion per K signatures per lane on every lane (the round-4
-  // finish).  Headline A/B, 200 steps: K = 2 450 M/s, tree 512 x 2 422, 128 x 2
-  // 454-459, 64 x 2 465-470, 64 x 1 384-387
-  w.finish_batch = c->finish_batch ? c->finish_batch : (n >= 16384 ? -2 : 1);
-  w.finish_tree_block = c->finish_tree_block;
-  if (c->finish_split && w.finish_batch < 0 && !small) {
-    // blocks x 9 limbs x 2T nodes: at most 18 n / K + 18 T words (T <= 128 in the split form)
-    CBFT_HIP(slot.tree.reserve((18 * n + 18 * 128) * sizeof(uint32_t)));
-    w.tree = slot.tree.as<uint32_t>();
-  }
-  w.long_groups = c->long_groups;
-  w.hash_prio = c->hash_prio;
-  w.long_prio = c->long_prio;
-  w.ladder_prefetch = c->ladder_prefetch;
+  // one inversion per finish block of 64 lanes x finish_k signatures (the tree finish, its root
+  // inverted on the scalar unit): 2 per lane from 16K signatures (512 blocks at 64K), else 1
+  w.finish_k = c->finish_k ? c->finish_k : (n >= 16384 ? 2 : 1);
   w.base_table = c->base_table.as<uint32_t>();
   w.h_soa = slot.h.as<uint32_t>();
   w.flags = slot.flags.as<uint8_t>();
@@ -776,11 +794,9 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
   if (sort) {
     w.perm = slot.perm.as<uint32_t>();
     w.buckets = slot.buckets.as<uint32_t>();
-    if (c->sha_long) {
-      w.aux = slot.aux;
-      w.fork_ev = slot.fork;
-      w.join_ev = slot.join;
-    }
+    w.aux = slot.aux;
+    w.fork_ev = slot.fork;
+    w.join_ev = slot.join;
   }
   if (table_id == CBFT_NO_KEY_TABLE) {
     // per-signature keys: decode + precompute per signature
@@ -796,12 +812,12 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     // pair ladder (fewer additions in total, 2 waves/SIMD) once a batch fills the chip with it;
     // the quad ladder (half the additions per lane) for the latency of small batches
     w.comb_lanes = c->ladder_lanes ? c->ladder_lanes : (n >= 32768 ? 2 : 4);
-    w.small = small ? c->small_waves : 0;
+    w.small = small ? 1 : 0;
   }
   // Stage order pays for big batches (their stages fill the chip; see cbft_ctx::stage_order).
   // Small batches are latency-bound single waves per stage: ordering them only serialises
   // concurrent callers' batches (the per-request coalescer keeps several in flight), so they run
-  // unordered ($CBFT_STAGE_ORDER_MIN, default 4,096 signatures).
+  // unordered (from 4,096 signatures).
   const int so = sort ? c->stage_order_var : c->stage_order;
   bool ordered = so && n >= c->stage_order_min && !w.small;
   if (ordered) {  // how many streams do the recent big batches use?
@@ -819,8 +835,8 @@ static int launch_locked(cbft_ctx* c, uint32_t table_id, const uint8_t* d_pk, co
     for (hipEvent_t& e : c->stage_done)
       if (!e) CBFT_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     order.wait = c->stage_used;
-    order.hash = so != 2;    // 2: ladders only
-    order.ladder = so != 3;  // 3: hashes only (two batches' ladders may share the SIMDs)
+    order.hash = so != 2;  // 2: ladders only
+    order.ladder = true;
     order.done[0] = c->stage_done[0];
     order.done[1] = c->stage_done[1];
     order.hash_early = c->hash_order_early != 0;
@@ -984,7 +1000,7 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
   const bool one_stream = pack && n <= c->small_max;
   hipStream_t cs = c->compute[t & 1];
   if (one_stream) {
-    hipStream_t& ss = c->small_streams[t % c->nsmall];
+    hipStream_t& ss = c->small_streams[t % CBFT_SMALL_STREAMS];
     if (!ss) CBFT_HIP(hipStreamCreateWithFlags(&ss, hipStreamNonBlocking));
     cs = ss;
   }
@@ -994,7 +1010,7 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
   // writes its verdict words straight into pinned memory: one launch and one event per batch
   // instead of two DMAs around the launch (the host API time of the copies bounded the
   // coalescer's batch rate)
-  bool zc = one_stream && kt && c->zero_copy && !c->ladder_lanes;
+  bool zc = one_stream && kt && !c->ladder_lanes;
   for (int k = 0; k < 5 && zc; k++)
     if (parts[k].bytes && pinned[k]) zc = false;
   if (zc) {
@@ -1007,7 +1023,7 @@ static int submit_host(cbft_ctx* c, uint32_t table_id, const uint8_t* pk, const 
                        fixed ? nullptr : reinterpret_cast<const uint32_t*>(zin + o_len), fixed_len, n,
                        static_cast<uint64_t*>(s.hverd.dev), cs, uniform_blocks);
     if (rc) return rc;
-    s.wait_ev = c->blocking_sync ? s.done_blk : s.done;
+    s.wait_ev = s.done_blk;
     CBFT_HIP(hipEventRecord(s.wait_ev, cs));
     s.ticket = t;
     s.pending = true;

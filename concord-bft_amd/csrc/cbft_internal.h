@@ -105,12 +105,11 @@ struct BlsKeySet {
 // batch i+1's hash run together, each alone would leave the SIMDs half idle); a slot's `done`
 // event orders its reuse after its previous batch.  With two streams two slots are enough (each
 // stream's order already serialises its own batches); callers with more streams in flight
-// (config #3's long-message tails) use more ($CBFT_WORK_SLOTS, default 4).
+// (config #3's long-message tails) use more (CBFT_OPT_WORK_SLOTS, default 4).
 #define CBFT_MAX_WORK_SLOTS 8
 struct WorkSlot {
   DevBuf h, flags, xyz, ps_tbl, ps_aok;
   DevBuf perm, buckets;  // hash order of a variable-length batch (counting sort by SHA-512 blocks)
-  DevBuf tree;           // the split tree finish's block trees
   hipStream_t aux = nullptr;                        // long-message hash stream (ed25519_hash_long_kernel)
   hipEvent_t fork = nullptr, join = nullptr;
   hipEvent_t done = nullptr;
@@ -159,10 +158,10 @@ struct cbft_ctx {
   hipStream_t compute[2] = {nullptr, nullptr};
   // fused small batches (the per-request path) rotate over their own streams, created on first
   // use, so that concurrent callers' batches run side by side instead of queueing on compute[]
-#define CBFT_SMALL_STREAMS 16
+  // (4 streams: kernels of different streams overlap only as far as the process has hardware
+  // queues, GPU_MAX_HW_QUEUES = 4 by default)
+#define CBFT_SMALL_STREAMS 4
   hipStream_t small_streams[CBFT_SMALL_STREAMS] = {};
-  int nsmall = 4;  // streams in use ($CBFT_SMALL_STREAMS, 1..16; kernels of different streams
-                   // overlap only as far as the process has hardware queues: GPU_MAX_HW_QUEUES)
   HostSlot hslots[CBFT_HOST_SLOTS];
   uint64_t next_ticket = 0;
   DevBuf base_table, base_comb;
@@ -171,46 +170,35 @@ struct cbft_ctx {
   uint32_t next_table_id = 1;
   // per-batch work buffers
   WorkSlot slots[CBFT_MAX_WORK_SLOTS];
-  int work_slots = 4;  // $CBFT_WORK_SLOTS (1 .. CBFT_MAX_WORK_SLOTS)
+  int work_slots = 4;  // CBFT_OPT_WORK_SLOTS (1 .. CBFT_MAX_WORK_SLOTS)
   // the next batch's hash waits for this batch's SHORT-message hash only, not for the long tail
-  // hashing on the slot's aux stream ($CBFT_HASH_ORDER_EARLY, default 1)
+  // hashing on the slot's aux stream (CBFT_OPT_HASH_ORDER_EARLY, default 1)
   int hash_order_early = 1;
-  int finish_split = 0;        // the split tree finish ($CBFT_FINISH_SPLIT)
-  int finish_tree_block = 64;  // lanes per tree-finish block ($CBFT_FINISH_TREE_BLOCK: 64/128/256/512; 0 = wave butterflies)
-  int long_groups = 0;  // $CBFT_SHA_LONG_GROUPS (0 = CBFT_SHA_LONG_GROUPS)
-  int hash_prio = 0;    // $CBFT_HASH_PRIO
-  int ladder_prefetch = 0;  // $CBFT_LADDER_PREFETCH
-  int long_prio = 0;    // $CBFT_HASH_LONG_PRIO  // lanes per tree-finish block ($CBFT_FINISH_TREE_BLOCK: 64/128/256/512)
   unsigned next_slot = 0;
-  int finish_batch = 0;  // K4: signatures per lane sharing one inversion ($CBFT_FINISH_BATCH; 0 = by batch size)
+  int finish_k = 0;  // signatures per finish lane (CBFT_OPT_FINISH_K; 0 = 2 from 16K, else 1)
   // Stage order across batches (any streams): batch i+1's hash starts after batch i's hash and
   // its ladder after batch i's ladder, so the pipeline runs hash(i+1) / finish(i) beside
   // ladder-to-ladder instead of two streams marching in phase (both finishes together, 7/8 of
-  // the SIMDs idle).  $CBFT_STAGE_ORDER: 0 off, 1 hash + ladder, 2 ladder only.
+  // the SIMDs idle).  CBFT_OPT_STAGE_ORDER: 0 off, 1 hash + ladder, 2 ladder only.
   int stage_order = 1;
-  // the same for variable-length (block-count sorted) batches: 2 = ladders only, so consecutive
-  // batches' hash stages (whose long-message tails set their latency) overlap ($CBFT_STAGE_ORDER_VAR;
-  // config #3 A/B: 1 -> 219, 2 -> 228-231 M/s)
-  int stage_order_var = 2;
+  // the same for variable-length (block-count sorted) batches: ladders only, so consecutive
+  // batches' hash stages (whose long-message tails set their latency) overlap (config #3 A/B:
+  // hash + ladder 219, ladders only 228-231 M/s)
+  static constexpr int stage_order_var = 2;
   // streams of the last ordered-size batches: with three or more distinct streams in flight each
   // stream's hash -> ladder -> finish chain already covers three batches, and the order only
-  // serialises them (headline at 20 steps, 3 streams: unordered 461-493 vs ordered 451-471 M/s)
+  // serialises them (headline at 20 steps, 3 streams: unordered 461-493 vs ordered 451-471 M/s);
+  // batches below 4,096 signatures (latency-bound single waves per stage) always run unordered
   hipStream_t recent_streams[4] = {};
   unsigned recent_n = 0;
-  int order_max_streams = 2;  // order only while at most this many streams are in use ($CBFT_ORDER_MAX_STREAMS)
-  size_t stage_order_min = 4096;  // smaller batches run unordered ($CBFT_STAGE_ORDER_MIN)
-  // key-table batches up to this size run as one fused launch (ed25519_small_kernel;
-  // $CBFT_SMALL_MAX, 0 = never): the per-request coalescer's batches
+  static constexpr int order_max_streams = 2;
+  static constexpr size_t stage_order_min = 4096;
+  // key-table batches up to this size run as one fused launch (ed25519_small3_kernel;
+  // CBFT_OPT_SMALL_MAX, 0 = never): the per-request coalescer's batches
   size_t small_max = 1024;
-  // fused small-batch kernel ($CBFT_SMALL_WAVES): 3 = [S]B on a wave of its own beside the hash +
-  // [h](-A) wave and the two R-decode waves (per-request p50 69 us vs 73 us for 2: one wave for both sums)
-  int small_waves = 3;
   size_t sha_sort_min = 4096;  // variable-length batches from this size hash in block-count order
-  int sha_long = 1;             // their long messages on a second stream ($CBFT_SHA_LONG, 0 = off)
-  int blocking_sync = 1;  // small batches' waiters sleep ($CBFT_BLOCKING_SYNC)
-  int zero_copy = 1;  // fused small batches read pinned inputs and write verdicts in place ($CBFT_ZERO_COPY)
-  int b_radix = CBFT_COMB_B_RADIX;  // radix of B's comb table ($CBFT_B_RADIX, 16..26)
-  int ladder_lanes = 0;             // comb ladder lanes per signature ($CBFT_LADDER_LANES 2 | 4; 0 = by batch)
+  int b_radix = CBFT_COMB_B_RADIX;  // radix of B's comb table (CBFT_OPT_B_RADIX, 16..26)
+  int ladder_lanes = 0;             // comb ladder lanes per signature (CBFT_OPT_LADDER_LANES 2 | 4; 0 = by batch)
   hipEvent_t stage_done[2] = {nullptr, nullptr};  // last hash, last ladder
   bool stage_used = false;
   DevBuf verdicts;

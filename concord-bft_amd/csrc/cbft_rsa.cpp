@@ -32,12 +32,7 @@ static int rsa_launch_locked(cbft_ctx* c, RsaKeyTable& kt, const uint32_t* d_kid
       for (hipEvent_t& e : c->rsa_ev) CBFT_HIP(hipEventCreate(&e));
     CBFT_HIP(hipEventRecord(c->rsa_ev[0], s));
   }
-  // the lane-pair radix-2^28 kernel by default; $CBFT_RSA_KERNEL=fios selects the one-lane kernel
-  static const int pair = [] {
-    const char* k = getenv("CBFT_RSA_KERNEL");
-    return (k && std::strcmp(k, "fios") == 0) ? 0 : 1;
-  }();
-  CBFT_HIP(cbft_rsa_launch_verify(b, c->rsa_scratch.as<uint32_t>(), d_verdicts, s, pair));
+  CBFT_HIP(cbft_rsa_launch_verify(b, c->rsa_scratch.as<uint32_t>(), d_verdicts, s));
   if (c->profiling) CBFT_HIP(hipEventRecord(c->rsa_ev[1], s));
   CBFT_HIP(hipEventRecord(c->rsa_done, s));
   c->rsa_used = true;

@@ -5,21 +5,11 @@
 #include <stddef.h>
 #include <stdint.h>
 
-#ifndef CBFT_WA
+// the windowed ladder of per-signature keys (ed25519_ladder_kernel)
 #define CBFT_WA 5  // signed window width for h (the -A table has 2^(WA-1)+1 entries)
-#endif
-#ifndef CBFT_WB
 #define CBFT_WB 7  // signed window width for S (the LDS base table has 2^(WB-1)+1 entries)
-#endif
-#ifndef CBFT_VERIFY_BLOCK
+#define CBFT_LADDER_MIN_WAVES 4  // waves/SIMD the windowed ladder is register-allocated for
 #define CBFT_VERIFY_BLOCK 256
-#endif
-#ifndef CBFT_COMB8_LDS
-#define CBFT_COMB8_LDS 1  // stage comb-table entries through LDS with global_load_lds
-#endif
-#ifndef CBFT_LADDER_MIN_WAVES
-#define CBFT_LADDER_MIN_WAVES 4  // waves/SIMD the ladder is register-allocated for
-#endif
 
 // A loaded key table lives in chunks of CBFT_KEY_CHUNK keys, so keys can be appended without
 // moving (or rebuilding) the ones already loaded: chunk c holds keys [c * CHUNK, (c + 1) * CHUNK)
@@ -120,17 +110,13 @@ struct Ed25519Work {
   const uint32_t* base_comb;   // comb table of B (key-table mode; the -A combs are in Batch::keys)
   CombLadder comb;             // their geometry
   int comb_lanes;              // lanes per signature of the comb ladder: 4 (quad) or 2 (pair)
-  int finish_batch;            // K4: K > 1 signatures per lane share one inversion (2/4/8/16/32);
-                               // -K: one inversion per block of finish_tree_block lanes, K per lane (1/2/4)
-  int finish_tree_block;       // 64 (default) / 128 / 256 / 512
-  uint32_t* tree;              // non-null: the split tree finish (up / root inversions / down), its
-                               // block trees here (9 x 2T words per block)
+  int finish_k;                // signatures per finish lane (1 or 2; one inversion per 64 x finish_k)
   const uint8_t* aok;          // A decoded OK per signature (per-signature key mode)
   uint32_t* h_soa;             // 8 x n words
   uint8_t* flags;              // n bytes
   uint32_t* xyz_soa;           // 27 x n words
   uint64_t* verdict_words;     // ceil(n/64) words; bit (i % 64) of word i/64 = accept
-  int small;                   // key-table batch in ONE launch (ed25519_small_kernel): small batches
+  int small;                   // key-table batch in ONE launch (ed25519_small3_kernel): small batches
   // Variable-length batches: hash signatures in order of their SHA-512 block count (a counting
   // sort into perm before K1), so a wave's lanes run the same number of blocks.  Nullable.
   uint32_t* perm;              // n words
@@ -140,19 +126,11 @@ struct Ed25519Work {
   // the rounds (ed25519_hash_long_kernel); null aux = off.
   hipStream_t aux;
   hipEvent_t fork_ev, join_ev;
-  int long_groups;  // cap of the long-message kernel's 64-signature groups (0 = CBFT_SHA_LONG_GROUPS)
-  int hash_prio;    // K1 waves at raised issue priority (s_setprio 2)
-  int long_prio;    // the long-message kernel's waves at s_setprio 3
-  int ladder_prefetch;  // K1 touches the pair ladder's first key-table entries (L2 / MALL warm-up)
 };
 // Block-count buckets of the hash sort: bucket min(nblocks, CBFT_SHA_BUCKETS - 1).
 #define CBFT_SHA_BUCKETS 256
-#ifndef CBFT_SHA_LONG_BLOCKS
-#define CBFT_SHA_LONG_BLOCKS 12
-#endif
-#ifndef CBFT_SHA_LONG_GROUPS
-#define CBFT_SHA_LONG_GROUPS 192
-#endif
+#define CBFT_SHA_LONG_BLOCKS 12   // messages of >= 12 blocks hash in the long-message kernel
+#define CBFT_SHA_LONG_GROUPS 192  // at most 192 x 64 of them (its 83-KB blocks must all be resident)
 
 size_t cbft_ed25519_table_words_per_unit();
 // staging words for `lanes` table-build lanes (18 KB each)

@@ -176,9 +176,6 @@ __global__ void __launch_bounds__(64) ed25519_base_table_kernel(uint32_t* tbl, i
 // Branch-free: dword k is read from index min(k, kmax) (kmax = last dword holding a byte of
 // M), or from `safe` (any readable dword) when no dword of this window holds one; bytes at or
 // past len are then masked off arithmetically, so a wave never splits on message length.
-#ifndef CBFT_SHA_PREFETCH  // 1: K1 loads block j + 1's message words before compressing block j
-#define CBFT_SHA_PREFETCH 1
-#endif
 template <int NW>
 __device__ __forceinline__ void fetch_msg_dwords(uint32_t* d, const uint8_t* m, uint32_t len, uint32_t base,
                                                  const uint32_t* safe) {
@@ -246,7 +243,6 @@ __device__ __forceinline__ void ed25519_hash_sig(const Ed25519Batch& b, size_t i
   uint32_t d[33];  // the message dwords of the next block, loaded while the current one compresses
   fetch_msg_dwords<8>(d, m, len, 0u, safe);
   for (uint32_t blk = 0; blk < nblocks; blk++) {
-    if (!CBFT_SHA_PREFETCH && blk > 0) fetch_msg_dwords<16>(d, m, len, 128u * blk - 64u, safe);
     if (blk == 0) {  // R || A || M[0..63]
 #pragma unroll
       for (int j = 0; j < 4; j++) W[j] = ((uint64_t)bswap32(Rw[2 * j]) << 32) | bswap32(Rw[2 * j + 1]);
@@ -256,7 +252,7 @@ __device__ __forceinline__ void ed25519_hash_sig(const Ed25519Batch& b, size_t i
     } else {
       assemble_msg_words<16>(W, d, m, len, 128u * blk - 64u);
     }
-    if (CBFT_SHA_PREFETCH && blk + 1 < nblocks) fetch_msg_dwords<16>(d, m, len, 128u * blk + 64u, safe);
+    if (blk + 1 < nblocks) fetch_msg_dwords<16>(d, m, len, 128u * blk + 64u, safe);  // the next block's words
     if (blk == nblocks - 1) {
       W[14] = 0;
       W[15] = (uint64_t)total << 3;
@@ -436,52 +432,9 @@ __global__ void __launch_bounds__(256) ed25519_bucket_scatter_kernel(const Ed255
 
 // perm: the block-count order (nullable); uniform: its flag word (perm unused when set);
 // nshort (nullable): positions from *nshort on are ed25519_hash_long_kernel's.
-// PRIO > 0: the waves raise their issue priority (s_setprio) over the kernels they share SIMDs with
-// (the other batch's ladder): the hash stage is on each batch's dependency chain.
-#define COMB_STRIDE 32  // words per comb entry (defined with the comb kernels below)
-__device__ __forceinline__ void add256(uint32_t* s, const uint32_t* off);
-// Touch the pair ladder's first key-table entries of signature i (steps 0 and 1 of both lanes,
-// the phased split's key positions 0, 1, naper, naper + 1): one word of each 128-byte entry, so
-// the ladder's 2,048 waves, which all start together, find them in L2 / MALL instead of opening
-// with a cold ~29 MB burst (CBFT_LADDER_STAMPS: ~9 us of every wave's ~100).  The words are
-// discarded.  $CBFT_LADDER_PREFETCH=1 (A/B only): isolated ladder 108.7 -> 108.2 us for +4 us of
-// hash, headline within noise (profiles/r05_ab/ladder_entry_prefetch.txt): the first-entry wait is
-// the burst itself, not cold lines.
-__device__ __forceinline__ void ladder_entry_prefetch(const Ed25519Batch& b, size_t i, const uint32_t* hw,
-                                                      const CombLadder& cl) {
-  uint32_t s[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) s[k] = hw[k];
-  add256(s, cl.offA);
-  const uint32_t na = (uint32_t)cl.a.npos, naper = (na + 1u) >> 1, w = (uint32_t)cl.a.w;
-  const uint32_t half = 1u << (w - 1u), ents = (uint32_t)cl.a.entries();
-  const uint32_t* akey = b.keys.comb(batch_unit(b, i));
-  uint32_t acc = 0;
-#pragma unroll
-  for (int t = 0; t < 4; t++) {
-    const uint32_t pos = (t >> 1) * naper + (t & 1);
-    if (pos >= na) continue;
-    const uint32_t off = pos * w, wi = off >> 5;
-    uint32_t lo = 0, hi = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {  // s[wi], s[wi + 1] without dynamic register indexing
-      lo = (uint32_t)k == wi ? s[k] : lo;
-      hi = (uint32_t)k == wi + 1u ? s[k] : hi;
-    }
-    const uint32_t ch = (uint32_t)((((uint64_t)hi << 32) | lo) >> (off & 31u)) & ((1u << w) - 1u);
-    const int d = pos == na - 1u ? (int)(ch < half ? ch : half) : (int)ch - (int)half;
-    const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
-    acc += akey[((size_t)pos * ents + ad) * COMB_STRIDE];
-  }
-  asm volatile("" ::"v"(acc));  // keep the loads
-}
-
-template <int PRIO>
 __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const Ed25519Batch b, const uint32_t* perm,
                                                                           const uint32_t* uniform, const uint32_t* nshort,
-                                                                          uint32_t* h_soa, uint8_t* flags,
-                                                                          const CombLadder cl, int prefetch) {
-  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+                                                                          uint32_t* h_soa, uint8_t* flags) {
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= b.n || (nshort && g >= *nshort)) return;
   const size_t i = perm && !*uniform ? (size_t)perm[g] : g;
@@ -491,7 +444,6 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const E
 #pragma unroll
   for (int k = 0; k < 8; k++) h_soa[k * b.n + i] = hw[k];
   flags[i] = flag ? 1 : 0;
-  if (prefetch) ladder_entry_prefetch(b, i, hw, cl);
 }
 
 // K1 for the sorted order's tail (messages of >= CBFT_SHA_LONG_BLOCKS blocks): 64 signatures per
@@ -502,12 +454,10 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_hash_kernel(const E
 // lane).  Runs on a second stream beside ed25519_hash_kernel (which skips these positions); one
 // barrier per block, the same count in both waves (the group's most blocks).
 #define HASH_LONG_BLOCK 128
-template <int PRIO>
 __global__ void __launch_bounds__(HASH_LONG_BLOCK) ed25519_hash_long_kernel(const Ed25519Batch b, const uint32_t* perm,
                                                                             const uint32_t* uniform,
                                                                             const uint32_t* nshort, uint32_t* h_soa,
                                                                             uint8_t* flags) {
-  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
   __shared__ uint64_t kwl[2][64 * KW_STRIDE];
   const size_t g0 = (size_t)*nshort + (size_t)blockIdx.x * 64;
   if (g0 >= b.n) return;  // the whole block
@@ -666,145 +616,35 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_LADDER_MIN_WAVES)
 }
 
 // ---------------------------------------------------------------------------------------
-// K4: encode R' and compare with R; verdict ballot per wave
-// ---------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK) ed25519_finish_kernel(const Ed25519Batch b, const uint32_t* xyz_soa,
-                                                                            const uint8_t* flags, const uint8_t* aok,
-                                                                            uint64_t* verdict_words) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  bool verdict = false;
-  if (i < b.n) {
-    fe X, Y, Z;
-    fe_load_soa(X, xyz_soa, b.n, i);
-    fe_load_soa(Y, xyz_soa + 9 * b.n, b.n, i);
-    fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
-    uint32_t Rp[8], Rw[8];
-    {  // encode R' (public: variable-time inversion)
-      fe zi, x, y;
-      fe_invert_var(zi, Z);
-      fe_mul<false>(x, X, zi);
-      fe_mul<false>(y, Y, zi);
-      fe_to_words(Rp, y);
-      Rp[7] ^= fe_isnegative(x) << 31;
-    }
-    load_words8(Rw, b.sig + i * 64);
-    uint32_t diff = 0;
-#pragma unroll
-    for (int k = 0; k < 8; k++) diff |= Rp[k] ^ Rw[k];
-    const uint32_t unit = batch_unit(b, i);
-    verdict = (diff == 0) && flags[i] && unit_aok(b, aok, unit);
-  }
-  const uint64_t ballot = __ballot(verdict);
-  if ((threadIdx.x & 63) == 0 && i < b.n) verdict_words[i >> 6] = ballot;
-}
-
-// K4' (batched): the same verdicts with one field inversion per K signatures per lane
-// (Montgomery's trick).  Lane l of block w handles signatures w*64K + 64j + l, j = 0..K-1:
-//   up:   acc_j = prod_{t <= j} Z_t  (prefix products kept in LDS, [j][limb][lane])
-//   inv = acc_{K-1}^-1  (254 S + 11 M, once per K signatures instead of once per signature)
-//   down: 1/Z_j = inv * acc_{j-1},  inv <- inv * Z_j;  x = X/Z, y = Y/Z, encode, compare with R.
-// A signature already rejected (S >= L, A not decodable) or with Z = 0 enters the product as 1,
-// so it cannot disturb its neighbours' inverses.  At 64K signatures and K = 8 the kernel is 128
-// waves: it does a quarter of K4's VALU work and leaves most SIMDs to the next batch's hash and
-// ladder (two batches in flight on two streams).
-template <int K>
-__global__ void __launch_bounds__(64) ed25519_finish_batch_kernel(const Ed25519Batch b, const uint32_t* xyz_soa,
-                                                                  const uint8_t* flags, const uint8_t* aok,
-                                                                  uint64_t* verdict_words) {
-  __shared__ uint32_t pre[K][FE_LIMBS][64];
-  const uint32_t ln = threadIdx.x;
-  const size_t base = (size_t)blockIdx.x * 64 * K;
-  fe acc;
-  fe_1(acc);
-  uint32_t okmask = 0;
-#pragma nounroll
-  for (int j = 0; j < K; j++) {
-    const size_t i = base + (size_t)j * 64 + ln;
-    fe Z;
-    fe_1(Z);
-    bool ok = false;
-    if (i < b.n) {
-      fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
-      const uint32_t unit = batch_unit(b, i);
-      ok = flags[i] && unit_aok(b, aok, unit) && !fe_iszero(Z);
-      if (!ok) fe_1(Z);
-    }
-    okmask |= (ok ? 1u : 0u) << j;
-    fe_mul<false>(acc, acc, Z);
-#pragma unroll
-    for (int k = 0; k < FE_LIMBS; k++) pre[j][k][ln] = acc.v[k];
-  }
-  fe inv;
-  fe_invert_var(inv, acc);
-#pragma nounroll
-  for (int j = K - 1; j >= 0; j--) {
-    const size_t i = base + (size_t)j * 64 + ln;
-    const bool ok = (okmask >> j) & 1u;
-    fe zi, Z;
-    if (j > 0) {
-      fe p;
-#pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) p.v[k] = pre[j - 1][k][ln];
-      fe_mul<false>(zi, inv, p);
-    } else {
-      fe_copy(zi, inv);
-    }
-    bool verdict = false;
-    if (ok) {
-      fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
-      fe_mul<false>(inv, inv, Z);
-      fe X, Y, x, y;
-      fe_load_soa(X, xyz_soa, b.n, i);
-      fe_load_soa(Y, xyz_soa + 9 * b.n, b.n, i);
-      fe_mul<false>(x, X, zi);
-      fe_mul<false>(y, Y, zi);
-      uint32_t Rp[8], Rw[8];
-      fe_to_words(Rp, y);
-      Rp[7] ^= fe_isnegative(x) << 31;
-      load_words8(Rw, b.sig + i * 64);
-      uint32_t diff = 0;
-#pragma unroll
-      for (int k = 0; k < 8; k++) diff |= Rp[k] ^ Rw[k];
-      verdict = diff == 0;
-    }
-    const uint64_t ballot = __ballot(verdict);
-    if (ln == 0 && base + (size_t)j * 64 < b.n) verdict_words[blockIdx.x * K + j] = ballot;
-  }
-}
-
-// K4'' (tree): the same verdicts with ONE field inversion per block of FINISH_TREE_BLOCK lanes x K
-// signatures.  K4' shares an inversion among the K signatures of one lane, so a 64K batch still runs
-// 32,768 of them (one per lane, 512 waves each waiting on a ~15 K-instruction safegcd chain): 80 % of
-// the finish kernel's instructions and 14 % of the whole verify's.  Here the block shares it:
-//   leaf   l = prod of lane l's K Z's (entries of rejected signatures / Z = 0 count as 1),
-//   up     a product tree over the block's lanes in LDS (heap: root 1, leaves T..2T-1),
-//   root   one lane inverts the root (variable time: R' is public),
+// K4: encode R' = (X : Y : Z) and compare it with R; verdict ballot per wave.
+//
+// One field inversion per block of FINISH_LANES lanes x K signatures (Montgomery's trick over a
+// product tree; R' is public, so the inversion is the variable-time safegcd):
+//   leaf   l = prod of lane l's K Z's (signatures already rejected -- S >= L, A not decodable --
+//          and Z = 0 enter as 1, so they cannot disturb their neighbours' inverses),
+//   up     a product tree over the block's lanes in LDS (heap: root 1, leaves T .. 2T - 1),
+//   root   inverted ONCE per block, on the scalar unit: every lane reads the root, the limbs are
+//          made wave-uniform (readfirstlane) and the safegcd chain compiles to SALU code
+//          (fe_invert_var<true>): ~17.5 K scalar instructions, ~40 of the kernel's ~51 us, while
+//          the SIMDs' vector pipes stay free for the other streams' ladders (the same chain on
+//          the VALU, every lane running it: 2 % slower alone and 5 % slower in the 3-stream
+//          pipeline, tools/probes/r06_ab2.sh),
 //   down   each node's inverse becomes its children's: 1/L = inv * R, 1/R = inv * L (in place),
-//   lane   1/Z_j from the leaf's inverse and the lane's prefix products, then x = X/Z, y = Y/Z,
-//          encode, compare with R, ballot.
-// Per signature that is ~3.5 M + 2 M + an encode, against one inversion per K signatures: the
-// tree's 2 x log2(T) levels are a short serial chain (one product per level) and the kernel is
-// FINISH_TREE_BLOCK x K = 1,024 signatures per block (64 blocks at 64K).
-//
-// Block size T: the tree's LDS is 72 T bytes.  It co-runs with the other stream's pair ladder,
-// whose 1,024 blocks of 36 KB exactly fill a 64K batch's LDS (4 per CU): a 512-lane tree block
-// (37 KB) on a CU pushes one ladder block into a second round (measured: ladder 113 -> 131 us in
-// the pipeline, 450 -> 422 M verifies/s), a 128-lane one (9 KB) fits beside four.
-//
-// M (the split form, $CBFT_FINISH_SPLIT): one inversion per BLOCK still costs a whole wave's time
-// for one lane's safegcd chain (~60 % of the kernel's instructions at 64 lanes per block).  M = 1
-// runs the leaves and the up-sweep and stores the block's tree ([limb][node], 72 T bytes) to
-// `tree`; ed25519_finish_root_kernel then inverts every block's root with ONE LANE PER ROOT (512
-// roots at 64K: 8 waves); M = 2 loads the tree back and runs the down-sweep and the lanes.  M = 0
-// is the one-launch form (the root inverted by lane 0 of its own block).
-template <int K, int T, int M>
-__global__ void __launch_bounds__(T) ed25519_finish_tree_kernel(const Ed25519Batch b, const uint32_t* xyz_soa,
-                                                                const uint8_t* flags, const uint8_t* aok,
-                                                                uint64_t* verdict_words, uint32_t* tree) {
+//   lane   1/Z_j from the leaf's inverse and the lane's prefix products; x = X/Z, y = Y/Z, encode,
+//          compare with R, ballot.
+// Per signature ~3.5 M of tree + 2 M + an encode.  K = 2 from 16K signatures (512 one-wave blocks
+// at 64K: the finish co-runs with the other streams' ladders, whose 1,024 blocks of 36 KB fill a
+// 64K batch's LDS, and a one-wave block's 4.6 KB of tree fits beside them), K = 1 below.
+// ---------------------------------------------------------------------------------------
+#define FINISH_LANES 64
+template <int K>
+__global__ void __launch_bounds__(FINISH_LANES) ed25519_finish_kernel(const Ed25519Batch b, const uint32_t* xyz_soa,
+                                                                      const uint8_t* flags, const uint8_t* aok,
+                                                                      uint64_t* verdict_words) {
+  constexpr uint32_t T = FINISH_LANES;
   __shared__ uint32_t node[FE_LIMBS][2 * T];  // [limb][heap node]: lanes touch consecutive nodes
   const uint32_t t = threadIdx.x;
   const size_t base = (size_t)blockIdx.x * T * K;
-  uint32_t* tb = tree ? tree + (size_t)blockIdx.x * FE_LIMBS * 2 * T : nullptr;  // this block's nodes
   fe pre[K];  // pre[j] = Z_0 * .. * Z_j of this lane
   uint32_t okmask = 0;
 #pragma unroll
@@ -821,51 +661,38 @@ __global__ void __launch_bounds__(T) ed25519_finish_tree_kernel(const Ed25519Bat
     okmask |= (ok ? 1u : 0u) << j;
     if (j == 0)
       fe_copy(pre[0], Z);
-    else if (M != 2 || j < K - 1)  // the down pass needs the prefixes below the leaf only
+    else
       fe_mul<false>(pre[j], pre[j - 1], Z);
   }
-  if (M != 2) {
 #pragma unroll
-    for (int k = 0; k < FE_LIMBS; k++) node[k][T + t] = pre[K - 1].v[k];
-    __syncthreads();
+  for (int k = 0; k < FE_LIMBS; k++) node[k][T + t] = pre[K - 1].v[k];
+  __syncthreads();
 #pragma nounroll
-    for (uint32_t m = T >> 1; m >= 1; m >>= 1) {  // up: node n = node 2n * node 2n+1
-      if (t < m) {
-        const uint32_t n = m + t;
-        fe l, r;
+  for (uint32_t m = T >> 1; m >= 1; m >>= 1) {  // up: node n = node 2n * node 2n+1
+    if (t < m) {
+      const uint32_t n = m + t;
+      fe l, r;
 #pragma unroll
-        for (int k = 0; k < FE_LIMBS; k++) {
-          l.v[k] = node[k][2 * n];
-          r.v[k] = node[k][2 * n + 1];
-        }
-        fe_mul<false>(l, l, r);
-#pragma unroll
-        for (int k = 0; k < FE_LIMBS; k++) node[k][n] = l.v[k];
+      for (int k = 0; k < FE_LIMBS; k++) {
+        l.v[k] = node[k][2 * n];
+        r.v[k] = node[k][2 * n + 1];
       }
-      __syncthreads();
-    }
-  }
-  if (M == 1) {  // the tree to HBM; the root kernel inverts node 1
+      fe_mul<false>(l, l, r);
 #pragma unroll
-    for (int k = 0; k < FE_LIMBS; k++) {
-      tb[k * 2 * T + t] = node[k][t];
-      tb[k * 2 * T + T + t] = node[k][T + t];
+      for (int k = 0; k < FE_LIMBS; k++) node[k][n] = l.v[k];
     }
-    return;
+    __syncthreads();
   }
-  if (M == 2) {  // the tree back, its root inverted
-#pragma unroll
-    for (int k = 0; k < FE_LIMBS; k++) {
-      node[k][t] = tb[k * 2 * T + t];
-      node[k][T + t] = tb[k * 2 * T + T + t];
-    }
-  } else if (t == 0) {  // every leaf is non-zero, so is the root
+  {  // every leaf is non-zero, so is the root: the scalar unit inverts it for the whole wave
     fe r;
 #pragma unroll
     for (int k = 0; k < FE_LIMBS; k++) r.v[k] = node[k][1];
-    fe_invert_var(r, r);
+    fe_invert_var<true>(r, r);
+    __syncthreads();  // (one wave: its LDS reads are in order before lane 0's write; kept for clarity)
+    if (t == 0) {
 #pragma unroll
-    for (int k = 0; k < FE_LIMBS; k++) node[k][1] = r.v[k];
+      for (int k = 0; k < FE_LIMBS; k++) node[k][1] = r.v[k];
+    }
   }
   __syncthreads();
 #pragma nounroll
@@ -923,141 +750,8 @@ __global__ void __launch_bounds__(T) ed25519_finish_tree_kernel(const Ed25519Bat
       verdict = diff == 0;
     }  // (a rejected entry entered the product as 1: inv is already 1 / pre[j-1])
     const uint64_t ballot = __ballot(verdict);
-    const size_t w0 = base + (size_t)j * T + (t & ~63u);  // this wave's first signature of step j
-    if ((t & 63u) == 0 && w0 < b.n) verdict_words[w0 >> 6] = ballot;
-  }
-}
-
-// The split tree finish's middle step: lane i inverts block i's root (node 1 of its stored tree).
-template <int T>
-__global__ void __launch_bounds__(64) ed25519_finish_root_kernel(uint32_t* tree, uint32_t nblocks) {
-  const uint32_t bi = blockIdx.x * 64 + threadIdx.x;
-  if (bi >= nblocks) return;
-  uint32_t* tb = tree + (size_t)bi * FE_LIMBS * 2 * T;
-  fe r;
-#pragma unroll
-  for (int k = 0; k < FE_LIMBS; k++) r.v[k] = tb[k * 2 * T + 1];
-  fe_invert_var(r, r);
-#pragma unroll
-  for (int k = 0; k < FE_LIMBS; k++) tb[k * 2 * T + 1] = r.v[k];
-}
-
-// K4 (wave tree): one inversion per 4-wave block (256 lanes x K signatures).  Each wave reduces
-// its 64 leaves with a butterfly (xor 1, 2, .., 32 partners: every lane ends with the wave's
-// product, keeping the six partial products it saw); the four wave products meet in LDS, lanes
-// 0..3 of wave 0 invert them (one safegcd chain's latency for four roots), and each lane walks its
-// butterfly back: 1/G_(d-1)(i) = 1/G_d(i) * G_(d-1)(i ^ 2^d).  Per lane 12 M of tree (the LDS tree:
-// 18 M), a quarter of the root inversions of the 64-lane tree, and 144 B of LDS per block, so it
-// sits beside the other stream's ladder blocks.
-#define FINISH_WAVE_BLOCK 256
-template <int CTRL>
-__device__ __forceinline__ void fe_dpp_w(fe& r, const fe& a) {
-#pragma unroll
-  for (int k = 0; k < FE_LIMBS; k++) r.v[k] = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)a.v[k], CTRL, 0xF, 0xF, false);
-}
-__device__ __forceinline__ void fe_xor_lane(fe& r, const fe& a, uint32_t m) {
-  if (m == 1) {
-    fe_dpp_w<0xB1>(r, a);  // quad_perm [1, 0, 3, 2]
-  } else if (m == 2) {
-    fe_dpp_w<0x4E>(r, a);  // quad_perm [2, 3, 0, 1]
-  } else {
-#pragma unroll
-    for (int k = 0; k < FE_LIMBS; k++) r.v[k] = (uint32_t)__shfl_xor((int)a.v[k], (int)m, 64);
-  }
-}
-template <int K>
-__global__ void __launch_bounds__(FINISH_WAVE_BLOCK) ed25519_finish_wave_kernel(const Ed25519Batch b,
-                                                                              const uint32_t* xyz_soa,
-                                                                              const uint8_t* flags, const uint8_t* aok,
-                                                                              uint64_t* verdict_words) {
-  constexpr uint32_t T = FINISH_WAVE_BLOCK;
-  __shared__ uint32_t roots[T / 64][FE_LIMBS];
-  const uint32_t t = threadIdx.x, wv = t >> 6;
-  const size_t base = (size_t)blockIdx.x * T * K;
-  fe pre[K];  // pre[j] = Z_0 * .. * Z_j of this lane
-  uint32_t okmask = 0;
-#pragma unroll
-  for (int j = 0; j < K; j++) {
-    const size_t i = base + (size_t)j * T + t;
-    fe Z;
-    fe_1(Z);
-    bool ok = false;
-    if (i < b.n) {
-      fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
-      ok = flags[i] && unit_aok(b, aok, batch_unit(b, i)) && !fe_iszero(Z);
-      if (!ok) fe_1(Z);
-    }
-    okmask |= (ok ? 1u : 0u) << j;
-    if (j == 0)
-      fe_copy(pre[0], Z);
-    else
-      fe_mul<false>(pre[j], pre[j - 1], Z);
-  }
-  fe G[6];  // G[d] = this lane's group product before butterfly level d (G[0] = the leaf)
-  fe v;
-  fe_copy(v, pre[K - 1]);
-#pragma unroll
-  for (int d = 0; d < 6; d++) {
-    fe_copy(G[d], v);
-    fe p;
-    fe_xor_lane(p, v, 1u << d);
-    fe_mul<false>(v, v, p);
-  }
-  if ((t & 63u) == 0) {
-#pragma unroll
-    for (int k = 0; k < FE_LIMBS; k++) roots[wv][k] = v.v[k];
-  }
-  __syncthreads();
-  if (t < T / 64) {  // every leaf is non-zero, so is every wave product
-    fe r;
-#pragma unroll
-    for (int k = 0; k < FE_LIMBS; k++) r.v[k] = roots[t][k];
-    fe_invert_var(r, r);
-#pragma unroll
-    for (int k = 0; k < FE_LIMBS; k++) roots[t][k] = r.v[k];
-  }
-  __syncthreads();
-  fe inv;  // 1 / (the wave's product), then down the butterfly to 1 / leaf
-#pragma unroll
-  for (int k = 0; k < FE_LIMBS; k++) inv.v[k] = roots[wv][k];
-#pragma unroll
-  for (int d = 5; d >= 0; d--) {
-    fe p;
-    fe_xor_lane(p, G[d], 1u << d);
-    fe_mul<false>(inv, inv, p);
-  }
-#pragma unroll
-  for (int j = K - 1; j >= 0; j--) {
-    const size_t i = base + (size_t)j * T + t;
-    const bool ok = (okmask >> j) & 1u;
-    fe zi;
-    if (j > 0)
-      fe_mul<false>(zi, inv, pre[j - 1]);
-    else
-      fe_copy(zi, inv);
-    bool verdict = false;
-    if (ok) {
-      fe Z, X, Y, x, y;
-      if (j > 0) {
-        fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
-        fe_mul<false>(inv, inv, Z);
-      }
-      fe_load_soa(X, xyz_soa, b.n, i);
-      fe_load_soa(Y, xyz_soa + 9 * b.n, b.n, i);
-      fe_mul<false>(x, X, zi);
-      fe_mul<false>(y, Y, zi);
-      uint32_t Rp[8], Rw[8];
-      fe_to_words(Rp, y);
-      Rp[7] ^= fe_isnegative(x) << 31;
-      load_words8(Rw, b.sig + i * 64);
-      uint32_t diff = 0;
-#pragma unroll
-      for (int k = 0; k < 8; k++) diff |= Rp[k] ^ Rw[k];
-      verdict = diff == 0;
-    }  // (a rejected entry entered the product as 1: inv is already 1 / pre[j-1])
-    const uint64_t ballot = __ballot(verdict);
-    const size_t w0 = base + (size_t)j * T + (t & ~63u);
-    if ((t & 63u) == 0 && w0 < b.n) verdict_words[w0 >> 6] = ballot;
+    const size_t w0 = base + (size_t)j * T;  // the wave's first signature of step j
+    if (t == 0 && w0 < b.n) verdict_words[w0 >> 6] = ballot;
   }
 }
 
@@ -1081,14 +775,6 @@ __global__ void __launch_bounds__(FINISH_WAVE_BLOCK) ed25519_finish_wave_kernel(
 // xor 1, xor 2) add the four partial sums: every lane of the quad ends with
 // R' = [S]B + [h](-A).  4,096 waves at 64K signatures: 4 waves per SIMD.
 // ---------------------------------------------------------------------------------------
-// CBFT_LADDER_LAZYSUM: the comb additions feed D + C (D = 2Z, C a product) into the next
-// products without a carry pass.  Its limbs stay < 3 (2^29 + 2^17) < 1.51 * 2^30; it is multiplied
-// by a reduced value (D - C, < 2^29 + 2^17) or by A + B (lazy, < 2^30 + 2^18): a column of nine such
-// products is < 9 * 2^30.59 * 2^30.0003 = 2^63.76, plus the fold (< 2^29 * 1216) and the carry in
-// (< 2^35): below 2^64, and the top column's carry (h8) stays < 2^32.  The product is reduced as usual.
-#ifndef CBFT_LADDER_LAZYSUM
-#define CBFT_LADDER_LAZYSUM 0
-#endif
 #define COMB_STRIDE 32  // words per entry: one 128-B line (y+x | y-x | 2dxy, 9 limbs each, + pad)
 #define COMB_CHUNK 128  // multiples built per table-build lane
 #define COMB_TMP_WORDS_PER_LANE (COMB_CHUNK * CACHED_WORDS)
@@ -1322,18 +1008,7 @@ __device__ __forceinline__ void add256(uint32_t* s, const uint32_t* off) {
   }
 }
 
-#ifndef CBFT_LADDER_NOFETCH
-#define CBFT_LADDER_NOFETCH 0
-#endif
-
-#ifndef CBFT_COMB_MIN_WAVES
-#define CBFT_COMB_MIN_WAVES 4
-#endif
-// CBFT_QUAD_FIRST_SET: each lane's first addition of the quad comb sum (from the identity) is a
-// point set, 1 M instead of 7 M (the quad ladder of batches < 32K and the fused small kernels)
-#ifndef CBFT_QUAD_FIRST_SET
-#define CBFT_QUAD_FIRST_SET 1
-#endif
+#define COMB_MIN_WAVES 4  // waves per SIMD the quad ladder is register-allocated for
 
 // Lane q's quarter of the comb sum [h](-A) + [S]B of signature i (h = h_in, 8 LE words): its
 // nper mixed additions from the key's and B's comb tables, entries staged through LDS one
@@ -1439,11 +1114,9 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
 #pragma unroll
       for (int s = 0; s < DEPTH; s++)
         if (slot == s) dq[s] = dn;
-#if !CBFT_LADDER_NOFETCH  // (probe builds only: compute without the table traffic, wrong verdicts)
       request(entry(jj + DEPTH, dn), slot);
-#endif
     }
-    if (CBFT_QUAD_FIRST_SET && jj == 0) {  // O + entry as a point set (see the pair ladder): 1 M
+    if (jj == 0) {  // the lane's first addition starts from the identity: a point set (see the pair ladder), 1 M
       fe ypx, ymx, E, H;
 #pragma unroll
       for (int k = 0; k < FE_LIMBS; k++) {
@@ -1481,7 +1154,7 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
       fe_sub(t.X, A, B);
       fe_add(t.Y, A, B);
       fe_add(s, D, C);
-      if (!CBFT_LADDER_LAZYSUM) fe_carry(s);
+      fe_carry(s);
       fe_sub(e, D, C);
 #pragma unroll
       for (int k = 0; k < FE_LIMBS; k++) {
@@ -1496,7 +1169,7 @@ __device__ __forceinline__ void comb_quad_sum(const Ed25519Batch& b, size_t i, u
   }
 }
 
-__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
+__global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, COMB_MIN_WAVES)
     ed25519_comb_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* btbl,
                                const CombLadder cl, uint32_t* xyz_soa) {
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1527,43 +1200,28 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_COMB_MIN_WAVES)
 }
 
 // ---------------------------------------------------------------------------------------
-// Small batches in ONE launch (the per-request path: a few coalesced verify() calls): one block
-// of two waves per 16 signatures.  Wave 0: a lane quad per signature -- every lane of the quad
-// hashes (the same digest, so no exchange), the quad runs the comb sum as K3q and combines it by
-// DPP.  Wave 1, meanwhile on another SIMD: decodes each signature's R.  The verdict then needs
-// no inversion: encode(R') == R (OpenSSL's memcmp of the encodings) holds exactly when R's y is
+// Small batches in ONE launch (the per-request path: a few coalesced verify() calls): a block of
+// four waves (four SIMDs) per 8 signatures.  Wave 0 hashes (a lane quad per signature, every lane
+// of the quad the same digest), then sums [h](-A) over its quads (the key comb's positions only)
+// and adds the [S]B half; wave 1 sums [S]B (B's comb positions: S is known before the hash) and
+// hands it over in LDS; waves 2 and 3 decode R (each signature's square-root chain on a 16-lane DPP
+// row, ge_frombytes_row; a fifth wave would share a SIMD: measured on gfx950, a decode wave that
+// shares wave 0's SIMD takes 80 us against 42 us, and slows the hash).  The verdict then needs no
+// inversion: encode(R') == R (OpenSSL's memcmp of the encodings) holds exactly when R's y is
 // canonical, R decodes, R is not "x = 0 with the sign bit set", and R' = (X : Y : Z) equals
 // (x_R, y_R) projectively (X = x_R Z, Y = y_R Z): the encoding is a bijection between points and
-// canonical encodings, and the decoder picks x by the sign bit.  The R decode (a square-root
-// chain) runs under the hash and the comb instead of an inversion after them.  The verdicts of
-// the block's signatures go out as one 8- or 16-bit piece; no per-signature state goes through HBM.
+// canonical encodings, and the decoder picks x by the sign bit.
 // ---------------------------------------------------------------------------------------
-// R decoders per block: CBFT_DECODE_ROW = 1 puts each signature's square-root chain on a 16-lane
-// DPP row (ge_frombytes_row), two waves for the block's 8 signatures, so a block is 3 waves (4 in
-// the three-wave form) and every wave has a SIMD of its own (a fifth wave would share one: measured
-// on gfx950, the decode wave that shares wave 0's SIMD takes 80 us against 42 us, and slows the
-// hash); 0 keeps one wave with a lane quad per signature on the one-lane chain, 16 signatures.
-#ifndef CBFT_DECODE_ROW
-#define CBFT_DECODE_ROW 1
-#endif
-#define SMALL_SIGS (CBFT_DECODE_ROW ? 8 : 16)
-// comb-table entries in flight per lane in the fused kernels (LDS: 7 KB per entry and comb wave).
-// PMC of the one-entry form: 44 % of the kernel's wave cycles in s_waitcnt (the key table's
-// random reads over tens of GB), but p50 @ 1K and the lone verify measured the same at 1, 2 and 4
-// in flight (A/B on one box): the waits are off the critical path (wave 0's SHA-512)
-#ifndef CBFT_SMALL_DEPTH
-#define CBFT_SMALL_DEPTH 2
-#endif
-#define SMALL_DEPTH CBFT_SMALL_DEPTH
-// three-wave kernel: the [S]B wave writes the SHA-512 message schedules (K[t] + W[t]) of messages
-// up to SMALL_KW_BLOCKS blocks (64 + len + 17 <= 1,024 B) to LDS first, so wave 0's hash is rounds
-// only (CBFT_SMALL_SPLIT_HASH=0: wave 0 hashes alone)
-#ifndef CBFT_SMALL_SPLIT_HASH
-#define CBFT_SMALL_SPLIT_HASH 1
-#endif
+#define SMALL_SIGS 8
+// comb-table entries in flight per lane (LDS: 7 KB per entry and comb wave).  PMC of the one-entry
+// form: 44 % of the kernel's wave cycles in s_waitcnt (the key table's random reads over tens of
+// GB), but p50 @ 1K and the lone verify measured the same at 1, 2 and 4 in flight (A/B on one
+// box): the waits are off the critical path (wave 0's SHA-512)
+#define SMALL_DEPTH 2
+// the [S]B wave writes the SHA-512 message schedules (K[t] + W[t]) of messages up to
+// SMALL_KW_BLOCKS blocks (64 + len + 17 <= 1,024 B) to LDS first, so wave 0's hash is rounds only
 #define SMALL_KW_BLOCKS 8
-#define SMALL_DEC_WAVES (CBFT_DECODE_ROW ? 2 : 1)
-#define SMALL_BLOCK (64 * (1 + SMALL_DEC_WAVES))
+#define SMALL_DEC_WAVES 2
 
 // The block's verdict bits (bit s = signature blk * SMALL_SIGS + s) as SMALL_SIGS / 8 bytes; the
 // last block also zeroes the bytes of its 64-bit verdict word that no block covers, so the call
@@ -1581,23 +1239,14 @@ __device__ __forceinline__ void small_store_bits(uint8_t* vb, uint32_t bits) {
 template <bool SYNC = false>  // SYNC: the wave joins one extra __syncthreads() (see ge_frombytes_row)
 __device__ __forceinline__ void small_decode_r(const Ed25519Batch& b, uint32_t blk, uint32_t dw, uint32_t ln,
                                                uint32_t (*rdec)[2 * FE_LIMBS + 1]) {
-  const uint32_t sl = CBFT_DECODE_ROW ? dw * 4 + (ln >> 4) : (ln >> 2);
-  const bool writer = CBFT_DECODE_ROW ? (ln & 15u) == 0 : (ln & 3u) == 0;
+  const uint32_t sl = dw * 4 + (ln >> 4);
+  const bool writer = (ln & 15u) == 0;
   size_t i = (size_t)blk * SMALL_SIGS + sl;
   if (i >= b.n) i = b.n - 1;
   uint32_t Rw[8];
   load_words8(Rw, b.sig + i * 64);
   fe X, Y;
-  bool ok;
-  if (CBFT_DECODE_ROW) {
-    ok = ge_frombytes_row<SYNC>(X, Y, Rw);
-  } else {
-    if (SYNC) __syncthreads();
-    ge_p3 R;
-    ok = ge_frombytes(R, Rw);
-    X = R.X;
-    Y = R.Y;
-  }
+  bool ok = ge_frombytes_row<SYNC>(X, Y, Rw);
   // y < p: the 255-bit y is not one of 2^255 - 19 .. 2^255 - 1
   bool top = (Rw[7] & 0x7fffffffu) == 0x7fffffffu && Rw[0] >= 0xffffffedu;
 #pragma unroll
@@ -1612,77 +1261,6 @@ __device__ __forceinline__ void small_decode_r(const Ed25519Batch& b, uint32_t b
     rdec[sl][2 * FE_LIMBS] = ok ? 1u : 0u;
   }
 }
-__global__ void __launch_bounds__(SMALL_BLOCK) ed25519_small_kernel(const Ed25519Batch b, const uint32_t* btbl,
-                                                                    const CombLadder cl, uint8_t* verdict_bytes) {
-  __shared__ int32_t sdig[COMB_MAX_STEPS * 64];
-  __shared__ uint4 stage[SMALL_DEPTH * 7 * 64];
-  __shared__ uint32_t rdec[SMALL_SIGS][2 * FE_LIMBS + 1];  // x_R | y_R | decodes
-  // quads past the block's signatures (lanes 32..63 with 8 signatures) repeat quads 0..7 unused
-  const uint32_t ln = threadIdx.x & 63u, wave = threadIdx.x >> 6, q = ln & 3u, sl = (ln >> 2) & (SMALL_SIGS - 1);
-  size_t i = (size_t)blockIdx.x * SMALL_SIGS + sl;
-  const bool live = i < b.n && (ln >> 2) < SMALL_SIGS;
-  if (!live) i = b.n - 1;
-#if CBFT_ED_PHASES  // probe builds: block 0's phase times (10 ns ticks), printed by lane 0
-  uint64_t ph[6];
-#define ED_STAMP(k) ph[k] = wall_clock64()
-#else
-#define ED_STAMP(k)
-#endif
-  if (wave >= 1) {
-#if CBFT_ED_PHASES
-    const uint64_t d0 = wall_clock64();
-#endif
-    small_decode_r(b, blockIdx.x, wave - 1, ln, rdec);
-#if CBFT_ED_PHASES
-    if (blockIdx.x == 0 && ln == 0) printf("ed25519_small block 0: R decode %.1f us\n", (wall_clock64() - d0) * 0.01);
-#endif
-    __syncthreads();
-    return;
-  }
-  ED_STAMP(0);
-  uint32_t hs[8];
-  bool flag;
-  ed25519_hash_sig(b, i, hs, flag);
-  ED_STAMP(1);
-  ge_p3 P;
-  comb_quad_sum<64, SMALL_DEPTH>(b, i, q, hs, btbl, cl, sdig, stage, P);
-  ED_STAMP(2);
-  quad_combine<0xB1>(P, true);
-  quad_combine<0x4E>(P, false);
-  ED_STAMP(3);
-  __syncthreads();  // wave 1's R decodes
-  fe xr, yr, t;
-#pragma unroll
-  for (int k = 0; k < FE_LIMBS; k++) {
-    xr.v[k] = rdec[sl][k];
-    yr.v[k] = rdec[sl][FE_LIMBS + k];
-  }
-  bool same = rdec[sl][2 * FE_LIMBS] != 0;
-  fe_mul<false>(t, xr, P.Z);
-  fe_sub(t, P.X, t);
-  same = same && fe_iszero(t);
-  fe_mul<false>(t, yr, P.Z);
-  fe_sub(t, P.Y, t);
-  same = same && fe_iszero(t);
-  ED_STAMP(4);
-#if CBFT_ED_PHASES
-  if (blockIdx.x == 0 && ln == 0)
-    printf("ed25519_small block 0 (us): hash %.1f comb %.1f combine %.1f check %.1f\n", (ph[1] - ph[0]) * 0.01,
-           (ph[2] - ph[1]) * 0.01, (ph[3] - ph[2]) * 0.01, (ph[4] - ph[3]) * 0.01);
-#endif
-  const bool verdict = live && same && flag && b.keys.aok(batch_unit(b, i));
-  const uint64_t bal = __ballot(verdict);
-  uint32_t bits = 0;
-#pragma unroll
-  for (int s2 = 0; s2 < SMALL_SIGS; s2++) bits |= (uint32_t)((bal >> (4 * s2)) & 1u) << s2;
-  if (ln == 0) small_store_bits(verdict_bytes, bits);
-}
-
-// The same verdicts with the work of a block of 16 signatures on THREE waves (three SIMDs):
-// wave 0 hashes, then sums [h](-A) over its quads (the key comb's positions only) and adds the
-// [S]B half; wave 1 sums [S]B (B's comb positions: S is known before the hash) and hands it over
-// in LDS; wave 2 decodes R.  Wave 0's critical path loses B's additions (12 of 32 positions).
-// Selected by $CBFT_SMALL_WAVES=3.
 #define SMALL3_BLOCK (64 * (2 + SMALL_DEC_WAVES))
 __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25519Batch b, const uint32_t* btbl,
                                                                       const CombLadder cl, uint8_t* verdict_bytes) {
@@ -1691,9 +1269,6 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
   __shared__ uint32_t rdec[SMALL_SIGS][2 * FE_LIMBS + 1];  // x_R | y_R | decodes
   __shared__ uint32_t sbp[SMALL_SIGS][4 * FE_LIMBS];       // [S]B as X | Y | Z | T
   __shared__ uint64_t kw[SMALL_SIGS][SMALL_KW_BLOCKS * KW_STRIDE];  // SHA-512 K[t] + W[t] per block
-#if CBFT_ED_PHASES
-  __shared__ uint64_t phend[6];  // per wave: end of its part (decode waves: also their start, +2)
-#endif
   const uint32_t ln = threadIdx.x & 63u, wave = threadIdx.x >> 6, q = ln & 3u, sl = (ln >> 2) & (SMALL_SIGS - 1);
   size_t i = (size_t)blockIdx.x * SMALL_SIGS + sl;
   const bool live = i < b.n && (ln >> 2) < SMALL_SIGS;
@@ -1704,21 +1279,14 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
   // decodes done".  The split hash runs when
   // every signature of the block fits SMALL_KW_BLOCKS SHA-512 blocks (a wave-uniform ballot that
   // waves 0 and 1 compute alike); otherwise wave 0 hashes on its own as before.
-  const bool split = CBFT_SMALL_SPLIT_HASH && __ballot(sig_sha_blocks(b, i) > SMALL_KW_BLOCKS) == 0;
+  const bool split = __ballot(sig_sha_blocks(b, i) > SMALL_KW_BLOCKS) == 0;
   if (wave >= 2) {  // (without the split every wave passes the first barrier at its start)
-#if CBFT_ED_PHASES
-    if (ln == 0) phend[wave] = wall_clock64();  // start of the decode (overwritten at its end)
-    if (ln == 0) phend[wave + 2] = phend[wave];
-#endif
     if (split) {
       small_decode_r<true>(b, blockIdx.x, wave - 2, ln, rdec);
     } else {
       __syncthreads();
       small_decode_r<false>(b, blockIdx.x, wave - 2, ln, rdec);
     }
-#if CBFT_ED_PHASES
-    if (ln == 0) phend[wave] = wall_clock64();  // (printed by wave 0 after the last barrier)
-#endif
     __syncthreads();
     return;
   }
@@ -1739,55 +1307,24 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
         sbp[sl][3 * FE_LIMBS + k] = P.T.v[k];
       }
     }
-#if CBFT_ED_PHASES
-    if (ln == 0) phend[1] = wall_clock64();
-#endif
     __syncthreads();
     return;
   }
   uint32_t hs[8];
   bool flag;
-#if CBFT_ED_PHASES
-  uint64_t ph3[5];
-  ph3[0] = wall_clock64();
-#endif
   if (split) {
     ed25519_hash_sig_kw(b, i, kw[sl], hs, flag, [&] {
-#if CBFT_ED_PHASES
-      ph3[1] = wall_clock64();
-#endif
       __syncthreads();  // wave 1's message schedules (block 0 is done meanwhile)
     });
   } else {
     __syncthreads();
-#if CBFT_ED_PHASES
-    ph3[1] = wall_clock64();
-#endif
     ed25519_hash_sig(b, i, hs, flag);
   }
-#if CBFT_ED_PHASES
-  ph3[2] = wall_clock64();
-#endif
   ge_p3 P;
   comb_quad_sum<64, SMALL_DEPTH>(b, i, q, hs, btbl, cl, sdig[0], stage[0], P, 0, na, (int)((na + 3) / 4));
   quad_combine<0xB1>(P, true);
   quad_combine<0x4E>(P, true);
-#if CBFT_ED_PHASES
-  ph3[3] = wall_clock64();
-#endif
   __syncthreads();  // wave 1's [S]B, wave 2's R
-#if CBFT_ED_PHASES
-  ph3[4] = wall_clock64();
-  // every time from wave 0's start; the printf runs after the last barrier (a device printf takes
-  // tens of microseconds and would otherwise stretch the wave that calls it)
-  if (blockIdx.x == 0 && ln == 0)
-    printf("ed25519_small3 block 0 (us from start): block-0 compress %.1f, rounds done %.1f, A-comb done %.1f | "
-           "[S]B done %.1f | R decode %.1f-%.1f, %.1f-%.1f | barrier %.1f (split %d)\n",
-           (ph3[1] - ph3[0]) * 0.01, (ph3[2] - ph3[0]) * 0.01, (ph3[3] - ph3[0]) * 0.01,
-           ((int64_t)(phend[1] - ph3[0])) * 0.01, ((int64_t)(phend[4] - ph3[0])) * 0.01,
-           ((int64_t)(phend[2] - ph3[0])) * 0.01, ((int64_t)(phend[5] - ph3[0])) * 0.01,
-           ((int64_t)(phend[3] - ph3[0])) * 0.01, (ph3[4] - ph3[0]) * 0.01, split ? 1 : 0);
-#endif
   {
     ge_p3 Q;
 #pragma unroll
@@ -1839,71 +1376,23 @@ __global__ void __launch_bounds__(SMALL3_BLOCK) ed25519_small3_kernel(const Ed25
 // its entry is requested.
 // ---------------------------------------------------------------------------------------
 #define COMB2_BLOCK 128
-#ifndef CBFT_LADDER_MUL2
-#define CBFT_LADDER_MUL2 0
-#endif
 #define COMB2_MAX_STEPS 24  // additions per lane: radix-2^8 keys + radix-2^16 B = 48 positions
-#ifndef CBFT_COMB2_MIN_WAVES
-#define CBFT_COMB2_MIN_WAVES 2
-#endif
-// CBFT_LADDER_FIRST_SET: each lane's first comb addition (from the identity) is a point set, 1 M
-#ifndef CBFT_LADDER_FIRST_SET
-#define CBFT_LADDER_FIRST_SET 1
-#endif
-// CBFT_LADDER_PHASED: both lanes of a pair walk the key positions, then B's (uniform table per step)
-#ifndef CBFT_LADDER_PHASED
-#define CBFT_LADDER_PHASED 1
-#endif
-
-// CBFT_LADDER_PRIO (A/B only): the two waves a SIMD holds at 64K run nearly one after the other
-// under the oldest-first issue arbitration (CBFT_LADDER_STAMPS: ~a quarter of the waves end by
-// ~60 us, half at 120-140 us), so the second runs its tail alone; a priority that falls with
-// progress (3, 2, 1, 0 by quarter of the steps) keeps the lagging wave ahead.  Isolated ladder
-// 109 -> 105 us, but the pipelined headline loses (494-506 vs 511-516 M/s at 200 steps: the
-// co-running finish and hash kernels are starved), profiles/r05_ab/ladder_wave_ends_prio.txt;
-// = 2 (priority 1 for the first half only): isolated -1.7 %, pipelined 503-505 vs 511-513 M/s.
-#ifndef CBFT_LADDER_PRIO
-#define CBFT_LADDER_PRIO 0
-#endif
-#ifndef CBFT_LADDER_NOPPAD
-#define CBFT_LADDER_NOPPAD 0
-#endif
-// CBFT_LADDER_STAMPS (probe builds only): per-wave wall-clock stamps of the pair ladder (start,
-// first entry landed, end; 10 ns ticks) stored per wave; the last wave of a launch folds them and
-// prints the spread of the end times (launches must not overlap).
-#ifndef CBFT_LADDER_STAMPS
-#define CBFT_LADDER_STAMPS 0
-#endif
-#if CBFT_LADDER_STAMPS
-__device__ unsigned long long g_lw[3 * 8192];  // per wave: start, first entry landed, end
-__device__ unsigned int g_lcount;
-__device__ unsigned int g_lhist[32];
-#endif
-__global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
+#define COMB2_MIN_WAVES 2
+__global__ void __launch_bounds__(COMB2_BLOCK, COMB2_MIN_WAVES)
     ed25519_comb2_ladder_kernel(const Ed25519Batch b, const uint32_t* h_soa, const uint32_t* btbl,
                                 const CombLadder cl, uint32_t* xyz_soa) {
   const size_t g = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-#if CBFT_LADDER_STAMPS
-  const uint64_t st0 = wall_clock64();
-  uint64_t st1 = st0;
-#endif
   const uint32_t q = threadIdx.x & 1u;
   size_t i = g >> 1;
   const bool live = i < b.n;
   if (!live) i = b.n - 1;  // tail pairs compute a copy (both lanes stay active for the DPP)
   const uint32_t na = (uint32_t)cl.a.npos, nb = (uint32_t)cl.b.npos;
-#if CBFT_LADDER_PHASED
   // Phased split: each lane takes half of the key positions, then half of B's, so at every step
   // both lanes of every pair read the same table (the step's table, radix and scalar are
   // wave-uniform: scalar branches, no per-lane selects).  ceil(na/2) + ceil(nb/2) steps: the same
   // 16 as ceil(32/2) at the default 20 + 12 positions.
   const uint32_t naper = (na + 1u) >> 1, nbper = (nb + 1u) >> 1;
   const uint32_t nper = naper + nbper;
-#else
-  const uint32_t ntot = na + nb;
-  const uint32_t nper = (ntot + 1u) >> 1;
-  const uint32_t first = q * nper;
-#endif
   __shared__ uint4 stage[COMB2_BLOCK / 64][2][7][64];  // per wave: two lane-linear 7 KB entry images
   __shared__ uint32_t sc[16][COMB2_BLOCK];              // h + offA (words 0..7), S + offB (8..15)
   {
@@ -1926,7 +1415,6 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
     const uint32_t hi = wi < 7u ? sc[base + wi + 1u][threadIdx.x] : 0u;  // bits >= 256 read as 0
     return (uint32_t)((((uint64_t)hi << 32) | lo) >> (off & 31u)) & ((1u << w) - 1u);
   };
-#if CBFT_LADDER_PHASED
   // signed digit of this lane's step jj (0 = the identity entry past the last position)
   auto digit = [&](uint32_t jj) -> int {
     if (jj >= nper) return 0;
@@ -1950,29 +1438,6 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
     const uint32_t pos = jj < nper ? q * nbper + (jj - naper) : 0u;
     return btbl + ((size_t)(pos < nb ? pos : 0u) * cl.b.entries() + ad) * COMB_STRIDE;
   };
-#else
-  // signed digit of this lane's step jj (0 = the identity entry past the last position)
-  auto digit = [&](uint32_t jj) -> int {
-    const uint32_t k = first + jj;
-    if (jj >= nper || k >= ntot) return 0;
-    const bool isA = k < na;
-    const uint32_t pos = isA ? k : k - na;
-    const uint32_t w = isA ? (uint32_t)cl.a.w : (uint32_t)cl.b.w;
-    const uint32_t top = (isA ? (uint32_t)cl.a.npos : (uint32_t)cl.b.npos) - 1u;
-    const uint32_t ch = chunk(isA ? 0u : 8u, pos * w, w);
-    const uint32_t half = 1u << (w - 1u);
-    // top digit in [0, 2^(w-1)]; only S >= L (flagged, rejected in K4) can exceed it
-    return pos == top ? (int)(ch < half ? ch : half) : (int)ch - (int)half;
-  };
-  const uint32_t* akey = b.keys.comb(batch_unit(b, i));
-  auto entry = [&](uint32_t jj, int d) {
-    const uint32_t k = first + jj;
-    const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
-    if (k < na) return akey + ((size_t)k * cl.a.entries() + ad) * COMB_STRIDE;
-    const uint32_t pos = k < ntot ? k - na : 0u;
-    return btbl + ((size_t)pos * cl.b.entries() + ad) * COMB_STRIDE;
-  };
-#endif
   const uint32_t wv = threadIdx.x >> 6, ln = threadIdx.x & 63u;
   auto request = [&](uint32_t slot, const uint32_t* e) {
 #pragma unroll
@@ -1988,37 +1453,12 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
 #pragma nounroll
   for (uint32_t jj = 0; jj < nper; jj++) {
     const uint32_t slot = jj & 1u;
-#if CBFT_LADDER_PRIO == 2
-    // two levels: the first half of the steps at priority 1, the rest at 0
-    if (jj == 0) __builtin_amdgcn_s_setprio(1);
-    if (jj == (nper >> 1)) __builtin_amdgcn_s_setprio(0);
-#elif CBFT_LADDER_PRIO
-    {  // issue priority falls with progress: a SIMD's lagging wave outranks its leading one
-      const uint32_t qtr = (jj * 4u) / nper;  // wave-uniform
-      if (qtr == 0)
-        __builtin_amdgcn_s_setprio(3);
-      else if (qtr == 1)
-        __builtin_amdgcn_s_setprio(2);
-      else if (qtr == 2)
-        __builtin_amdgcn_s_setprio(1);
-      else
-        __builtin_amdgcn_s_setprio(0);
-    }
-#endif
-#if CBFT_LADDER_NOPPAD  // probe builds: pad each step with N 4-byte s_nop (instruction-fetch sensitivity)
-#define CBFT_STR2(x) #x
-#define CBFT_STR(x) CBFT_STR2(x)
-    asm volatile(".rept " CBFT_STR(CBFT_LADDER_NOPPAD) "\n\ts_nop 0\n\t.endr" ::: "memory");
-#endif
     if (jj + 1u < nper)
       asm volatile("s_waitcnt vmcnt(7)" ::: "memory");  // entry jj landed; jj + 1 may still fly
     else
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     // The stage is read with asm ds_reads: the compiler would otherwise see LDS reads after
     // global_load_lds writes and wait for ALL of them (vmcnt(0)), serialising the two stages.
-#if CBFT_LADDER_STAMPS
-    if (jj == 0) st1 = wall_clock64();
-#endif
     uint32_t ew[28];
     {
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
@@ -2048,40 +1488,7 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
       dnext = digit(jj + 2u);
       request(slot, entry(jj + 2u, dnext));
     }
-#if CBFT_LADDER_MUL2
-    // the same addition with its independent products paired (fe_mul2: two mad chains
-    // interleaved per column): (A, B), C, (T, X), (Y, Z)
-    {
-      ge_p1p1 t;
-      fe A, B, C, D, s1, s2, e1, e2;
-#pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) {
-        e1.v[k] = neg ? ew[9 + k] : ew[k];
-        e2.v[k] = neg ? ew[k] : ew[9 + k];
-      }
-      fe_add(s1, P.Y, P.X);
-      fe_sub(s2, P.Y, P.X);
-      fe_mul2(A, s1, e1, B, s2, e2);
-#pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) e1.v[k] = ew[18 + k];
-      fe_mul(C, e1, P.T);
-      fe_add(D, P.Z, P.Z);
-      fe_sub(t.X, A, B);
-      fe_add(t.Y, A, B);
-      fe_add(s1, D, C);
-      if (!CBFT_LADDER_LAZYSUM) fe_carry(s1);
-      fe_sub(e1, D, C);
-#pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) {
-        t.Z.v[k] = neg ? e1.v[k] : s1.v[k];
-        t.T.v[k] = neg ? s1.v[k] : e1.v[k];
-      }
-      fe_mul2(P.T, t.X, t.Y, P.X, t.X, t.T);
-      fe_mul2(P.Y, t.Y, t.Z, P.Z, t.Z, t.T);
-    }
-  }
-#else
-    if (CBFT_LADDER_FIRST_SET && jj == 0) {
+    if (jj == 0) {
       // The lane's first addition starts from the identity: O + (x, y) needs no product but T.
       // With E = (y+x) - (y-x) = 2x and H = (y+x) + (y-x) = 2y (swapped for a negative digit,
       // giving -x), P = (2E : 2H : 4 : E H) = (x : y : 1 : xy) scaled by 4 (XY = ZT holds):
@@ -2105,25 +1512,27 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
       continue;
     }
     ge_p1p1 t;
+    // the addition's independent products as interleaved pairs (fe_mul2_oneasm: two mad chains in
+    // one asm statement, each instruction followed by the other product's independent one): (A, B),
+    // then C alone, then (T, X) and (Y, Z).  Isolated ladder -2.3 %, 200-step headline -2 % against
+    // seven single products (tools/probes/r06_ab2.sh); three- and four-way groups measured slower.
     {
-      // niels (y+x, y-x, 2dxy), negated by swapping y+x <-> y-x and C <-> -C (ge_add_mem)
-      fe A, B, C, D, s, e;
+      fe A, B, C, D, s1, s2, e1, e2, e3, s, e;
 #pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) e.v[k] = neg ? ew[9 + k] : ew[k];
-      fe_add(s, P.Y, P.X);
-      fe_mul(A, s, e);
-#pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) e.v[k] = neg ? ew[k] : ew[9 + k];
-      fe_sub(s, P.Y, P.X);
-      fe_mul(B, s, e);
-#pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) e.v[k] = ew[18 + k];
-      fe_mul(C, e, P.T);
+      for (int k = 0; k < FE_LIMBS; k++) {
+        e1.v[k] = neg ? ew[9 + k] : ew[k];  // niels (y+x, y-x, 2dxy), negated by swapping y+x <-> y-x
+        e2.v[k] = neg ? ew[k] : ew[9 + k];  // and C <-> -C (ge_add_mem)
+        e3.v[k] = ew[18 + k];
+      }
+      fe_add(s1, P.Y, P.X);
+      fe_sub(s2, P.Y, P.X);
+      fe_mul2_oneasm(A, s1, e1, B, s2, e2);
+      fe_mul(C, e3, P.T);
       fe_add(D, P.Z, P.Z);
       fe_sub(t.X, A, B);
       fe_add(t.Y, A, B);
       fe_add(s, D, C);
-      if (!CBFT_LADDER_LAZYSUM) fe_carry(s);
+      fe_carry(s);
       fe_sub(e, D, C);
 #pragma unroll
       for (int k = 0; k < FE_LIMBS; k++) {
@@ -2131,60 +1540,15 @@ __global__ void __launch_bounds__(COMB2_BLOCK, CBFT_COMB2_MIN_WAVES)
         t.T.v[k] = neg ? s.v[k] : e.v[k];
       }
     }
-    fe_mul(P.T, t.X, t.Y);
-    fe_mul(P.X, t.X, t.T);
-    fe_mul(P.Y, t.Y, t.Z);
-    fe_mul(P.Z, t.Z, t.T);
+    fe_mul2_oneasm(P.T, t.X, t.Y, P.X, t.X, t.T);
+    fe_mul2_oneasm(P.Y, t.Y, t.Z, P.Z, t.Z, t.T);
   }
-#endif
   quad_combine<0xB1>(P, false);  // P += partner lane's P
   if (live && q == 0) {
     fe_store_soa(xyz_soa, b.n, i, P.X);
     fe_store_soa(xyz_soa + 9 * b.n, b.n, i, P.Y);
     fe_store_soa(xyz_soa + 18 * b.n, b.n, i, P.Z);
   }
-#if CBFT_LADDER_STAMPS
-  {
-    const unsigned wid = (unsigned)(g >> 6), waves = (unsigned)((gridDim.x * (size_t)blockDim.x) >> 6);
-    if ((threadIdx.x & 63u) == 0 && wid < 8192u) {
-      g_lw[3 * wid] = st0;
-      g_lw[3 * wid + 1] = st1;
-      g_lw[3 * wid + 2] = wall_clock64();
-    }
-    __threadfence();
-    unsigned last = 0;
-    if ((threadIdx.x & 63u) == 0) last = atomicAdd(&g_lcount, 1u) == waves - 1u;
-    last = __shfl(last, 0);
-    if (last && waves <= 8192u) {  // the last wave: every lane folds waves ln, ln + 64, ...
-      __threadfence();
-      const unsigned ln2 = threadIdx.x & 63u;
-      unsigned long long mn0 = ~0ull, mx0 = 0, sdur = 0, swait = 0;
-      for (unsigned w = ln2; w < waves; w += 64) mn0 = min(mn0, g_lw[3 * w]);
-      for (int o = 32; o; o >>= 1) mn0 = min(mn0, (unsigned long long)__shfl_xor((long long)mn0, o));
-      for (unsigned w = ln2; w < waves; w += 64) {
-        const unsigned long long t0 = g_lw[3 * w], t1 = g_lw[3 * w + 1], t2 = g_lw[3 * w + 2];
-        mx0 = max(mx0, t2);
-        sdur += t2 - t0;
-        swait += t1 - t0;
-        const unsigned bk = (unsigned)((t2 - mn0) / 500u);  // 5 us buckets of the END time
-        atomicAdd(&g_lhist[bk < 31u ? bk : 31u], 1u);
-      }
-      for (int o = 32; o; o >>= 1) {
-        mx0 = max(mx0, (unsigned long long)__shfl_xor((long long)mx0, o));
-        sdur += (unsigned long long)__shfl_xor((long long)sdur, o);
-        swait += (unsigned long long)__shfl_xor((long long)swait, o);
-      }
-      __threadfence();
-      if (ln2 == 0) {
-        printf("comb2 ladder %u waves: last end %.1f us, mean wave %.1f, mean first-entry wait %.1f; ends per 5 us: ",
-               waves, (mx0 - mn0) * 0.01, sdur * 0.01 / waves, swait * 0.01 / waves);
-        for (int k = 0; k < 32; k++) printf("%u ", atomicExch(&g_lhist[k], 0u));
-        printf("\n");
-        atomicExch(&g_lcount, 0u);
-      }
-    }
-  }
-#endif
 }
 
 // ---------------------------------------------------------------------------------------
@@ -2247,12 +1611,8 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
     if (w.comb.nper > COMB_MAX_STEPS) return hipErrorInvalidValue;
     if (ev)
       for (int k = 0; k < 3; k++) (void)hipEventRecord(ev[k], stream);
-    if (w.small == 3)
-      hipLaunchKernelGGL(ed25519_small3_kernel, dim3((unsigned)((b.n + SMALL_SIGS - 1) / SMALL_SIGS)), dim3(SMALL3_BLOCK), 0,
-                         stream, b, w.base_comb, w.comb, reinterpret_cast<uint8_t*>(w.verdict_words));
-    else
-      hipLaunchKernelGGL(ed25519_small_kernel, dim3((unsigned)((b.n + SMALL_SIGS - 1) / SMALL_SIGS)), dim3(SMALL_BLOCK), 0,
-                         stream, b, w.base_comb, w.comb, reinterpret_cast<uint8_t*>(w.verdict_words));
+    hipLaunchKernelGGL(ed25519_small3_kernel, dim3((unsigned)((b.n + SMALL_SIGS - 1) / SMALL_SIGS)), dim3(SMALL3_BLOCK), 0,
+                       stream, b, w.base_comb, w.comb, reinterpret_cast<uint8_t*>(w.verdict_words));
     if (ev) (void)hipEventRecord(ev[3], stream);
     return hipGetLastError();
   }
@@ -2264,7 +1624,7 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
     const dim3 g256((unsigned)((b.n + 255) / 256)), b256(256);
     hipLaunchKernelGGL(ed25519_bucket_count_kernel, g256, b256, 0, stream, b, w.buckets);
     hipLaunchKernelGGL(ed25519_bucket_scan_kernel, dim3(1), b256, 0, stream, w.buckets, w.buckets + CBFT_SHA_BUCKETS,
-                       (uint32_t)(w.long_groups > 0 ? w.long_groups : CBFT_SHA_LONG_GROUPS));
+                       (uint32_t)CBFT_SHA_LONG_GROUPS);
     hipLaunchKernelGGL(ed25519_bucket_scatter_kernel, g256, b256, 0, stream, b, w.buckets + CBFT_SHA_BUCKETS, w.perm);
   }
   const uint32_t* uniform_w = sorted ? (const uint32_t*)(w.buckets + 2 * CBFT_SHA_BUCKETS) : nullptr;
@@ -2272,21 +1632,12 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   if (nshort_w) {  // the long messages on the second stream, beside the short ones
     if ((e = hipEventRecord(w.fork_ev, stream)) != hipSuccess || (e = hipStreamWaitEvent(w.aux, w.fork_ev, 0)) != hipSuccess)
       return e;
-    if (w.long_prio)
-      hipLaunchKernelGGL(ed25519_hash_long_kernel<3>, dim3((unsigned)((b.n + 63) / 64)), dim3(HASH_LONG_BLOCK), 0, w.aux, b,
-                         (const uint32_t*)w.perm, uniform_w, nshort_w, w.h_soa, w.flags);
-    else
-      hipLaunchKernelGGL(ed25519_hash_long_kernel<0>, dim3((unsigned)((b.n + 63) / 64)), dim3(HASH_LONG_BLOCK), 0, w.aux, b,
-                         (const uint32_t*)w.perm, uniform_w, nshort_w, w.h_soa, w.flags);
+    hipLaunchKernelGGL(ed25519_hash_long_kernel, dim3((unsigned)((b.n + 63) / 64)), dim3(HASH_LONG_BLOCK), 0, w.aux, b,
+                       (const uint32_t*)w.perm, uniform_w, nshort_w, w.h_soa, w.flags);
     if ((e = hipEventRecord(w.join_ev, w.aux)) != hipSuccess) return e;
   }
-  const int pf = comb && w.comb_lanes == 2 && b.key_idx && w.ladder_prefetch ? 1 : 0;
-  if (w.hash_prio)
-    hipLaunchKernelGGL(ed25519_hash_kernel<2>, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
-                       uniform_w, nshort_w, w.h_soa, w.flags, w.comb, pf);
-  else
-    hipLaunchKernelGGL(ed25519_hash_kernel<0>, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
-                       uniform_w, nshort_w, w.h_soa, w.flags, w.comb, pf);
+  hipLaunchKernelGGL(ed25519_hash_kernel, grid, block, 0, stream, b, sorted ? (const uint32_t*)w.perm : nullptr,
+                     uniform_w, nshort_w, w.h_soa, w.flags);
   // the next batch's hash may start behind this batch's short hashes while the long tail still
   // runs on the aux stream (hash_early), or only after the whole hash stage
   if (order && order->hash_early && (e = hipEventRecord(order->done[0], stream)) != hipSuccess) return e;
@@ -2306,58 +1657,12 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   }
   if (order && (e = hipEventRecord(order->done[1], stream)) != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[2], stream);
-  switch (w.finish_batch) {
-#define CBFT_FINISH_TREE_LAUNCH(K, T)                                                                         \
-  hipLaunchKernelGGL((ed25519_finish_tree_kernel<K, T, 0>), dim3((unsigned)((b.n + (size_t)(T) * K - 1) / ((size_t)(T) * K))), \
-                     dim3(T), 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words, (uint32_t*)nullptr)
-#define CBFT_FINISH_SPLIT_LAUNCH(K, T)                                                                        \
-  do {                                                                                                        \
-    const unsigned nb = (unsigned)((b.n + (size_t)(T) * K - 1) / ((size_t)(T) * K));                          \
-    hipLaunchKernelGGL((ed25519_finish_tree_kernel<K, T, 1>), dim3(nb), dim3(T), 0, stream, b, w.xyz_soa, w.flags,   \
-                       w.aok, w.verdict_words, w.tree);                                                       \
-    hipLaunchKernelGGL((ed25519_finish_root_kernel<T>), dim3((nb + 63) / 64), dim3(64), 0, stream, w.tree, nb);     \
-    hipLaunchKernelGGL((ed25519_finish_tree_kernel<K, T, 2>), dim3(nb), dim3(T), 0, stream, b, w.xyz_soa, w.flags,   \
-                       w.aok, w.verdict_words, w.tree);                                                       \
-  } while (0)
-#define CBFT_FINISH_TREE_CASE(K)                                       \
-  case -K:                                                             \
-    if (w.finish_tree_block == 0)                                      \
-      hipLaunchKernelGGL((ed25519_finish_wave_kernel<K>),              \
-                         dim3((unsigned)((b.n + (size_t)FINISH_WAVE_BLOCK * K - 1) / ((size_t)FINISH_WAVE_BLOCK * K))), \
-                         dim3(FINISH_WAVE_BLOCK), 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words); \
-    else if (w.tree && w.finish_tree_block == 128)                          \
-      CBFT_FINISH_SPLIT_LAUNCH(K, 128);                                \
-    else if (w.tree)                                                   \
-      CBFT_FINISH_SPLIT_LAUNCH(K, 64);                                 \
-    else if (w.finish_tree_block == 512)                               \
-      CBFT_FINISH_TREE_LAUNCH(K, 512);                                 \
-    else if (w.finish_tree_block == 256)                               \
-      CBFT_FINISH_TREE_LAUNCH(K, 256);                                 \
-    else if (w.finish_tree_block == 64)                                \
-      CBFT_FINISH_TREE_LAUNCH(K, 64);                                  \
-    else                                                               \
-      CBFT_FINISH_TREE_LAUNCH(K, 128);                                 \
-    break;
-    CBFT_FINISH_TREE_CASE(1)
-    CBFT_FINISH_TREE_CASE(2)
-    CBFT_FINISH_TREE_CASE(4)
-#undef CBFT_FINISH_TREE_CASE
-#undef CBFT_FINISH_SPLIT_LAUNCH
-#undef CBFT_FINISH_TREE_LAUNCH
-#define CBFT_FINISH_CASE(K)                                                                                     \
-  case K:                                                                                                       \
-    hipLaunchKernelGGL(ed25519_finish_batch_kernel<K>, dim3((unsigned)((b.n + 64 * K - 1) / (64 * K))), dim3(64), \
-                       0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words);                               \
-    break;
-    CBFT_FINISH_CASE(2)
-    CBFT_FINISH_CASE(4)
-    CBFT_FINISH_CASE(8)
-    CBFT_FINISH_CASE(16)
-    CBFT_FINISH_CASE(32)
-#undef CBFT_FINISH_CASE
-    default:
-      hipLaunchKernelGGL(ed25519_finish_kernel, grid, block, 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words);
-  }
+  if (w.finish_k == 2)
+    hipLaunchKernelGGL(ed25519_finish_kernel<2>, dim3((unsigned)((b.n + 2 * FINISH_LANES - 1) / (2 * FINISH_LANES))),
+                       dim3(FINISH_LANES), 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words);
+  else
+    hipLaunchKernelGGL(ed25519_finish_kernel<1>, dim3((unsigned)((b.n + FINISH_LANES - 1) / FINISH_LANES)),
+                       dim3(FINISH_LANES), 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words);
   if (ev) (void)hipEventRecord(ev[3], stream);
   return hipGetLastError();
 }

@@ -27,16 +27,6 @@
 #define RSA_KEY_P_R2 216
 #define RSA_KEY_P_R1 296
 #define RSA_KEY_P_N0INV 376
-#ifndef CBFT_RSA_MIN_WAVES
-#define CBFT_RSA_MIN_WAVES 2  // waves/SIMD the verify kernel is register-allocated for
-#endif
-#ifndef CBFT_RSA_PREFETCH
-#define CBFT_RSA_PREFETCH 1  // software-pipeline the LDS reads of x one limb group ahead
-#endif
-#ifndef CBFT_RSA_BLOCK
-#define CBFT_RSA_BLOCK 64  // one wave per block: LDS (16 KB) then admits 2 waves/SIMD at any mix
-#endif
-
 // One batch, all pointers in device memory.  Signature i is sig[256 i .. 256 i + 256), big-endian
 // (sig must be 4-byte aligned).
 struct RsaBatch {
@@ -53,8 +43,7 @@ struct RsaBatch {
 // Build key records from nkeys big-endian moduli (256 B each) and 32-bit public exponents.
 hipError_t cbft_rsa_launch_keys(const uint8_t* d_mod, const uint32_t* d_exp, uint32_t nkeys, uint32_t* d_keys,
                                 hipStream_t stream);
-// Verify a batch; writes ceil(n/64) verdict words.  d_scratch: RSA_LIMBS * round_up(n, block) words.
-// pair = 1: the lane-pair radix-2^28 kernel, 0: the one-lane FIOS kernel (same verdicts).
-hipError_t cbft_rsa_launch_verify(const RsaBatch& b, uint32_t* d_scratch, uint64_t* d_verdicts, hipStream_t stream,
-                                  int pair = 1);
+// Verify a batch (the lane-pair radix-2^28 kernel); writes ceil(n/64) verdict words.  d_scratch:
+// cbft_rsa_scratch_words(n) words.
+hipError_t cbft_rsa_launch_verify(const RsaBatch& b, uint32_t* d_scratch, uint64_t* d_verdicts, hipStream_t stream);
 size_t cbft_rsa_scratch_words(size_t n);

@@ -6,15 +6,11 @@
 // Verdict = ((s mod n)^e mod n == 00 01 FF.. 00 || DigestInfo(SHA-256) || SHA-256(m)), exactly as
 // oracle/rsa_ref.py restates it (s is not range-checked against n, as in Crypto++).
 //
-// Design: big-integer work with a 32-bit multiply at its core — no MFMA.  One lane
-// per signature; the 2048-bit operand b and the modulus stay in VGPRs for the whole
-// exponentiation (64 + 64 + 65 accumulator registers, two waves per SIMD), the row operand a_i is
-// read from LDS (this lane's own column, conflict-free) or, for the multiply by s, from a
-// coalesced [limb][signature] scratch array.  Montgomery products use the two-carry FIOS form:
-// per (i, j) two v_mad_u64_u32 with independent carry chains c1 (a*b) and c2 (m*n), so a row's
-// two chains interleave and a wave carries no cross-lane traffic at all.  Lanes of one wave may
-// hold different exponents (e = 17 replica keys next to e = 65537 client keys): the
-// square-and-multiply schedule runs over the wave's highest exponent bit and masks the
+// Design: big-integer work with a 32-bit multiply at its core — no MFMA.  Two lanes
+// per signature, radix 2^28 (rsa_verify_pair_kernel below): each Montgomery row is one
+// v_mad_u64_u32 per column for a*x and one for m*n with no per-column carry instructions.  Lanes
+// of one wave may hold different exponents (e = 17 replica keys next to e = 65537 client keys):
+// the square-and-multiply schedule runs over the wave's highest exponent bit and masks the
 // multiplies per lane.
 #include <hip/hip_runtime.h>
 
@@ -40,99 +36,6 @@ __device__ __forceinline__ uint32_t em_byte(int p) {
 __device__ __forceinline__ uint32_t em_limb(int k) {
   const int p = 252 - 4 * k;
   return (em_byte(p) << 24) | (em_byte(p + 1) << 16) | (em_byte(p + 2) << 8) | em_byte(p + 3);
-}
-
-// a * b + c on v_mad_u64_u32.  Inline asm keeps the compiler from hoisting zero-extended 64-bit
-// copies of the loop-invariant modulus limbs out of the row loop (they would need 64 more
-// registers and spill).
-__device__ __forceinline__ uint64_t mad64(uint32_t a, uint32_t b, uint64_t c) {
-  uint64_t r, carry_mask;
-  asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(r), "=s"(carry_mask) : "v"(a), "v"(b), "v"(c));
-  return r;
-}
-
-// a + b as a 64-bit value (carry in the high word).  The carry is materialised with
-// v_addc_co_u32 (VCC read as carry-in, no wait states) instead of the compiler's v_cndmask
-// (VCC read as a lane mask after a VALU write needs two wait states: 2 s_nop per product).
-__device__ __forceinline__ uint64_t add32x2(uint32_t a, uint32_t b) {
-  uint32_t lo, hi;
-  asm("v_add_co_u32 %0, vcc, %2, %3\n\tv_addc_co_u32 %1, vcc, 0, 0, vcc" : "=&v"(lo), "=v"(hi) : "v"(a), "v"(b) : "vcc");
-  return ((uint64_t)hi << 32) | lo;
-}
-
-// Montgomery product t = a * x * 2^-2048 mod n (fully reduced), written back into x for the lanes
-// with `take` set.  x lives in LDS in this lane's own column (xl[q][lane] holds limbs 4q..4q+3);
-// a(i) returns limb i of the row operand; the modulus stays in registers.
-template <class ARow>
-__device__ __forceinline__ void mont_mul(uint4 (*xl)[CBFT_RSA_BLOCK], uint32_t lane, const uint32_t (&nn)[L],
-                                         uint32_t n0inv, ARow a, bool take) {
-  uint32_t t[L + 1];
-#pragma unroll
-  for (int j = 0; j <= L; j++) t[j] = 0;
-  uint32_t a_next = a(0);
-#pragma unroll 1
-  for (int i = 0; i < L; i++) {
-    // keep the x limbs streaming from LDS row by row (hoisting them out of the loop would need
-    // 64 more VGPRs than a two-wave-per-SIMD budget has)
-    asm volatile("" ::: "memory");
-    const uint32_t ai = a_next;
-    if (i + 1 < L) a_next = a(i + 1);  // the next row operand (maybe a global load) overlaps this row
-    uint64_t c1 = 0, c2 = 0;
-    uint32_t m = 0;
-#if CBFT_RSA_PREFETCH
-    uint4 nxt = xl[0][lane];
-#endif
-#pragma unroll
-    for (int q = 0; q < L / 4; q++) {
-#if CBFT_RSA_PREFETCH
-      const uint4 b4 = nxt;  // x limbs 4q..4q+3; the next group's LDS read is in flight meanwhile
-      if (q + 1 < L / 4) nxt = xl[q + 1][lane];
-#else
-      const uint4 b4 = xl[q][lane];
-#endif
-      const uint32_t bv[4] = {b4.x, b4.y, b4.z, b4.w};
-#pragma unroll
-      for (int r = 0; r < 4; r++) {
-        const int j = 4 * q + r;
-        if (j == 0) {
-          const uint64_t X = mad64(ai, bv[0], add32x2(t[0], 0u));
-          m = (uint32_t)X * n0inv;
-          const uint64_t Y = mad64(m, nn[0], add32x2((uint32_t)X, 0u));  // low word is 0
-          c1 = X >> 32;
-          c2 = Y >> 32;
-        } else {
-          // X = ai b_j + t_j + c1 <= (2^32-1)^2 + 2 (2^32-1) = 2^64 - 1; two independent carry
-          // chains (a*b and m*n) per row
-          const uint64_t X = mad64(ai, bv[r], add32x2(t[j], (uint32_t)c1));
-          const uint64_t Y = mad64(m, nn[j], add32x2((uint32_t)X, (uint32_t)c2));
-          c1 = X >> 32;
-          c2 = Y >> 32;
-          t[j - 1] = (uint32_t)Y;
-        }
-      }
-    }
-    unsigned int k1, k2;
-    const uint32_t s1 = __builtin_addc(t[L], (uint32_t)c1, 0u, &k1);
-    t[L - 1] = __builtin_addc(s1, (uint32_t)c2, 0u, &k2);
-    t[L] = k1 + k2;
-  }
-  // t < 2n: subtract n once if t >= n.  First pass: the borrow only; second pass: select.
-  unsigned int br = 0;
-#pragma unroll
-  for (int j = 0; j < L; j++) (void)__builtin_subc(t[j], nn[j], br, &br);
-  const bool ge = t[L] != 0 || br == 0;
-  if (!take) return;
-  br = 0;
-#pragma unroll
-  for (int q = 0; q < L / 4; q++) {
-    uint32_t r[4];
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const uint32_t d = __builtin_subc(t[4 * q + k], nn[4 * q + k], br, &br);
-      r[k] = ge ? d : t[4 * q + k];
-    }
-    xl[q][lane] = make_uint4(r[0], r[1], r[2], r[3]);
-  }
 }
 
 __device__ __forceinline__ uint32_t load_be32(const uint8_t* p) {
@@ -235,113 +138,6 @@ __global__ void __launch_bounds__(64) rsa_keys_kernel(const uint8_t* mod, const 
   for (int i = RSA_KEY_P_N0INV + 1; i < RSA_KEY_WORDS; i++) rec[i] = 0;
 }
 
-// ---------------------------------------------------------------- verify ---------------------
-__global__ void __launch_bounds__(CBFT_RSA_BLOCK, CBFT_RSA_MIN_WAVES) rsa_verify_kernel(const RsaBatch b, uint32_t* scratch,
-                                                                    uint64_t* verdicts) {
-  __shared__ uint4 xl[L / 4][CBFT_RSA_BLOCK];  // the running operand x, [limb/4][lane] (conflict-free)
-  const uint32_t tid = threadIdx.x;
-  const size_t idx = (size_t)blockIdx.x * CBFT_RSA_BLOCK + tid;
-  const size_t stride = (size_t)gridDim.x * CBFT_RSA_BLOCK;  // scratch row pitch
-  const bool live = idx < b.n;
-  const size_t si = live ? idx : 0;
-  uint32_t kidx = b.key_idx[si];
-  bool ok = live && kidx < b.nkeys;
-  if (kidx >= b.nkeys) kidx = 0;
-  const uint32_t* rec = b.keys + (size_t)kidx * RSA_KEY_WORDS;
-
-  uint32_t nn[L];
-#pragma unroll
-  for (int q = 0; q < L / 4; q++) {
-    const uint4 v = *reinterpret_cast<const uint4*>(rec + RSA_KEY_N + 4 * q);
-    nn[4 * q] = v.x, nn[4 * q + 1] = v.y, nn[4 * q + 2] = v.z, nn[4 * q + 3] = v.w;
-    xl[q][tid] = *reinterpret_cast<const uint4*>(rec + RSA_KEY_R2 + 4 * q);  // x = R^2 mod n
-  }
-  const uint32_t n0inv = rec[RSA_KEY_N0INV];
-  const uint32_t e = ok ? rec[RSA_KEY_E] : 0u;
-  ok = ok && rec[RSA_KEY_OK];
-  const uint8_t* sg = b.sig + si * RSA_MOD_BYTES;
-
-  // The wave's highest exponent bit (lanes may hold different e).
-  int top = -1;
-  if (__ballot(e != 0)) {
-    for (int bit = 31; bit >= 0; bit--)
-      if (__ballot((e >> bit) & 1u)) {
-        top = bit;
-        break;
-      }
-  }
-  // One Montgomery-product call site drives the whole schedule (a single inlined copy):
-  //   CONV  sm = s * R^2 * R^-1 = s R        a = s (signature bytes), then sm -> scratch, x = R mod n
-  //   MUL   x = x * sm  (lanes with bit set)  a = sm (scratch, coalesced [limb][signature])
-  //   SQR   x = x * x                         a = x (LDS)
-  //   REDC  x = x * 1 * R^-1                  a = 1
-  enum { CONV, MUL, SQR, REDC };
-  int op = CONV, bit = top;
-  for (;;) {
-    const bool take = op != MUL || ((e >> bit) & 1u);
-    mont_mul(
-        xl, tid, nn, n0inv,
-        [&](int i) -> uint32_t {
-          if (op == MUL) return scratch[(size_t)i * stride + idx];
-          if (op == REDC) return i == 0 ? 1u : 0u;
-          if (op == CONV)  // limb i of s: big-endian word 63 - i of the (4-byte aligned) signature
-            return __builtin_bswap32(*reinterpret_cast<const uint32_t*>(sg + RSA_MOD_BYTES - 4 * (i + 1)));
-          const uint4 v = xl[i >> 2][tid];
-          const int r = i & 3;
-          return r == 0 ? v.x : r == 1 ? v.y : r == 2 ? v.z : v.w;
-        },
-        take);
-    if (op == REDC) break;
-    if (op == CONV) {
-      unsigned int br = 0;  // sm -> scratch; x = R mod n = 2^2048 - n (Montgomery 1)
-#pragma unroll
-      for (int q = 0; q < L / 4; q++) {
-        const uint4 v = xl[q][tid];
-        scratch[(size_t)(4 * q) * stride + idx] = v.x;
-        scratch[(size_t)(4 * q + 1) * stride + idx] = v.y;
-        scratch[(size_t)(4 * q + 2) * stride + idx] = v.z;
-        scratch[(size_t)(4 * q + 3) * stride + idx] = v.w;
-        uint32_t r[4];
-#pragma unroll
-        for (int k = 0; k < 4; k++) r[k] = __builtin_subc(0u, nn[4 * q + k], br, &br);
-        xl[q][tid] = make_uint4(r[0], r[1], r[2], r[3]);
-      }
-      op = top >= 0 ? MUL : REDC;  // the top bit is set in some lane: x = 1 * sm there
-      continue;
-    }
-    // after MUL or SQR at `bit`: square for the next bit, multiplying where it is set
-    if (op == SQR && __ballot((e >> bit) & 1u)) {
-      op = MUL;
-      continue;
-    }
-    if (bit == 0) {
-      op = REDC;
-      continue;
-    }
-    bit--;
-    op = SQR;
-  }
-
-  // SHA-256 of the message (PKCS1v15 encodes the digest; crypto_utils.cpp:103 SHA256)
-  uint32_t hw[8];
-  sha256_words(hw, b.msg + (live ? b.msg_off[si] : 0), live ? b.msg_len[si] : 0);
-
-  // compare x with the encoded digest
-  bool eq = true;
-#pragma unroll
-  for (int q = 0; q < L / 4; q++) {
-    const uint4 v = xl[q][tid];
-    const uint32_t xv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-      const int j = 4 * q + k;
-      eq = eq && xv[k] == (j < 8 ? hw[7 - j] : em_limb(j));
-    }
-  }
-  const uint64_t word = __ballot(ok && eq);
-  if ((tid & 63) == 0 && idx < b.n) verdicts[idx >> 6] = word;
-}
-
 
 // ---------------------------------------------------------------- lane-pair verify -----------
 // Two lanes per signature, radix 2^28 (74 limbs, R' = 2^2072 > 4n), lazy Montgomery (operands
@@ -349,7 +145,7 @@ __global__ void __launch_bounds__(CBFT_RSA_BLOCK, CBFT_RSA_MIN_WAVES) rsa_verify
 // the even lane ("L") holds positions 0..37, the odd lane ("H") 38..75, each with the modulus
 // limbs its columns meet.  A product of two limbs is < 2^56, so a column absorbs every one of its
 // <= 148 products without overflow: a row is exactly one v_mad_u64_u32 per column for a*x and one
-// for m*n — no per-column carry instructions (the one-lane 32-bit kernel needs four).  Two rows
+// for m*n — no per-column carry instructions (a 32-bit-limb FIOS form needs four).  Two rows
 // per iteration, then a two-column shift (the two columns crossing from H to L move with DPP);
 // m is computed in L and broadcast to H with DPP.  x (80 slots: slot 1 + j = limb j, slot 0 = 0)
 // lives in LDS per signature and is read once per row pair; the multiply-by-s operand streams
@@ -483,7 +279,7 @@ __global__ void __launch_bounds__(64, 2) rsa_verify_pair_kernel(const RsaBatch b
         break;
       }
   }
-  // schedule as in rsa_verify_kernel: CONV (s R'), MUL / SQR over the wave's top exponent bit, REDC
+  // schedule: CONV (s R'), MUL / SQR over the wave's top exponent bit, REDC
   enum { CONV, MUL, SQR, REDC };
   int op = CONV, bit = top;
   for (;;) {
@@ -574,11 +370,7 @@ __global__ void __launch_bounds__(64, 2) rsa_verify_pair_kernel(const RsaBatch b
 
 }  // namespace
 
-size_t cbft_rsa_scratch_words(size_t n) {
-  const size_t a = ((n + CBFT_RSA_BLOCK - 1) / CBFT_RSA_BLOCK) * CBFT_RSA_BLOCK * RSA_LIMBS;
-  const size_t b = ((n + PSIG - 1) / PSIG) * PSIG * RSA_NL;
-  return a > b ? a : b;
-}
+size_t cbft_rsa_scratch_words(size_t n) { return ((n + PSIG - 1) / PSIG) * PSIG * RSA_NL; }
 
 hipError_t cbft_rsa_launch_keys(const uint8_t* d_mod, const uint32_t* d_exp, uint32_t nkeys, uint32_t* d_keys,
                                 hipStream_t stream) {
@@ -587,16 +379,10 @@ hipError_t cbft_rsa_launch_keys(const uint8_t* d_mod, const uint32_t* d_exp, uin
   return hipGetLastError();
 }
 
-hipError_t cbft_rsa_launch_verify(const RsaBatch& b, uint32_t* d_scratch, uint64_t* d_verdicts, hipStream_t stream,
-                                  int pair) {
+hipError_t cbft_rsa_launch_verify(const RsaBatch& b, uint32_t* d_scratch, uint64_t* d_verdicts, hipStream_t stream) {
   if (!b.n) return hipSuccess;
-  if (pair) {
-    const unsigned blocks = (unsigned)((b.n + PSIG - 1) / PSIG);
-    hipLaunchKernelGGL(rsa_verify_pair_kernel, dim3(blocks), dim3(64), 0, stream, b, d_scratch,
-                       reinterpret_cast<uint32_t*>(d_verdicts));
-  } else {
-    const unsigned blocks = (unsigned)((b.n + CBFT_RSA_BLOCK - 1) / CBFT_RSA_BLOCK);
-    hipLaunchKernelGGL(rsa_verify_kernel, dim3(blocks), dim3(CBFT_RSA_BLOCK), 0, stream, b, d_scratch, d_verdicts);
-  }
+  const unsigned blocks = (unsigned)((b.n + PSIG - 1) / PSIG);
+  hipLaunchKernelGGL(rsa_verify_pair_kernel, dim3(blocks), dim3(64), 0, stream, b, d_scratch,
+                     reinterpret_cast<uint32_t*>(d_verdicts));
   return hipGetLastError();
 }

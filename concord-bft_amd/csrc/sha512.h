@@ -43,15 +43,12 @@ __device__ __forceinline__ uint64_t rotr64(uint64_t x) {
 // gfx950 v_bitop3_b32: any 3-input boolean function in one instruction; the truth table is
 // indexed by (S0, S1, S2) with S0 <-> 0xf0, S1 <-> 0xcc, S2 <-> 0xaa (0x96 = xor3, 0xe8 = majority,
 // 0xca = S0 ? S1 : S2).  The compiler does not form it from a ^ b ^ c by itself.
-#ifndef CBFT_SHA_PAIR_PIN
-#define CBFT_SHA_PAIR_PIN 1
-#endif
 template <uint32_t T>
 __device__ __forceinline__ uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
   const uint32_t lo = __builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, T);
   const uint32_t hi = __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), T);
   uint64_t r = ((uint64_t)hi << 32) | lo;
-#if CBFT_SHA_PAIR_PIN && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
   // one 64-bit value in a register pair: otherwise LLVM splits the following 64-bit adds into
   // zero-extended halves (~6 v_mov + 4 extra v_lshl_add_u64 per 16 rounds' schedule words)
   asm("" : "+v"(r));
@@ -76,102 +73,7 @@ __device__ __forceinline__ uint64_t shr64(uint64_t x) {
     h = t1_ + S0_ + mj_;                                                                  \
   } while (0)
 
-#ifndef CBFT_SHA_PAIRS
-#define CBFT_SHA_PAIRS 0
-#endif
 
-#if CBFT_SHA_PAIRS
-// The compression function on explicit 32-bit halves: 64-bit adds as v_add_co_u32 +
-// v_addc_co_u32 (__builtin_addc), rotates as v_alignbit_b32 pairs, 3-input logic as v_bitop3_b32.
-// Kept apart from uint64_t so that LLVM does not re-form 64-bit values: its v_lshl_add_u64 adds
-// need aligned register pairs, which cost ~95 v_mov per 16 rounds once the halves come from
-// separate bitop3 results.
-struct Sha64 {
-  uint32_t lo, hi;
-};
-__device__ __forceinline__ Sha64 sha_split(uint64_t x) { return {(uint32_t)x, (uint32_t)(x >> 32)}; }
-__device__ __forceinline__ uint64_t sha_join(Sha64 x) { return ((uint64_t)x.hi << 32) | x.lo; }
-__device__ __forceinline__ Sha64 sha_add(Sha64 a, Sha64 b) {
-  unsigned c, c2;
-  Sha64 r;
-  r.lo = __builtin_addc(a.lo, b.lo, 0u, &c);
-  r.hi = __builtin_addc(a.hi, b.hi, c, &c2);
-  return r;
-}
-template <int N>
-__device__ __forceinline__ Sha64 sha_rotr(Sha64 x) {
-  if (N < 32) return {__builtin_amdgcn_alignbit(x.hi, x.lo, N), __builtin_amdgcn_alignbit(x.lo, x.hi, N)};
-  return {__builtin_amdgcn_alignbit(x.lo, x.hi, N - 32), __builtin_amdgcn_alignbit(x.hi, x.lo, N - 32)};
-}
-template <int N>
-__device__ __forceinline__ Sha64 sha_shr(Sha64 x) {
-  return {__builtin_amdgcn_alignbit(x.hi, x.lo, N), x.hi >> N};
-}
-template <uint32_t T>
-__device__ __forceinline__ Sha64 sha_bop3(Sha64 a, Sha64 b, Sha64 c) {
-  return {(uint32_t)__builtin_amdgcn_bitop3_b32(a.lo, b.lo, c.lo, T),
-          (uint32_t)__builtin_amdgcn_bitop3_b32(a.hi, b.hi, c.hi, T)};
-}
-
-#define SHA512P_ROUND(a, b, c, d, e, f, g, h, k, w)                                                  \
-  do {                                                                                              \
-    const Sha64 S1_ = sha_bop3<0x96>(sha_rotr<14>(e), sha_rotr<18>(e), sha_rotr<41>(e));            \
-    const Sha64 ch_ = sha_bop3<0xca>(e, f, g);                                                      \
-    const Sha64 t1_ = sha_add(sha_add(h, sha_add((k), (w))), sha_add(S1_, ch_));                   \
-    const Sha64 S0_ = sha_bop3<0x96>(sha_rotr<28>(a), sha_rotr<34>(a), sha_rotr<39>(a));            \
-    const Sha64 mj_ = sha_bop3<0xe8>(a, b, c);                                                      \
-    d = sha_add(d, t1_);                                                                            \
-    h = sha_add(t1_, sha_add(S0_, mj_));                                                            \
-  } while (0)
-
-__device__ __forceinline__ void sha512_compress(uint64_t* H, uint64_t* W64) {
-  Sha64 W[16];
-#pragma unroll
-  for (int j = 0; j < 16; j++) W[j] = sha_split(W64[j]);
-  Sha64 a = sha_split(H[0]), b = sha_split(H[1]), c = sha_split(H[2]), d = sha_split(H[3]);
-  Sha64 e = sha_split(H[4]), f = sha_split(H[5]), g = sha_split(H[6]), h = sha_split(H[7]);
-#pragma unroll
-  for (int j = 0; j < 16; j += 8) {
-    SHA512P_ROUND(a, b, c, d, e, f, g, h, sha_split(kSha512K[j + 0]), W[j + 0]);
-    SHA512P_ROUND(h, a, b, c, d, e, f, g, sha_split(kSha512K[j + 1]), W[j + 1]);
-    SHA512P_ROUND(g, h, a, b, c, d, e, f, sha_split(kSha512K[j + 2]), W[j + 2]);
-    SHA512P_ROUND(f, g, h, a, b, c, d, e, sha_split(kSha512K[j + 3]), W[j + 3]);
-    SHA512P_ROUND(e, f, g, h, a, b, c, d, sha_split(kSha512K[j + 4]), W[j + 4]);
-    SHA512P_ROUND(d, e, f, g, h, a, b, c, sha_split(kSha512K[j + 5]), W[j + 5]);
-    SHA512P_ROUND(c, d, e, f, g, h, a, b, sha_split(kSha512K[j + 6]), W[j + 6]);
-    SHA512P_ROUND(b, c, d, e, f, g, h, a, sha_split(kSha512K[j + 7]), W[j + 7]);
-  }
-#pragma nounroll
-  for (int r = 16; r < 80; r += 16) {
-#pragma unroll
-    for (int j = 0; j < 16; j++) {
-      const Sha64 w15 = W[(j + 1) & 15], w2 = W[(j + 14) & 15];
-      const Sha64 s0 = sha_bop3<0x96>(sha_rotr<1>(w15), sha_rotr<8>(w15), sha_shr<7>(w15));
-      const Sha64 s1 = sha_bop3<0x96>(sha_rotr<19>(w2), sha_rotr<61>(w2), sha_shr<6>(w2));
-      W[j] = sha_add(sha_add(W[j], s0), sha_add(W[(j + 9) & 15], s1));
-    }
-#pragma unroll
-    for (int j = 0; j < 16; j += 8) {
-      SHA512P_ROUND(a, b, c, d, e, f, g, h, sha_split(kSha512K[r + j + 0]), W[j + 0]);
-      SHA512P_ROUND(h, a, b, c, d, e, f, g, sha_split(kSha512K[r + j + 1]), W[j + 1]);
-      SHA512P_ROUND(g, h, a, b, c, d, e, f, sha_split(kSha512K[r + j + 2]), W[j + 2]);
-      SHA512P_ROUND(f, g, h, a, b, c, d, e, sha_split(kSha512K[r + j + 3]), W[j + 3]);
-      SHA512P_ROUND(e, f, g, h, a, b, c, d, sha_split(kSha512K[r + j + 4]), W[j + 4]);
-      SHA512P_ROUND(d, e, f, g, h, a, b, c, sha_split(kSha512K[r + j + 5]), W[j + 5]);
-      SHA512P_ROUND(c, d, e, f, g, h, a, b, sha_split(kSha512K[r + j + 6]), W[j + 6]);
-      SHA512P_ROUND(b, c, d, e, f, g, h, a, sha_split(kSha512K[r + j + 7]), W[j + 7]);
-    }
-  }
-  H[0] = sha_join(sha_add(sha_split(H[0]), a));
-  H[1] = sha_join(sha_add(sha_split(H[1]), b));
-  H[2] = sha_join(sha_add(sha_split(H[2]), c));
-  H[3] = sha_join(sha_add(sha_split(H[3]), d));
-  H[4] = sha_join(sha_add(sha_split(H[4]), e));
-  H[5] = sha_join(sha_add(sha_split(H[5]), f));
-  H[6] = sha_join(sha_add(sha_split(H[6]), g));
-  H[7] = sha_join(sha_add(sha_split(H[7]), h));
-}
-#else
 // Rounds 0-15 straight from the block, then 4 x 16 rounds with the message schedule in a
 // 16-word ring (no data-dependent control flow: an `if (r > 0)` inside the unrolled window
 // made the compiler copy the whole ring every round).  The 8 working variables rotate by
@@ -219,7 +121,6 @@ __device__ __forceinline__ void sha512_compress(uint64_t* H, uint64_t* W) {
   H[6] += g;
   H[7] += h;
 }
-#endif  // CBFT_SHA_PAIRS
 
 // The compression function in two halves that two waves can run: sha512_schedule_kw expands a
 // block's 16 words into kw[t] = K[t] + W[t], t = 0..79 (one wave writes them to LDS), and

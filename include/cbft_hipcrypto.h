@@ -77,6 +77,31 @@ int cbft_open_devices(cbft_ctx** out, const int* devices, int ndevices, size_t m
 int cbft_device_of(cbft_ctx* ctx, int* out_devices, int max_out);
 void cbft_close(cbft_ctx* ctx);
 
+/* ---------------------------------------------------------------- tuning ------------------
+ * Every kernel a context runs is the measured default; nothing in the process environment
+ * selects another kernel.  The environment variables the library and its C++ plugin layer read
+ * are all here:
+ *   CBFT_COMB_BUDGET_GB   HBM budget of one Ed25519 key table's comb tables (default 64 GB):
+ *                         picks the widest comb radix of 13 / 11 / 8 that fits (cbft_ed25519_load_keys)
+ *   CBFT_COMB_RADIX       a fixed comb radix 8..15 instead
+ *   CBFT_DEVICE           the GPU the C++ verifiers open (host layer; default 0)
+ *   CBFT_ENGINE_INFLIGHT  per-request engine: coalesced batches in flight (host layer)
+ *   CBFT_ENGINE_SPIN_US   per-request engine: waiter spin before sleeping (host layer; default 0)
+ *   CBFT_EXPECTED_KEYS    key-table sizing hint of the C++ SigManager (host layer)
+ * Geometry and scheduling switches that tests exercise on purpose (both ladder layouts, other B
+ * comb radices, the three-kernel path at small sizes, ...) are per-context options, set after
+ * cbft_open and before the first batch that should use them; a multi-GPU context applies them
+ * to every device.  CBFT_EINVAL for an unknown option or an out-of-range value. */
+#define CBFT_OPT_LADDER_LANES 1     /* comb ladder lanes per signature: 0 = by batch (2 from 32K, else 4), 2, 4 */
+#define CBFT_OPT_B_RADIX 2          /* radix of B's comb table, 16..26 (default 22); rebuilds it, synchronously */
+#define CBFT_OPT_WORK_SLOTS 3       /* work-buffer slots big batches rotate over, 1..8 (default 4) */
+#define CBFT_OPT_SMALL_MAX 4        /* key-table batches up to this size run as one fused launch (default 1024; 0 = never) */
+#define CBFT_OPT_SHA_SORT_MIN 5     /* variable-length batches from this size hash in SHA-block-count order (4096; 0 = never) */
+#define CBFT_OPT_STAGE_ORDER 6      /* cross-batch stage order of big batches: 0 off, 1 hash + ladder (default), 2 ladder only */
+#define CBFT_OPT_HASH_ORDER_EARLY 7 /* the next batch's hash waits for the short-message hash only (default 1) */
+#define CBFT_OPT_FINISH_K 8         /* signatures per finish lane: 0 = by batch (2 from 16K, else 1), 1, 2 */
+int cbft_set_option(cbft_ctx* ctx, int option, int64_t value);
+
 /* Page-locked host memory, DMA-able by every device.  A caller that builds its batches directly
  * in such memory (signatures, key indices, the message blob) saves the host copy: the
  * host-buffer entry points move any input lying inside a cbft_host_alloc block to the GPU with

@@ -71,14 +71,14 @@ def test_golden_key_table_radix(ctx, golden, radix):
 
 @pytest.mark.parametrize("b_radix", [16, 17, 20, 24, 26])
 @pytest.mark.parametrize("radix", [8, 13])
-def test_golden_base_table_radix(golden, monkeypatch, b_radix, radix):
-    """B's comb radix ($CBFT_B_RADIX; the default 22 is covered above): the ladder's lane split
+def test_golden_base_table_radix(golden, b_radix, radix):
+    """B's comb radix (CBFT_OPT_B_RADIX; the default 22 is covered above): the ladder's lane split
     changes with it (radix-2^13 keys: 9 additions per lane at B radix 16, 9 at 17, 9 at 20, 8 at 22,
     8 at 24, 8 at 26; radix 26 is a 42.9 GB table of 10 positions)."""
-    monkeypatch.setenv("CBFT_B_RADIX", str(b_radix))
     keys = sorted({v.pk for v in golden})
     index = {k: i for i, k in enumerate(keys)}
     with cb.Context(device=0) as c:
+        c.set_option(cb.OPT_B_RADIX, b_radix)
         tid = c.load_keys(keys, radix=radix)
         n = len(golden)
         got = _bools(c.verify(tid, [index[v.pk] for v in golden], [v.sig for v in golden],
@@ -88,12 +88,12 @@ def test_golden_base_table_radix(golden, monkeypatch, b_radix, radix):
 
 
 @pytest.mark.parametrize("b_radix", [24, 26])
-def test_pair_ladder_wide_base_table(monkeypatch, b_radix):
+def test_pair_ladder_wide_base_table(b_radix):
     """The pair ladder (batches from 32K) over B radix 2^24 / 2^26: 31 / 30 additions dealt to two
     lanes (16 / 15 each), 10 % invalid signatures, verdicts equal to OpenSSL's."""
-    monkeypatch.setenv("CBFT_B_RADIX", str(b_radix))
     ss = sigsets.make_sigset(40000, nkeys=64, msg_len=256, seed=0xB26 + b_radix, invalid_frac=0.1)
     with cb.Context(device=0, max_batch=40000) as c:
+        c.set_option(cb.OPT_B_RADIX, b_radix)
         tid = c.load_keys(ss.pk, radix=13)
         got = _bools(c.verify_packed(tid, ss.key_idx, ss.sig, ss.blob, ss.off, ss.len), 40000)
     assert np.array_equal(got, ss.expected), np.nonzero(got != ss.expected)[0][:10]
@@ -213,23 +213,23 @@ def test_fresh_context_without_presizing(golden):
         assert np.array_equal(got, np.array([bool(v.verdict) for v in vs]))
 
 
-@pytest.mark.parametrize("k,tree_block,split", [(1, 64, 0), (2, 64, 0), (4, 64, 0), (8, 64, 0), (16, 64, 0),
-                                                (32, 64, 0), (-1, 128, 0), (-2, 128, 0), (-4, 128, 0), (-2, 64, 0),
-                                                (-2, 256, 0), (-1, 512, 0), (-2, 512, 0), (-1, 64, 1), (-2, 64, 1),
-                                                (-4, 64, 1), (-2, 128, 1), (-1, 0, 0), (-2, 0, 0),
-                                                (-4, 0, 0)])
-def test_finish_inversion_batching(golden, monkeypatch, k, tree_block, split):
-    # K4' shares one inversion among K signatures per lane (Montgomery's trick); rejected items
-    # (S >= L, undecodable A) enter the product as 1.  K < 0: the tree finish (one inversion per
-    # block of tree_block lanes, |K| signatures per lane: 64 .. 2,048 signatures per block; split:
-    # the block trees go through HBM and one lane per block root inverts them; tree_block 0: the
-    # wave-butterfly tree, four waves per inversion).  Every K
-    # must give the golden verdicts, including the ragged last block (1,145 vectors is not a
-    # multiple of 64 K).
-    monkeypatch.setenv("CBFT_FINISH_BATCH", str(k))
-    monkeypatch.setenv("CBFT_FINISH_TREE_BLOCK", str(tree_block))
-    monkeypatch.setenv("CBFT_FINISH_SPLIT", str(split))
+@pytest.mark.parametrize("k", [1, 2])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 127, 128, 129, 1145])
+def test_finish_tree_both_forms(golden, k, n):
+    # The tree finish: one inversion per block of 64 lanes x K signatures (Montgomery's trick over
+    # an LDS product tree, the root inverted on the scalar unit); rejected items (S >= L,
+    # undecodable A) enter the product as 1.  Both K (1 below 16K signatures, 2 from 16K) on the
+    # golden set and its prefixes: partial blocks, a lone lane, a block boundary +- 1.
+    sub = golden[:n]
     with cb.Context(device=0) as c:
+        c.set_option(cb.OPT_FINISH_K, k)
+        got = _bools(c.verify_pk([v.pk for v in sub], [v.sig for v in sub], [v.msg for v in sub]), len(sub))
+    assert np.array_equal(got, np.array([bool(v.verdict) for v in sub]))
+
+
+def test_finish_k2_full_golden(golden):
+    with cb.Context(device=0) as c:
+        c.set_option(cb.OPT_FINISH_K, 2)
         got = _bools(c.verify_pk([v.pk for v in golden], [v.sig for v in golden], [v.msg for v in golden]),
                      len(golden))
     assert np.array_equal(got, np.array([bool(v.verdict) for v in golden]))
@@ -279,11 +279,10 @@ class _Hip:
 
 
 @pytest.mark.parametrize("order", ["1", "0"])
-def test_device_path_two_streams_stage_order(monkeypatch, order):
+def test_device_path_two_streams_stage_order(order):
     # the bench's schedule: device-resident batches alternating over two streams, the library's
     # cross-batch stage order (hash after hash, ladder after ladder) and two rotating work slots.
     # Batches with different corruption patterns must each keep their own verdicts.
-    monkeypatch.setenv("CBFT_STAGE_ORDER", order)
     hip = _Hip()
     n = 65536
     nwords = (n + 63) // 64
@@ -298,6 +297,7 @@ def test_device_path_two_streams_stage_order(monkeypatch, order):
         variants.append((hip.to_dev(sig.reshape(-1)), exp))
     try:
         with cb.Context(device=0, max_batch=n) as c:
+            c.set_option(cb.OPT_STAGE_ORDER, int(order))
             tid = c.load_keys(base.pk)
             d_kidx = hip.to_dev(base.key_idx)
             d_blob = hip.to_dev(base.blob)
@@ -317,14 +317,12 @@ def test_device_path_two_streams_stage_order(monkeypatch, order):
 
 
 @pytest.mark.parametrize("streams,slots,early", [(4, 4, "1"), (4, 4, "0"), (3, 2, "1"), (2, 4, "1")])
-def test_device_path_mixed_lengths_many_streams(monkeypatch, streams, slots, early):
+def test_device_path_mixed_lengths_many_streams(streams, slots, early):
     # config #3's device-resident schedule: variable-length batches (sorted hash, long-message
     # tail on the slot's aux stream) over several streams and work slots; with
-    # CBFT_HASH_ORDER_EARLY the next batch's hash waits only for this batch's short hashes.  Every
+    # CBFT_OPT_HASH_ORDER_EARLY the next batch's hash waits only for this batch's short hashes.  Every
     # batch keeps its own verdicts (different corruption per batch, a slot reused while the
     # previous tail may still run).
-    monkeypatch.setenv("CBFT_WORK_SLOTS", str(slots))
-    monkeypatch.setenv("CBFT_HASH_ORDER_EARLY", early)
     hip = _Hip()
     n = 16384
     nwords = (n + 63) // 64
@@ -339,6 +337,7 @@ def test_device_path_mixed_lengths_many_streams(monkeypatch, streams, slots, ear
         variants.append((hip.to_dev(sig.reshape(-1)), exp))
     try:
         with cb.Context(device=0, max_batch=n) as c:
+            c.set_option(cb.OPT_WORK_SLOTS, slots).set_option(cb.OPT_HASH_ORDER_EARLY, int(early))
             tid = c.load_keys(base.pk)
             d_kidx = hip.to_dev(base.key_idx)
             d_blob = hip.to_dev(base.blob)
@@ -379,15 +378,14 @@ def test_per_batch_profiling_ring(golden):
 
 
 @pytest.mark.parametrize("radix,b_radix", [(8, 22), (11, 22), (13, 16), (13, 22), (15, 22), (14, 24)])
-def test_pair_ladder_golden_geometries(golden, monkeypatch, radix, b_radix):
+def test_pair_ladder_golden_geometries(golden, radix, b_radix):
     """The pair ladder over the golden set at several key / B comb geometries: each lane's first
-    addition is a point set from the identity (CBFT_LADDER_FIRST_SET), whichever table (a key
-    position or B) and digit sign (including the identity entry of a zero digit) it starts on."""
-    monkeypatch.setenv("CBFT_LADDER_LANES", "2")
-    monkeypatch.setenv("CBFT_B_RADIX", str(b_radix))
+    addition is a point set from the identity, whichever table (a key position or B) and digit
+    sign (including the identity entry of a zero digit) it starts on."""
     keys = sorted({v.pk for v in golden})
     index = {k: i for i, k in enumerate(keys)}
     with cb.Context(device=0) as c:
+        c.set_option(cb.OPT_LADDER_LANES, 2).set_option(cb.OPT_B_RADIX, b_radix)
         tid = c.load_keys(keys, radix=radix)
         got = _bools(c.verify(tid, [index[v.pk] for v in golden], [v.sig for v in golden],
                               [v.msg for v in golden]), len(golden))
@@ -396,13 +394,13 @@ def test_pair_ladder_golden_geometries(golden, monkeypatch, radix, b_radix):
 
 
 @pytest.mark.parametrize("lanes", ["2", "4"])
-def test_ladder_layouts_both_sizes(golden, monkeypatch, lanes):
-    """Each comb-ladder layout ($CBFT_LADDER_LANES) at the sizes the default does not pick it for:
-    the pair ladder on the small golden batch, the quad ladder on a 64K batch."""
-    monkeypatch.setenv("CBFT_LADDER_LANES", lanes)
+def test_ladder_layouts_both_sizes(golden, lanes):
+    """Each comb-ladder layout (CBFT_OPT_LADDER_LANES) at the sizes the default does not pick it
+    for: the pair ladder on the small golden batch, the quad ladder on a 64K batch."""
     keys = sorted({v.pk for v in golden})
     index = {k: i for i, k in enumerate(keys)}
     with cb.Context(device=0, max_batch=1 << 16) as c:
+        c.set_option(cb.OPT_LADDER_LANES, int(lanes))
         tid = c.load_keys(keys)
         got = _bools(c.verify(tid, [index[v.pk] for v in golden], [v.sig for v in golden],
                               [v.msg for v in golden]), len(golden))
@@ -429,18 +427,14 @@ def test_config3_full_shape(ctx):
 
 @pytest.mark.parametrize("chunk", [1, 15, 16, 17, 64, 65, 300, 1024])
 def test_golden_small_batches_fused_kernel(ctx, golden, chunk):
-    """Key-table batches up to 1,024 signatures run as ONE fused launch (ed25519_small_kernel:
-    hash + quad comb + finish, 16 signatures per wave, 16-bit verdict words): the golden set in
-    batches of `chunk` gives the golden verdicts, equal to the three-kernel path
-    ($CBFT_SMALL_MAX=0) batch for batch, including partial words and tail quads."""
+    """Key-table batches up to 1,024 signatures run as ONE fused launch (ed25519_small3_kernel:
+    hash + quad comb + R decode on four waves, 8 signatures per block, 8-bit verdict pieces): the
+    golden set in batches of `chunk` gives the golden verdicts, equal to the three-kernel path
+    (CBFT_OPT_SMALL_MAX = 0) batch for batch, including partial words and tail quads."""
     keys = sorted({v.pk for v in golden})
     index = {k: i for i, k in enumerate(keys)}
     exp = np.array([bool(v.verdict) for v in golden])
-    os.environ["CBFT_SMALL_MAX"] = "0"
-    try:
-        three = cb.Context(device=0)
-    finally:
-        del os.environ["CBFT_SMALL_MAX"]
+    three = cb.Context(device=0).set_option(cb.OPT_SMALL_MAX, 0)
     tid, tid3 = ctx.load_keys(keys), three.load_keys(keys)
     try:
         for lo in range(0, len(golden), chunk):
@@ -554,7 +548,7 @@ def test_fixed_device_64k_streams_planted_invalid(streams):
 
 
 @pytest.mark.parametrize("n", [1, 100, 257, 5000])
-def test_hash_block_count_sort(golden, n, monkeypatch):
+def test_hash_block_count_sort(golden, n):
     """Variable-length batches hash in order of their SHA-512 block count (a counting sort into a
     permutation before K1; a batch whose messages share one block count keeps the identity order):
     verdicts equal OpenSSL's and the unsorted path's for every signature, across ragged sizes and
@@ -564,22 +558,22 @@ def test_hash_block_count_sort(golden, n, monkeypatch):
     vs = [golden[i % len(golden)] for i in range(n)]
     args = ([index[v.pk] for v in vs], [v.sig for v in vs], [v.msg for v in vs])
     exp = np.array([bool(v.verdict) for v in vs])
-    monkeypatch.setenv("CBFT_SMALL_MAX", "0")  # the three-kernel path, where the sort runs
     out = {}
-    for label, sort_min in (("sorted", "1"), ("unsorted", "0")):
-        monkeypatch.setenv("CBFT_SHA_SORT_MIN", sort_min)
+    for label, sort_min in (("sorted", 1), ("unsorted", 0)):
         with cb.Context(device=0) as c:
+            # the three-kernel path, where the sort runs
+            c.set_option(cb.OPT_SMALL_MAX, 0).set_option(cb.OPT_SHA_SORT_MIN, sort_min)
             tid = c.load_keys(keys)
             out[label] = _bools(c.verify(tid, *args), n)
             # a second batch through the same work slot: the bucket counters were reset
             out[label + "2"] = _bools(c.verify(tid, *args), n)
     for k, v in out.items():
         assert np.array_equal(v, exp), k
-    monkeypatch.setenv("CBFT_SHA_SORT_MIN", "1")
     # random lengths, then one length for all (every signature in one bucket: the identity order)
     for msg_len in ((1, 4096), 200):
         ss = sigsets.make_sigset(n, nkeys=16, msg_len=msg_len, seed=77 + n, invalid_frac=0.1)
         with cb.Context(device=0) as c:
+            c.set_option(cb.OPT_SMALL_MAX, 0).set_option(cb.OPT_SHA_SORT_MIN, 1)
             tid = c.load_keys(ss.pk)
             got = _bools(c.verify_packed(tid, ss.key_idx, ss.sig, ss.blob, ss.off, ss.len), n)
             got2 = _bools(c.verify_packed(tid, ss.key_idx, ss.sig, ss.blob, ss.off, ss.len), n)
@@ -587,13 +581,10 @@ def test_hash_block_count_sort(golden, n, monkeypatch):
         assert np.array_equal(got2, ss.expected), msg_len
 
 
-@pytest.mark.parametrize("waves", [2, 3])
 @pytest.mark.parametrize("chunk", [1, 17, 300, 1024])
-def test_golden_small_batches_three_wave_kernel(golden, chunk, waves, monkeypatch):
-    """$CBFT_SMALL_WAVES=3 (the default): the fused kernel with [S]B on its own wave beside the hash
-    and [h](-A) wave and the R-decode waves; 2: both sums on one wave.  Each gives the golden
-    verdicts batch for batch, partial words and tail quads included."""
-    monkeypatch.setenv("CBFT_SMALL_WAVES", str(waves))
+def test_golden_small_batches_three_wave_kernel(golden, chunk):
+    """The fused kernel with [S]B on its own wave beside the hash and [h](-A) wave and the R-decode
+    waves gives the golden verdicts batch for batch, partial words and tail quads included."""
     keys = sorted({v.pk for v in golden})
     index = {k: i for i, k in enumerate(keys)}
     exp = np.array([bool(v.verdict) for v in golden])
