@@ -488,6 +488,24 @@ BN_HDN void fp_inv_var(fp& r, const fp& a) {
   f_mul(r, y, r3);  // A^-1 R^3 / R = a^-1 R
 }
 
+#if defined(__HIP_DEVICE_COMPILE__)
+// the same for a value every lane of the wave holds, the whole wave active (a pairing check's
+// norm): safegcd30.h sg_inv30_var_wave -- scalar divsteps, lane-parallel limb updates
+__device__ __forceinline__ void fp_inv_var_wave(fp& r, const fp& a) {
+  fp c = a;
+  f_canon(c);
+  Sg30 x;
+  sg_from_limbs29(x, c.v);
+  sg_inv30_var_wave<BnS30Mod>(x);
+  fp y;
+  sg_to_limbs29(y.v, x);
+  fp r3;
+#pragma unroll
+  for (int i = 0; i < 9; i++) r3.v[i] = BnS30Mod::R3[i];
+  f_mul(r, y, r3);
+}
+#endif
+
 BN_HDN void fr_inv(fr& r, const fr& a) {
   uint32_t e[8];
 #pragma unroll

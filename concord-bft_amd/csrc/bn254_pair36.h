@@ -484,7 +484,18 @@ __device__ __noinline__ void p36_inv(fp& r, const fp& x, const P36& g) {
     fp2_add(u, R0, R1);
     fp2_mul_xi(u, u);
     fp2_add(nn, R2, u);
-    fp2_inv<true>(nn, nn);
+    {  // nn^-1: every lane holds nn (gathered from lanes 0..2), so the Fp inversion is the wave form
+      fp n2, t2;
+      f_sqr(n2, nn.a);
+      f_sqr(t2, nn.b);
+      f_add(n2, n2, t2);
+#if defined(__HIP_DEVICE_COMPILE__)
+      fp_inv_var_wave(n2, n2);
+#endif
+      f_mul(nn.a, nn.a, n2);
+      f_mul(t2, nn.b, n2);
+      f_neg(nn.b, t2);
+    }
     // this lane's coefficient of the inverse: t_(k/2) N^-1 (k odd: unused)
     fp2 tk = t0;
     p12_sel2(tk, t1, g.k == 2 || g.k == 3);

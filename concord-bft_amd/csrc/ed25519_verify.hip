@@ -618,141 +618,141 @@ __global__ void __launch_bounds__(CBFT_VERIFY_BLOCK, CBFT_LADDER_MIN_WAVES)
 // ---------------------------------------------------------------------------------------
 // K4: encode R' = (X : Y : Z) and compare it with R; verdict ballot per wave.
 //
-// One field inversion per block of FINISH_LANES lanes x K signatures (Montgomery's trick over a
-// product tree; R' is public, so the inversion is the variable-time safegcd):
-//   leaf   l = prod of lane l's K Z's (signatures already rejected -- S >= L, A not decodable --
-//          and Z = 0 enter as 1, so they cannot disturb their neighbours' inverses),
-//   up     a product tree over the block's lanes in LDS (heap: root 1, leaves T .. 2T - 1),
-//   root   inverted ONCE per block, on the scalar unit: every lane reads the root, the limbs are
-//          made wave-uniform (readfirstlane) and the safegcd chain compiles to SALU code
-//          (fe_invert_var<true>): ~17.5 K scalar instructions, ~40 of the kernel's ~51 us, while
-//          the SIMDs' vector pipes stay free for the other streams' ladders (the same chain on
-//          the VALU, every lane running it: 2 % slower alone and 5 % slower in the 3-stream
-//          pipeline, tools/probes/r06_ab2.sh),
-//   down   each node's inverse becomes its children's: 1/L = inv * R, 1/R = inv * L (in place),
-//   lane   1/Z_j from the leaf's inverse and the lane's prefix products; x = X/Z, y = Y/Z, encode,
-//          compare with R, ballot.
-// Per signature ~3.5 M of tree + 2 M + an encode.  K = 2 from 16K signatures (512 one-wave blocks
-// at 64K: the finish co-runs with the other streams' ladders, whose 1,024 blocks of 36 KB fill a
-// 64K batch's LDS, and a one-wave block's 4.6 KB of tree fits beside them), K = 1 below.
+// One field inversion per block of 64 lanes x K signatures (Montgomery's trick; R' is public, so
+// the inversion is the variable-time safegcd), on TWO waves so that one product follows it.  Lane t
+// of each wave sees the same K signatures (i = base + j 64 + t) and forms the same leaf
+// L_t = prod_j Z_j (signatures already rejected -- S >= L, A not decodable -- and Z = 0 enter as
+// 1, so they cannot disturb their neighbours' inverses).
+//   wave 0  root = prod_t L_t by a 6-level butterfly (__shfl_xor), inverted by the whole wave
+//           (fe_invert_var<true>: safegcd30.h sg_inv30_var_wave, the divsteps on the scalar unit,
+//           the limb updates lane-parallel with DPP neighbour exchanges; ~18 us of the kernel, the
+//           scalar-unit chain it replaced 31 us), published in LDS;
+//   wave 1  meanwhile the cofactor of every signature: E_t = prod_{s != t} L_s from inclusive
+//           prefix and suffix scans over the lanes (6 levels, both scans in one fe_mul2), times
+//           the lane's other Z (K = 2), times X and Y: X' = X root / Z, Y' = Y root / Z, into LDS;
+//   tail    after one barrier wave j finishes slot j: x = X' root^-1, y = Y' root^-1 (one fe_mul2),
+//           encode, compare with R (requested at the start), ballot.
+// The critical path is the leaves, 6 products, the inversion and one product pair (the one-wave
+// product tree of round 5 put 6 product pairs and the slots one after another behind the
+// inversion): 35.4-35.9 us against 38.3 (same box, ladder_probe events, profiles/ab/r06/).  K = 2
+// from 16K signatures (512 blocks at 64K: the finish co-runs with the other streams' ladders,
+// whose 1,024 blocks of 36 KB fill a 64K batch's LDS, and a block's 9.2 KB fits beside them), K = 1
+// below.
 // ---------------------------------------------------------------------------------------
-#define FINISH_LANES 64
+#define FINISH_BLOCK 128
 template <int K>
-__global__ void __launch_bounds__(FINISH_LANES) ed25519_finish_kernel(const Ed25519Batch b, const uint32_t* xyz_soa,
+__global__ void __launch_bounds__(FINISH_BLOCK) ed25519_finish_kernel(const Ed25519Batch b, const uint32_t* xyz_soa,
                                                                       const uint8_t* flags, const uint8_t* aok,
                                                                       uint64_t* verdict_words) {
-  constexpr uint32_t T = FINISH_LANES;
-  __shared__ uint32_t node[FE_LIMBS][2 * T];  // [limb][heap node]: lanes touch consecutive nodes
-  const uint32_t t = threadIdx.x;
+  static_assert(K == 1 || K == 2, "one or two signatures per lane");
+  constexpr uint32_t T = 64;
+  __shared__ uint32_t xy[K][2][FE_LIMBS][T];  // X' | Y' per slot, [limb][lane]
+  __shared__ uint32_t rinv[FE_LIMBS];         // root^-1
+  const uint32_t t = threadIdx.x & 63u, wave = threadIdx.x >> 6;
   const size_t base = (size_t)blockIdx.x * T * K;
-  fe pre[K];  // pre[j] = Z_0 * .. * Z_j of this lane
+  fe Z[K];
   uint32_t okmask = 0;
 #pragma unroll
   for (int j = 0; j < K; j++) {
     const size_t i = base + (size_t)j * T + t;
-    fe Z;
-    fe_1(Z);
+    fe_1(Z[j]);
     bool ok = false;
     if (i < b.n) {
-      fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
-      ok = flags[i] && unit_aok(b, aok, batch_unit(b, i)) && !fe_iszero(Z);
-      if (!ok) fe_1(Z);
+      fe_load_soa(Z[j], xyz_soa + 18 * b.n, b.n, i);
+      ok = flags[i] && unit_aok(b, aok, batch_unit(b, i)) && !fe_iszero(Z[j]);
+      if (!ok) fe_1(Z[j]);
     }
     okmask |= (ok ? 1u : 0u) << j;
-    if (j == 0)
-      fe_copy(pre[0], Z);
-    else
-      fe_mul<false>(pre[j], pre[j - 1], Z);
   }
+  const uint32_t jt = wave;  // the slot this wave finishes (wave < K)
+  const size_t it = base + (size_t)jt * T + t;
+  uint32_t Rw[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (jt < (uint32_t)K && it < b.n) load_words8(Rw, b.sig + it * 64);  // needed after the barrier
+  fe leaf;
+  if (K == 2)
+    fe_mul(leaf, Z[0], Z[K - 1]);
+  else
+    fe_copy(leaf, Z[0]);
+  if (wave == 0) {
+    fe r = leaf;
 #pragma unroll
-  for (int k = 0; k < FE_LIMBS; k++) node[k][T + t] = pre[K - 1].v[k];
-  __syncthreads();
-#pragma nounroll
-  for (uint32_t m = T >> 1; m >= 1; m >>= 1) {  // up: node n = node 2n * node 2n+1
-    if (t < m) {
-      const uint32_t n = m + t;
-      fe l, r;
+    for (int d = 1; d < 64; d <<= 1) {
+      fe o;
 #pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) {
-        l.v[k] = node[k][2 * n];
-        r.v[k] = node[k][2 * n + 1];
-      }
-      fe_mul<false>(l, l, r);
-#pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) node[k][n] = l.v[k];
+      for (int k = 0; k < FE_LIMBS; k++) o.v[k] = (uint32_t)__shfl_xor((int)r.v[k], d);
+      fe_mul(r, r, o);
     }
-    __syncthreads();
-  }
-  {  // every leaf is non-zero, so is the root: the scalar unit inverts it for the whole wave
-    fe r;
-#pragma unroll
-    for (int k = 0; k < FE_LIMBS; k++) r.v[k] = node[k][1];
-    fe_invert_var<true>(r, r);
-    __syncthreads();  // (one wave: its LDS reads are in order before lane 0's write; kept for clarity)
+    fe_invert_var<true>(r, r);  // every leaf is non-zero, so is the root
     if (t == 0) {
 #pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) node[k][1] = r.v[k];
+      for (int k = 0; k < FE_LIMBS; k++) rinv[k] = r.v[k];
+    }
+  } else {
+    fe P = leaf, S = leaf;  // inclusive prefix / suffix products over the lanes
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      fe p, q;
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        p.v[k] = (uint32_t)__shfl_up((int)P.v[k], d);
+        q.v[k] = (uint32_t)__shfl_down((int)S.v[k], d);
+      }
+      if (t < (uint32_t)d) fe_1(p);
+      if (t + d >= 64u) fe_1(q);
+      fe_mul2_oneasm(P, P, p, S, S, q);
+    }
+    fe pe, se, E;  // P_(t-1), S_(t+1): E_t = the product of every other lane's leaf
+#pragma unroll
+    for (int k = 0; k < FE_LIMBS; k++) {
+      pe.v[k] = (uint32_t)__shfl_up((int)P.v[k], 1);
+      se.v[k] = (uint32_t)__shfl_down((int)S.v[k], 1);
+    }
+    if (t == 0) fe_1(pe);
+    if (t == 63) fe_1(se);
+    fe_mul(E, pe, se);
+    fe c[K];  // 1 / Z_j * root: E times the lane's other signature's Z
+    if (K == 2)
+      fe_mul2_oneasm(c[0], E, Z[K - 1], c[K - 1], E, Z[0]);
+    else
+      fe_copy(c[0], E);
+#pragma unroll
+    for (int j = 0; j < K; j++) {
+      if (!((okmask >> j) & 1u)) continue;
+      const size_t i = base + (size_t)j * T + t;
+      fe X, Y;
+      fe_load_soa(X, xyz_soa, b.n, i);
+      fe_load_soa(Y, xyz_soa + 9 * b.n, b.n, i);
+      fe_mul2_oneasm(X, X, c[j], Y, Y, c[j]);
+#pragma unroll
+      for (int k = 0; k < FE_LIMBS; k++) {
+        xy[j][0][k][t] = X.v[k];
+        xy[j][1][k][t] = Y.v[k];
+      }
     }
   }
   __syncthreads();
-#pragma nounroll
-  for (uint32_t m = 1; m < T; m <<= 1) {  // down: the inverse of node n gives its children's
-    if (t < m) {
-      const uint32_t n = m + t;
-      fe inv, l, r;
+  if (jt >= (uint32_t)K) return;
+  bool verdict = false;
+  if ((okmask >> jt) & 1u) {
+    fe inv, X, Y, x, y;
 #pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) {
-        inv.v[k] = node[k][n];
-        l.v[k] = node[k][2 * n];
-        r.v[k] = node[k][2 * n + 1];
-      }
-      fe li, ri;
-      fe_mul<false>(li, inv, r);
-      fe_mul<false>(ri, inv, l);
-#pragma unroll
-      for (int k = 0; k < FE_LIMBS; k++) {
-        node[k][2 * n] = li.v[k];
-        node[k][2 * n + 1] = ri.v[k];
-      }
+    for (int k = 0; k < FE_LIMBS; k++) {
+      inv.v[k] = rinv[k];
+      X.v[k] = xy[jt][0][k][t];
+      Y.v[k] = xy[jt][1][k][t];
     }
-    __syncthreads();
+    fe_mul2_oneasm(x, X, inv, y, Y, inv);
+    uint32_t Rp[8];
+    fe_to_words(Rp, y);
+    Rp[7] ^= fe_isnegative(x) << 31;
+    uint32_t diff = 0;
+#pragma unroll
+    for (int k = 0; k < 8; k++) diff |= Rp[k] ^ Rw[k];
+    verdict = diff == 0;
   }
-  fe inv;  // 1 / pre[K-1]
-#pragma unroll
-  for (int k = 0; k < FE_LIMBS; k++) inv.v[k] = node[k][T + t];
-#pragma unroll
-  for (int j = K - 1; j >= 0; j--) {
-    const size_t i = base + (size_t)j * T + t;
-    const bool ok = (okmask >> j) & 1u;
-    fe zi;
-    if (j > 0)
-      fe_mul<false>(zi, inv, pre[j - 1]);
-    else
-      fe_copy(zi, inv);
-    bool verdict = false;
-    if (ok) {
-      fe Z, X, Y, x, y;
-      if (j > 0) {
-        fe_load_soa(Z, xyz_soa + 18 * b.n, b.n, i);
-        fe_mul<false>(inv, inv, Z);
-      }
-      fe_load_soa(X, xyz_soa, b.n, i);
-      fe_load_soa(Y, xyz_soa + 9 * b.n, b.n, i);
-      fe_mul<false>(x, X, zi);
-      fe_mul<false>(y, Y, zi);
-      uint32_t Rp[8], Rw[8];
-      fe_to_words(Rp, y);
-      Rp[7] ^= fe_isnegative(x) << 31;
-      load_words8(Rw, b.sig + i * 64);
-      uint32_t diff = 0;
-#pragma unroll
-      for (int k = 0; k < 8; k++) diff |= Rp[k] ^ Rw[k];
-      verdict = diff == 0;
-    }  // (a rejected entry entered the product as 1: inv is already 1 / pre[j-1])
-    const uint64_t ballot = __ballot(verdict);
-    const size_t w0 = base + (size_t)j * T;  // the wave's first signature of step j
-    if (t == 0 && w0 < b.n) verdict_words[w0 >> 6] = ballot;
-  }
+  const uint64_t ballot = __ballot(verdict);
+  const size_t w0 = base + (size_t)jt * T;
+  if (t == 0 && w0 < b.n) verdict_words[w0 >> 6] = ballot;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1658,11 +1658,11 @@ hipError_t cbft_ed25519_launch_verify(const Ed25519Batch& b, const Ed25519Work& 
   if (order && (e = hipEventRecord(order->done[1], stream)) != hipSuccess) return e;
   if (ev) (void)hipEventRecord(ev[2], stream);
   if (w.finish_k == 2)
-    hipLaunchKernelGGL(ed25519_finish_kernel<2>, dim3((unsigned)((b.n + 2 * FINISH_LANES - 1) / (2 * FINISH_LANES))),
-                       dim3(FINISH_LANES), 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words);
+    hipLaunchKernelGGL(ed25519_finish_kernel<2>, dim3((unsigned)((b.n + 127) / 128)), dim3(FINISH_BLOCK), 0, stream, b,
+                       w.xyz_soa, w.flags, w.aok, w.verdict_words);
   else
-    hipLaunchKernelGGL(ed25519_finish_kernel<1>, dim3((unsigned)((b.n + FINISH_LANES - 1) / FINISH_LANES)),
-                       dim3(FINISH_LANES), 0, stream, b, w.xyz_soa, w.flags, w.aok, w.verdict_words);
+    hipLaunchKernelGGL(ed25519_finish_kernel<1>, dim3((unsigned)((b.n + 63) / 64)), dim3(FINISH_BLOCK), 0, stream, b,
+                       w.xyz_soa, w.flags, w.aok, w.verdict_words);
   if (ev) (void)hipEventRecord(ev[3], stream);
   return hipGetLastError();
 }

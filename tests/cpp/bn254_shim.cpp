@@ -53,7 +53,95 @@ static void rf_mul_check(const HU& a, const HU& b) {
   }
 }
 
+// ---- safegcd30.h's wave inversion (sg_inv30_var_wave) over an emulated 64-lane wave: the same
+// stage functions (sg_w_split1 / sg_w_split2 / sg_w_m / sg_canon30 / sg_divsteps30_var) with the
+// DPP row shifts written out (row_shl:1 / row_shr:1 within 16-lane rows, 0 past a row's edge)
+struct Sg25519 {
+  static constexpr int32_t P[9] = {0x3fffffed, 0x3fffffff, 0x3fffffff, 0x3fffffff, 0x3fffffff,
+                                   0x3fffffff, 0x3fffffff, 0x3fffffff, 0x00007fff};
+  static constexpr uint32_t PINV30 = 0x179435e5u;
+};
+static long g_sgw_batches = 0, g_sgw_redundant = 0;
+static void sgw_column(int32_t* out, const int64_t* c) {
+  uint32_t lo[64], la[64];
+  int64_t hi[64];
+  int32_t lo2[64], hi2[64];
+  for (int l = 0; l < 64; l++) sg_w_split1(c[l], lo[l], hi[l]);
+  for (int l = 0; l < 64; l++) la[l] = (l & 15) == 15 ? 0u : lo[l + 1];
+  for (int l = 0; l < 64; l++) sg_w_split2(hi[l], la[l], l == 8, lo2[l], hi2[l]);
+  for (int l = 0; l < 64; l++) out[l] = lo2[l] + ((l & 15) == 0 ? 0 : hi2[l - 1]);
+}
+template <class M>
+static void sgw_inv(Sg30& x) {
+  int32_t P[64] = {0}, f[64], g[64] = {0}, d[64] = {0}, e[64] = {0};
+  for (int k = 0; k < 9; k++) {
+    P[k] = M::P[k];
+    g[k] = x.v[k];
+  }
+  std::memcpy(f, P, sizeof f);
+  e[0] = 1;
+  int32_t eta = -1;
+  for (int it = 0; it < 64; it++) {
+    g_sgw_batches++;
+    int32_t t[4], md, me;
+    eta = sg_divsteps30_var(eta, (uint32_t)f[0], (uint32_t)g[0], t);
+    sg_w_m<M>(md, me, t, d[0], e[0], d[8], e[8]);
+    int64_t cd[64], ce[64], cf[64], cg[64];
+    for (int l = 0; l < 64; l++) {
+      cd[l] = (int64_t)t[0] * d[l] + (int64_t)t[1] * e[l] + (int64_t)P[l] * md;
+      ce[l] = (int64_t)t[2] * d[l] + (int64_t)t[3] * e[l] + (int64_t)P[l] * me;
+      cf[l] = (int64_t)t[0] * f[l] + (int64_t)t[1] * g[l];
+      cg[l] = (int64_t)t[2] * f[l] + (int64_t)t[3] * g[l];
+    }
+    sgw_column(d, cd);
+    sgw_column(e, ce);
+    sgw_column(f, cf);
+    sgw_column(g, cg);
+    for (int l = 0; l < 8; l++)
+      if (d[l] < 0 || d[l] > (int32_t)SG_M30 || e[l] < 0 || e[l] > (int32_t)SG_M30) g_sgw_redundant++;
+    bool far = false;  // some limb cannot be part of a zero value
+    for (int l = 0; l < 64; l++) far = far || !sg_w_zero_limb(g[l]);
+    if (!far) {
+      Sg30 gg;
+      for (int k = 0; k < 9; k++) gg.v[k] = g[k];
+      if (sg_is_zero30(gg)) break;
+    }
+  }
+  const int32_t fsign = f[0] == 1 ? 1 : -1;
+  for (int k = 0; k < 9; k++) x.v[k] = d[k];
+  sg_canon30<M>(x, fsign);
+}
+
 extern "C" {
+
+// sg_inv30_var_wave's emulation on x (32-byte big-endian, < p; which = 0: BN-P254's p, 1:
+// 2^255 - 19): out = x^-1 (big-endian, canonical).  Returns the batches run; *redundant counts the
+// batches that left some low limb of d or e outside [0, 2^30).
+long shim_sg_wave_inv(int which, const uint8_t* x32, uint8_t* out32, long* redundant) {
+  uint32_t w[8];
+  be32_to_words(w, x32);
+  Sg30 x;
+  for (int j = 0; j < 9; j++) {
+    const int b = 30 * j, i = b >> 5, sh = b & 31;
+    const uint64_t v = ((uint64_t)(i + 1 < 8 ? w[i + 1] : 0u) << 32) | (i < 8 ? w[i] : 0u);
+    x.v[j] = (int32_t)((v >> sh) & SG_M30);
+  }
+  g_sgw_batches = 0;
+  g_sgw_redundant = 0;
+  if (which == 0)
+    sgw_inv<BnS30Mod>(x);
+  else
+    sgw_inv<Sg25519>(x);
+  for (int i = 0; i < 8; i++) {
+    const int b = 32 * i, j = b / 30, sh = b % 30;
+    const uint64_t v = ((uint64_t)(uint32_t)(j + 2 < 9 ? x.v[j + 2] : 0) << 60) |
+                       ((uint64_t)(uint32_t)(j + 1 < 9 ? x.v[j + 1] : 0) << 30) | (uint32_t)x.v[j];
+    w[i] = (uint32_t)(v >> sh);
+  }
+  words_to_be32(out32, w);
+  *redundant = g_sgw_redundant;
+  return g_sgw_batches;
+}
 
 // f_add / f_sub / f_addsub on Montgomery forms of a, b (< p, 32-byte big-endian): writes the
 // canonical results of add, sub, addsub(add = 1), addsub(add = 0); returns 1 if the reduced

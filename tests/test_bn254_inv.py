@@ -258,3 +258,24 @@ def test_sha256_key_msg_matches_hashlib(shim):
         shim.shim_sha256_key_msg((ctypes.c_uint32 * 8)(*key), x, msg, m, out)
         kb = bytes(b ^ x for b in struct.pack("<8I", *key))
         assert out.raw == hashlib.sha256(kb + msg).digest(), m
+
+
+@pytest.mark.parametrize("which,p", [(0, P), (1, 2**255 - 19)])
+def test_wave_inversion_emulated(shim, which, p):
+    """safegcd30.h's wave form (sg_inv30_var_wave: scalar divsteps, lane-parallel limb updates in
+    redundant limbs, exact zero test, sg_canon30) over an emulated 64-lane wave, for BN-P254's p
+    (the pairing checks' Fp inversion) and 2^255 - 19 (the Ed25519 finish root): equal to x^(p-2),
+    0 -> 0, within the batch bound, and the redundant-limb case actually exercised."""
+    shim.shim_sg_wave_inv.restype = ctypes.c_long
+    rng = random.Random(0x5A7E + which)
+    xs = [0, 1, 2, 3, 19, p - 1, p - 2, (p - 1) // 2, (p + 1) // 2, 2**253 % p, 2**128, 2**128 - 1]
+    xs += [(1 << k) % p for k in range(0, 255, 3)] + [p - (1 << k) for k in range(0, 250, 9)]
+    xs += [rng.randrange(p) for _ in range(3000)]
+    red_total = 0
+    for x in xs:
+        out, red = ctypes.create_string_buffer(32), ctypes.c_long()
+        nb = shim.shim_sg_wave_inv(which, x.to_bytes(32, "big"), out, ctypes.byref(red))
+        assert int.from_bytes(out.raw, "big") == (pow(x, p - 2, p) if x else 0), hex(x)
+        assert 1 <= nb <= 25
+        red_total += red.value
+    assert red_total > 0

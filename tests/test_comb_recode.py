@@ -12,7 +12,7 @@ import pytest
 L = 2**252 + 27742317777372353535851937790883648493
 NPOS = {8: 32, 9: 29, 10: 26, 11: 23, 12: 22, 13: 20, 14: 19, 15: 17, 16: 16, 17: 15, 18: 15, 19: 14, 20: 13,
         21: 13, 22: 12, 23: 11, 24: 11, 25: 11, 26: 10}
-B_RADICES = (16, 22, 24, 26)  # B's table: CBFT_COMB_B_RADIX (22) and $CBFT_B_RADIX alternatives
+B_RADICES = (16, 22, 24, 26)  # B's table: CBFT_COMB_B_RADIX (22) and cbft_set_option(CBFT_OPT_B_RADIX) alternatives
 
 
 def offset(w, npos):

@@ -120,8 +120,8 @@ def test_ragged_batch_sizes(ctx, golden, n):
 
 @pytest.mark.parametrize("n", [8191, 8192, 8193, 20000])
 def test_host_staging_boundary(ctx, n):
-    # host-buffer batches up to 8,192 go through one packed pinned staging copy, larger ones
-    # through per-array copies (cbft_hipcrypto.cpp, CBFT_STAGE_MAX_N): both sides of the switch,
+    # host-buffer batches whose pageable inputs fit CBFT_PACK_MAX go through one packed pinned
+    # staging copy, larger ones through per-array copies (cbft_hipcrypto.cpp): both sides of it,
     # key-table and per-signature keys, mixed lengths with 10 % invalid
     ss = sigsets.make_sigset(n, nkeys=97, msg_len=(1, 700), seed=n, invalid_frac=0.10)
     tid = ctx.load_keys(ss.pk)

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Build an A/B variant of libcbft_hipcrypto.so: one TU (default ed25519_verify; TU=bls_pairing etc.)
 # recompiled with extra -D flags, linked with the default objects of every other TU (`make lib` first).
-#   [TU=name] tools/build_variant.sh NAME "-DCBFT_DECODE_ROW=0 ..."   -> build/lib_NAME.so
+#   [TU=name] tools/build_variant.sh NAME "-DCBFT_INV_WAVE=0 ..."   -> build/lib_NAME.so
 set -e
 cd "$(dirname "$0")/.."
 name=$1; shift

@@ -1,7 +1,7 @@
 """Ladder timing probe (device-resident path, one batch at a time, HIP-event stage times).
 
 python tools/ladder_probe.py [--nkeys 1 4096] [--nocheck]
-Runs on whatever libcbft_hipcrypto $CBFT_LIB names; $CBFT_B_RADIX etc. apply as usual.  With
+Runs on whatever libcbft_hipcrypto $CBFT_LIB names (an A/B build, tools/build_variant.sh).  With
 --nocheck the verdicts are not compared (probe builds that skip the table loads)."""
 import argparse
 import json
@@ -57,8 +57,7 @@ def main():
             for k, v in ctx.stage_times_ms().items():
                 st[k].append(v)
         ctx.set_profiling(False)
-        print(json.dumps({"lib": os.environ.get("CBFT_LIB", "default"), "b_radix": os.environ.get("CBFT_B_RADIX", "22"),
-                          "nkeys": nk, "verdicts_ok": ok,
+        print(json.dumps({"lib": os.environ.get("CBFT_LIB", "default"), "nkeys": nk, "verdicts_ok": ok,
                           "us": {k: round(statistics.median(v) * 1e3, 1) for k, v in st.items()}}), flush=True)
         ctx.close()
 

@@ -23,5 +23,4 @@ with cb.Context(device=0) as ctx:
     tid = ctx.load_keys(ss.pk)
     value, hash_ms, _steps = bench._mixed_device_resident(ctx, tid, ss, args)
 print(json.dumps({"device_resident_value": value, "hash_ms": hash_ms, "streams": args.mixed_streams,
-                  "work_slots": os.environ.get("CBFT_WORK_SLOTS", "default"),
-                  "hash_order_early": os.environ.get("CBFT_HASH_ORDER_EARLY", "default")}))
+                  "lib": os.environ.get("CBFT_LIB", "default")}))
