@@ -164,11 +164,15 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # CBFT_BENCH_SHARED_GPU=1: a rehearsal of the N > 1 rank path on a one-GPU box -- every rank on
+    # device 0, a gloo process group (cbft_multigpu stages the collectives through the host).  It
+    # runs the same code as an N-GPU run except RCCL; its rates are not a scaling measurement.
+    shared_gpu = world > 1 and os.environ.get("CBFT_BENCH_SHARED_GPU") == "1"
     dist = None
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")  # RCCL on ROCm
+        torch.cuda.set_device(0 if shared_gpu else local)
+        dist.init_process_group("gloo" if shared_gpu else "nccl")  # RCCL on ROCm
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -515,11 +519,11 @@ def main():
     # same per-device batch as a shard of one N x batch call, verdicts gated as above
     single = None
     sp_devices = [int(x) for x in args.single_process_devices.split(",") if x] or \
-        (list(range(world)) if world > 1 else [])
+        (([0] * world if shared_gpu else list(range(world))) if world > 1 else [])
     if world > 1:
         dist.barrier()
     if rank == 0 and sp_devices:
-        single = bench_single_process(args, ss, sp_devices, mask=(world > 1 and not args.single_process_devices))
+        single = bench_single_process(args, ss, sp_devices, mask=(world > 1 and not args.single_process_devices and not shared_gpu))
     if world > 1:
         dist.barrier()
 
@@ -618,8 +622,10 @@ def main():
                                   "GPU at N = 8 (= --batch 131072 per rank), one RCCL all-gather of verdict words",
                        "pcie_inclusive_inputs": "pinned host memory (cbft_host_alloc) -> GPU each step; bitmap -> host",
                        "inflight_batches": depth,
-                       "parallelism": f"static shard x{world}" + (", RCCL all-gather of verdict bitmaps"
-                                                                  if world > 1 else ""),
+                       "parallelism": f"static shard x{world}" + (
+                           ", REHEARSAL: every rank on GPU 0, gloo process group (CBFT_BENCH_SHARED_GPU=1), "
+                           "not a scaling measurement" if shared_gpu else
+                           ", RCCL all-gather of verdict bitmaps" if world > 1 else ""),
                        "rank0_numa_node": numa},
             "roofline": roofline, "cpu_baseline": cpu,
             "gpu_vs_cpu": (value / cpu["value"]) if cpu else None,

@@ -27,6 +27,31 @@ def shard_bounds(n: int, world: int, rank: int) -> Tuple[int, int]:
     return lo, min(n, lo + s)
 
 
+def _host_staged(dist, t) -> bool:
+    """gloo has no all-gather of device tensors: a rehearsal of the rank path on a gloo process
+    group (bench.py with CBFT_BENCH_SHARED_GPU=1: several ranks sharing one GPU) stages device
+    tensors through the host.  RCCL runs take the device path untouched."""
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
+def _all_gather_into(out, t, dist):
+    if _host_staged(dist, t):
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, t.cpu())
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, t)
+
+
+def _all_reduce(t, op, dist):
+    if _host_staged(dist, t):
+        c = t.cpu()
+        dist.all_reduce(c, op=op)
+        t.copy_(c)
+    else:
+        dist.all_reduce(t, op=op)
+
+
 def gather_verdicts(local_words, n: int, world: int, dist):
     """All-gather each rank's verdict words (int64 tensor of shard_size/64 words, zero-padded)
     and return the global ceil(n/64)-word bitmap on every rank."""
@@ -35,7 +60,7 @@ def gather_verdicts(local_words, n: int, world: int, dist):
     words = shard_size(n, world) // 64
     assert local_words.numel() == words, (local_words.numel(), words)
     out = torch.empty(world * words, dtype=local_words.dtype, device=local_words.device)
-    dist.all_gather_into_tensor(out, local_words)
+    _all_gather_into(out, local_words, dist)
     return out[: (n + 63) // 64]
 
 
@@ -71,7 +96,7 @@ def max_over_ranks(x: float, dist, device) -> float:
     import torch
 
     t = torch.tensor([x], dtype=torch.float64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    _all_reduce(t, dist.ReduceOp.MAX, dist)
     return float(t.item())
 
 
@@ -79,7 +104,7 @@ def sum_over_ranks(x: int, dist, device) -> int:
     import torch
 
     t = torch.tensor([x], dtype=torch.int64, device=device)
-    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    _all_reduce(t, dist.ReduceOp.SUM, dist)
     return int(t.item())
 
 
@@ -106,7 +131,7 @@ def all_gather_rows(t, world: int, dist):
     import torch
 
     out = torch.empty((world * t.numel(),), dtype=t.dtype, device=t.device)
-    dist.all_gather_into_tensor(out, t.contiguous().view(-1))
+    _all_gather_into(out, t.contiguous().view(-1), dist)
     return out.view(world, *t.shape)
 
 
@@ -130,7 +155,7 @@ class StepVerdicts:
         return self.local[j].data_ptr()
 
     def _gather(self, j: int):
-        self.dist.all_gather_into_tensor(self.gathered[j].view(-1), self.local[j])
+        _all_gather_into(self.gathered[j].view(-1), self.local[j], self.dist)
 
     def after_step(self, j: int, launch_stream=None):
         """Row j was written by work queued on launch_stream: all-gather it (N > 1)."""
@@ -231,7 +256,7 @@ def _gather_bytes(blob: bytes, world: int, dist, device) -> list:
 
     t = torch.from_numpy(np.frombuffer(blob, dtype=np.uint8).copy()).to(device)
     out = torch.empty(world * len(blob), dtype=torch.uint8, device=device)
-    dist.all_gather_into_tensor(out, t)
+    _all_gather_into(out, t, dist)
     raw = out.cpu().numpy().tobytes()
     return [raw[r * len(blob):(r + 1) * len(blob)] for r in range(world)]
 
