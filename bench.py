@@ -526,6 +526,8 @@ def main():
         single = bench_single_process(args, ss, sp_devices, mask=(world > 1 and not args.single_process_devices and not shared_gpu))
     if world > 1:
         dist.barrier()
+    # config #4 sharded over the ranks (the BLS multi-GPU rows); the single-GPU legs below run at N = 1
+    bls_sharded = bench_bls_sharded(ctx, args, cpu_threads, world, rank, dist, dev) if (world > 1 and args.extras) else None
 
     out = None
     if rank == 0:
@@ -596,7 +598,8 @@ def main():
         detail = _write_detail({"workload_gen_s": gen_s, "flood_config5": flood, "step_spread": step_spread, "gpu_clocks": gpu_clk, "comb_radix_cliff": cliff,
                                 "comb_radix_cliff_fields": "comb radix, M verifies/s, MB per key, max keys in budget",
                                 "parity": parity, "roofline": roofline, "mixed_config3": mixed, "bls_config4": bls,
-                                "rsa_2048": rsa, "per_request_path": per_request, "single_process_multi_gpu": single})
+                                "rsa_2048": rsa, "per_request_path": per_request, "single_process_multi_gpu": single,
+                                "bls_config4_sharded": bls_sharded})
         small_name = "ed25519_small3_kernel"  # the fused small-batch kernel
         small_k, small_stat = _pmc_record("pmc_ed25519_small.json", small_name)
         # The line: the contract's keys first, then side measurements, and LAST what the driver's
@@ -636,6 +639,7 @@ def main():
             "cold_start_ms_per_step": cold_elapsed / args.steps * 1e3,
             "pageable_host_value": pageable,
             "single_process_multi_gpu": _brief(single, ("value", "devices", "open", "ms_per_step")),
+            "bls_config4_sharded": bls_sharded,
             "step_spread_ms": [round(step_spread[k], 4) for k in ("median_ms", "min_ms", "max_ms",
                                                                    "steady_ms_per_step")],
             "sclk_mhz": _clk_brief(gpu_clk),
@@ -1213,6 +1217,66 @@ def bench_bls(ctx, args, cpu_threads):
                                          f"own BN-P254 code compiled for the host: an UNOPTIMISED port, not RELIC "
                                          f"(absent) and not an optimized CPU pairing; no speed-up is claimed "
                                          f"against it"}
+    return out
+
+
+def bench_bls_sharded(ctx, args, cpu_threads, world, rank, dist, dev):
+    """Config #4 across the ranks (N > 1), through cbft_multigpu: each
+    rank verifies its slice of the 760 shares (one all-gather of the validity bitmap), each rank
+    Lagrange-sums its slice of the 683 valid shares (one all-gather of the G1 partials, then the
+    sum), and the multisig public key is summed by id range (one all-gather of G2 partials) before
+    the pairing check.  Every rank builds the same certificate; every result is checked on every
+    rank; times are the contract's (barrier + synchronize, max over ranks), median of 5."""
+    n, k = 1024, 683
+    cert = workload.make_bls_cert(n, k, extra=77, bad_frac=0.10, seed=2024, threads=cpu_threads)
+    kid = ctx.bls_load_keys(cert.pk, cert.vks)
+    exp = np.array([j not in cert.bad for j in range(len(cert.shares))])
+    use = [s for j, s in enumerate(cert.shares) if exp[j]][:k]
+    bitmap = bytearray(256)
+    for i in (int.from_bytes(s[:4], "big") for s in use):
+        bitmap[(i - 1) // 8] |= 1 << ((i - 1) % 8)
+    bitmap = bytes(bitmap)
+    bad = 0
+
+    def shares():
+        return mg.bls_verify_shares_sharded(ctx, kid, cert.msg, cert.shares, world, rank, dist, dev)
+
+    def combine():
+        return mg.bls_combine_sharded(ctx, use, world, rank, dist, dev)
+
+    def multisig():
+        msig = mg.bls_combine_sharded(ctx, use, world, rank, dist, dev, multisig=True)
+        return mg.bls_verify_multisig_sharded(ctx, kid, n, cert.msg, msig, bitmap, world, rank, dist, dev)
+
+    def certificate():
+        v = shares()
+        c = mg.bls_combine_sharded(ctx, [s for j, s in enumerate(cert.shares) if v[j]][:k], world, rank, dist, dev)
+        return c == cert.expected_sig and ctx.bls_verify(kid, cert.msg, c)
+
+    try:
+        bad += int((np.asarray(shares(), dtype=bool) != exp).sum())
+        bad += int(combine() != cert.expected_sig)
+        bad += int(not multisig())
+        bad += int(not certificate())
+        bad = mg.sum_over_ranks(bad, dist, dev)
+        if bad:
+            raise SystemExit(f"rank {rank}: sharded BLS config #4: {bad} results differ from the expected ones")
+
+        import torch
+
+        def med(fn):
+            ts = [mg.timed_region(lambda _s: fn(), 1, dist, torch.cuda.synchronize, dev) * 1e3 for _ in range(5)]
+            return statistics.median(ts)
+
+        out = {"config": f"config #4 over {world} ranks: n={n}, k={k}, {len(cert.shares)} shares "
+                         f"({len(cert.bad)} bad)",
+               "share_verify_ms": med(shares), "combine_ms": med(combine), "multisig_ms": med(multisig),
+               "certificate_ms": med(certificate),
+               "shares_per_rank": mg.share_slice(len(cert.shares), world, 0)[1],
+               "verdicts": "share bitmap == planted bad set, combined sig == sk*H(m), multisig verifies, on "
+                           "every rank"}
+    finally:
+        ctx.bls_unload_keys(kid)
     return out
 
 

@@ -14,5 +14,5 @@ import json; d=json.loads(open('$o/bench.json').read().strip().splitlines()[-1])
 print('n_gpus', d['n_gpus'], 'value', round(d['value']/1e6,1), 'cold', round(d['cold_start_value']/1e6,1), 'pcie', round(d['pcie_inclusive_value']/1e6,1))
 print('parity', d['parity']['all_exact'], d['parity']['blocks'].get('config2_headline'), d['parity']['blocks'].get('config5_flood'))
 print('flood', d['flood_config5']); print('single', d.get('single_process_multi_gpu')); print('par', d['config']['parallelism'])
-print('cpu', d['cpu_baseline']['value'] if d.get('cpu_baseline') else None)
+print('cpu', d['cpu_baseline']['value'] if d.get('cpu_baseline') else None); print('bls_sharded', d.get('bls_config4_sharded'))
 "
