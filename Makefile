@@ -12,8 +12,8 @@ ORACLE_LIB := oracle/libcbft_oracle.so
 # host SIMD emulation of the same source is exact).  Costs one v_mov_dpp per move.
 ROWFLAGS := -mllvm -amdgpu-dpp-combine=false
 
-.PHONY: all lib oracle clean shim fe_row_shim sanitize
-all: lib oracle cpu host shim fe_row_shim
+.PHONY: all lib oracle clean shim fe_row_shim sanitize selftest
+all: lib oracle cpu host shim fe_row_shim selftest
 
 lib: $(LIB)
 
@@ -118,3 +118,9 @@ $(MB)/%: $(MB)/%.hip
 $(MB)/pack_probe: $(MB)/pack_probe.cpp
 	$(HIPCC) -O2 -std=c++17 -o $@ $< -lpthread
 .PHONY: microbench
+
+# test-only device harness of the wave inversion (tests/test_inv_gpu.py; not the product library)
+SELFTEST := tests/hip/libinv_selftest.so
+selftest: $(SELFTEST)
+$(SELFTEST): tests/hip/inv_selftest.hip $(CSRC)/safegcd30.h
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $<
