@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--nkeys", type=int, nargs="+", default=[4096])
     ap.add_argument("--batch", type=int, default=65536)
     ap.add_argument("--radix", type=int, default=13)
+    ap.add_argument("--b-radix", type=int, default=0, help="B's comb radix (cbft_set_option; 0 = default 22)")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--nocheck", action="store_true")
     a = ap.parse_args()
@@ -30,6 +31,8 @@ def main():
     for nk in a.nkeys:
         ss = workload.make_sigset(a.batch, nkeys=nk, msg_len=256, seed=0xC0FFEE, threads=16)
         ctx = cb.Context(device=0, max_batch=a.batch)
+        if a.b_radix:
+            ctx.set_option(cb.OPT_B_RADIX, a.b_radix)
         tid = ctx.load_keys(ss.pk, radix=a.radix)
 
         def to_dev(x, dt):
