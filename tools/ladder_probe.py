@@ -25,11 +25,18 @@ def main():
     ap.add_argument("--b-radix", type=int, default=0, help="B's comb radix (cbft_set_option; 0 = default 22)")
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--nocheck", action="store_true")
+    ap.add_argument("--sort-keys", action="store_true", help="order the batch by key index (table locality probe)")
     a = ap.parse_args()
     import torch
     dev = torch.device("cuda", 0)
     for nk in a.nkeys:
         ss = workload.make_sigset(a.batch, nkeys=nk, msg_len=256, seed=0xC0FFEE, threads=16)
+        if a.sort_keys:  # fixed 256-B messages: permute key indices, signatures, message rows, verdicts
+            o = np.argsort(ss.key_idx, kind="stable")
+            ss.key_idx = np.ascontiguousarray(ss.key_idx[o])
+            ss.sig = np.ascontiguousarray(ss.sig.reshape(a.batch, 64)[o]).reshape(ss.sig.shape)
+            ss.blob = np.ascontiguousarray(ss.blob[: a.batch * 256].reshape(a.batch, 256)[o]).reshape(-1)
+            ss.expected = ss.expected[o]
         ctx = cb.Context(device=0, max_batch=a.batch)
         if a.b_radix:
             ctx.set_option(cb.OPT_B_RADIX, a.b_radix)
@@ -60,7 +67,8 @@ def main():
             for k, v in ctx.stage_times_ms().items():
                 st[k].append(v)
         ctx.set_profiling(False)
-        print(json.dumps({"lib": os.environ.get("CBFT_LIB", "default"), "nkeys": nk, "verdicts_ok": ok,
+        print(json.dumps({"lib": os.environ.get("CBFT_LIB", "default"), "nkeys": nk, "sorted": a.sort_keys,
+                          "radix": a.radix, "verdicts_ok": ok,
                           "us": {k: round(statistics.median(v) * 1e3, 1) for k, v in st.items()}}), flush=True)
         ctx.close()
 

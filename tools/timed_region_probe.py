@@ -32,6 +32,8 @@ ap.add_argument("--ramp", type=int, default=0, help="after 2 s idle, N steps wit
 ap.add_argument("--nkeys", type=int, default=4096, help="client keys (key-table footprint 10.5 MB each at radix 13)")
 ap.add_argument("--distinct", type=int, default=1,
                 help="distinct batches cycled over the steps (1 = the same batch every step, as bench.py)")
+ap.add_argument("--radix", type=int, default=13, help="key comb radix")
+ap.add_argument("--sort-keys", action="store_true", help="every batch ordered by key index (table locality probe)")
 args = ap.parse_args()
 
 import numpy as np  # noqa: E402
@@ -41,9 +43,15 @@ torch.cuda.set_device(0)
 dev = torch.device("cuda", 0)
 n, L = 65536, 256
 sets = [workload.make_sigset(n, nkeys=args.nkeys, msg_len=L, seed=0xC0FFEE + 7919 * k, threads=16) for k in range(args.distinct)]
+if args.sort_keys:  # fixed 256-B messages: permute key indices, signatures, message rows
+    for t in sets:
+        o = np.argsort(t.key_idx, kind="stable")
+        t.key_idx = np.ascontiguousarray(t.key_idx[o])
+        t.sig = np.ascontiguousarray(t.sig.reshape(n, 64)[o])
+        t.blob = np.ascontiguousarray(t.blob[: n * L].reshape(n, L)[o]).reshape(-1)
 ss = sets[0]
 ctx = cb.Context(device=0, max_batch=n)
-tid = ctx.load_keys(ss.pk, radix=13)
+tid = ctx.load_keys(ss.pk, radix=args.radix)
 for t in sets[1:]:
     assert np.array_equal(t.pk, ss.pk), "same key set"
 
